@@ -1,0 +1,734 @@
+// Fused MLP training step for CDNA4 (gfx950): forward + loss + backward of a
+// [Linear -> act -> BatchNorm1d]* -> Linear network in ONE workgroup, bf16 MFMA
+// (v_mfma_f32_16x16x32_bf16) with fp32 accumulation, followed by a wide fused
+// Adam/AdamW/SGD kernel that also refreshes the bf16 weight images.
+//
+// Why one workgroup: the reference workloads (NYC_Model in examples/pytorch_nyctaxi.py:69-92,
+// batch 64; the stroke tutorial MLPs; DLRM's MLP towers) are ~6 MFLOP per step, so the step is
+// latency bound. A chain of ~60 PyTorch launches costs far more than the math; here the whole
+// dependency chain (10 GEMMs, 4 BatchNorm reductions, loss) runs in one CU with every
+// activation resident in LDS, and column reductions stay inside a wave (each wave owns whole
+// 16-column output tiles, so BN statistics are wave-local shuffles).
+//
+// Layouts (all bf16 LDS matrices have a +16 B row pad: ds_read_b128 of 16 rows at the same
+// column then hits 16 distinct 16-B slots of the 256-B bank row -> conflict free):
+//   R  [Bpad][max_k]    row-major activations (fwd A operand) / gradients (dgrad A operand)
+//   GT [max_n][Bpad]    transposed gradient (wgrad A operand)
+//   XT_l [in_n][Bpad]   transposed layer inputs saved for wgrad (wgrad B operand)
+// Weights come from global memory as two bf16 images written by the optimizer kernel:
+//   W  [out_n][in_k]  (fwd B operand, K = in contiguous)
+//   Wt [in_n][out_k]  (dgrad B operand, K = out contiguous)
+#include "rx_common.h"
+
+#define RX_MAXL 8
+#define RX_NW 8          // waves per workgroup
+#define RX_THREADS (RX_NW * RX_WAVE)
+
+struct MlpLayer {
+  int in, out;
+  int in_k, out_k;   // K padding (multiple of 32)
+  int in_n, out_n;   // N padding (multiple of 16)
+  const u16* W;
+  const u16* Wt;
+  int w_off, b_off;  // offsets into the flat fp32 parameter / gradient vectors
+  int act;           // 0 identity, 1 relu
+  int bn;            // 0 none, 1 act->bn, 2 bn->act
+  int g_off, be_off; // BN affine params (-1: not affine)
+  float* run_mean;
+  float* run_var;
+  float eps, momentum;
+  int xt_off;        // LDS byte offset of XT_l
+  int stat_off;      // float offset of (mean, invstd) pairs for this layer's outputs in LDS
+  int r_off;         // float offset of the saved pre-BN values in the scratch buffer
+};
+
+struct MlpDesc {
+  int L;
+  int r_lds_off, gt_lds_off, stats_lds_off, lds_bytes;
+  int max_k, max_n;
+  int loss;          // 0 mse, 1 smooth_l1, 2 l1
+  float beta;        // smooth_l1 beta
+  int out_dim;
+  int feat_k;        // row stride of the bf16 feature matrix
+  MlpLayer layer[RX_MAXL];
+};
+
+namespace {
+
+template <int MT>
+struct Tile {
+  static constexpr int BP = MT * 16;         // padded batch rows
+  static constexpr int NTW = 16 / MT;        // max output n-tiles per wave (64 acc regs)
+  static constexpr int XS = BP + 8;          // stride (elements) of transposed matrices
+};
+
+__device__ __forceinline__ float act_fwd(int act, float z) { return act == 1 ? fmaxf(z, 0.f) : z; }
+
+// ------------------------------------------------------------------------------------------
+// forward of layer l for the rows of this workgroup. Leaves y (the layer output after
+// act/BN) in R (row-major) and in XT_{l+1}; for the last layer computes loss, metrics and
+// writes dL/dy into R/GT as G_{L-1}.
+// ------------------------------------------------------------------------------------------
+template <int MT, bool TRAIN>
+__device__ void layer_forward(const MlpDesc& d, int l, char* smem, const float* __restrict__ P,
+                              float* __restrict__ Gr, const float* __restrict__ labels,
+                              const int* __restrict__ rowidx, int nvalid, float* __restrict__ scratch,
+                              double* __restrict__ metrics) {
+  using T = Tile<MT>;
+  const MlpLayer& ly = d.layer[l];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int RS = d.max_k + 8;
+  u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
+  u16* GT = reinterpret_cast<u16*>(smem + d.gt_lds_off);
+  float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
+  const bool last = (l == d.L - 1);
+  const int ntiles = ly.out_n >> 4;
+
+  f32x4 acc[T::NTW * MT];
+#pragma unroll
+  for (int i = 0; i < T::NTW * MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < ly.in_k; k0 += 32) {
+#pragma unroll
+    for (int j = 0; j < T::NTW; ++j) {
+      const int n = wave + j * RX_NW;
+      if (n < ntiles) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(ly.W + (n * 16 + lr) * ly.in_k + k0 + 8 * lg);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(R + (mt * 16 + lr) * RS + k0 + 8 * lg);
+          acc[j * MT + mt] = rx_mfma16(a, b, acc[j * MT + mt]);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue in registers: bias, act, BN (train: batch stats; eval: running stats) ----
+  float y[T::NTW * MT * 4];
+  float gsum[T::NTW];  // last layer: db (column sums of dL/dy)
+#pragma unroll
+  for (int j = 0; j < T::NTW; ++j) {
+    gsum[j] = 0.f;
+    const int n = wave + j * RX_NW;
+    const int c = n * 16 + lr;
+    const bool colok = (n < ntiles) && (c < ly.out);
+    const float bias = (colok && ly.b_off >= 0) ? P[ly.b_off + c] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float z = acc[j * MT + mt][r] + bias;
+        y[(j * MT + mt) * 4 + r] = z;
+      }
+    if (n >= ntiles) continue;
+    if (ly.bn == 0) {
+#pragma unroll
+      for (int q = 0; q < MT * 4; ++q) y[j * MT * 4 + q] = act_fwd(ly.act, y[j * MT * 4 + q]);
+    } else {
+      if (ly.bn == 1) {
+#pragma unroll
+        for (int q = 0; q < MT * 4; ++q) y[j * MT * 4 + q] = act_fwd(ly.act, y[j * MT * 4 + q]);
+      }
+      float mean, invstd;
+      if (TRAIN) {
+        float s = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = mt * 16 + lg * 4 + r;
+            s += (row < nvalid) ? y[(j * MT + mt) * 4 + r] : 0.f;
+          }
+        s = rx_colsum16(s);
+        mean = s / (float)nvalid;
+        float v = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = mt * 16 + lg * 4 + r;
+            const float dv = y[(j * MT + mt) * 4 + r] - mean;
+            v += (row < nvalid) ? dv * dv : 0.f;
+          }
+        v = rx_colsum16(v);
+        const float var = v / (float)nvalid;
+        invstd = rsqrtf(var + ly.eps);
+        if (colok && lg == 0) {
+          stats[ly.stat_off + 2 * c] = mean;
+          stats[ly.stat_off + 2 * c + 1] = invstd;
+          const float unb = nvalid > 1 ? var * (float)nvalid / (float)(nvalid - 1) : var;
+          ly.run_mean[c] = (1.f - ly.momentum) * ly.run_mean[c] + ly.momentum * mean;
+          ly.run_var[c] = (1.f - ly.momentum) * ly.run_var[c] + ly.momentum * unb;
+        }
+        // save the BN input for the backward pass (thread-private slots)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = mt * 16 + lg * 4 + r;
+            scratch[ly.r_off + row * ly.out_n + c] = y[(j * MT + mt) * 4 + r];
+          }
+      } else {
+        mean = colok ? ly.run_mean[c] : 0.f;
+        invstd = colok ? rsqrtf(ly.run_var[c] + ly.eps) : 0.f;
+      }
+      const float gam = (colok && ly.g_off >= 0) ? P[ly.g_off + c] : 1.f;
+      const float bet = (colok && ly.be_off >= 0) ? P[ly.be_off + c] : 0.f;
+#pragma unroll
+      for (int q = 0; q < MT * 4; ++q) {
+        float t = (y[j * MT * 4 + q] - mean) * invstd * gam + bet;
+        if (ly.bn == 2) t = act_fwd(ly.act, t);
+        y[j * MT * 4 + q] = t;
+      }
+    }
+    if (!colok) {
+#pragma unroll
+      for (int q = 0; q < MT * 4; ++q) y[j * MT * 4 + q] = 0.f;
+    }
+    if (TRAIN && ly.bn == 0 && !last) {
+      // ReLU mask source for the backward pass
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + lg * 4 + r;
+          scratch[ly.r_off + row * ly.out_n + c] = y[(j * MT + mt) * 4 + r];
+        }
+    }
+    // padded rows carry exact zeros through every GEMM
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + lg * 4 + r;
+        if (row >= nvalid) y[(j * MT + mt) * 4 + r] = 0.f;
+      }
+    if (last) {
+      // loss, metrics and dL/dy (mean reduction over nvalid * out_dim elements)
+      float lsum = 0.f, asum = 0.f, ssum = 0.f;
+      const float inv_n = 1.f / (float)(nvalid * ly.out);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + lg * 4 + r;
+          float g = 0.f;
+          if (colok && row < nvalid) {
+            const float t = labels[rowidx[row] * d.out_dim + c];
+            const float e = y[(j * MT + mt) * 4 + r] - t;
+            const float ae = fabsf(e);
+            asum += ae;
+            ssum += e * e;
+            if (d.loss == 0) {
+              lsum += e * e;
+              g = 2.f * e;
+            } else if (d.loss == 1) {
+              if (ae < d.beta) {
+                lsum += 0.5f * e * e / d.beta;
+                g = e / d.beta;
+              } else {
+                lsum += ae - 0.5f * d.beta;
+                g = e > 0.f ? 1.f : -1.f;
+              }
+            } else {
+              lsum += ae;
+              g = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+            }
+            g *= inv_n;
+          }
+          y[(j * MT + mt) * 4 + r] = g;  // y now holds G_{L-1}
+          gsum[j] += g;
+        }
+      lsum = rx_wavesum(lsum);
+      asum = rx_wavesum(asum);
+      ssum = rx_wavesum(ssum);
+      if (lane == 0) {
+        atomicAdd(&metrics[0], (double)(lsum * inv_n));
+        atomicAdd(&metrics[1], (double)asum);
+        atomicAdd(&metrics[2], (double)ssum);
+        if (n == 0) {
+          atomicAdd(&metrics[3], (double)(nvalid * ly.out));
+          atomicAdd(&metrics[4], 1.0);
+        }
+      }
+      if (TRAIN) {
+        gsum[j] = rx_colsum16(gsum[j]);
+        if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum[j];
+      }
+    }
+  }
+  __syncthreads();  // every wave finished reading R for this layer
+  if (last && !TRAIN) return;
+
+  // ---- publish y (or G_{L-1}) as bf16: row-major into R, transposed into XT_{l+1} / GT ----
+  const int XS = T::XS;
+  u16* dstT = last ? GT : reinterpret_cast<u16*>(smem + d.layer[l + 1].xt_off);
+  const int tstride = last ? (T::BP + 8) : XS;
+#pragma unroll
+  for (int j = 0; j < T::NTW; ++j) {
+    const int n = wave + j * RX_NW;
+    if (n >= ntiles) continue;
+    const int c = n * 16 + lr;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      u16 h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        h[r] = rx_f2bf(y[(j * MT + mt) * 4 + r]);
+        R[(mt * 16 + lg * 4 + r) * RS + c] = h[r];
+      }
+      if (TRAIN || !last) {
+        uint2 pk;
+        pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+        pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+        *reinterpret_cast<uint2*>(dstT + c * tstride + mt * 16 + lg * 4) = pk;
+      }
+    }
+  }
+  // zero the K padding columns [out_n, out_k) of R so the next GEMM's K tail is exact
+  const int kpad = (last ? ly.out_k : d.layer[l + 1].in_k) - ly.out_n;
+  if (kpad > 0) {
+    for (int idx = threadIdx.x; idx < T::BP * kpad; idx += RX_THREADS) {
+      const int row = idx / kpad, cc = ly.out_n + idx % kpad;
+      R[row * RS + cc] = 0;
+    }
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------
+// backward of layer l: G_l is in R (row-major) and GT (transposed).
+// ------------------------------------------------------------------------------------------
+template <int MT>
+__device__ void layer_backward(const MlpDesc& d, int l, char* smem, const float* __restrict__ P,
+                               float* __restrict__ Gr, int nvalid, const float* __restrict__ scratch) {
+  using T = Tile<MT>;
+  const MlpLayer& ly = d.layer[l];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int RS = d.max_k + 8;
+  const int XS = T::XS;
+  u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
+  u16* GT = reinterpret_cast<u16*>(smem + d.gt_lds_off);
+  const u16* XT = reinterpret_cast<const u16*>(smem + ly.xt_off);
+  float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
+
+  // ---- wgrad: dW[o][i] = sum_b G[b][o] X[b][i]  (A = GT, B = XT, K = Bpad) ----
+  {
+    const int mo_tiles = ly.out_n >> 4, ni_tiles = ly.in_n >> 4;
+    const int ntile = mo_tiles * ni_tiles;
+    for (int t = wave; t < ntile; t += RX_NW) {
+      const int mo = t / ni_tiles, ni = t % ni_tiles;
+      f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < T::BP; k0 += 32) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(GT + (mo * 16 + lr) * XS + k0 + 8 * lg);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(XT + (ni * 16 + lr) * XS + k0 + 8 * lg);
+        a4 = rx_mfma16(a, b, a4);
+      }
+      const int i = ni * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = mo * 16 + lg * 4 + r;
+        if (o < ly.out && i < ly.in) Gr[ly.w_off + o * ly.in + i] = a4[r];
+      }
+    }
+  }
+  if (l == 0) return;
+
+  // ---- dgrad: dX[b][i] = sum_o G[b][o] W[o][i]  (A = R, B = Wt, K = out_k) ----
+  const MlpLayer& pv = d.layer[l - 1];  // owns the post-ops between layer l-1 and l
+  const int ntiles = ly.in_n >> 4;
+  f32x4 acc[T::NTW * MT];
+#pragma unroll
+  for (int i = 0; i < T::NTW * MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < ly.out_k; k0 += 32) {
+#pragma unroll
+    for (int j = 0; j < T::NTW; ++j) {
+      const int n = wave + j * RX_NW;
+      if (n < ntiles) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(ly.Wt + (n * 16 + lr) * ly.out_k + k0 + 8 * lg);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(R + (mt * 16 + lr) * RS + k0 + 8 * lg);
+          acc[j * MT + mt] = rx_mfma16(a, b, acc[j * MT + mt]);
+        }
+      }
+    }
+  }
+  __syncthreads();  // all reads of G_l (R, GT) are done; they are overwritten with G_{l-1}
+
+  // ---- post-op backward of layer l-1 (BN / act), producing G_{l-1} ----
+#pragma unroll
+  for (int j = 0; j < T::NTW; ++j) {
+    const int n = wave + j * RX_NW;
+    if (n >= ntiles) continue;
+    const int c = n * 16 + lr;
+    const bool colok = c < pv.out;
+    float g[MT * 4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + lg * 4 + r;
+        g[mt * 4 + r] = (row < nvalid && colok) ? acc[j * MT + mt][r] : 0.f;
+      }
+    if (pv.bn == 0) {
+      if (pv.act == 1) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = mt * 16 + lg * 4 + r;
+            const float a = scratch[pv.r_off + row * pv.out_n + c];
+            if (!(a > 0.f)) g[mt * 4 + r] = 0.f;
+          }
+      }
+    } else {
+      const float mean = colok ? stats[pv.stat_off + 2 * c] : 0.f;
+      const float invstd = colok ? stats[pv.stat_off + 2 * c + 1] : 0.f;
+      const float gam = (colok && pv.g_off >= 0) ? P[pv.g_off + c] : 1.f;
+      const float bet = (colok && pv.be_off >= 0) ? P[pv.be_off + c] : 0.f;
+      float xh[MT * 4], s[MT * 4];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + lg * 4 + r;
+          s[mt * 4 + r] = scratch[pv.r_off + row * pv.out_n + c];
+          xh[mt * 4 + r] = (s[mt * 4 + r] - mean) * invstd;
+          if (pv.bn == 2 && pv.act == 1 && !(xh[mt * 4 + r] * gam + bet > 0.f)) g[mt * 4 + r] = 0.f;
+        }
+      float sg = 0.f, sgx = 0.f;
+#pragma unroll
+      for (int q = 0; q < MT * 4; ++q) {
+        sg += g[q];
+        sgx += g[q] * xh[q];
+      }
+      sg = rx_colsum16(sg);
+      sgx = rx_colsum16(sgx);
+      if (colok && lg == 0) {
+        if (pv.g_off >= 0) Gr[pv.g_off + c] = sgx;
+        if (pv.be_off >= 0) Gr[pv.be_off + c] = sg;
+      }
+      const float inv_n = 1.f / (float)nvalid;
+      const float k1 = gam * invstd;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + lg * 4 + r;
+          const int q = mt * 4 + r;
+          float dz = k1 * (g[q] - sg * inv_n - xh[q] * sgx * inv_n);
+          if (pv.bn == 1 && pv.act == 1 && !(s[q] > 0.f)) dz = 0.f;
+          g[q] = (row < nvalid && colok) ? dz : 0.f;
+        }
+    }
+    // bias grad of layer l-1
+    float bs = 0.f;
+#pragma unroll
+    for (int q = 0; q < MT * 4; ++q) bs += g[q];
+    bs = rx_colsum16(bs);
+    if (colok && lg == 0 && pv.b_off >= 0) Gr[pv.b_off + c] = bs;
+    // publish G_{l-1}
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      u16 h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        h[r] = rx_f2bf(g[mt * 4 + r]);
+        R[(mt * 16 + lg * 4 + r) * RS + c] = h[r];
+      }
+      uint2 pk;
+      pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+      pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+      *reinterpret_cast<uint2*>(GT + c * XS + mt * 16 + lg * 4) = pk;
+    }
+  }
+  // zero the K tail [out_n, out_k) of G_{l-1} in R for the next dgrad
+  const int kpad = pv.out_k - pv.out_n;
+  if (kpad > 0) {
+    for (int idx = threadIdx.x; idx < T::BP * kpad; idx += RX_THREADS) {
+      const int row = idx / kpad, cc = pv.out_n + idx % kpad;
+      R[row * RS + cc] = 0;
+    }
+  }
+  __syncthreads();
+}
+
+// load the batch's feature rows (gathered through the epoch permutation) into R and XT_0
+template <int MT>
+__device__ void load_inputs(const MlpDesc& d, char* smem, const u16* __restrict__ feats,
+                            const int* __restrict__ rowidx, int nvalid, bool need_t) {
+  using T = Tile<MT>;
+  const int RS = d.max_k + 8;
+  u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
+  u16* XT = reinterpret_cast<u16*>(smem + d.layer[0].xt_off);
+  const int in_n = d.layer[0].in_n;
+  const int chunks = d.feat_k >> 3;  // 8 bf16 per 16-B chunk
+  for (int idx = threadIdx.x; idx < T::BP * chunks; idx += RX_THREADS) {
+    const int row = idx / chunks, ch = idx % chunks;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < nvalid) v = *reinterpret_cast<const uint4*>(feats + (size_t)rowidx[row] * d.feat_k + ch * 8);
+    *reinterpret_cast<uint4*>(R + row * RS + ch * 8) = v;
+    if (need_t) {
+      const u16* h = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = ch * 8 + e;
+        if (k < in_n) XT[k * T::XS + row] = h[e];
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int MT>
+__global__ __launch_bounds__(RX_THREADS) void mlp_train_step_kernel(
+    MlpDesc d, const float* __restrict__ P, float* __restrict__ Gr, const u16* __restrict__ feats,
+    const float* __restrict__ labels, const int* __restrict__ perm, int row0, int nvalid,
+    float* __restrict__ scratch, double* __restrict__ metrics) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int rowidx[Tile<MT>::BP];
+  for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS)
+    rowidx[i] = i < nvalid ? (perm ? perm[row0 + i] : row0 + i) : 0;
+  __syncthreads();
+  load_inputs<MT>(d, smem, feats, rowidx, nvalid, true);
+  for (int l = 0; l < d.L; ++l)
+    layer_forward<MT, true>(d, l, smem, P, Gr, labels, rowidx, nvalid, scratch, metrics);
+  for (int l = d.L - 1; l >= 0; --l) layer_backward<MT>(d, l, smem, P, Gr, nvalid, scratch);
+}
+
+template <int MT>
+__global__ __launch_bounds__(RX_THREADS) void mlp_eval_kernel(
+    MlpDesc d, const float* __restrict__ P, const u16* __restrict__ feats,
+    const float* __restrict__ labels, int n_rows, int batch, double* __restrict__ metrics,
+    float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int rowidx[Tile<MT>::BP];
+  const int row0 = blockIdx.x * batch;
+  const int nvalid = min(batch, n_rows - row0);
+  for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS) rowidx[i] = i < nvalid ? row0 + i : 0;
+  __syncthreads();
+  load_inputs<MT>(d, smem, feats, rowidx, nvalid, false);
+  for (int l = 0; l < d.L; ++l) {
+    if (l == d.L - 1 && out != nullptr) {
+      // prediction mode is handled by the host (not needed by the estimator path)
+    }
+    layer_forward<MT, false>(d, l, smem, P, nullptr, labels, rowidx, nvalid, nullptr, metrics);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// optimizer: fused Adam / AdamW / SGD(momentum, nesterov) over the flat parameter vector,
+// refreshing the bf16 W / Wt images of every Linear weight in the same pass.
+// ------------------------------------------------------------------------------------------
+#define RX_MAXSEG (3 * RX_MAXL)
+struct OptSeg {
+  int start, len, kind;  // kind 1: linear weight (needs bf16 images)
+  int out, in, in_k, out_k;
+  u16* W;
+  u16* Wt;
+};
+struct OptDesc {
+  int nseg, total;
+  int algo;  // 0 adam, 1 adamw, 2 sgd
+  float b1, b2, eps, wd, momentum, dampening;
+  int nesterov, maximize;
+  OptSeg seg[RX_MAXSEG];
+};
+
+__global__ __launch_bounds__(256) void opt_step_kernel(OptDesc o, float* __restrict__ p,
+                                                       const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       float lr, float bc1, float bc2, float gscale,
+                                                       int first) {
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < o.total; idx += gridDim.x * blockDim.x) {
+    float gr = g[idx] * gscale;
+    if (o.maximize) gr = -gr;
+    float pv = p[idx];
+    if (o.algo == 2) {
+      if (o.wd != 0.f) gr += o.wd * pv;
+      if (o.momentum != 0.f) {
+        float b = first ? gr : o.momentum * m[idx] + (1.f - o.dampening) * gr;
+        m[idx] = b;
+        gr = o.nesterov ? gr + o.momentum * b : b;
+      }
+      pv -= lr * gr;
+    } else {
+      if (o.algo == 1) pv *= (1.f - lr * o.wd);
+      else if (o.wd != 0.f) gr += o.wd * pv;
+      const float mm = o.b1 * m[idx] + (1.f - o.b1) * gr;
+      const float vv = o.b2 * v[idx] + (1.f - o.b2) * gr * gr;
+      m[idx] = mm;
+      v[idx] = vv;
+      const float denom = sqrtf(vv) / sqrtf(bc2) + o.eps;
+      pv -= (lr / bc1) * mm / denom;
+    }
+    p[idx] = pv;
+    for (int s = 0; s < o.nseg; ++s) {
+      const OptSeg& sg = o.seg[s];
+      if (idx >= sg.start && idx < sg.start + sg.len) {
+        if (sg.kind == 1) {
+          const int q = idx - sg.start;
+          const int oo = q / sg.in, ii = q - oo * sg.in;
+          const u16 h = rx_f2bf(pv);
+          sg.W[oo * sg.in_k + ii] = h;
+          sg.Wt[ii * sg.out_k + oo] = h;
+        }
+        break;
+      }
+    }
+  }
+}
+
+template <int MT>
+int set_lds(int bytes) {
+  RX_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_step_kernel<MT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  RX_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_eval_kernel<MT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  return 0;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// C API
+// ------------------------------------------------------------------------------------------
+typedef int (*rx_allreduce_fn)(float* buf, int n, void* ctx, hipStream_t s);
+
+extern "C" {
+
+int rx_mlp_desc_size() { return (int)sizeof(MlpDesc); }
+int rx_opt_desc_size() { return (int)sizeof(OptDesc); }
+
+// One or more training steps over rows [first_row, first_row + nsteps * batch) of the epoch
+// permutation. Per step: fused fwd/bwd kernel -> (optional) gradient all-reduce -> optimizer.
+int rx_mlp_train_steps(const MlpDesc* d, const OptDesc* o, int mt, float* params, float* grads,
+                       float* m, float* v, const u16* feats, const float* labels, const int* perm,
+                       int n_rows, int batch, int first_step, int nsteps, const float* lrs,
+                       const float* bc1s, const float* bc2s, float gscale, int opt_first_step,
+                       float* scratch, double* metrics, hipStream_t stream,
+                       rx_allreduce_fn allreduce, void* ar_ctx) {
+  static int lds_set[9] = {0};
+  if (mt != 2 && mt != 4 && mt != 8) return -1;
+  if (lds_set[mt] < d->lds_bytes) {
+    int rc = mt == 2 ? set_lds<2>(d->lds_bytes) : mt == 4 ? set_lds<4>(d->lds_bytes) : set_lds<8>(d->lds_bytes);
+    if (rc) return rc;
+    lds_set[mt] = d->lds_bytes;
+  }
+  const int opt_blocks = (o->total + 255) / 256 < 1024 ? (o->total + 255) / 256 : 1024;
+  for (int s = 0; s < nsteps; ++s) {
+    const int step = first_step + s;
+    const int row0 = step * batch;
+    const int nvalid = n_rows - row0 < batch ? n_rows - row0 : batch;
+    if (nvalid <= 0) break;
+    if (mt == 2)
+      hipLaunchKernelGGL(mlp_train_step_kernel<2>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+                         params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
+    else if (mt == 4)
+      hipLaunchKernelGGL(mlp_train_step_kernel<4>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+                         params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
+    else
+      hipLaunchKernelGGL(mlp_train_step_kernel<8>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+                         params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
+    if (allreduce) {
+      int rc = allreduce(grads, o->total, ar_ctx, stream);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(opt_step_kernel, dim3(opt_blocks), dim3(256), 0, stream, *o, params, grads, m, v,
+                       lrs[s], bc1s[s], bc2s[s], gscale, (opt_first_step && s == 0) ? 1 : 0);
+  }
+  return (int)hipGetLastError();
+}
+
+// Single pieces of a step for callers that interleave their own collective between the
+// backward and the optimizer (torch.distributed fallback path).
+int rx_mlp_fwdbwd(const MlpDesc* d, int mt, const float* params, float* grads, const u16* feats,
+                  const float* labels, const int* perm, int n_rows, int batch, int step,
+                  float* scratch, double* metrics, hipStream_t stream) {
+  static int lds_set[9] = {0};
+  if (mt != 2 && mt != 4 && mt != 8) return -1;
+  if (lds_set[mt] < d->lds_bytes) {
+    int rc = mt == 2 ? set_lds<2>(d->lds_bytes) : mt == 4 ? set_lds<4>(d->lds_bytes) : set_lds<8>(d->lds_bytes);
+    if (rc) return rc;
+    lds_set[mt] = d->lds_bytes;
+  }
+  const int row0 = step * batch;
+  const int nvalid = n_rows - row0 < batch ? n_rows - row0 : batch;
+  if (nvalid <= 0) return 0;
+  if (mt == 2)
+    hipLaunchKernelGGL(mlp_train_step_kernel<2>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+                       params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
+  else if (mt == 4)
+    hipLaunchKernelGGL(mlp_train_step_kernel<4>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+                       params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
+  else
+    hipLaunchKernelGGL(mlp_train_step_kernel<8>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+                       params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
+  return (int)hipGetLastError();
+}
+
+int rx_opt_step(const OptDesc* o, float* params, const float* grads, float* m, float* v, float lr,
+                float bc1, float bc2, float gscale, int first, hipStream_t stream) {
+  const int opt_blocks = (o->total + 255) / 256 < 1024 ? (o->total + 255) / 256 : 1024;
+  hipLaunchKernelGGL(opt_step_kernel, dim3(opt_blocks), dim3(256), 0, stream, *o, params, grads, m, v,
+                     lr, bc1, bc2, gscale, first);
+  return (int)hipGetLastError();
+}
+
+int rx_mlp_eval(const MlpDesc* d, int mt, const float* params, const u16* feats, const float* labels,
+                int n_rows, int batch, double* metrics, hipStream_t stream) {
+  static int lds_set[9] = {0};
+  if (mt != 2 && mt != 4 && mt != 8) return -1;
+  if (lds_set[mt] < d->lds_bytes) {
+    int rc = mt == 2 ? set_lds<2>(d->lds_bytes) : mt == 4 ? set_lds<4>(d->lds_bytes) : set_lds<8>(d->lds_bytes);
+    if (rc) return rc;
+    lds_set[mt] = d->lds_bytes;
+  }
+  const int nb = (n_rows + batch - 1) / batch;
+  if (nb <= 0) return 0;
+  if (mt == 2)
+    hipLaunchKernelGGL(mlp_eval_kernel<2>, dim3(nb), dim3(RX_THREADS), d->lds_bytes, stream, *d, params,
+                       feats, labels, n_rows, batch, metrics, nullptr);
+  else if (mt == 4)
+    hipLaunchKernelGGL(mlp_eval_kernel<4>, dim3(nb), dim3(RX_THREADS), d->lds_bytes, stream, *d, params,
+                       feats, labels, n_rows, batch, metrics, nullptr);
+  else
+    hipLaunchKernelGGL(mlp_eval_kernel<8>, dim3(nb), dim3(RX_THREADS), d->lds_bytes, stream, *d, params,
+                       feats, labels, n_rows, batch, metrics, nullptr);
+  return (int)hipGetLastError();
+}
+
+// Refresh the bf16 images from the fp32 master weights (initialisation / after load).
+int rx_mlp_refresh_images(const OptDesc* o, const float* params, hipStream_t stream);
+
+}  // extern "C"
+
+namespace {
+__global__ void refresh_kernel(OptDesc o, const float* __restrict__ p) {
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < o.total; idx += gridDim.x * blockDim.x) {
+    for (int s = 0; s < o.nseg; ++s) {
+      const OptSeg& sg = o.seg[s];
+      if (idx >= sg.start && idx < sg.start + sg.len) {
+        if (sg.kind == 1) {
+          const int q = idx - sg.start;
+          const int oo = q / sg.in, ii = q - oo * sg.in;
+          const u16 h = rx_f2bf(p[idx]);
+          sg.W[oo * sg.in_k + ii] = h;
+          sg.Wt[ii * sg.out_k + oo] = h;
+        }
+        break;
+      }
+    }
+  }
+}
+}  // namespace
+
+extern "C" int rx_mlp_refresh_images(const OptDesc* o, const float* params, hipStream_t stream) {
+  const int blocks = (o->total + 255) / 256 < 1024 ? (o->total + 255) / 256 : 1024;
+  hipLaunchKernelGGL(refresh_kernel, dim3(blocks), dim3(256), 0, stream, *o, params);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,43 @@
+// Shared device helpers for the gfx950 kernels (wave64, bf16 MFMA, bf16 packing).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define RX_WAVE 64
+
+// round-to-nearest-even fp32 -> bf16 bits
+__device__ __forceinline__ u16 rx_f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u16)0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+
+__device__ __forceinline__ float rx_bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// sum over the 4 lanes that share (lane & 15): lanes l, l^16, l^32, l^48
+__device__ __forceinline__ float rx_colsum16(float v) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+__device__ __forceinline__ float rx_wavesum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ f32x4 rx_mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+#define RX_CHECK(x)                                                     \
+  do {                                                                  \
+    hipError_t e_ = (x);                                                \
+    if (e_ != hipSuccess) return (int)e_;                               \
+  } while (0)

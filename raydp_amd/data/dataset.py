@@ -1,0 +1,361 @@
+"""Distributed Arrow ``Dataset`` (the Ray Data surface RayDP relies on).
+
+Blocks are Arrow tables held in the object store (``ObjectRef``) or inline. Reference call
+sites: ``ray.data.from_arrow_refs`` (``python/raydp/spark/dataset.py:222``),
+``Dataset.random_shuffle`` (``torch/estimator.py:335-338``), ``session.get_dataset_shard(...)
+.to_torch(...)`` (``torch/estimator.py:226-241``), ``iter_internal_ref_bundles`` /
+``to_spark`` (``tests/test_spark_cluster.py:169-216``).
+
+MI355X path: ``to_device_tensors`` packs the requested columns of every block of a shard into
+ONE pinned host staging buffer and moves it to HBM with one DMA, then the HIP ``arrow_ingest``
+kernel decodes/casts/null-fills in HBM (``raydp_amd/ops/ingest.py``); epochs then run from
+device-resident tensors with a device-side shuffle permutation.
+"""
+import builtins
+import math
+from typing import Any, Callable, Dict, Iterator, List, Optional, Union
+
+import numpy as np
+import pyarrow as pa
+
+from raydp_amd.runtime.objects import ObjectRef, get as _get, put as _put
+
+
+class BlockMetadata:
+    def __init__(self, num_rows, size_bytes, schema):
+        self.num_rows, self.size_bytes, self.schema = num_rows, size_bytes, schema
+
+
+class RefBundle:
+    def __init__(self, blocks):
+        self.blocks = blocks
+
+
+def _resolve(b) -> pa.Table:
+    if isinstance(b, ObjectRef):
+        b = _get(b)
+    if isinstance(b, (bytes, bytearray, memoryview)):
+        b = pa.ipc.open_stream(pa.py_buffer(b)).read_all()
+    if isinstance(b, pa.RecordBatch):
+        b = pa.Table.from_batches([b])
+    return b
+
+
+class Dataset:
+    def __init__(self, blocks: List[Union[ObjectRef, pa.Table]], schema: Optional[pa.Schema] = None):
+        self._blocks = list(blocks)
+        self._schema = schema
+        self._tables: Optional[List[pa.Table]] = None
+
+    # ---------------------------------------------------------------- internals ----------
+    def _get_tables(self) -> List[pa.Table]:
+        if self._tables is None:
+            self._tables = [_resolve(b) for b in self._blocks]
+        return self._tables
+
+    def _from_tables(self, tables):
+        return Dataset(tables, self.schema())
+
+    # ---------------------------------------------------------------- metadata -----------
+    def schema(self) -> pa.Schema:
+        if self._schema is None:
+            ts = self._get_tables()
+            self._schema = ts[0].schema if ts else pa.schema([])
+        return self._schema
+
+    def columns(self) -> List[str]:
+        return list(self.schema().names)
+
+    def count(self) -> int:
+        return int(sum(t.num_rows for t in self._get_tables()))
+
+    def num_blocks(self) -> int:
+        return len(self._blocks)
+
+    def size_bytes(self) -> int:
+        return int(sum(t.nbytes for t in self._get_tables()))
+
+    def get_internal_block_refs(self) -> List[ObjectRef]:
+        refs = []
+        for i, b in enumerate(self._blocks):
+            if not isinstance(b, ObjectRef):
+                b = _put(b)
+                self._blocks[i] = b
+            refs.append(b)
+        return refs
+
+    def iter_internal_ref_bundles(self):
+        for r, t in zip(self.get_internal_block_refs(), self._get_tables()):
+            yield RefBundle([(r, BlockMetadata(t.num_rows, t.nbytes, t.schema))])
+
+    def materialize(self):
+        self._get_tables()
+        return self
+
+    def stats(self) -> str:
+        return f"Dataset(num_blocks={self.num_blocks()}, num_rows={self.count()})"
+
+    def __repr__(self):
+        return f"Dataset(num_blocks={self.num_blocks()}, schema={self.schema()})"
+
+    # ---------------------------------------------------------------- consumption --------
+    def to_arrow(self) -> pa.Table:
+        ts = self._get_tables()
+        if not ts:
+            return self.schema().empty_table()
+        return pa.concat_tables(ts, promote_options="permissive")
+
+    def to_pandas(self, limit=None):
+        t = self.to_arrow()
+        return (t if limit is None else t.slice(0, limit)).to_pandas()
+
+    def to_arrow_refs(self):
+        return self.get_internal_block_refs()
+
+    def take(self, limit: int = 20) -> List[Dict[str, Any]]:
+        out = []
+        for t in self._get_tables():
+            if len(out) >= limit:
+                break
+            out.extend(t.slice(0, limit - len(out)).to_pylist())
+        return out
+
+    def take_all(self):
+        return self.to_arrow().to_pylist()
+
+    def show(self, limit=20):
+        for r in self.take(limit):
+            print(r)
+
+    def iter_rows(self):
+        for t in self._get_tables():
+            yield from t.to_pylist()
+
+    def iter_batches(self, batch_size: int = 256, batch_format: str = "numpy",
+                     drop_last: bool = False) -> Iterator:
+        carry = None
+        for t in self._get_tables():
+            if carry is not None and carry.num_rows:
+                t = pa.concat_tables([carry, t])
+            off = 0
+            while t.num_rows - off >= batch_size:
+                yield _format_batch(t.slice(off, batch_size), batch_format)
+                off += batch_size
+            carry = t.slice(off)
+        if carry is not None and carry.num_rows and not drop_last:
+            yield _format_batch(carry, batch_format)
+
+    def iter_torch_batches(self, batch_size=256, dtypes=None, device="cpu", drop_last=False):
+        import torch
+        for b in self.iter_batches(batch_size, "numpy", drop_last):
+            yield {k: torch.as_tensor(v, dtype=(dtypes.get(k) if isinstance(dtypes, dict) else dtypes),
+                                      device=device) for k, v in b.items()}
+
+    def to_torch(self, *, label_column=None, feature_columns=None, label_column_dtype=None,
+                 feature_column_dtypes=None, batch_size=1, prefetch_blocks=0, drop_last=False,
+                 unsqueeze_label_tensor=True, unsqueeze_feature_tensors=True, device="cpu"):
+        """Legacy Ray-Data ``to_torch`` contract used by the reference estimator.
+
+        Returns an iterable of ``(features, label)``. ``feature_columns`` as a list of names
+        with one dtype → one ``[B, F]`` tensor; a list of lists → a list of tensors; a dict
+        → a dict of tensors.
+        """
+        from raydp_amd.data.torch_iter import TorchBatchIterable
+        return TorchBatchIterable(self, label_column, feature_columns, label_column_dtype,
+                                  feature_column_dtypes, batch_size, drop_last,
+                                  unsqueeze_label_tensor, device)
+
+    # ---------------------------------------------------------------- transforms ---------
+    def random_shuffle(self, seed: Optional[int] = None, num_blocks: Optional[int] = None):
+        t = self.to_arrow()
+        rng = np.random.default_rng(seed)
+        perm = rng.permutation(t.num_rows)
+        t = t.take(pa.array(perm))
+        n = num_blocks or max(1, self.num_blocks())
+        return Dataset(_split(t, n), t.schema)
+
+    def randomize_block_order(self, seed=None):
+        rng = np.random.default_rng(seed)
+        order = rng.permutation(self.num_blocks())
+        return Dataset([self._blocks[i] for i in order], self._schema)
+
+    def repartition(self, num_blocks: int, shuffle: bool = False):
+        t = self.to_arrow()
+        return Dataset(_split(t, num_blocks), t.schema)
+
+    def split(self, n: int, equal: bool = False, locality_hints=None) -> List["Dataset"]:
+        tables = self._get_tables()
+        if equal:
+            t = self.to_arrow()
+            per = t.num_rows // n
+            return [Dataset([t.slice(i * per, per)], t.schema) for i in builtins.range(n)]
+        if len(tables) >= n:
+            # keep blocks whole, balance rows greedily
+            sizes = [(t.num_rows, i) for i, t in enumerate(tables)]
+            sizes.sort(reverse=True)
+            buckets = [[] for _ in builtins.range(n)]
+            loads = [0] * n
+            for rows, i in sizes:
+                j = int(np.argmin(loads))
+                buckets[j].append(i)
+                loads[j] += rows
+            return [Dataset([self._blocks[i] for i in sorted(b)], self._schema) for b in buckets]
+        t = self.to_arrow()
+        return [Dataset([p], t.schema) for p in _split(t, n)]
+
+    def split_at_indices(self, indices: List[int]) -> List["Dataset"]:
+        t = self.to_arrow()
+        bounds = [0] + list(indices) + [t.num_rows]
+        return [Dataset([t.slice(a, b - a)], t.schema) for a, b in zip(bounds[:-1], bounds[1:])]
+
+    def train_test_split(self, test_size=0.25, shuffle=False, seed=None):
+        ds = self.random_shuffle(seed) if shuffle else self
+        n = ds.count()
+        k = int(n * (1 - test_size)) if isinstance(test_size, float) else n - int(test_size)
+        return ds.split_at_indices([k])
+
+    def limit(self, n: int):
+        return Dataset([self.to_arrow().slice(0, n)], self.schema())
+
+    def union(self, *others):
+        blocks = list(self._blocks)
+        for o in others:
+            blocks += o._blocks
+        return Dataset(blocks, self._schema)
+
+    def map_batches(self, fn: Callable, batch_size=None, batch_format="pandas", **kw):
+        out = []
+        for t in self._get_tables():
+            res = fn(_format_batch(t, batch_format))
+            out.append(_to_table(res))
+        return Dataset(out)
+
+    def map(self, fn: Callable):
+        rows = [fn(r) for r in self.iter_rows()]
+        return from_items(rows)
+
+    def filter(self, fn: Callable):
+        out = []
+        for t in self._get_tables():
+            mask = [bool(fn(r)) for r in t.to_pylist()]
+            out.append(t.filter(pa.array(mask, pa.bool_())))
+        return Dataset(out, self._schema)
+
+    def add_column(self, name, fn):
+        return Dataset([t.append_column(name, pa.array(fn(t.to_pandas()))) for t in self._get_tables()])
+
+    def drop_columns(self, cols):
+        return Dataset([t.drop(cols) for t in self._get_tables()])
+
+    def select_columns(self, cols):
+        return Dataset([t.select(cols) for t in self._get_tables()])
+
+    def write_parquet(self, path: str):
+        import os
+        import pyarrow.parquet as pq
+        path = path[len("file://"):] if path.startswith("file://") else path
+        os.makedirs(path, exist_ok=True)
+        for i, t in enumerate(self._get_tables()):
+            pq.write_table(t, os.path.join(path, f"part-{i:05d}.parquet"))
+
+    def to_spark(self, spark):
+        from raydp_amd.spark.dataset import ray_dataset_to_spark_dataframe
+        return ray_dataset_to_spark_dataframe(spark, self.schema(), self.get_internal_block_refs())
+
+    # ---------------------------------------------------------------- device path -------
+    def to_device_tensors(self, feature_columns, label_column, feature_dtype, label_dtype,
+                          device):
+        """Whole shard → HBM in one DMA + HIP decode (see ``raydp_amd.ops.ingest``)."""
+        from raydp_amd.ops.ingest import ingest_tables
+        return ingest_tables(self._get_tables(), feature_columns, label_column, feature_dtype,
+                             label_dtype, device)
+
+
+def _format_batch(t: pa.Table, fmt: str):
+    if fmt in ("pandas",):
+        return t.to_pandas()
+    if fmt in ("pyarrow", "arrow"):
+        return t
+    return {n: c.to_numpy(zero_copy_only=False) for n, c in zip(t.column_names, t.columns)}
+
+
+def _to_table(res) -> pa.Table:
+    import pandas as pd
+    if isinstance(res, pa.Table):
+        return res
+    if isinstance(res, pd.DataFrame):
+        return pa.Table.from_pandas(res, preserve_index=False)
+    if isinstance(res, dict):
+        return pa.table({k: np.asarray(v) for k, v in res.items()})
+    raise TypeError(type(res))
+
+
+def _split(t: pa.Table, n: int) -> List[pa.Table]:
+    n = max(1, int(n))
+    b = np.linspace(0, t.num_rows, n + 1).astype(np.int64)
+    return [t.slice(int(b[i]), int(b[i + 1] - b[i])) for i in builtins.range(n)]
+
+
+# ------------------------------------------------------------------------------ creation --
+def from_arrow(tables) -> Dataset:
+    if isinstance(tables, (pa.Table, pa.RecordBatch)):
+        tables = [tables]
+    ts = [_resolve(t) for t in tables]
+    return Dataset(ts, ts[0].schema if ts else None)
+
+
+def from_arrow_refs(refs: List[ObjectRef]) -> Dataset:
+    return Dataset(list(refs))
+
+
+def from_pandas(dfs) -> Dataset:
+    import pandas as pd
+    if isinstance(dfs, pd.DataFrame):
+        dfs = [dfs]
+    return from_arrow([pa.Table.from_pandas(d, preserve_index=False) for d in dfs])
+
+
+def from_pandas_refs(refs):
+    return from_pandas([_get(r) for r in refs])
+
+
+def from_items(items: List[Any], parallelism: int = 1) -> Dataset:
+    if items and not isinstance(items[0], dict):
+        items = [{"item": x} for x in items]
+    t = pa.Table.from_pylist(items)
+    return Dataset(_split(t, min(max(1, parallelism), max(1, t.num_rows))), t.schema)
+
+
+def from_numpy(arr) -> Dataset:
+    arr = np.asarray(arr)
+    if arr.ndim == 1:
+        return from_arrow(pa.table({"data": arr}))
+    return from_arrow(pa.table({"data": pa.FixedSizeListArray.from_arrays(arr.ravel(), arr.shape[1])}))
+
+
+def range(n: int, parallelism: int = 1) -> Dataset:  # noqa: A001
+    t = pa.table({"id": np.arange(n, dtype=np.int64)})
+    return Dataset(_split(t, parallelism), t.schema)
+
+
+def read_parquet(paths, file_extensions=None, **kw) -> Dataset:
+    from raydp_amd.spark.sources import ParquetSource
+    src = ParquetSource(paths)
+    files = src.files
+    if file_extensions:
+        files = [f for f in files if any(f.endswith("." + e) or f.endswith(e) for e in file_extensions)]
+    import pyarrow.parquet as pq
+    return Dataset([pq.read_table(f) for f in files])
+
+
+def read_csv(paths, **kw) -> Dataset:
+    from raydp_amd.spark.sources import CsvSource
+    import builtins
+    src = CsvSource(paths, header=True, infer_schema=True)
+    return Dataset([src.load(i) for i in builtins.range(src.num_partitions())])
+
+
+def from_spark(df, parallelism: Optional[int] = None) -> Dataset:
+    """``ray.data.from_spark`` equivalent (recoverable conversion)."""
+    from raydp_amd.spark.dataset import spark_dataframe_to_ray_dataset
+    return spark_dataframe_to_ray_dataset(df, parallelism)

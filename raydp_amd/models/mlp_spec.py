@@ -1,0 +1,127 @@
+"""Recognise fusable MLPs in user ``nn.Module``s (torch.fx pattern match).
+
+A model qualifies for the fused HIP trainer when its traced graph is a single chain of
+``Linear`` layers, each hidden one followed by an optional activation (ReLU / identity) and an
+optional ``BatchNorm1d`` in either order, ending in a bare ``Linear``. That covers the
+reference's ``NYC_Model`` (``examples/pytorch_nyctaxi.py:69-92``: Linear→ReLU→BN ×4 →
+Linear), the ``LinearModel`` of ``tests/test_torch.py`` and DLRM-style MLP towers.
+Anything else (dropout, residuals, embeddings, custom ops) returns ``None`` and the generic
+device-resident PyTorch loop is used instead.
+"""
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass
+class LayerSpec:
+    linear: nn.Linear
+    act: int = 0        # 0 identity, 1 relu
+    bn: int = 0         # 0 none, 1 act->bn, 2 bn->act
+    bn_module: Optional[nn.BatchNorm1d] = None
+
+
+@dataclass
+class MlpSpec:
+    layers: List[LayerSpec] = field(default_factory=list)
+
+    @property
+    def in_features(self):
+        return self.layers[0].linear.in_features
+
+    @property
+    def out_features(self):
+        return self.layers[-1].linear.out_features
+
+
+_RELU_FUNCS = {F.relu, torch.relu, torch.nn.functional.relu}
+
+
+def extract_mlp_spec(model: nn.Module) -> Optional[MlpSpec]:
+    try:
+        import torch.fx as fx
+        gm = fx.symbolic_trace(model)
+    except Exception:  # noqa: BLE001 - untraceable models are simply not fused
+        return None
+    mods = dict(gm.named_modules())
+    spec = MlpSpec()
+    cur = None          # current LayerSpec being extended
+    prev_node = None
+    placeholder = None
+    saw_act_after_bn = False
+    for node in gm.graph.nodes:
+        if node.op == "placeholder":
+            if placeholder is not None:
+                return None  # multi-input models are not MLP chains
+            placeholder = node
+            prev_node = node
+            continue
+        if node.op == "output":
+            if node.args[0] is not prev_node:
+                return None
+            break
+        # every op must consume the previous op's output (a single chain)
+        if not node.args or node.args[0] is not prev_node:
+            return None
+        if node.op == "call_module":
+            m = mods[node.target]
+            if isinstance(m, nn.Linear):
+                cur = LayerSpec(linear=m)
+                spec.layers.append(cur)
+            elif isinstance(m, nn.ReLU):
+                if cur is None or cur.act:
+                    return None
+                cur.act = 1
+                if cur.bn:
+                    cur.bn = 2
+            elif isinstance(m, nn.BatchNorm1d):
+                if cur is None or cur.bn or not m.track_running_stats or m.momentum is None:
+                    return None
+                cur.bn_module = m
+                cur.bn = 1 if cur.act else 2
+                if not cur.act:
+                    cur.bn = 2  # provisional: BN first; becomes act-after if a ReLU follows
+            elif isinstance(m, (nn.Identity,)):
+                pass
+            elif isinstance(m, nn.Dropout) and m.p == 0.0:
+                pass
+            else:
+                return None
+        elif node.op == "call_function":
+            if node.target in _RELU_FUNCS and len(node.args) == 1 and not node.kwargs.get("inplace", False):
+                if cur is None or cur.act:
+                    return None
+                cur.act = 1
+            else:
+                return None
+        elif node.op == "call_method":
+            if node.target == "relu" and len(node.args) == 1:
+                if cur is None or cur.act:
+                    return None
+                cur.act = 1
+            else:
+                return None
+        else:
+            return None
+        prev_node = node
+    if not spec.layers:
+        return None
+    # fix BN/act order: bn==2 means BN came before the activation (or no activation)
+    last = spec.layers[-1]
+    if last.act or last.bn:
+        return None
+    for ly in spec.layers:
+        if ly.bn and not ly.act:
+            ly.bn = 2
+    for a, b in zip(spec.layers[:-1], spec.layers[1:]):
+        if a.linear.out_features != b.linear.in_features:
+            return None
+    for ly in spec.layers:
+        if ly.linear.in_features > 512 or ly.linear.out_features > 512:
+            return None
+    if len(spec.layers) > 8:
+        return None
+    return spec

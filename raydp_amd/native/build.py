@@ -1,0 +1,97 @@
+"""Build the in-tree native libraries.
+
+* ``libexec_kernels.so``  — CPU shuffle/hash kernels (g++).
+* ``libraydp_runtime.so`` — shared-memory object store + actor supervisor + framed IPC (g++).
+* ``libhipkernels.so``    — CDNA4 HIP kernels for gfx950 (hipcc ``--offload-arch=gfx950``).
+
+Usage: ``python -m raydp_amd.native.build [name ...]``.
+"""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
+CSRC = os.path.join(ROOT, "csrc")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("RAYDP_GPU_ARCH", "gfx950")
+
+
+def _hip_sources():
+    d = os.path.join(CSRC, "hip")
+    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".hip"))
+
+
+def _runtime_sources():
+    d = os.path.join(CSRC, "runtime")
+    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".cc"))
+
+
+LIBS = {
+    "exec_kernels": dict(kind="cpu", sources=lambda: [os.path.join(CSRC, "exec", "exec_kernels.cc")]),
+    "raydp_runtime": dict(kind="cpu", sources=_runtime_sources, libs=["-lpthread", "-lrt", "-ldl"]),
+    "hipkernels": dict(kind="hip", sources=_hip_sources),
+}
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def _newer(out, srcs):
+    if not os.path.exists(out):
+        return False
+    t = os.path.getmtime(out)
+    deps = list(srcs)
+    for d in ("common", "hip", "runtime", "exec", "comm"):
+        p = os.path.join(CSRC, d)
+        if os.path.isdir(p):
+            deps += [os.path.join(p, f) for f in os.listdir(p) if f.endswith((".h", ".hpp", ".cuh"))]
+    return all(os.path.getmtime(s) <= t for s in deps)
+
+
+def build_one(name: str, force: bool = False) -> str:
+    spec = LIBS[name]
+    srcs = spec["sources"]()
+    out = os.path.join(HERE, f"lib{name}.so")
+    if not force and _newer(out, srcs):
+        return out
+    tmp = out + f".tmp{os.getpid()}"
+    inc = ["-I", os.path.join(CSRC, "common"), "-I", CSRC]
+    if spec["kind"] == "cpu":
+        cxx = shutil.which("g++") or "c++"
+        cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-function"] + \
+            inc + srcs + ["-o", tmp] + spec.get("libs", [])
+        _run(cmd)
+    else:
+        hipcc = os.path.join(ROCM, "bin", "hipcc")
+        objs = []
+        with tempfile.TemporaryDirectory() as td:
+            for s in srcs:
+                o = os.path.join(td, os.path.basename(s) + ".o")
+                _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+                      "-munsafe-fp-atomics", "-c", s, "-o", o] + inc)
+                objs.append(o)
+            _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", tmp])
+    os.replace(tmp, out)
+    return out
+
+
+def build_all(names=None, force=False):
+    for n in names or LIBS:
+        if LIBS[n]["kind"] == "hip" and not os.path.exists(os.path.join(ROCM, "bin", "hipcc")):
+            raise RuntimeError("hipcc not found; cannot build the gfx950 kernels")
+        if not LIBS[n]["sources"]():
+            continue
+        p = build_one(n, force=force)
+        print(f"built {p}")
+
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[1:] if not a.startswith("-")]
+    build_all(args or None, force="--force" in sys.argv)

@@ -1,0 +1,118 @@
+"""ctypes front end of ``libhipkernels.so`` (gfx950 kernels in ``csrc/hip``).
+
+The structs below mirror the C structs byte for byte (checked against the ``rx_*_size``
+exports at load time). GPU ops never fall back to eager PyTorch silently: if the library is
+missing or was built for another architecture the call raises.
+"""
+import ctypes
+
+from raydp_amd.native import loader
+
+MAXL = 8
+MAXSEG = 3 * MAXL
+MAXCOLS = 64
+
+
+class MlpLayer(ctypes.Structure):
+    _fields_ = [
+        ("in_", ctypes.c_int), ("out", ctypes.c_int),
+        ("in_k", ctypes.c_int), ("out_k", ctypes.c_int),
+        ("in_n", ctypes.c_int), ("out_n", ctypes.c_int),
+        ("W", ctypes.c_void_p), ("Wt", ctypes.c_void_p),
+        ("w_off", ctypes.c_int), ("b_off", ctypes.c_int),
+        ("act", ctypes.c_int), ("bn", ctypes.c_int),
+        ("g_off", ctypes.c_int), ("be_off", ctypes.c_int),
+        ("run_mean", ctypes.c_void_p), ("run_var", ctypes.c_void_p),
+        ("eps", ctypes.c_float), ("momentum", ctypes.c_float),
+        ("xt_off", ctypes.c_int), ("stat_off", ctypes.c_int), ("r_off", ctypes.c_int),
+    ]
+
+
+class MlpDesc(ctypes.Structure):
+    _fields_ = [
+        ("L", ctypes.c_int),
+        ("r_lds_off", ctypes.c_int), ("gt_lds_off", ctypes.c_int),
+        ("stats_lds_off", ctypes.c_int), ("lds_bytes", ctypes.c_int),
+        ("max_k", ctypes.c_int), ("max_n", ctypes.c_int),
+        ("loss", ctypes.c_int), ("beta", ctypes.c_float),
+        ("out_dim", ctypes.c_int), ("feat_k", ctypes.c_int),
+        ("layer", MlpLayer * MAXL),
+    ]
+
+
+class OptSeg(ctypes.Structure):
+    _fields_ = [
+        ("start", ctypes.c_int), ("len", ctypes.c_int), ("kind", ctypes.c_int),
+        ("out", ctypes.c_int), ("in_", ctypes.c_int), ("in_k", ctypes.c_int), ("out_k", ctypes.c_int),
+        ("W", ctypes.c_void_p), ("Wt", ctypes.c_void_p),
+    ]
+
+
+class OptDesc(ctypes.Structure):
+    _fields_ = [
+        ("nseg", ctypes.c_int), ("total", ctypes.c_int), ("algo", ctypes.c_int),
+        ("b1", ctypes.c_float), ("b2", ctypes.c_float), ("eps", ctypes.c_float),
+        ("wd", ctypes.c_float), ("momentum", ctypes.c_float), ("dampening", ctypes.c_float),
+        ("nesterov", ctypes.c_int), ("maximize", ctypes.c_int),
+        ("seg", OptSeg * MAXSEG),
+    ]
+
+
+class IngestCol(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_int), ("pad_", ctypes.c_int), ("offset", ctypes.c_longlong),
+        ("values", ctypes.c_void_p), ("valid", ctypes.c_void_p),
+        ("fill", ctypes.c_float), ("pad2_", ctypes.c_int),
+    ]
+
+
+class IngestArgs(ctypes.Structure):
+    _fields_ = [
+        ("ncols", ctypes.c_int), ("out_stride", ctypes.c_int), ("out_bf16", ctypes.c_int),
+        ("pad_", ctypes.c_int), ("nrows", ctypes.c_longlong), ("out_row0", ctypes.c_longlong),
+        ("col", IngestCol * MAXCOLS),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    """Load the HIP kernel library (requires a ROCm PyTorch already initialised)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401 - torch's HIP runtime must be loaded first (shared SONAME)
+    L = loader.load("hipkernels", build_if_missing=True)
+    vp, i, f, ll = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_longlong
+    L.rx_mlp_desc_size.restype = i
+    L.rx_opt_desc_size.restype = i
+    L.rx_ingest_args_size.restype = i
+    L.rx_mlp_train_steps.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, vp, vp, vp,
+                                     f, i, vp, vp, vp, vp, vp]
+    L.rx_mlp_fwdbwd.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, vp, vp, vp]
+    L.rx_opt_step.argtypes = [vp, vp, vp, vp, vp, f, f, f, f, i, vp]
+    L.rx_mlp_eval.argtypes = [vp, i, vp, vp, vp, i, i, vp, vp]
+    L.rx_mlp_refresh_images.argtypes = [vp, vp, vp]
+    L.rx_arrow_ingest.argtypes = [vp, vp, vp]
+    L.rx_gather_rows.argtypes = [vp, vp, vp, ll, i, vp]
+    for fn in ("rx_mlp_train_steps", "rx_mlp_fwdbwd", "rx_opt_step", "rx_mlp_eval",
+               "rx_mlp_refresh_images", "rx_arrow_ingest", "rx_gather_rows"):
+        getattr(L, fn).restype = i
+    for name, cls in (("rx_mlp_desc_size", MlpDesc), ("rx_opt_desc_size", OptDesc),
+                      ("rx_ingest_args_size", IngestArgs)):
+        got = getattr(L, name)()
+        if got != ctypes.sizeof(cls):
+            raise RuntimeError(f"ABI mismatch for {cls.__name__}: C {got} vs ctypes {ctypes.sizeof(cls)}")
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with HIP error code {rc}")
+
+
+def stream_ptr(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

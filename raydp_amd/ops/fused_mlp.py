@@ -1,0 +1,302 @@
+"""Host side of the fused MLP trainer (``csrc/hip/fused_mlp.hip``).
+
+``FusedMLPTrainer`` owns the device state of one MLP replica: the flat fp32 master
+parameters, gradients and optimizer moments, the bf16 ``W``/``Wt`` weight images the kernel
+reads, the BatchNorm running buffers, the LDS layout and the per-step scratch. An epoch is a
+single native call that enqueues ``fused fwd/bwd kernel → [all-reduce] → optimizer kernel``
+per batch with no host synchronisation; metrics accumulate on the device and are read back
+once per epoch (the reference syncs on ``loss.item()`` every step,
+``python/raydp/torch/estimator.py:280``).
+"""
+import ctypes
+import math
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from raydp_amd.models.mlp_spec import MlpSpec
+from raydp_amd.ops import _hip
+
+_LOSSES = {nn.MSELoss: 0, nn.SmoothL1Loss: 1, nn.L1Loss: 2}
+
+
+def _ru(x, m):
+    return (x + m - 1) // m * m
+
+
+def loss_code(loss) -> Optional[tuple]:
+    """(code, beta) for a supported mean-reduced regression loss, else None."""
+    if isinstance(loss, type) and issubclass(loss, nn.Module):
+        try:
+            loss = loss()
+        except TypeError:
+            return None
+    for cls, code in _LOSSES.items():
+        if type(loss) is cls and getattr(loss, "reduction", "mean") == "mean":
+            return code, float(getattr(loss, "beta", 1.0))
+    return None
+
+
+def optimizer_config(opt) -> Optional[dict]:
+    if opt is None or len(opt.param_groups) != 1:
+        return None
+    g = opt.param_groups[0]
+    if isinstance(opt, torch.optim.AdamW):
+        if g.get("amsgrad"):
+            return None
+        return dict(algo=1, lr=g["lr"], b1=g["betas"][0], b2=g["betas"][1], eps=g["eps"],
+                    wd=g["weight_decay"], maximize=g.get("maximize", False))
+    if isinstance(opt, torch.optim.Adam):
+        if g.get("amsgrad") or g.get("decoupled_weight_decay", False):
+            return None
+        return dict(algo=0, lr=g["lr"], b1=g["betas"][0], b2=g["betas"][1], eps=g["eps"],
+                    wd=g["weight_decay"], maximize=g.get("maximize", False))
+    if isinstance(opt, torch.optim.SGD):
+        return dict(algo=2, lr=g["lr"], momentum=g["momentum"], dampening=g["dampening"],
+                    wd=g["weight_decay"], nesterov=g["nesterov"], maximize=g.get("maximize", False))
+    return None
+
+
+def pick_mt(batch: int) -> Optional[int]:
+    for mt in (2, 4, 8):
+        if batch <= mt * 16:
+            return mt
+    return None
+
+
+class FusedMLPTrainer:
+    def __init__(self, spec: MlpSpec, opt_cfg: dict, loss: tuple, batch_size: int,
+                 device: torch.device, lr_schedule: Optional[Callable[[int], float]] = None):
+        self.spec, self.cfg, self.device = spec, opt_cfg, torch.device(device)
+        self.batch = int(batch_size)
+        self.mt = pick_mt(self.batch)
+        if self.mt is None:
+            raise ValueError("batch too large for the fused trainer")
+        self.bp = self.mt * 16
+        self.loss_code, self.beta = loss
+        self.lr_schedule = lr_schedule
+        self.step_count = 0
+        self.lib = _hip.lib()
+        self._build()
+
+    # ----------------------------------------------------------------------- layout -------
+    def _build(self):
+        spec, dev, bp, mt = self.spec, self.device, self.bp, self.mt
+        L = len(spec.layers)
+        ntw = 16 // mt
+        flat: List[torch.Tensor] = []
+        off = 0
+        self.layout = []
+        d = _hip.MlpDesc()
+        o = _hip.OptDesc()
+        d.L = L
+        max_k = max_n = 0
+        dims = []
+        for ly in spec.layers:
+            i, oo = ly.linear.in_features, ly.linear.out_features
+            dims.append((i, oo, _ru(i, 32), _ru(oo, 32), _ru(i, 16), _ru(oo, 16)))
+            max_k = max(max_k, _ru(i, 32), _ru(oo, 32))
+            max_n = max(max_n, _ru(oo, 16))
+            if _ru(oo, 16) // 16 > ntw * 8 or _ru(i, 16) // 16 > ntw * 8:
+                raise ValueError("layer too wide for this batch size in the fused trainer")
+        self.W_img, self.Wt_img = [], []
+        self.run_bufs = []
+        xs = bp + 8
+        lds = 0
+
+        def alloc(nbytes):
+            nonlocal lds
+            start = lds
+            lds = _ru(lds + nbytes, 16)
+            return start
+
+        d.r_lds_off = alloc(bp * (max_k + 8) * 2)
+        d.gt_lds_off = alloc(max_n * xs * 2)
+        stat_total = sum(2 * dm[5] for dm in dims)
+        d.stats_lds_off = alloc(stat_total * 4)
+        scratch_off = 0
+        stat_off = 0
+        nseg = 0
+        for li, (ly, dm) in enumerate(zip(spec.layers, dims)):
+            i, oo, in_k, out_k, in_n, out_n = dm
+            lin = ly.linear
+            x = d.layer[li]
+            x.in_, x.out, x.in_k, x.out_k, x.in_n, x.out_n = i, oo, in_k, out_k, in_n, out_n
+            W = torch.zeros(out_n, in_k, dtype=torch.bfloat16, device=dev)
+            Wt = torch.zeros(in_n, out_k, dtype=torch.bfloat16, device=dev)
+            self.W_img.append(W)
+            self.Wt_img.append(Wt)
+            x.W, x.Wt = W.data_ptr(), Wt.data_ptr()
+            x.w_off = off
+            flat.append(lin.weight.detach().reshape(-1).float())
+            seg = o.seg[nseg]
+            seg.start, seg.len, seg.kind = off, oo * i, 1
+            seg.out, seg.in_, seg.in_k, seg.out_k = oo, i, in_k, out_k
+            seg.W, seg.Wt = W.data_ptr(), Wt.data_ptr()
+            nseg += 1
+            self.layout.append(("weight", lin, off, oo * i))
+            off += oo * i
+            if lin.bias is not None:
+                x.b_off = off
+                flat.append(lin.bias.detach().reshape(-1).float())
+                self.layout.append(("bias", lin, off, oo))
+                off += oo
+            else:
+                x.b_off = -1
+            x.act, x.bn = ly.act, ly.bn
+            x.g_off = x.be_off = -1
+            if ly.bn:
+                bn = ly.bn_module
+                if bn.affine:
+                    x.g_off = off
+                    flat.append(bn.weight.detach().reshape(-1).float())
+                    self.layout.append(("gamma", bn, off, oo))
+                    off += oo
+                    x.be_off = off
+                    flat.append(bn.bias.detach().reshape(-1).float())
+                    self.layout.append(("beta", bn, off, oo))
+                    off += oo
+                rm = bn.running_mean.detach().to(dev, torch.float32).clone()
+                rv = bn.running_var.detach().to(dev, torch.float32).clone()
+                self.run_bufs.append((bn, rm, rv))
+                x.run_mean, x.run_var = rm.data_ptr(), rv.data_ptr()
+                x.eps, x.momentum = float(bn.eps), float(bn.momentum)
+            x.xt_off = alloc(in_n * xs * 2)
+            x.stat_off = stat_off
+            stat_off += 2 * out_n
+            x.r_off = scratch_off
+            scratch_off += bp * out_n
+        d.lds_bytes = lds
+        d.max_k, d.max_n = max_k, max_n
+        d.loss, d.beta = self.loss_code, self.beta
+        d.out_dim = spec.out_features
+        d.feat_k = dims[0][2]
+        if lds > 160 * 1024:
+            raise ValueError(f"fused MLP needs {lds} B of LDS (> 160 KiB)")
+        self.desc = d
+        self.feat_k = d.feat_k
+        total = off
+        self.params = torch.cat(flat).to(dev).contiguous()
+        self.grads = torch.zeros_like(self.params)
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.scratch = torch.zeros(max(1, scratch_off), dtype=torch.float32, device=dev)
+        self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
+        cfg = self.cfg
+        o.nseg, o.total, o.algo = nseg, total, cfg["algo"]
+        o.b1, o.b2, o.eps = cfg.get("b1", 0.9), cfg.get("b2", 0.999), cfg.get("eps", 1e-8)
+        o.wd, o.momentum, o.dampening = cfg.get("wd", 0.0), cfg.get("momentum", 0.0), cfg.get("dampening", 0.0)
+        o.nesterov, o.maximize = int(cfg.get("nesterov", False)), int(cfg.get("maximize", False))
+        self.opt = o
+        self.lds_bytes = lds
+        _hip.check(self.lib.rx_mlp_refresh_images(ctypes.byref(o), ctypes.c_void_p(self.params.data_ptr()),
+                                                   _hip.stream_ptr(dev)), "refresh_images")
+
+    # ----------------------------------------------------------------------- running ------
+    def _lr(self, t: int) -> float:
+        return float(self.lr_schedule(t)) if self.lr_schedule is not None else float(self.cfg["lr"])
+
+    def train_epoch(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int,
+                    perm: Optional[torch.Tensor], allreduce: Optional[Callable] = None,
+                    world_size: int = 1, drop_last: bool = False) -> Dict[str, float]:
+        """Run one epoch; ``allreduce(grads)`` (sum) is called between backward and step."""
+        nsteps = n_rows // self.batch if drop_last else -(-n_rows // self.batch)
+        self.metrics.zero_()
+        if nsteps == 0:
+            return self._read_metrics()
+        b1, b2 = self.opt.b1, self.opt.b2
+        lrs = (ctypes.c_float * nsteps)()
+        bc1 = (ctypes.c_float * nsteps)()
+        bc2 = (ctypes.c_float * nsteps)()
+        for s in range(nsteps):
+            t = self.step_count + s + 1
+            lrs[s] = self._lr(self.step_count + s)
+            bc1[s] = 1.0 - b1 ** t
+            bc2[s] = 1.0 - b2 ** t
+        stream = _hip.stream_ptr(self.device)
+        pp = ctypes.c_void_p
+        perm_p = pp(perm.data_ptr()) if perm is not None else pp(0)
+        gscale = 1.0 / world_size
+        if allreduce is None:
+            rc = self.lib.rx_mlp_train_steps(
+                ctypes.byref(self.desc), ctypes.byref(self.opt), self.mt, pp(self.params.data_ptr()),
+                pp(self.grads.data_ptr()), pp(self.m.data_ptr()), pp(self.v.data_ptr()),
+                pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, 0, nsteps,
+                lrs, bc1, bc2, ctypes.c_float(gscale), int(self.step_count == 0), pp(self.scratch.data_ptr()),
+                pp(self.metrics.data_ptr()), stream, pp(0), pp(0))
+            _hip.check(rc, "rx_mlp_train_steps")
+        else:
+            for s in range(nsteps):
+                rc = self.lib.rx_mlp_fwdbwd(
+                    ctypes.byref(self.desc), self.mt, pp(self.params.data_ptr()), pp(self.grads.data_ptr()),
+                    pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, s,
+                    pp(self.scratch.data_ptr()), pp(self.metrics.data_ptr()), stream)
+                _hip.check(rc, "rx_mlp_fwdbwd")
+                allreduce(self.grads)
+                rc = self.lib.rx_opt_step(ctypes.byref(self.opt), pp(self.params.data_ptr()),
+                                          pp(self.grads.data_ptr()), pp(self.m.data_ptr()),
+                                          pp(self.v.data_ptr()), ctypes.c_float(lrs[s]),
+                                          ctypes.c_float(bc1[s]), ctypes.c_float(bc2[s]),
+                                          ctypes.c_float(gscale), int(self.step_count + s == 0), stream)
+                _hip.check(rc, "rx_opt_step")
+        self.step_count += nsteps
+        self.steps_in_epoch = nsteps
+        return self._read_metrics()
+
+    def forward_backward(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int,
+                         perm: Optional[torch.Tensor] = None, step: int = 0) -> torch.Tensor:
+        """One fused fwd/bwd (no optimizer) — returns the flat fp32 gradient (for tests)."""
+        pp = ctypes.c_void_p
+        self.metrics.zero_()
+        rc = self.lib.rx_mlp_fwdbwd(
+            ctypes.byref(self.desc), self.mt, pp(self.params.data_ptr()), pp(self.grads.data_ptr()),
+            pp(feats.data_ptr()), pp(labels.data_ptr()),
+            pp(perm.data_ptr()) if perm is not None else pp(0), n_rows, self.batch, step,
+            pp(self.scratch.data_ptr()), pp(self.metrics.data_ptr()), _hip.stream_ptr(self.device))
+        _hip.check(rc, "rx_mlp_fwdbwd")
+        return self.grads
+
+    def unflatten(self, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """Map a flat vector (params/grads) onto ``{module_param_name: tensor}`` by identity."""
+        out = {}
+        for kind, mod, off, n in self.layout:
+            attr = {"weight": "weight", "bias": "bias", "gamma": "weight", "beta": "bias"}[kind]
+            out[(id(mod), attr)] = flat[off:off + n].view_as(getattr(mod, attr))
+        return out
+
+    def evaluate(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int) -> Dict[str, float]:
+        self.metrics.zero_()
+        pp = ctypes.c_void_p
+        rc = self.lib.rx_mlp_eval(ctypes.byref(self.desc), self.mt, pp(self.params.data_ptr()),
+                                  pp(feats.data_ptr()), pp(labels.data_ptr()), n_rows, self.batch,
+                                  pp(self.metrics.data_ptr()), _hip.stream_ptr(self.device))
+        _hip.check(rc, "rx_mlp_eval")
+        return self._read_metrics()
+
+    def _read_metrics(self) -> Dict[str, float]:
+        m = self.metrics.cpu().numpy()
+        nb = max(m[4], 1.0)
+        cnt = max(m[3], 1.0)
+        return {"loss": float(m[0] / nb), "mae": float(m[1] / cnt), "mse": float(m[2] / cnt),
+                "count": float(m[3]), "batches": float(m[4])}
+
+    # ----------------------------------------------------------------------- state --------
+    @torch.no_grad()
+    def write_back(self):
+        """Copy fp32 master params / BN running stats back into the user's modules."""
+        p = self.params.detach().cpu()
+        for kind, mod, off, n in self.layout:
+            t = {"weight": "weight", "bias": "bias", "gamma": "weight", "beta": "bias"}[kind]
+            dst = getattr(mod, t)
+            dst.data.copy_(p[off:off + n].view_as(dst).to(dst.dtype))
+        for bn, rm, rv in self.run_bufs:
+            bn.running_mean.copy_(rm.cpu())
+            bn.running_var.copy_(rv.cpu())
+            if bn.num_batches_tracked is not None:
+                bn.num_batches_tracked.add_(getattr(self, "_tracked_pending", 0))
+        self._tracked_pending = 0
+
+    def note_steps(self, n):
+        self._tracked_pending = getattr(self, "_tracked_pending", 0) + n

@@ -1,0 +1,182 @@
+"""A runtime node: resource accounting, object store, actor supervisor.
+
+One driver process hosts the *head*: the cluster resource table (one or more virtual nodes,
+each with its own CPU/GPU/memory/custom resources and its own shared-memory object-store
+arena — the analogue of ``ray.cluster_utils.Cluster`` used by the reference's multi-node
+tests, ``python/raydp/tests/test_spark_cluster.py:90-110``), the named-actor registry and the
+placement-group table. Actor processes are supervised natively (``csrc/runtime``).
+"""
+import os
+import threading
+import uuid
+from typing import Dict, List, Optional
+
+from raydp_amd.utils import get_node_ip_address, parse_memory_size
+
+
+class ResourceError(RuntimeError):
+    pass
+
+
+class VirtualNode:
+    def __init__(self, node_id: str, resources: Dict[str, float], store=None, ip: str = None):
+        self.node_id = node_id
+        self.total = dict(resources)
+        self.available = dict(resources)
+        self.store = store
+        self.alive = True
+        self.ip = ip or get_node_ip_address()
+
+    def fits(self, req: Dict[str, float]) -> bool:
+        return self.alive and all(self.available.get(k, 0.0) + 1e-9 >= v for k, v in req.items() if v)
+
+    def acquire(self, req: Dict[str, float]):
+        for k, v in req.items():
+            if v:
+                self.available[k] = self.available.get(k, 0.0) - v
+
+    def release(self, req: Dict[str, float]):
+        for k, v in req.items():
+            if v:
+                self.available[k] = min(self.total.get(k, 0.0), self.available.get(k, 0.0) + v)
+
+
+class ClusterState:
+    def __init__(self):
+        self.lock = threading.RLock()
+        self.nodes: Dict[str, VirtualNode] = {}
+        self.order: List[str] = []
+
+    def add(self, n: VirtualNode):
+        with self.lock:
+            self.nodes[n.node_id] = n
+            self.order.append(n.node_id)
+
+    def alive_nodes(self) -> List[VirtualNode]:
+        with self.lock:
+            return [self.nodes[i] for i in self.order if self.nodes[i].alive]
+
+    def pick_node(self, req: Dict[str, float], prefer: Optional[str] = None) -> VirtualNode:
+        with self.lock:
+            if prefer and prefer in self.nodes and self.nodes[prefer].fits(req):
+                return self.nodes[prefer]
+            for n in self.alive_nodes():
+                if n.fits(req):
+                    return n
+        raise ResourceError(f"no node can satisfy resource request {req}")
+
+    def place_group(self, pg):
+        with self.lock:
+            nodes = self.alive_nodes()
+            chosen: List[VirtualNode] = []
+            snapshot = {n.node_id: dict(n.available) for n in nodes}
+            try:
+                for i, b in enumerate(pg.bundle_specs):
+                    cand = nodes
+                    if pg.strategy == "STRICT_PACK" and chosen:
+                        cand = [chosen[0]]
+                    elif pg.strategy == "STRICT_SPREAD":
+                        cand = [n for n in nodes if n not in chosen]
+                    elif pg.strategy == "SPREAD":
+                        cand = sorted(nodes, key=lambda n: sum(1 for c in chosen if c is n))
+                    elif pg.strategy == "PACK" and chosen:
+                        cand = [chosen[-1]] + [n for n in nodes if n is not chosen[-1]]
+                    node = next((n for n in cand if n.fits(b)), None)
+                    if node is None:
+                        raise ResourceError(f"cannot place bundle {i} {b} with strategy {pg.strategy}")
+                    node.acquire(b)
+                    chosen.append(node)
+            except ResourceError:
+                for n in nodes:
+                    n.available = snapshot[n.node_id]
+                raise
+            pg.bundle_nodes = [n.node_id for n in chosen]
+            # bundle reservations become the bundle's private pool
+            pg.bundle_free = [dict(b) for b in pg.bundle_specs]
+
+    def release_group(self, pg):
+        with self.lock:
+            for nid, b in zip(pg.bundle_nodes, pg.bundle_specs):
+                n = self.nodes.get(nid)
+                if n is not None:
+                    n.release(b)
+
+
+def _default_resources(num_cpus=None, num_gpus=None, memory=None, resources=None):
+    if num_cpus is None:
+        num_cpus = os.cpu_count() or 1
+    if num_gpus is None:
+        num_gpus = 0
+        try:
+            import torch
+            num_gpus = torch.cuda.device_count()
+        except Exception:  # noqa: BLE001
+            pass
+    if memory is None:
+        try:
+            import psutil
+            memory = int(psutil.virtual_memory().total * 0.7)
+        except Exception:  # noqa: BLE001
+            memory = 8 << 30
+    r = {"CPU": float(num_cpus), "GPU": float(num_gpus), "memory": float(memory)}
+    r.update({k: float(v) for k, v in (resources or {}).items()})
+    return r
+
+
+class Node:
+    def __init__(self, namespace=None):
+        self.node_id = uuid.uuid4().hex[:16]
+        self.namespace = namespace or "default"
+        self.job_id = uuid.uuid4().hex[:8]
+        self.address = f"{get_node_ip_address()}:0"
+        self.cluster = ClusterState()
+        self.session_dir = None
+        self.store = None
+        self.supervisor = None
+        self.actors = None
+
+    @classmethod
+    def create(cls, address=None, num_cpus=None, num_gpus=None, resources=None,
+               object_store_memory=None, namespace=None, memory=None):
+        import tempfile
+        n = cls(namespace)
+        n.session_dir = tempfile.mkdtemp(prefix=f"raydp_session_{n.node_id[:8]}_")
+        os.makedirs(os.path.join(n.session_dir, "logs"), exist_ok=True)
+        from raydp_amd.runtime.store import open_store
+        n.store = open_store(n.node_id, object_store_memory, n.session_dir)
+        head = VirtualNode(n.node_id, _default_resources(num_cpus, num_gpus, memory, resources),
+                           n.store)
+        n.cluster.add(head)
+        from raydp_amd.runtime.actors import ActorManager
+        n.actors = ActorManager(n)
+        return n
+
+    def add_virtual_node(self, num_cpus=1, num_gpus=0, resources=None, object_store_memory=None,
+                         memory=None) -> VirtualNode:
+        from raydp_amd.runtime.store import open_store
+        nid = uuid.uuid4().hex[:16]
+        store = open_store(nid, object_store_memory, self.session_dir)
+        vn = VirtualNode(nid, _default_resources(num_cpus, num_gpus, memory or (2 << 30), resources), store)
+        self.cluster.add(vn)
+        return vn
+
+    def remove_virtual_node(self, node_id: str):
+        vn = self.cluster.nodes[node_id]
+        vn.alive = False
+        if self.actors is not None:
+            self.actors.on_node_removed(node_id)
+        if vn.store is not None and vn.store is not self.store:
+            vn.store.destroy()
+
+    def info(self):
+        return {"node_id": self.node_id, "address": self.address, "session_dir": self.session_dir,
+                "namespace": self.namespace}
+
+    def shutdown(self):
+        if self.actors is not None:
+            self.actors.shutdown()
+        for vn in list(self.cluster.nodes.values()):
+            if vn.store is not None:
+                vn.store.destroy()
+        from raydp_amd.runtime import pgroup as pg
+        pg._reset()

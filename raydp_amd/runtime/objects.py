@@ -1,0 +1,132 @@
+"""Object references and the object-store front end (``put`` / ``get`` / ``free``).
+
+Objects live in the node's shared-memory store (``csrc/runtime/objstore.cc`` via
+``raydp_amd.runtime.store``) when a runtime node is up; Arrow tables are stored as Arrow IPC
+so every process reads them zero-copy from the mapped arena. Without a running node the
+objects stay in this process (driver-only use, unit tests).
+
+An ``ObjectRef`` may carry *lineage* — the task that produced it — so a lost object
+(its node was removed, or the store entry was evicted) is transparently re-created on
+``get`` (parity: ``@ray.remote(max_retries=-1)`` fetch tasks in
+``python/raydp/spark/dataset.py:54``).
+"""
+import threading
+import uuid
+from typing import Any, Callable, Dict, Optional
+
+_local_lock = threading.RLock()
+_local: Dict[str, Any] = {}
+
+
+class ObjectLostError(RuntimeError):
+    pass
+
+
+class ObjectRef:
+    __slots__ = ("id", "owner", "node_id", "_lineage", "__weakref__")
+
+    def __init__(self, oid: Optional[str] = None, owner: str = "driver",
+                 node_id: Optional[str] = None, lineage: Optional[Callable[[], Any]] = None):
+        self.id = oid or uuid.uuid4().hex
+        self.owner = owner
+        self.node_id = node_id
+        self._lineage = lineage
+
+    def hex(self):
+        return self.id
+
+    def binary(self):
+        return bytes.fromhex(self.id)
+
+    def task_id(self):
+        return self.id[:16]
+
+    def __repr__(self):
+        return f"ObjectRef({self.id})"
+
+    def __hash__(self):
+        return hash(self.id)
+
+    def __eq__(self, other):
+        return isinstance(other, ObjectRef) and other.id == self.id
+
+    def __reduce__(self):
+        # lineage closures stay with the owner; a deserialized ref resolves by id
+        return (ObjectRef, (self.id, self.owner, self.node_id, None))
+
+    def future(self):
+        import concurrent.futures
+        f = concurrent.futures.Future()
+        f.set_result(get(self))
+        return f
+
+
+def _store():
+    from raydp_amd.runtime import core
+    node = core.current_node_store()
+    return node
+
+
+def put(value: Any, _owner: str = "driver", _lineage=None) -> ObjectRef:
+    ref = ObjectRef(owner=_owner, lineage=_lineage)
+    store = _store()
+    if store is not None:
+        store.put(ref.id, value)
+        ref.node_id = store.node_id
+    else:
+        with _local_lock:
+            _local[ref.id] = value
+    return ref
+
+
+def put_with_id(oid: str, value: Any):
+    store = _store()
+    if store is not None:
+        store.put(oid, value)
+    else:
+        with _local_lock:
+            _local[oid] = value
+
+
+def contains(ref: ObjectRef) -> bool:
+    store = _store()
+    if store is not None and store.contains(ref.id):
+        return True
+    with _local_lock:
+        return ref.id in _local
+
+
+def get(ref, timeout: Optional[float] = None):
+    if isinstance(ref, (list, tuple)):
+        return [get(r, timeout) for r in ref]
+    if not isinstance(ref, ObjectRef):
+        return ref
+    from raydp_amd.runtime import core
+    pending = core.pending_result(ref)
+    if pending is not None:
+        return pending.result(timeout)
+    store = _store()
+    if store is not None:
+        found, value = store.get(ref.id)
+        if found:
+            return value
+    with _local_lock:
+        if ref.id in _local:
+            return _local[ref.id]
+    if ref._lineage is not None:
+        # reconstruct from lineage (re-run the producing task) and re-seal under the same id
+        value = ref._lineage()
+        put_with_id(ref.id, value)
+        return value
+    raise ObjectLostError(f"object {ref.id} is lost and has no lineage to reconstruct it")
+
+
+def free(refs):
+    if isinstance(refs, ObjectRef):
+        refs = [refs]
+    store = _store()
+    for r in refs:
+        if store is not None:
+            store.delete(r.id)
+        with _local_lock:
+            _local.pop(r.id, None)

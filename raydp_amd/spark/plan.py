@@ -1,0 +1,380 @@
+"""Logical/physical plan of the Arrow-native DataFrame engine.
+
+A plan is a DAG of partition-wise operators. Narrow operators (filter, project, sample,
+explode, mapInPandas) are fused into one per-partition task chain; wide operators (repartition,
+join, groupBy, orderBy, window, distinct) are stage boundaries whose shuffle output is
+materialised once, bottom-up, before the consuming stage runs (Spark's ``ShuffleMapStage``
+→ ``ResultStage`` split, ``RayAppMaster``/executor task model in the reference's L4).
+
+Tasks run through a pluggable ``TaskScheduler``: in-process threads (Arrow kernels release
+the GIL), or the executor actor processes of a Spark-on-runtime session
+(``raydp_amd/spark/cluster.py``).
+"""
+import io
+import math
+import os
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+
+_tls = threading.local()
+
+
+def current_partition_index() -> int:
+    return getattr(_tls, "partition", 0)
+
+
+class _PartitionScope:
+    def __init__(self, i):
+        self.i = i
+
+    def __enter__(self):
+        self.prev = getattr(_tls, "partition", 0)
+        _tls.partition = self.i
+
+    def __exit__(self, *a):
+        _tls.partition = self.prev
+
+
+# ------------------------------------------------------------------------------------------
+# Scheduler
+# ------------------------------------------------------------------------------------------
+class TaskScheduler:
+    """Runs ``fn(i)`` for a list of partition indices; subclasses may ship tasks elsewhere."""
+
+    def __init__(self, parallelism: int = 1):
+        self.parallelism = max(1, int(parallelism))
+        self._pool = ThreadPoolExecutor(max_workers=self.parallelism,
+                                        thread_name_prefix="raydp-task")
+
+    def map(self, fn: Callable[[int], object], indices: Sequence[int]) -> List[object]:
+        indices = list(indices)
+        if len(indices) <= 1 or self.parallelism == 1:
+            return [fn(i) for i in indices]
+        return list(self._pool.map(fn, indices))
+
+    def run_plan(self, plan: "Plan", indices=None) -> List[pa.Table]:
+        prepare(plan, self)
+        idx = range(plan.num_partitions()) if indices is None else indices
+        return self.map(plan.compute, idx)
+
+    def shutdown(self):
+        self._pool.shutdown(wait=False, cancel_futures=True)
+
+
+_default_scheduler: Optional[TaskScheduler] = None
+
+
+def get_scheduler() -> TaskScheduler:
+    global _default_scheduler
+    from raydp_amd.spark import session as _s
+    active = _s.SparkSession.getActiveSession()
+    if active is not None and active._scheduler is not None:
+        return active._scheduler
+    if _default_scheduler is None:
+        _default_scheduler = TaskScheduler(os.cpu_count() or 1)
+    return _default_scheduler
+
+
+# ------------------------------------------------------------------------------------------
+# Plans
+# ------------------------------------------------------------------------------------------
+class Plan:
+    _schema: Optional[pa.Schema] = None
+
+    def children(self) -> List["Plan"]:
+        return []
+
+    def num_partitions(self) -> int:
+        raise NotImplementedError
+
+    def compute(self, i: int) -> pa.Table:
+        raise NotImplementedError
+
+    def empty(self) -> pa.Table:
+        """Zero-row table with this plan's output schema (schema inference by execution)."""
+        raise NotImplementedError
+
+    @property
+    def schema(self) -> pa.Schema:
+        if self._schema is None:
+            self._schema = self.empty().schema
+        return self._schema
+
+    def is_wide(self) -> bool:
+        return False
+
+    def materialize(self, scheduler: TaskScheduler):
+        pass
+
+
+def prepare(plan: Plan, scheduler: TaskScheduler):
+    """Materialise every wide operator below ``plan`` bottom-up (stage scheduling)."""
+    for c in plan.children():
+        prepare(c, scheduler)
+    if plan.is_wide():
+        plan.materialize(scheduler)
+
+
+def _empty_like(schema: pa.Schema) -> pa.Table:
+    return schema.empty_table()
+
+
+class SourcePlan(Plan):
+    def __init__(self, source):
+        self.source = source
+
+    def num_partitions(self):
+        return self.source.num_partitions()
+
+    def compute(self, i):
+        with _PartitionScope(i):
+            return self.source.load(i)
+
+    def empty(self):
+        return _empty_like(self.source.schema())
+
+
+class MapPlan(Plan):
+    """Narrow per-partition operator: ``fn(table, partition_index) -> table``."""
+
+    def __init__(self, child: Plan, fn: Callable, desc: str = "map"):
+        self.child, self.fn, self.desc = child, fn, desc
+
+    def children(self):
+        return [self.child]
+
+    def num_partitions(self):
+        return self.child.num_partitions()
+
+    def compute(self, i):
+        t = self.child.compute(i)
+        with _PartitionScope(i):
+            return self.fn(t, i)
+
+    def empty(self):
+        with _PartitionScope(0):
+            return self.fn(self.child.empty(), 0)
+
+
+class UnionPlan(Plan):
+    def __init__(self, plans: List[Plan], by_name=False):
+        self.plans, self.by_name = plans, by_name
+        self._offsets = None
+
+    def children(self):
+        return list(self.plans)
+
+    def _offs(self):
+        if self._offsets is None:
+            self._offsets = np.cumsum([0] + [p.num_partitions() for p in self.plans])
+        return self._offsets
+
+    def num_partitions(self):
+        return int(self._offs()[-1])
+
+    def _conform(self, t: pa.Table) -> pa.Table:
+        target = self.plans[0].schema
+        if self.by_name:
+            t = t.select(target.names)
+        else:
+            t = t.rename_columns(target.names)
+        if t.schema != target:
+            t = t.cast(target, safe=False)
+        return t
+
+    def compute(self, i):
+        offs = self._offs()
+        k = int(np.searchsorted(offs, i, side="right") - 1)
+        return self._conform(self.plans[k].compute(i - int(offs[k])))
+
+    def empty(self):
+        return self.plans[0].empty()
+
+
+class MaterializedPlan(Plan):
+    """Already-computed partitions (a cached DataFrame or a finished shuffle)."""
+
+    def __init__(self, tables: List[pa.Table], schema: pa.Schema):
+        self.tables, self._schema = tables, schema
+
+    def num_partitions(self):
+        return len(self.tables)
+
+    def compute(self, i):
+        return self.tables[i]
+
+    def empty(self):
+        return _empty_like(self._schema)
+
+
+class WidePlan(Plan):
+    """Stage boundary: output partitions are produced by a shuffle of the children."""
+
+    def __init__(self):
+        self._out: Optional[List[pa.Table]] = None
+        self._lock = threading.Lock()
+
+    def is_wide(self):
+        return True
+
+    def materialize(self, scheduler):
+        with self._lock:
+            if self._out is None:
+                self._out = self.execute(scheduler)
+
+    def execute(self, scheduler) -> List[pa.Table]:
+        raise NotImplementedError
+
+    def compute(self, i):
+        if self._out is None:
+            self.materialize(get_scheduler())
+        return self._out[i]
+
+
+# ------------------------------------------------------------------------------------------
+# shuffle primitives
+# ------------------------------------------------------------------------------------------
+def hash_columns(t: pa.Table, keys: List[str]) -> np.ndarray:
+    """64-bit row hash of the key columns, consistent across partitions/processes."""
+    from raydp_amd.native import exec_kernels
+    h = np.zeros(t.num_rows, dtype=np.uint64)
+    for k in keys:
+        h = exec_kernels.hash_combine(h, t.column(k))
+    return h
+
+
+def hash_partition(t: pa.Table, keys: List[str], n: int) -> List[pa.Table]:
+    if n == 1:
+        return [t]
+    if t.num_rows == 0:
+        return [t.slice(0, 0) for _ in range(n)]
+    from raydp_amd.native import exec_kernels
+    part = (hash_columns(t, keys) % np.uint64(n)).astype(np.int64)
+    order, counts = exec_kernels.partition_order(part, n)
+    st = t.take(pa.array(order))
+    out, off = [], 0
+    for c in counts:
+        out.append(st.slice(off, int(c)))
+        off += int(c)
+    return out
+
+
+def concat(tables: List[pa.Table], schema: pa.Schema) -> pa.Table:
+    tables = [t for t in tables if t is not None]
+    if not tables:
+        return _empty_like(schema)
+    try:
+        return pa.concat_tables(tables, promote_options="permissive").combine_chunks()
+    except pa.ArrowInvalid:
+        return pa.concat_tables([t.cast(schema, safe=False) for t in tables]).combine_chunks()
+
+
+class RepartitionPlan(WidePlan):
+    """``repartition(n)`` (round-robin) or ``repartition(n, *cols)`` (hash)."""
+
+    def __init__(self, child: Plan, n: int, keys: Optional[List[str]] = None):
+        super().__init__()
+        self.child, self.n, self.keys = child, max(1, int(n)), keys
+
+    def children(self):
+        return [self.child]
+
+    def num_partitions(self):
+        return self.n
+
+    def empty(self):
+        return self.child.empty()
+
+    def execute(self, scheduler):
+        n = self.n
+        keys = self.keys
+
+        def split(i):
+            t = self.child.compute(i)
+            if keys:
+                return hash_partition(t, keys, n)
+            # round robin starting at a partition-dependent offset (Spark's distribution)
+            if n == 1:
+                return [t]
+            assign = (np.arange(t.num_rows) + i) % n
+            order = np.argsort(assign, kind="stable")
+            counts = np.bincount(assign, minlength=n)
+            st = t.take(pa.array(order))
+            res, off = [], 0
+            for c in counts:
+                res.append(st.slice(off, int(c)))
+                off += int(c)
+            return res
+
+        pieces = scheduler.map(split, range(self.child.num_partitions()))
+        schema = self.child.schema
+        return [concat([p[j] for p in pieces], schema) for j in range(n)]
+
+
+class CoalescePlan(Plan):
+    """Narrow merge of adjacent partitions (``coalesce(n)``)."""
+
+    def __init__(self, child: Plan, n: int):
+        self.child = child
+        m = child.num_partitions()
+        self.n = max(1, min(int(n), m)) if m else 1
+        self.groups = np.array_split(np.arange(m), self.n) if m else [np.arange(0)]
+
+    def children(self):
+        return [self.child]
+
+    def num_partitions(self):
+        return self.n
+
+    def compute(self, i):
+        return concat([self.child.compute(int(j)) for j in self.groups[i]], self.child.schema)
+
+    def empty(self):
+        return self.child.empty()
+
+
+class SortPlan(WidePlan):
+    def __init__(self, child: Plan, sort_keys, n_out: Optional[int] = None):
+        super().__init__()
+        self.child, self.sort_keys = child, sort_keys  # list of (expr, ascending, nulls_first)
+        self.n_out = n_out or child.num_partitions()
+
+    def children(self):
+        return [self.child]
+
+    def num_partitions(self):
+        return max(1, self.n_out)
+
+    def empty(self):
+        return self.child.empty()
+
+    def execute(self, scheduler):
+        parts = scheduler.map(self.child.compute, range(self.child.num_partitions()))
+        t = concat(parts, self.child.schema)
+        t = sort_table(t, self.sort_keys)
+        n = self.num_partitions()
+        rows = t.num_rows
+        bounds = np.linspace(0, rows, n + 1).astype(np.int64)
+        return [t.slice(int(bounds[j]), int(bounds[j + 1] - bounds[j])) for j in range(n)]
+
+
+def sort_table(t: pa.Table, sort_keys) -> pa.Table:
+    if t.num_rows == 0:
+        return t
+    tmp = t
+    keys = []
+    null_first = None
+    for j, (e, asc, nulls_first) in enumerate(sort_keys):
+        name = f"__sk{j}"
+        from raydp_amd.spark.column import as_array
+        tmp = tmp.append_column(name, as_array(e.eval(t), t.num_rows))
+        keys.append((name, "ascending" if asc else "descending"))
+        null_first = nulls_first if null_first is None else null_first
+    idx = pc.sort_indices(tmp, sort_keys=keys,
+                          null_placement="at_start" if null_first else "at_end")
+    return t.take(idx)

@@ -1,0 +1,224 @@
+"""Partitioned data sources: in-memory Arrow, ``range``, CSV byte-splits, Parquet files.
+
+CSV follows Spark's file-split model: each file is cut into ``spark.sql.files.maxPartitionBytes``
+byte ranges aligned to line boundaries, and every split is parsed independently by Arrow's
+multi-threaded C++ CSV reader with the schema inferred once from the head of the first file
+(``inferSchema=true``) so all partitions agree on column types.
+"""
+import glob
+import io
+import os
+from typing import List, Optional
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.csv as pacsv
+import pyarrow.parquet as pq
+
+
+class Source:
+    def num_partitions(self) -> int:
+        raise NotImplementedError
+
+    def load(self, i: int) -> pa.Table:
+        raise NotImplementedError
+
+    def schema(self) -> pa.Schema:
+        raise NotImplementedError
+
+
+class TableSource(Source):
+    def __init__(self, tables: List[pa.Table], schema: Optional[pa.Schema] = None):
+        self.tables = tables
+        self._schema = schema if schema is not None else (tables[0].schema if tables else pa.schema([]))
+
+    def num_partitions(self):
+        return len(self.tables)
+
+    def load(self, i):
+        return self.tables[i]
+
+    def schema(self):
+        return self._schema
+
+
+def split_table(t: pa.Table, n: int) -> List[pa.Table]:
+    n = max(1, int(n))
+    bounds = np.linspace(0, t.num_rows, n + 1).astype(np.int64)
+    return [t.slice(int(bounds[j]), int(bounds[j + 1] - bounds[j])) for j in range(n)]
+
+
+class RangeSource(Source):
+    def __init__(self, start, end, step, num_partitions):
+        self.start, self.end, self.step = int(start), int(end), int(step)
+        self.n = max(1, int(num_partitions))
+        total = max(0, -(-(self.end - self.start) // self.step)) if self.step > 0 else \
+            max(0, -(-(self.start - self.end) // -self.step))
+        self.total = total
+        self.bounds = np.linspace(0, total, self.n + 1).astype(np.int64)
+
+    def num_partitions(self):
+        return self.n
+
+    def load(self, i):
+        lo, hi = int(self.bounds[i]), int(self.bounds[i + 1])
+        ids = self.start + np.arange(lo, hi, dtype=np.int64) * self.step
+        return pa.table({"id": pa.array(ids, type=pa.int64())})
+
+    def schema(self):
+        return pa.schema([pa.field("id", pa.int64(), False)])
+
+
+def _expand_paths(path) -> List[str]:
+    paths = [path] if isinstance(path, str) else list(path)
+    out = []
+    for p in paths:
+        if p.startswith("file://"):
+            p = p[len("file://"):]
+        if os.path.isdir(p):
+            for root, _, files in os.walk(p):
+                for f in sorted(files):
+                    if f.startswith(("_", ".")) or f.endswith(".crc"):
+                        continue
+                    out.append(os.path.join(root, f))
+        elif any(ch in p for ch in "*?["):
+            out.extend(sorted(glob.glob(p)))
+        else:
+            out.append(p)
+    if not out:
+        raise FileNotFoundError(f"Path does not exist: {path}")
+    return out
+
+
+def _downcast_ints(t: pa.Table) -> pa.Table:
+    """Spark's CSV inference picks int for values that fit 32 bits."""
+    cols = []
+    changed = False
+    for name, c in zip(t.column_names, t.columns):
+        if pa.types.is_int64(c.type) and len(c) > 0:
+            import pyarrow.compute as pc
+            mm = pc.min_max(c)
+            lo, hi = mm["min"].as_py(), mm["max"].as_py()
+            if lo is not None and -2 ** 31 <= lo and hi < 2 ** 31:
+                c = c.cast(pa.int32())
+                changed = True
+        cols.append(c)
+    return pa.table(cols, names=t.column_names) if changed else t
+
+
+class CsvSource(Source):
+    def __init__(self, path, header=True, infer_schema=False, sep=",", schema=None,
+                 max_partition_bytes=128 * 1024 * 1024, null_value=None):
+        self.files = _expand_paths(path)
+        self.header, self.sep = header, sep
+        self.null_value = null_value
+        self.splits = []
+        for f in self.files:
+            size = os.path.getsize(f)
+            nsplit = max(1, int(np.ceil(size / max_partition_bytes)))
+            b = np.linspace(0, size, nsplit + 1).astype(np.int64)
+            for j in range(nsplit):
+                self.splits.append((f, int(b[j]), int(b[j + 1])))
+        self._header_line = None
+        if schema is not None:
+            self._schema = schema
+        else:
+            self._schema = self._infer(infer_schema)
+
+    def _read_opts(self, column_names=None):
+        ro = pacsv.ReadOptions(column_names=column_names, autogenerate_column_names=not self.header
+                               and column_names is None, use_threads=True)
+        return ro
+
+    def _infer(self, infer):
+        f = self.files[0]
+        with open(f, "rb") as fh:
+            head = fh.read(1 << 20)
+        cut = head.rfind(b"\n")
+        if cut > 0 and len(head) == (1 << 20):
+            head = head[:cut + 1]
+        first_nl = head.find(b"\n")
+        self._header_line = head[:first_nl + 1] if self.header else b""
+        conv = pacsv.ConvertOptions(strings_can_be_null=True) if infer else pacsv.ConvertOptions(
+            column_types=None)
+        t = pacsv.read_csv(io.BytesIO(head), read_options=self._read_opts(),
+                           parse_options=pacsv.ParseOptions(delimiter=self.sep),
+                           convert_options=conv)
+        if not infer:
+            return pa.schema([pa.field(n, pa.string()) for n in t.column_names])
+        t = _downcast_ints(t)
+        fields = []
+        for fld in t.schema:
+            ty = fld.type
+            if pa.types.is_null(ty):
+                ty = pa.string()
+            fields.append(pa.field(fld.name, ty))
+        return pa.schema(fields)
+
+    def num_partitions(self):
+        return len(self.splits)
+
+    def schema(self):
+        return self._schema
+
+    def load(self, i):
+        f, lo, hi = self.splits[i]
+        with open(f, "rb") as fh:
+            header = b""
+            if self.header:
+                header = fh.readline()
+            if lo > 0:
+                fh.seek(lo - 1)
+                prev = fh.read(1)
+                if prev != b"\n":
+                    fh.readline()  # finish the line owned by the previous split
+            start = max(fh.tell(), len(header))
+            if start >= hi and lo > 0:
+                return self._schema.empty_table()
+            fh.seek(start)
+            data = fh.read(max(0, hi - start))
+            if data and not data.endswith(b"\n"):
+                data += fh.readline()
+        names = self._schema.names
+        conv = pacsv.ConvertOptions(column_types={f.name: f.type for f in self._schema},
+                                    strings_can_be_null=True,
+                                    null_values=[self.null_value] if self.null_value else None)
+        if not data.strip():
+            return self._schema.empty_table()
+        t = pacsv.read_csv(io.BytesIO(data),
+                           read_options=pacsv.ReadOptions(column_names=names, use_threads=True),
+                           parse_options=pacsv.ParseOptions(delimiter=self.sep),
+                           convert_options=conv)
+        return t
+
+
+class ParquetSource(Source):
+    def __init__(self, path):
+        self.files = [f for f in _expand_paths(path) if not os.path.basename(f).startswith(("_", "."))]
+        self._schema = pq.read_schema(self.files[0])
+
+    def num_partitions(self):
+        return len(self.files)
+
+    def load(self, i):
+        return pq.read_table(self.files[i])
+
+    def schema(self):
+        return self._schema
+
+
+class JsonSource(Source):
+    def __init__(self, path):
+        import pyarrow.json as pj
+        self.files = _expand_paths(path)
+        self._pj = pj
+        self._schema = pj.read_json(self.files[0]).schema
+
+    def num_partitions(self):
+        return len(self.files)
+
+    def load(self, i):
+        return self._pj.read_json(self.files[i]).cast(self._schema)
+
+    def schema(self):
+        return self._schema

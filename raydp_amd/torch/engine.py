@@ -1,0 +1,230 @@
+"""Per-worker training engines behind ``TorchEstimator``.
+
+* ``FusedMLPEngine`` — MI355X fast path. The worker's whole data shard is ingested into HBM
+  once (one pinned DMA + the ``arrow_ingest`` HIP kernel); every epoch is one native call that
+  enqueues, per batch, the single-workgroup fused fwd/bwd kernel, the (optional) RCCL
+  all-reduce and the fused optimizer kernel; the epoch shuffle is a device permutation read by
+  the kernel's row gather. Used when the model is a fusable MLP (``models/mlp_spec.py``), the
+  loss is MSE/SmoothL1/L1, the optimizer Adam/AdamW/SGD and the metrics are MAE/MSE.
+* ``TorchLoopEngine`` — any other model. Still device-resident (data ingested once, batches are
+  device slices of a permuted index), loss and metrics accumulated on the device and read once
+  per epoch; DDP via ``raydp_amd.parallel.ddp`` when ``world_size > 1``.
+
+Both report the reference's per-epoch dicts ``{epoch, train_res, train_loss}`` and
+``{epoch, eval_res, test_loss}`` (``python/raydp/torch/estimator.py:245-253``).
+"""
+import copy
+from typing import Any, Callable, Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from raydp_amd.train import session
+
+
+def _to_tensor_spec(feature_columns, feature_types):
+    """Normalise (feature_columns, feature_types) into groups of (cols, dtype)."""
+    if feature_columns and isinstance(feature_columns[0], (list, tuple)):
+        groups = [list(g) for g in feature_columns]
+        if isinstance(feature_types, (list, tuple)):
+            dts = list(feature_types)
+        else:
+            dts = [feature_types] * len(groups)
+        return groups, [d or torch.float32 for d in dts], True
+    dt = feature_types
+    if isinstance(dt, (list, tuple)):
+        uniq = {d for d in dt if d is not None}
+        if len(uniq) > 1:
+            # one tensor per column, each with its own dtype (DLRM-style multi-input models)
+            return [[c] for c in feature_columns], [d or torch.float32 for d in dt], True
+        dt = uniq.pop() if uniq else torch.float32
+    return [list(feature_columns)], [dt or torch.float32], False
+
+
+class _ShardTensors:
+    def __init__(self, ds, feature_columns, feature_types, label_column, label_type, device,
+                 fused_stride: Optional[int] = None):
+        tables = ds._get_tables() if ds is not None else []
+        self.n = int(sum(t.num_rows for t in tables))
+        from raydp_amd.ops.ingest import ingest_columns
+        self.groups, self.dtypes, self.multi = _to_tensor_spec(feature_columns, feature_types)
+        self.device = device
+        if fused_stride is not None:
+            self.feats_bf16 = ingest_columns(tables, self.groups[0], device, True, fused_stride)
+            self.feats = None
+        else:
+            self.feats = [ingest_columns(tables, g, device, False).to(d) for g, d in
+                          zip(self.groups, self.dtypes)]
+        lab = ingest_columns(tables, [label_column], device, False)
+        self.labels = lab.to(label_type or torch.float32)
+
+
+class FusedMLPEngine:
+    name = "fused_mlp_hip"
+
+    @staticmethod
+    def applicable(model, optimizer, loss, metrics, device, batch_size, feature_columns,
+                   feature_types) -> Optional[tuple]:
+        if device.type != "cuda":
+            return None
+        from raydp_amd.models.mlp_spec import extract_mlp_spec
+        from raydp_amd.ops.fused_mlp import loss_code, optimizer_config, pick_mt
+        if pick_mt(batch_size) is None:
+            return None
+        if feature_columns and isinstance(feature_columns[0], (list, tuple)):
+            return None
+        if isinstance(feature_types, (list, tuple)) and len({t for t in feature_types}) > 1:
+            return None
+        if any(n not in ("MeanAbsoluteError", "MeanSquaredError") for n in metrics.names):
+            return None
+        spec = extract_mlp_spec(model)
+        lc = loss_code(loss)
+        oc = optimizer_config(optimizer)
+        if spec is None or lc is None or oc is None:
+            return None
+        if spec.in_features != len(feature_columns):
+            return None
+        return spec, lc, oc
+
+    def __init__(self, model, optimizer, spec, lc, oc, metrics, device, config, lr_scheduler_fn):
+        from raydp_amd.ops.fused_mlp import FusedMLPTrainer
+        self.model, self.metrics_names, self.device = model, metrics.names, device
+        self.world = session.get_world_size()
+        model.to(device)
+        self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn)
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.broadcast(self.trainer.params, 0)
+            from raydp_amd.ops import _hip
+            import ctypes
+            _hip.check(self.trainer.lib.rx_mlp_refresh_images(
+                ctypes.byref(self.trainer.opt), ctypes.c_void_p(self.trainer.params.data_ptr()),
+                _hip.stream_ptr(device)), "refresh")
+        self.drop_last = bool(config.get("drop_last", False))
+        self.shuffle = bool(config.get("shuffle", True))
+        self.gen = torch.Generator(device=device)
+        self.gen.manual_seed(1234 + session.get_world_rank())
+
+    def load(self, train_ds, eval_ds, config):
+        fc, ft = config["feature_columns"], config["feature_types"]
+        k = self.trainer.feat_k
+        self.train = _ShardTensors(train_ds, fc, ft, config["label_column"], torch.float32,
+                                   self.device, fused_stride=k)
+        self.eval = _ShardTensors(eval_ds, fc, ft, config["label_column"], torch.float32, self.device,
+                                  fused_stride=k) if eval_ds is not None else None
+
+    def _res(self, m):
+        out = {}
+        if "MeanAbsoluteError" in self.metrics_names:
+            out["MeanAbsoluteError"] = m["mae"]
+        if "MeanSquaredError" in self.metrics_names:
+            out["MeanSquaredError"] = m["mse"]
+        return out
+
+    def train_epoch(self):
+        t = self.train
+        perm = None
+        if self.shuffle:
+            perm = torch.randperm(t.n, device=self.device, generator=self.gen).to(torch.int32)
+        ar = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            def ar(g):
+                dist.all_reduce(g)
+        m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, allreduce=ar,
+                                     world_size=self.world, drop_last=self.drop_last)
+        self.trainer.note_steps(self.trainer.steps_in_epoch)
+        return self._res(m), m["loss"]
+
+    def evaluate_epoch(self):
+        e = self.eval
+        m = self.trainer.evaluate(e.feats_bf16, e.labels, e.n)
+        return self._res(m), m["loss"]
+
+    def state_dict(self):
+        self.trainer.write_back()
+        return self.model.state_dict()
+
+
+class TorchLoopEngine:
+    name = "torch_loop"
+
+    def __init__(self, model, optimizer, loss, metrics, device, config, lr_scheduler):
+        self.device = device
+        self.world = session.get_world_size()
+        self.raw_model = model.to(device)
+        if self.world > 1:
+            from raydp_amd.parallel.ddp import DistributedDataParallel
+            self.model = DistributedDataParallel(self.raw_model)
+        else:
+            self.model = self.raw_model
+        # optimizer state may reference CPU tensors; move them
+        for st in optimizer.state.values():
+            for k, v in list(st.items()):
+                if isinstance(v, torch.Tensor) and k != "step":
+                    st[k] = v.to(device)
+        self.optimizer, self.loss, self.metrics = optimizer, loss, metrics
+        self.scheduler = lr_scheduler
+        self.batch = int(config["batch_size"])
+        self.drop_last = bool(config.get("drop_last", False))
+        self.shuffle = bool(config.get("shuffle", True))
+        self.gen = torch.Generator(device=device)
+        self.gen.manual_seed(1234 + session.get_world_rank())
+
+    def load(self, train_ds, eval_ds, config):
+        fc, ft = config["feature_columns"], config["feature_types"]
+        lt = config.get("label_type") or torch.float32
+        self.train = _ShardTensors(train_ds, fc, ft, config["label_column"], lt, self.device)
+        self.eval = _ShardTensors(eval_ds, fc, ft, config["label_column"], lt, self.device) \
+            if eval_ds is not None else None
+
+    def _batches(self, data: _ShardTensors, shuffle: bool):
+        n = data.n
+        idx = torch.randperm(n, device=self.device, generator=self.gen) if shuffle else None
+        stop = n - n % self.batch if self.drop_last else n
+        for s in range(0, stop, self.batch):
+            if idx is not None:
+                sel = idx[s:s + self.batch]
+                feats = [f.index_select(0, sel) for f in data.feats]
+                lab = data.labels.index_select(0, sel)
+            else:
+                feats = [f[s:s + self.batch] for f in data.feats]
+                lab = data.labels[s:s + self.batch]
+            yield (feats if data.multi else feats[0]), lab
+
+    def train_epoch(self):
+        self.model.train()
+        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        nb = 0
+        for inputs, targets in self._batches(self.train, self.shuffle):
+            outputs = self.model(*inputs) if isinstance(inputs, list) else self.model(inputs)
+            loss = self.loss(outputs, targets)
+            total += loss.detach()
+            self.metrics.update(outputs, targets)
+            self.optimizer.zero_grad(set_to_none=True)
+            loss.backward()
+            self.optimizer.step()
+            if self.scheduler is not None:
+                self.scheduler.step()
+            nb += 1
+        res = self.metrics.compute()
+        self.metrics.reset()
+        return res, (total / max(nb, 1)).item()
+
+    @torch.no_grad()
+    def evaluate_epoch(self):
+        self.model.eval()
+        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        nb = 0
+        for inputs, targets in self._batches(self.eval, False):
+            outputs = self.model(*inputs) if isinstance(inputs, list) else self.model(inputs)
+            total += self.loss(outputs, targets).detach()
+            self.metrics.update(outputs, targets)
+            nb += 1
+        res = self.metrics.compute()
+        self.metrics.reset()
+        return res, (total / max(nb, 1)).item()
+
+    def state_dict(self):
+        return self.raw_model.state_dict()

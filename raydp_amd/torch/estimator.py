@@ -1,0 +1,263 @@
+"""``TorchEstimator``: scikit-learn style distributed PyTorch training on Spark DataFrames.
+
+API parity with ``python/raydp/torch/estimator.py`` (constructor kwargs :76-170,
+``fit`` :312-356, ``fit_on_spark`` :358-390, ``get_model`` :392-396, ``train_func`` :177-270):
+model instance or creator, optimizer instance (re-instantiated with ``lr=0.1`` then
+``load_state_dict``, :190-196) or creator, loss class/instance/creator, per-batch LR scheduler,
+per-epoch ``session.report`` dicts, rank-0 ``model.pt`` checkpoint.
+
+Differences by design (MI355X): the worker shard is ingested into HBM once and every epoch runs
+device-resident (fused HIP MLP trainer when the model allows it, otherwise a torch loop with
+on-device loss/metric accumulation); ``extra_config`` is honoured (``use_gpu``, ``shuffle_seed``)
+instead of being silently dropped (:163).
+"""
+import copy
+import inspect
+import os
+import tempfile
+from typing import Any, Callable, Dict, List, NoReturn, Optional, Union
+
+import torch
+from torch.nn.modules.loss import _Loss as TLoss
+
+from raydp_amd.estimator import EstimatorInterface
+from raydp_amd.spark.interfaces import DF, OPTIONAL_DF, SparkEstimatorInterface
+from raydp_amd.torch.config import TorchConfig
+from raydp_amd.torch.metrics import TorchMetric
+from raydp_amd.train import session
+from raydp_amd.train.checkpoint import Checkpoint, TorchCheckpoint
+from raydp_amd.train.config import FailureConfig, RunConfig, ScalingConfig
+from raydp_amd.train.trainer import TorchTrainer
+
+
+def _make_lr_schedule(opt_template: torch.optim.Optimizer, creator, config):
+    """Per-step learning rates of ``creator(optimizer, config)`` for the fused engine."""
+    dummy = torch.nn.Parameter(torch.zeros(1))
+    g = dict(opt_template.param_groups[0])
+    g.pop("params")
+    opt = type(opt_template)([dummy], **{k: v for k, v in g.items()
+                                         if k in inspect.signature(type(opt_template)).parameters})
+    sched = creator(opt, config)
+    cache: List[float] = []
+
+    def lr_at(t: int) -> float:
+        while len(cache) <= t:
+            cache.append(float(opt.param_groups[0]["lr"]))
+            opt.step()
+            sched.step()
+        return cache[t]
+    return lr_at
+
+
+class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
+    def __init__(self,
+                 num_workers: int = 1,
+                 resources_per_worker: Optional[Dict[str, float]] = None,
+                 model: Union[torch.nn.Module, Callable] = None,
+                 optimizer: Union[torch.optim.Optimizer, Callable] = None,
+                 loss: Union[TLoss, Callable] = None,
+                 lr_scheduler_creator: Optional[Callable] = None,
+                 scheduler_step_freq="batch",
+                 feature_columns: List[str] = None,
+                 feature_types: Optional[List[torch.dtype]] = None,
+                 label_column: str = None,
+                 label_type: Optional[torch.dtype] = None,
+                 batch_size: int = None,
+                 drop_last: bool = False,
+                 num_epochs: int = None,
+                 shuffle: bool = True,
+                 num_processes_for_data_loader: int = 0,
+                 placement_strategy="PACK",
+                 metrics_name: Optional[List[Union[str, Callable]]] = None,
+                 metrics_config: Optional[Dict[str, Dict[str, Any]]] = None,
+                 use_ccl: bool = False,
+                 **extra_config):
+        self._num_workers = num_workers
+        self._resources_per_worker = resources_per_worker
+        self._model = model
+        self._optimizer = optimizer
+        self._loss = loss
+        self._lr_scheduler_creator = lr_scheduler_creator
+        self._feature_columns = feature_columns
+        self._feature_types = feature_types
+        self._label_column = label_column
+        self._label_type = label_type
+        self._batch_size = batch_size
+        self._drop_last = drop_last
+        self._num_epochs = num_epochs
+        self._shuffle = shuffle
+        self._num_processes_for_data_loader = num_processes_for_data_loader
+        self._placement_strategy = placement_strategy
+        self._metrics = TorchMetric(metrics_name, metrics_config)
+        self._use_ccl = use_ccl
+        self._extra_config = extra_config
+        if self._num_processes_for_data_loader > 0:
+            raise TypeError("multiple processes for data loader has not supported")
+        self._trainer: Optional[TorchTrainer] = None
+        self._trained_results = None
+        self._check()
+
+    def _check(self):
+        assert self._model is not None, "Model must be provided"
+        assert self._optimizer is not None, "Optimizer must be provided"
+        assert self._loss is not None, "Loss must be provided"
+
+    # ------------------------------------------------------------------------- worker -----
+    @staticmethod
+    def train_func(config):
+        # model
+        if isinstance(config["model"], torch.nn.Module):
+            model = copy.deepcopy(config["model"])
+        elif callable(config["model"]):
+            model = config["model"](config)
+        else:
+            raise Exception("Unsupported parameter, we only support torch.nn.Model instance "
+                            "or a function(dict -> model)")
+        device = session.get_device() or torch.device("cpu")
+        model = model.to(device)
+        # optimizer (instance -> re-instantiate on this worker's parameters)
+        if isinstance(config["optimizer"], torch.optim.Optimizer):
+            optimizer_cls = config["optimizer"].__class__
+            state = config["optimizer"].state_dict()
+            optimizer = optimizer_cls(model.parameters(), lr=0.1)
+            optimizer.load_state_dict(state)
+        elif callable(config["optimizer"]):
+            optimizer = config["optimizer"](model, config)
+        else:
+            raise Exception("Unsupported parameter, we only support torch.optim.Optimizer subclass "
+                            "instance or a function((models, dict) -> optimizer)")
+        # loss
+        if inspect.isclass(config["loss"]) and issubclass(config["loss"], TLoss):
+            loss = config["loss"]()
+        elif isinstance(config["loss"], TLoss):
+            loss = config["loss"]
+        elif callable(config["loss"]):
+            loss = config["loss"](config)
+        else:
+            raise Exception("Unsupported parameter, we only support torch.nn.modules.loss._Loss "
+                            "subclass, subclass instance or a function(dict -> loss)")
+        metrics = copy.deepcopy(config["metrics"])
+
+        train_ds = session.get_dataset_shard("train")
+        eval_ds = session.get_dataset_shard("evaluate") if config["evaluate"] else None
+
+        from raydp_amd.torch.engine import FusedMLPEngine, TorchLoopEngine
+        engine = None
+        fused = None
+        if config.get("fused", True):
+            fused = FusedMLPEngine.applicable(model, optimizer, loss, metrics, device,
+                                              config["batch_size"], config["feature_columns"],
+                                              config["feature_types"])
+        if fused is not None:
+            spec, lc, oc = fused
+            lr_fn = None
+            if config["lr_scheduler_creator"]:
+                lr_fn = _make_lr_schedule(optimizer, config["lr_scheduler_creator"], config)
+            engine = FusedMLPEngine(model, optimizer, spec, lc, oc, metrics, device, config, lr_fn)
+        else:
+            sched = config["lr_scheduler_creator"](optimizer, config) if config["lr_scheduler_creator"] else None
+            engine = TorchLoopEngine(model, optimizer, loss, metrics, device, config, sched)
+        engine.load(train_ds, eval_ds, config)
+        config.setdefault("_engine_name", engine.name)
+        for epoch in range(config["num_epochs"]):
+            train_res, train_loss = engine.train_epoch()
+            session.report(dict(epoch=epoch, train_res=train_res, train_loss=train_loss,
+                                engine=engine.name))
+            if eval_ds is not None:
+                eval_res, test_loss = engine.evaluate_epoch()
+                session.report(dict(epoch=epoch, eval_res=eval_res, test_loss=test_loss))
+        states = engine.state_dict()
+        states = {k: v.detach().cpu() for k, v in states.items()}
+        with tempfile.TemporaryDirectory() as temp_checkpoint_dir:
+            checkpoint = None
+            if session.get_world_rank() == 0:
+                torch.save(states, os.path.join(temp_checkpoint_dir, "model.pt"))
+                checkpoint = Checkpoint.from_directory(temp_checkpoint_dir)
+            session.report({}, checkpoint=checkpoint)
+
+    # ------------------------------------------------------------------------- driver -----
+    def fit(self, train_ds, evaluate_ds=None, max_retries=3) -> NoReturn:
+        train_loop_config = {
+            "model": self._model,
+            "optimizer": self._optimizer,
+            "loss": self._loss,
+            "lr_scheduler_creator": self._lr_scheduler_creator,
+            "feature_columns": self._feature_columns,
+            "feature_types": self._feature_types,
+            "label_column": self._label_column,
+            "label_type": self._label_type,
+            "batch_size": self._batch_size,
+            "num_epochs": self._num_epochs,
+            "drop_last": self._drop_last,
+            "shuffle": self._shuffle,
+            "evaluate": True,
+            "metrics": self._metrics,
+            "fused": self._extra_config.get("fused", True),
+        }
+        use_gpu = self._extra_config.get("use_gpu")
+        if self._resources_per_worker and "GPU" in self._resources_per_worker:
+            use_gpu = self._resources_per_worker["GPU"] > 0
+        scaling_config = ScalingConfig(num_workers=self._num_workers, use_gpu=use_gpu,
+                                       resources_per_worker=self._resources_per_worker,
+                                       placement_strategy=self._placement_strategy)
+        run_config = RunConfig(failure_config=FailureConfig(max_failures=max_retries),
+                               storage_path=self._extra_config.get("storage_path"))
+        if self._shuffle:
+            seed = self._extra_config.get("shuffle_seed")
+            train_ds = train_ds.random_shuffle(seed=seed)
+            if evaluate_ds:
+                evaluate_ds = evaluate_ds.random_shuffle(seed=seed)
+        datasets = {"train": train_ds}
+        if evaluate_ds is None:
+            train_loop_config["evaluate"] = False
+        else:
+            datasets["evaluate"] = evaluate_ds
+        torch_config = TorchConfig(backend="ccl") if self._use_ccl else None
+        self._trainer = TorchTrainer(TorchEstimator.train_func,
+                                     train_loop_config=train_loop_config,
+                                     scaling_config=scaling_config,
+                                     run_config=run_config,
+                                     torch_config=torch_config,
+                                     datasets=datasets,
+                                     local_shards=bool(self._extra_config.get("spmd_local_shards")))
+        self._trained_results = self._trainer.fit()
+        return self._trained_results
+
+    def fit_on_spark(self, train_df: DF, evaluate_df: OPTIONAL_DF = None, max_retries=3,
+                     fs_directory: Optional[str] = None, compression: Optional[str] = None,
+                     stop_spark_after_conversion=False):
+        super().fit_on_spark(train_df, evaluate_df)
+        train_df = self._check_and_convert(train_df)
+        evaluate_ds = None
+        if fs_directory is not None:
+            from raydp_amd.spark.dataset import read_spark_parquet
+            app_id = train_df.sparkSession.sparkContext.applicationId
+            path = fs_directory.rstrip("/") + f"/{app_id}"
+            train_df.write.parquet(path + "/train", compression=compression)
+            train_ds = read_spark_parquet(path + "/train")
+            if evaluate_df is not None:
+                evaluate_df = self._check_and_convert(evaluate_df)
+                evaluate_df.write.parquet(path + "/test", compression=compression)
+                evaluate_ds = read_spark_parquet(path + "/test")
+        else:
+            from raydp_amd.spark.dataset import (get_raydp_master_owner,
+                                                 spark_dataframe_to_ray_dataset)
+            owner = None
+            if stop_spark_after_conversion:
+                owner = get_raydp_master_owner(train_df.sparkSession)
+            train_ds = spark_dataframe_to_ray_dataset(train_df, owner=owner)
+            if evaluate_df is not None:
+                evaluate_df = self._check_and_convert(evaluate_df)
+                evaluate_ds = spark_dataframe_to_ray_dataset(evaluate_df, owner=owner)
+        if stop_spark_after_conversion:
+            from raydp_amd.context import stop_spark
+            stop_spark(cleanup_data=False)
+        return self.fit(train_ds, evaluate_ds, max_retries)
+
+    def get_model(self):
+        assert self._trainer is not None, "Must call fit first"
+        return TorchCheckpoint(self._trained_results.checkpoint.to_directory()).get_model(self._model)
+
+    @property
+    def results(self):
+        return self._trained_results

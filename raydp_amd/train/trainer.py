@@ -1,0 +1,291 @@
+"""Worker-group trainer (Ray Train ``TorchTrainer`` equivalent), one process per GPU.
+
+``TorchTrainer.fit()`` runs ``train_loop_per_worker(config)`` on ``num_workers`` ranks joined
+by ``torch.distributed`` — backend ``"nccl"`` (= RCCL over xGMI on ROCm) when the workers own
+GPUs, Gloo otherwise — with datasets split into equal row shards (equal shards keep every rank
+on the same step count, so collectives never deadlock). Three launch modes:
+
+* **in-process** — ``num_workers == 1``: the loop runs in the caller (no fork cost).
+* **SPMD** — the caller already is one rank of a ``torchrun`` job (``WORLD_SIZE`` env matches):
+  every process runs its own rank in-process; this is how ``bench.py`` scales to 8 GPUs.
+* **spawned** — otherwise ``num_workers`` child processes are started (spawn context), each
+  pinned to ``cuda:<local_rank>`` when GPUs are used.
+
+Failures restart the whole group up to ``FailureConfig.max_failures`` times (reference:
+``RunConfig(failure_config=FailureConfig(max_failures=max_retries))`` at
+``python/raydp/torch/estimator.py:334``).
+"""
+import os
+import pickle
+import shutil
+import socket
+import tempfile
+import time
+import traceback
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+from raydp_amd.train import session as S
+from raydp_amd.train.checkpoint import Checkpoint
+from raydp_amd.train.config import FailureConfig, RunConfig, ScalingConfig
+
+
+class TrainingFailedError(RuntimeError):
+    pass
+
+
+@dataclass
+class Result:
+    metrics: Dict[str, Any]
+    checkpoint: Optional[Checkpoint]
+    path: str
+    error: Optional[BaseException] = None
+    metrics_history: List[Dict[str, Any]] = field(default_factory=list)
+
+    @property
+    def metrics_dataframe(self):
+        import pandas as pd
+        return pd.DataFrame(self.metrics_history)
+
+    @property
+    def best_checkpoints(self):
+        return [(self.checkpoint, self.metrics)] if self.checkpoint else []
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cuda_available() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def _shard(datasets: Dict[str, Any], rank: int, world: int) -> Dict[str, Any]:
+    if not datasets:
+        return {}
+    out = {}
+    for k, ds in datasets.items():
+        out[k] = ds if world == 1 else ds.split(world, equal=True)[rank]
+    return out
+
+
+def _init_dist(backend: str, rank: int, world: int, addr: str, port: int):
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return False
+    dist.init_process_group(backend, init_method=f"tcp://{addr}:{port}", rank=rank,
+                            world_size=world)
+    return True
+
+
+def _worker_entry(rank, world, port, payload, queue):
+    """Child-process entry of a spawned worker group."""
+    import cloudpickle
+    try:
+        fn, config, shards, use_gpu, storage, name = cloudpickle.loads(payload)
+        import torch
+        device = torch.device("cpu")
+        if use_gpu:
+            n = torch.cuda.device_count()
+            torch.cuda.set_device(rank % n)
+            device = torch.device("cuda", rank % n)
+        backend = "nccl" if use_gpu else "gloo"
+        _init_dist(backend, rank, world, "127.0.0.1", port)
+
+        def reporter(r, metrics, ckpt):
+            queue.put(("report", r, metrics, ckpt))
+        ctx = S.TrainContext(rank, world, rank, world, 0, device, name, storage)
+        S._set_session(S._Session(ctx, shards, reporter, storage))
+        fn(config) if _accepts_arg(fn) else fn()
+        queue.put(("done", rank, None, None))
+    except BaseException as e:  # noqa: BLE001
+        queue.put(("error", rank, traceback.format_exc(), None))
+        raise
+    finally:
+        try:
+            import torch.distributed as dist
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def _accepts_arg(fn) -> bool:
+    import inspect
+    try:
+        return len(inspect.signature(fn).parameters) >= 1
+    except (TypeError, ValueError):
+        return True
+
+
+class DataParallelTrainer:
+    backend_default = "gloo"
+
+    def __init__(self, train_loop_per_worker: Callable, *, train_loop_config: Optional[dict] = None,
+                 scaling_config: Optional[ScalingConfig] = None, run_config: Optional[RunConfig] = None,
+                 datasets: Optional[Dict[str, Any]] = None, torch_config=None,
+                 resume_from_checkpoint: Optional[Checkpoint] = None,
+                 local_shards: bool = False, **kw):
+        self.fn = train_loop_per_worker
+        self.config = train_loop_config or {}
+        self.scaling = scaling_config or ScalingConfig()
+        self.run_config = run_config or RunConfig()
+        self.datasets = datasets or {}
+        self.torch_config = torch_config
+        self.resume = resume_from_checkpoint
+        # SPMD jobs (torchrun) may pass each rank's own data: do not split it again
+        self.local_shards = local_shards
+
+    # ------------------------------------------------------------------------------------
+    def _use_gpu(self) -> bool:
+        if self.scaling.use_gpu is not None:
+            return bool(self.scaling.use_gpu) and _cuda_available()
+        r = self.scaling.resources_per_worker or {}
+        if "GPU" in r:
+            return float(r["GPU"]) > 0 and _cuda_available()
+        return _cuda_available()
+
+    def _storage(self) -> str:
+        base = self.run_config.storage_path or os.path.join(tempfile.gettempdir(), "raydp_results")
+        if base.startswith("file://"):
+            base = base[len("file://"):]
+        name = self.run_config.name or f"TorchTrainer_{time.strftime('%Y-%m-%d_%H-%M-%S')}_{os.getpid()}"
+        path = os.path.join(base, name)
+        os.makedirs(path, exist_ok=True)
+        return path
+
+    def fit(self) -> Result:
+        failures = 0
+        max_f = self.run_config.failure_config.max_failures
+        last_err = None
+        while True:
+            try:
+                return self._fit_once()
+            except _WorkerFailure as e:
+                last_err = e
+                failures += 1
+                if max_f >= 0 and failures > max_f:
+                    raise TrainingFailedError(f"training failed after {failures} attempt(s):\n{e}") from None
+
+    def _fit_once(self) -> Result:
+        world = int(self.scaling.num_workers)
+        storage = self._storage()
+        use_gpu = self._use_gpu()
+        history: List[Dict[str, Any]] = []
+        ckpts: List[str] = []
+
+        def reporter(rank, metrics, ckpt):
+            if rank == 0:
+                history.append(metrics)
+            if ckpt:
+                ckpts.append(ckpt)
+
+        env_world = int(os.environ.get("WORLD_SIZE", "1"))
+        if world == 1 or (env_world == world and "RANK" in os.environ):
+            self._run_inprocess(world, env_world, use_gpu, storage, reporter)
+        else:
+            self._run_spawned(world, use_gpu, storage, reporter)
+        ck = Checkpoint(ckpts[-1]) if ckpts else None
+        return Result(metrics=history[-1] if history else {}, checkpoint=ck, path=storage,
+                      metrics_history=history)
+
+    def _run_inprocess(self, world, env_world, use_gpu, storage, reporter):
+        import torch
+        if world > 1:
+            rank = int(os.environ["RANK"])
+            local = int(os.environ.get("LOCAL_RANK", rank))
+        else:
+            rank, local = 0, 0
+        device = torch.device("cpu")
+        if use_gpu:
+            n = torch.cuda.device_count()
+            torch.cuda.set_device(local % n)
+            device = torch.device("cuda", local % n)
+        created = False
+        if world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                dist.init_process_group("nccl" if use_gpu else "gloo")
+                created = True
+        shards = dict(self.datasets) if self.local_shards else _shard(self.datasets, rank, world)
+        ctx = S.TrainContext(rank, world, local, world, 0, device, "raydp", storage)
+        sess = S._Session(ctx, shards, reporter, storage, self.resume)
+        S._set_session(sess)
+        try:
+            self.fn(self.config) if _accepts_arg(self.fn) else self.fn()
+        except Exception as e:  # noqa: BLE001
+            raise _WorkerFailure(traceback.format_exc()) from e
+        finally:
+            S._set_session(None)
+            if created:
+                import torch.distributed as dist
+                dist.destroy_process_group()
+
+    def _run_spawned(self, world, use_gpu, storage, reporter):
+        import multiprocessing as mp
+        import cloudpickle
+        ctx = mp.get_context("spawn")
+        queue = ctx.Queue()
+        port = _free_port()
+        procs = []
+        for r in range(world):
+            shards = _shard(self.datasets, r, world)
+            for ds in shards.values():
+                if hasattr(ds, "materialize"):
+                    ds.materialize()
+            payload = cloudpickle.dumps((self.fn, self.config, shards, use_gpu, storage, "raydp"))
+            p = ctx.Process(target=_worker_entry, args=(r, world, port, payload, queue), daemon=True)
+            p.start()
+            procs.append(p)
+        done = set()
+        error = None
+        while len(done) < world and error is None:
+            try:
+                kind, rank, a, b = queue.get(timeout=1.0)
+            except Exception:  # noqa: BLE001 - queue.Empty
+                dead = [p for p in procs if not p.is_alive() and p.exitcode not in (0, None)]
+                if dead:
+                    error = f"worker process exited with code {dead[0].exitcode}"
+                continue
+            if kind == "report":
+                reporter(rank, a, b)
+            elif kind == "done":
+                done.add(rank)
+            elif kind == "error":
+                error = a
+        for p in procs:
+            if error is not None and p.is_alive():
+                p.terminate()
+            p.join(timeout=30)
+        if error is not None:
+            raise _WorkerFailure(error)
+
+
+class _WorkerFailure(Exception):
+    pass
+
+
+class TorchTrainer(DataParallelTrainer):
+    pass
+
+
+def prepare_model(model, move_to_device=True, parallel_strategy="ddp"):
+    """``ray.train.torch.prepare_model``: move to the worker device, wrap in DDP if world>1."""
+    import torch
+    import torch.distributed as dist
+    ctx = S.get_context()
+    dev = ctx.device or torch.device("cpu")
+    if move_to_device:
+        model = model.to(dev)
+    if ctx.world_size > 1 and dist.is_initialized():
+        from raydp_amd.parallel.ddp import DistributedDataParallel
+        model = DistributedDataParallel(model)
+    return model

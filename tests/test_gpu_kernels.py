@@ -1,0 +1,225 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references."""
+import copy
+
+import numpy as np
+import pyarrow as pa
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+class NYC(nn.Module):
+    def __init__(self, cols=20):
+        super().__init__()
+        self.fc1 = nn.Linear(cols, 256)
+        self.fc2 = nn.Linear(256, 128)
+        self.fc3 = nn.Linear(128, 64)
+        self.fc4 = nn.Linear(64, 16)
+        self.fc5 = nn.Linear(16, 1)
+        self.bn1 = nn.BatchNorm1d(256)
+        self.bn2 = nn.BatchNorm1d(128)
+        self.bn3 = nn.BatchNorm1d(64)
+        self.bn4 = nn.BatchNorm1d(16)
+
+    def forward(self, x):
+        x = self.bn1(F.relu(self.fc1(x)))
+        x = self.bn2(F.relu(self.fc2(x)))
+        x = self.bn3(F.relu(self.fc3(x)))
+        x = self.bn4(F.relu(self.fc4(x)))
+        return self.fc5(x)
+
+
+class BnFirst(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(13, 64), nn.BatchNorm1d(64), nn.ReLU(),
+                                 nn.Linear(64, 48), nn.ReLU(), nn.Linear(48, 3))
+
+    def forward(self, x):
+        return self.net(x)
+
+
+def _relerr(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def _setup(model, loss, opt_cls, batch, n_rows, in_f, out_f, seed=0, **opt_kw):
+    from raydp_amd.models.mlp_spec import extract_mlp_spec
+    from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+    torch.manual_seed(seed)
+    dev = torch.device("cuda")
+    ref = copy.deepcopy(model).to(dev)
+    opt = opt_cls(model.parameters(), **opt_kw)
+    spec = extract_mlp_spec(model)
+    assert spec is not None
+    tr = FusedMLPTrainer(spec, optimizer_config(opt), loss_code(loss), batch, dev)
+    X = torch.randn(n_rows, in_f) * 2.0
+    Y = torch.randn(n_rows, out_f) * 3.0 + 1.0
+    feats = torch.zeros(n_rows, tr.feat_k, dtype=torch.bfloat16)
+    feats[:, :in_f] = X.to(torch.bfloat16)
+    return tr, ref, opt_cls(ref.parameters(), **opt_kw), feats.to(dev), Y.to(dev), X.to(dev)
+
+
+@pytest.mark.parametrize("nvalid", [64, 38])
+@pytest.mark.parametrize("loss", [nn.SmoothL1Loss(), nn.MSELoss(), nn.L1Loss()])
+def test_fused_mlp_one_step_matches_torch(nvalid, loss):
+    model = NYC()
+    tr, ref, ropt, feats, Y, X = _setup(model, loss, torch.optim.Adam, 64, nvalid, 20, 1, lr=1e-3)
+    g = tr.forward_backward(feats, Y, nvalid).clone()
+    m = tr._read_metrics()
+    # fp32 reference on the bf16-rounded inputs
+    ref.train()
+    xin = X.to(torch.bfloat16).float()
+    out = ref(xin)
+    l = loss(out, Y)
+    l.backward()
+    assert abs(m["loss"] - l.item()) / max(abs(l.item()), 1e-6) < 3e-2
+    gmap = tr.unflatten(g)
+    rmods = dict(ref.named_modules())
+    for name, mod in model.named_modules():
+        for attr in ("weight", "bias"):
+            key = (id(mod), attr)
+            if key in gmap:
+                rg = getattr(rmods[name], attr).grad
+                err = _relerr(gmap[key], rg)
+                assert err < 5e-2, (name, attr, err)
+    # optimizer step + BN running stats
+    tr.metrics.zero_()
+    rc = tr.lib.rx_opt_step(
+        __import__("ctypes").byref(tr.opt), *[__import__("ctypes").c_void_p(t.data_ptr())
+                                               for t in (tr.params, tr.grads, tr.m, tr.v)],
+        __import__("ctypes").c_float(1e-3), __import__("ctypes").c_float(1 - 0.9),
+        __import__("ctypes").c_float(1 - 0.999), __import__("ctypes").c_float(1.0), 1,
+        __import__("raydp_amd.ops._hip", fromlist=["x"]).stream_ptr())
+    assert rc == 0
+    ropt.step()
+    pmap = tr.unflatten(tr.params)
+    for name, mod in model.named_modules():
+        for attr in ("weight", "bias"):
+            key = (id(mod), attr)
+            if key in pmap:
+                err = _relerr(pmap[key], getattr(rmods[name], attr).data)
+                assert err < 1e-2, (name, attr, err)
+    for bn, rm, rv in tr.run_bufs:
+        name = [n for n, mm in model.named_modules() if mm is bn][0]
+        assert _relerr(rm, rmods[name].running_mean) < 3e-2
+        assert _relerr(rv, rmods[name].running_var) < 3e-2
+
+
+def test_fused_mlp_bn_before_relu_sgd_momentum():
+    model = BnFirst()
+    tr, ref, ropt, feats, Y, X = _setup(model, nn.MSELoss(), torch.optim.SGD, 32, 29, 13, 3,
+                                        lr=0.05, momentum=0.9)
+    g = tr.forward_backward(feats, Y, 29).clone()
+    ref.train()
+    out = ref(X.to(torch.bfloat16).float())
+    nn.MSELoss()(out, Y).backward()
+    gmap = tr.unflatten(g)
+    rmods = dict(ref.named_modules())
+    for name, mod in model.named_modules():
+        for attr in ("weight", "bias"):
+            key = (id(mod), attr)
+            if key in gmap:
+                err = _relerr(gmap[key], getattr(rmods[name], attr).grad)
+                assert err < 5e-2, (name, attr, err)
+
+
+def test_fused_mlp_training_converges_like_torch():
+    torch.manual_seed(3)
+    n = 2048
+    X = torch.randn(n, 20)
+    w = torch.randn(20, 1)
+    Y = X @ w + 0.5 * torch.sin(X[:, :1] * 3)
+    model = NYC()
+    from raydp_amd.models.mlp_spec import extract_mlp_spec
+    from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+    dev = torch.device("cuda")
+    ref = copy.deepcopy(model).to(dev)
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    tr = FusedMLPTrainer(extract_mlp_spec(model),
+                         optimizer_config(torch.optim.Adam(model.parameters(), lr=1e-3)),
+                         loss_code(nn.MSELoss()), 64, dev)
+    feats = torch.zeros(n, tr.feat_k, dtype=torch.bfloat16)
+    feats[:, :20] = X.to(torch.bfloat16)
+    feats, Yd = feats.to(dev), Y.to(dev)
+    for ep in range(5):
+        m = tr.train_epoch(feats, Yd, n, None)
+        ref.train()
+        tot = 0.0
+        for s in range(0, n, 64):
+            out = ref(X[s:s + 64].to(dev).to(torch.bfloat16).float())
+            l = F.mse_loss(out, Yd[s:s + 64])
+            ropt.zero_grad()
+            l.backward()
+            ropt.step()
+            tot += l.item()
+        rl = tot / (n // 64)
+    assert m["loss"] < 0.5 * F.mse_loss(torch.zeros_like(Y), Y).item()
+    assert abs(m["loss"] - rl) / rl < 0.35, (m["loss"], rl)
+    ev = tr.evaluate(feats, Yd, n)
+    ref.eval()
+    with torch.no_grad():
+        tr.write_back()
+    assert np.isfinite(ev["loss"])
+
+
+def test_arrow_ingest_matches_numpy():
+    from raydp_amd.ops.ingest import ingest_columns
+    rng = np.random.default_rng(0)
+    n = 1000
+    t = pa.table({
+        "a": pa.array(rng.standard_normal(n)),
+        "b": pa.array(rng.integers(-50, 50, n).astype(np.int32)),
+        "c": pa.array([None if i % 7 == 0 else float(i) for i in range(n)], pa.float32()),
+        "d": pa.array(rng.integers(0, 2, n).astype(bool)),
+        "e": pa.array(rng.integers(-3, 3, n).astype(np.int64)),
+    })
+    sl = t.slice(13, 700)
+    for out_bf16 in (False, True):
+        got = ingest_columns([sl, t.slice(0, 5)], ["a", "b", "c", "d", "e"], "cuda", out_bf16,
+                             stride=8, fill=-1.0).float().cpu().numpy()
+        exp = np.zeros((705, 8), np.float32)
+        for tab, r0 in ((sl, 0), (t.slice(0, 5), 700)):
+            for j, c in enumerate("abcde"):
+                v = tab.column(c).to_pandas().to_numpy(dtype=np.float64, na_value=-1.0)
+                exp[r0:r0 + tab.num_rows, j] = v
+        tol = 1e-2 if out_bf16 else 1e-6
+        np.testing.assert_allclose(got, exp, rtol=tol, atol=tol)
+
+
+def test_estimator_uses_fused_engine_on_gpu():
+    import os
+    import raydp_amd
+    from raydp_amd import runtime
+    from raydp_amd.torch import TorchEstimator
+    from data_process import nyc_taxi_preprocess
+    runtime.shutdown()
+    runtime.init(num_cpus=4)
+    try:
+        spark = raydp_amd.init_spark("gpu-est", 1, 2, "500M")
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        df = spark.read.format("csv").option("header", "true").option("inferSchema", "true") \
+            .load(os.path.join(root, "examples", "data", "fake_nyctaxi.csv"))
+        df = nyc_taxi_preprocess(df)
+        tr, te = df.randomSplit([0.9, 0.1], 0)
+        feats = [c for c in tr.columns if c != "fare_amount"]
+        model = NYC(len(feats))
+        est = TorchEstimator(num_workers=1, model=model,
+                             optimizer=torch.optim.Adam(model.parameters(), lr=1e-3),
+                             loss=nn.SmoothL1Loss(), feature_columns=feats, feature_types=torch.float,
+                             label_column="fare_amount", label_type=torch.float, batch_size=64,
+                             num_epochs=4, metrics_name=["MeanAbsoluteError", "MeanSquaredError"])
+        est.fit_on_spark(tr, te)
+        hist = est.results.metrics_history
+        assert hist[0]["engine"] == "fused_mlp_hip"
+        losses = [h["train_loss"] for h in hist if "train_loss" in h]
+        assert losses[-1] < losses[0]
+        m = est.get_model()
+        assert m(torch.randn(4, len(feats))).shape == (4, 1)
+    finally:
+        raydp_amd.stop_spark()
+        runtime.shutdown()
