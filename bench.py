@@ -161,6 +161,7 @@ def main():
     samples = args.steps * BATCH * world
     value = samples / dt
     engine = res.metrics_history[0].get("engine") if res.metrics_history else None
+    from raydp_amd.torch.estimator import LAST_TIMINGS
     if rank == 0:
         out = {
             "metric": "end-to-end samples/sec (Spark ETL+train) NYCTaxi TorchEstimator",
@@ -181,7 +182,8 @@ def main():
                        "engine": engine,
                        "timed_region": "csv read+ETL+from_spark+shuffle+HBM ingest+train+checkpoint",
                        "final_train_loss": res.metrics_history[0].get("train_loss")
-                       if res.metrics_history else None},
+                       if res.metrics_history else None,
+                       "rank0_breakdown_s": {k: round(v, 4) for k, v in LAST_TIMINGS.items()}},
         }
         print(json.dumps(out), flush=True)
     context.stop_spark()

@@ -64,6 +64,37 @@ struct Tile {
 
 __device__ __forceinline__ float act_fwd(int act, float z) { return act == 1 ? fmaxf(z, 0.f) : z; }
 
+// C[Bpad x 16-col tile n] += A (LDS, row-major, K contiguous) x Bt (global bf16, [n][K]).
+// The weight fragments of up to KC k-steps are fetched in ONE burst of unconditional
+// (address-clamped) 16-B loads before any MFMA consumes them, so a layer costs one global
+// round trip per 16-column tile instead of one per 32-deep k-step: the step is latency bound
+// and the weights arrive from the Infinity Cache / another XCD's L2 after each optimizer step.
+template <int MT>
+__device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
+                                          const u16* __restrict__ Brow, int K, int lg) {
+  constexpr int KC = 8;
+  const int nks = K >> 5;
+  for (int kc = 0; kc < nks; kc += KC) {
+    bf16x8 bfr[KC];
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      const int ks = min(kc + s, nks - 1);
+      bfr[s] = *reinterpret_cast<const bf16x8*>(Brow + ks * 32 + 8 * lg);
+    }
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      if (kc + s < nks) {
+        const int k0 = (kc + s) * 32 + 8 * lg;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(Arow + mt * 16 * RS + k0);
+          acc[mt] = rx_mfma16(a, bfr[s], acc[mt]);
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // forward of layer l for the rows of this workgroup. Leaves y (the layer output after
 // act/BN) in R (row-major) and in XT_{l+1}; for the last layer computes loss, metrics and
@@ -87,174 +118,147 @@ __device__ void layer_forward(const MlpDesc& d, int l, char* smem, const float* 
 
   f32x4 acc[T::NTW * MT];
 #pragma unroll
-  for (int i = 0; i < T::NTW * MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int k0 = 0; k0 < ly.in_k; k0 += 32) {
+  for (int j = 0; j < T::NTW; ++j) {
+    f32x4 part[MT];
 #pragma unroll
-    for (int j = 0; j < T::NTW; ++j) {
-      const int n = wave + j * RX_NW;
-      if (n < ntiles) {
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(ly.W + (n * 16 + lr) * ly.in_k + k0 + 8 * lg);
+    for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int n = wave + j * RX_NW;
+    if (n < ntiles) gemm_tile<MT>(part, R + lr * RS, RS, ly.W + (n * 16 + lr) * ly.in_k, ly.in_k, lg);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(R + (mt * 16 + lr) * RS + k0 + 8 * lg);
-          acc[j * MT + mt] = rx_mfma16(a, b, acc[j * MT + mt]);
-        }
-      }
-    }
+    for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
 
-  // ---- epilogue in registers: bias, act, BN (train: batch stats; eval: running stats) ----
-  float y[T::NTW * MT * 4];
-  float gsum[T::NTW];  // last layer: db (column sums of dL/dy)
+  // ---- epilogue in registers, in place on acc: bias, act, BN, loss ----
 #pragma unroll
   for (int j = 0; j < T::NTW; ++j) {
-    gsum[j] = 0.f;
     const int n = wave + j * RX_NW;
-    const int c = n * 16 + lr;
-    const bool colok = (n < ntiles) && (c < ly.out);
-    const float bias = (colok && ly.b_off >= 0) ? P[ly.b_off + c] : 0.f;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float z = acc[j * MT + mt][r] + bias;
-        y[(j * MT + mt) * 4 + r] = z;
-      }
-    if (n >= ntiles) continue;
-    if (ly.bn == 0) {
-#pragma unroll
-      for (int q = 0; q < MT * 4; ++q) y[j * MT * 4 + q] = act_fwd(ly.act, y[j * MT * 4 + q]);
-    } else {
-      if (ly.bn == 1) {
-#pragma unroll
-        for (int q = 0; q < MT * 4; ++q) y[j * MT * 4 + q] = act_fwd(ly.act, y[j * MT * 4 + q]);
-      }
-      float mean, invstd;
-      if (TRAIN) {
-        float s = 0.f;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = mt * 16 + lg * 4 + r;
-            s += (row < nvalid) ? y[(j * MT + mt) * 4 + r] : 0.f;
-          }
-        s = rx_colsum16(s);
-        mean = s / (float)nvalid;
-        float v = 0.f;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = mt * 16 + lg * 4 + r;
-            const float dv = y[(j * MT + mt) * 4 + r] - mean;
-            v += (row < nvalid) ? dv * dv : 0.f;
-          }
-        v = rx_colsum16(v);
-        const float var = v / (float)nvalid;
-        invstd = rsqrtf(var + ly.eps);
-        if (colok && lg == 0) {
-          stats[ly.stat_off + 2 * c] = mean;
-          stats[ly.stat_off + 2 * c + 1] = invstd;
-          const float unb = nvalid > 1 ? var * (float)nvalid / (float)(nvalid - 1) : var;
-          ly.run_mean[c] = (1.f - ly.momentum) * ly.run_mean[c] + ly.momentum * mean;
-          ly.run_var[c] = (1.f - ly.momentum) * ly.run_var[c] + ly.momentum * unb;
-        }
-        // save the BN input for the backward pass (thread-private slots)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = mt * 16 + lg * 4 + r;
-            scratch[ly.r_off + row * ly.out_n + c] = y[(j * MT + mt) * 4 + r];
-          }
-      } else {
-        mean = colok ? ly.run_mean[c] : 0.f;
-        invstd = colok ? rsqrtf(ly.run_var[c] + ly.eps) : 0.f;
-      }
-      const float gam = (colok && ly.g_off >= 0) ? P[ly.g_off + c] : 1.f;
-      const float bet = (colok && ly.be_off >= 0) ? P[ly.be_off + c] : 0.f;
-#pragma unroll
-      for (int q = 0; q < MT * 4; ++q) {
-        float t = (y[j * MT * 4 + q] - mean) * invstd * gam + bet;
-        if (ly.bn == 2) t = act_fwd(ly.act, t);
-        y[j * MT * 4 + q] = t;
-      }
-    }
-    if (!colok) {
-#pragma unroll
-      for (int q = 0; q < MT * 4; ++q) y[j * MT * 4 + q] = 0.f;
-    }
-    if (TRAIN && ly.bn == 0 && !last) {
-      // ReLU mask source for the backward pass
+    if (n < ntiles) {
+      const int c = n * 16 + lr;
+      const bool colok = c < ly.out;
+      const float bias = (colok && ly.b_off >= 0) ? P[ly.b_off + c] : 0.f;
+      const bool act_first = ly.bn != 2;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = mt * 16 + lg * 4 + r;
-          scratch[ly.r_off + row * ly.out_n + c] = y[(j * MT + mt) * 4 + r];
+          const float z = acc[j * MT + mt][r] + bias;
+          acc[j * MT + mt][r] = act_first ? act_fwd(ly.act, z) : z;
         }
-    }
-    // padded rows carry exact zeros through every GEMM
+      if (ly.bn != 0) {
+        float mean, invstd;
+        if (TRAIN) {
+          float s = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+          for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = mt * 16 + lg * 4 + r;
-        if (row >= nvalid) y[(j * MT + mt) * 4 + r] = 0.f;
-      }
-    if (last) {
-      // loss, metrics and dL/dy (mean reduction over nvalid * out_dim elements)
-      float lsum = 0.f, asum = 0.f, ssum = 0.f;
-      const float inv_n = 1.f / (float)(nvalid * ly.out);
+            for (int r = 0; r < 4; ++r)
+              s += (mt * 16 + lg * 4 + r < nvalid) ? acc[j * MT + mt][r] : 0.f;
+          s = rx_colsum16(s);
+          mean = s / (float)nvalid;
+          float v = 0.f;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+          for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mt * 16 + lg * 4 + r;
-          float g = 0.f;
-          if (colok && row < nvalid) {
-            const float t = labels[rowidx[row] * d.out_dim + c];
-            const float e = y[(j * MT + mt) * 4 + r] - t;
-            const float ae = fabsf(e);
-            asum += ae;
-            ssum += e * e;
-            if (d.loss == 0) {
-              lsum += e * e;
-              g = 2.f * e;
-            } else if (d.loss == 1) {
-              if (ae < d.beta) {
-                lsum += 0.5f * e * e / d.beta;
-                g = e / d.beta;
-              } else {
-                lsum += ae - 0.5f * d.beta;
-                g = e > 0.f ? 1.f : -1.f;
-              }
-            } else {
-              lsum += ae;
-              g = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+            for (int r = 0; r < 4; ++r) {
+              const float dv = acc[j * MT + mt][r] - mean;
+              v += (mt * 16 + lg * 4 + r < nvalid) ? dv * dv : 0.f;
             }
-            g *= inv_n;
+          v = rx_colsum16(v);
+          const float var = v / (float)nvalid;
+          invstd = rsqrtf(var + ly.eps);
+          if (colok && lg == 0) {
+            stats[ly.stat_off + 2 * c] = mean;
+            stats[ly.stat_off + 2 * c + 1] = invstd;
+            const float unb = nvalid > 1 ? var * (float)nvalid / (float)(nvalid - 1) : var;
+            ly.run_mean[c] = (1.f - ly.momentum) * ly.run_mean[c] + ly.momentum * mean;
+            ly.run_var[c] = (1.f - ly.momentum) * ly.run_var[c] + ly.momentum * unb;
           }
-          y[(j * MT + mt) * 4 + r] = g;  // y now holds G_{L-1}
-          gsum[j] += g;
+          // save the BN input for the backward pass (thread-private slots)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              scratch[ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c] = acc[j * MT + mt][r];
+        } else {
+          mean = colok ? ly.run_mean[c] : 0.f;
+          invstd = colok ? rsqrtf(ly.run_var[c] + ly.eps) : 0.f;
         }
-      lsum = rx_wavesum(lsum);
-      asum = rx_wavesum(asum);
-      ssum = rx_wavesum(ssum);
-      if (lane == 0) {
-        atomicAdd(&metrics[0], (double)(lsum * inv_n));
-        atomicAdd(&metrics[1], (double)asum);
-        atomicAdd(&metrics[2], (double)ssum);
-        if (n == 0) {
-          atomicAdd(&metrics[3], (double)(nvalid * ly.out));
-          atomicAdd(&metrics[4], 1.0);
-        }
+        const float gam = (colok && ly.g_off >= 0) ? P[ly.g_off + c] : 1.f;
+        const float bet = (colok && ly.be_off >= 0) ? P[ly.be_off + c] : 0.f;
+        const bool act_after = ly.bn == 2;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float t = (acc[j * MT + mt][r] - mean) * invstd * gam + bet;
+            acc[j * MT + mt][r] = act_after ? act_fwd(ly.act, t) : t;
+          }
+      } else if (TRAIN && !last) {
+        // ReLU mask source for the backward pass
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            scratch[ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c] = colok ? acc[j * MT + mt][r] : 0.f;
       }
-      if (TRAIN) {
-        gsum[j] = rx_colsum16(gsum[j]);
-        if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum[j];
+      // padded rows / columns carry exact zeros through every GEMM
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (!colok || mt * 16 + lg * 4 + r >= nvalid) acc[j * MT + mt][r] = 0.f;
+      if (last) {
+        // loss, metrics and dL/dy (mean reduction over nvalid * out_dim elements)
+        float lsum = 0.f, asum = 0.f, ssum = 0.f, gsum = 0.f;
+        const float inv_n = 1.f / (float)(nvalid * ly.out);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = mt * 16 + lg * 4 + r;
+            float g = 0.f;
+            if (colok && row < nvalid) {
+              const float t = labels[rowidx[row] * d.out_dim + c];
+              const float e = acc[j * MT + mt][r] - t;
+              const float ae = fabsf(e);
+              asum += ae;
+              ssum += e * e;
+              if (d.loss == 0) {
+                lsum += e * e;
+                g = 2.f * e;
+              } else if (d.loss == 1) {
+                if (ae < d.beta) {
+                  lsum += 0.5f * e * e / d.beta;
+                  g = e / d.beta;
+                } else {
+                  lsum += ae - 0.5f * d.beta;
+                  g = e > 0.f ? 1.f : -1.f;
+                }
+              } else {
+                lsum += ae;
+                g = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+              }
+              g *= inv_n;
+            }
+            acc[j * MT + mt][r] = g;  // acc now holds G_{L-1}
+            gsum += g;
+          }
+        lsum = rx_wavesum(lsum);
+        asum = rx_wavesum(asum);
+        ssum = rx_wavesum(ssum);
+        if (lane == 0) {
+          atomicAdd(&metrics[0], (double)(lsum * inv_n));
+          atomicAdd(&metrics[1], (double)asum);
+          atomicAdd(&metrics[2], (double)ssum);
+          if (n == 0) {
+            atomicAdd(&metrics[3], (double)(nvalid * ly.out));
+            atomicAdd(&metrics[4], 1.0);
+          }
+        }
+        if (TRAIN) {
+          gsum = rx_colsum16(gsum);
+          if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum;
+        }
       }
     }
   }
@@ -268,21 +272,22 @@ __device__ void layer_forward(const MlpDesc& d, int l, char* smem, const float* 
 #pragma unroll
   for (int j = 0; j < T::NTW; ++j) {
     const int n = wave + j * RX_NW;
-    if (n >= ntiles) continue;
-    const int c = n * 16 + lr;
+    if (n < ntiles) {
+      const int c = n * 16 + lr;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      u16 h[4];
+      for (int mt = 0; mt < MT; ++mt) {
+        u16 h[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        h[r] = rx_f2bf(y[(j * MT + mt) * 4 + r]);
-        R[(mt * 16 + lg * 4 + r) * RS + c] = h[r];
-      }
-      if (TRAIN || !last) {
-        uint2 pk;
-        pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-        pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
-        *reinterpret_cast<uint2*>(dstT + c * tstride + mt * 16 + lg * 4) = pk;
+        for (int r = 0; r < 4; ++r) {
+          h[r] = rx_f2bf(acc[j * MT + mt][r]);
+          R[(mt * 16 + lg * 4 + r) * RS + c] = h[r];
+        }
+        if (TRAIN || !last) {
+          uint2 pk;
+          pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+          pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+          *reinterpret_cast<uint2*>(dstT + c * tstride + mt * 16 + lg * 4) = pk;
+        }
       }
     }
   }
@@ -342,20 +347,14 @@ __device__ void layer_backward(const MlpDesc& d, int l, char* smem, const float*
   const int ntiles = ly.in_n >> 4;
   f32x4 acc[T::NTW * MT];
 #pragma unroll
-  for (int i = 0; i < T::NTW * MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < ly.out_k; k0 += 32) {
+  for (int j = 0; j < T::NTW; ++j) {
+    f32x4 part[MT];
 #pragma unroll
-    for (int j = 0; j < T::NTW; ++j) {
-      const int n = wave + j * RX_NW;
-      if (n < ntiles) {
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(ly.Wt + (n * 16 + lr) * ly.out_k + k0 + 8 * lg);
+    for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int n = wave + j * RX_NW;
+    if (n < ntiles) gemm_tile<MT>(part, R + lr * RS, RS, ly.Wt + (n * 16 + lr) * ly.out_k, ly.out_k, lg);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(R + (mt * 16 + lr) * RS + k0 + 8 * lg);
-          acc[j * MT + mt] = rx_mfma16(a, b, acc[j * MT + mt]);
-        }
-      }
-    }
+    for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
   __syncthreads();  // all reads of G_l (R, GT) are done; they are overwritten with G_{l-1}
 
@@ -486,9 +485,10 @@ __device__ void load_inputs(const MlpDesc& d, char* smem, const u16* __restrict_
 
 template <int MT>
 __global__ __launch_bounds__(RX_THREADS) void mlp_train_step_kernel(
-    MlpDesc d, const float* __restrict__ P, float* __restrict__ Gr, const u16* __restrict__ feats,
+    const MlpDesc* __restrict__ dp, const float* __restrict__ P, float* __restrict__ Gr, const u16* __restrict__ feats,
     const float* __restrict__ labels, const int* __restrict__ perm, int row0, int nvalid,
     float* __restrict__ scratch, double* __restrict__ metrics) {
+  const MlpDesc& d = *dp;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int rowidx[Tile<MT>::BP];
   for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS)
@@ -502,9 +502,10 @@ __global__ __launch_bounds__(RX_THREADS) void mlp_train_step_kernel(
 
 template <int MT>
 __global__ __launch_bounds__(RX_THREADS) void mlp_eval_kernel(
-    MlpDesc d, const float* __restrict__ P, const u16* __restrict__ feats,
+    const MlpDesc* __restrict__ dp, const float* __restrict__ P, const u16* __restrict__ feats,
     const float* __restrict__ labels, int n_rows, int batch, double* __restrict__ metrics,
     float* __restrict__ out) {
+  const MlpDesc& d = *dp;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int rowidx[Tile<MT>::BP];
   const int row0 = blockIdx.x * batch;
@@ -539,11 +540,87 @@ struct OptDesc {
   OptSeg seg[RX_MAXSEG];
 };
 
-__global__ __launch_bounds__(256) void opt_step_kernel(OptDesc o, float* __restrict__ p,
+__device__ __forceinline__ float opt_update(const OptDesc& o, int idx, float* __restrict__ p,
+                                            const float* __restrict__ g, float* __restrict__ m,
+                                            float* __restrict__ v, float lr, float bc1, float bc2,
+                                            float gscale, int first) {
+  float gr = g[idx] * gscale;
+  if (o.maximize) gr = -gr;
+  float pv = p[idx];
+  if (o.algo == 2) {
+    if (o.wd != 0.f) gr += o.wd * pv;
+    if (o.momentum != 0.f) {
+      const float b = first ? gr : o.momentum * m[idx] + (1.f - o.dampening) * gr;
+      m[idx] = b;
+      gr = o.nesterov ? gr + o.momentum * b : b;
+    }
+    pv -= lr * gr;
+  } else {
+    if (o.algo == 1) pv *= (1.f - lr * o.wd);
+    else if (o.wd != 0.f) gr += o.wd * pv;
+    const float mm = o.b1 * m[idx] + (1.f - o.b1) * gr;
+    const float vv = o.b2 * v[idx] + (1.f - o.b2) * gr * gr;
+    m[idx] = mm;
+    v[idx] = vv;
+    pv -= (lr / bc1) * mm / (sqrtf(vv) / sqrtf(bc2) + o.eps);
+  }
+  p[idx] = pv;
+  return pv;
+}
+
+// Tiled optimizer: block b -> (segment, 32x32 weight tile | 1024-element vector chunk).
+// Weight tiles update p/m/v coalesced along `in`, then transpose through LDS so the W
+// ([out][in_k]) and Wt ([in][out_k]) bf16 images are both written with coalesced rows.
+__global__ __launch_bounds__(256) void opt_tiled_kernel(const OptDesc* __restrict__ op, float* __restrict__ p,
+                                                        const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        float lr, float bc1, float bc2, float gscale,
+                                                        int first) {
+  const OptDesc& o = *op;
+  __shared__ u16 tile[32][33];
+  int b = blockIdx.x;
+  int s = 0;
+  for (; s < o.nseg; ++s) {
+    const OptSeg& sg = o.seg[s];
+    const int nb = sg.kind == 1 ? ((sg.out + 31) / 32) * ((sg.in + 31) / 32) : (sg.len + 1023) / 1024;
+    if (b < nb) break;
+    b -= nb;
+  }
+  if (s >= o.nseg) return;
+  const OptSeg& sg = o.seg[s];
+  if (sg.kind != 1) {
+    for (int q = b * 1024 + threadIdx.x; q < min(sg.len, (b + 1) * 1024); q += 256)
+      opt_update(o, sg.start + q, p, g, m, v, lr, bc1, bc2, gscale, first);
+    return;
+  }
+  const int tiles_i = (sg.in + 31) / 32;
+  const int o0 = (b / tiles_i) * 32, i0 = (b % tiles_i) * 32;
+  const int ti = threadIdx.x & 31, to = threadIdx.x >> 5;  // 8 rows per pass
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int oo = o0 + to + r * 8, ii = i0 + ti;
+    u16 h = 0;
+    if (oo < sg.out && ii < sg.in) {
+      const float pv = opt_update(o, sg.start + oo * sg.in + ii, p, g, m, v, lr, bc1, bc2, gscale, first);
+      h = rx_f2bf(pv);
+      sg.W[oo * sg.in_k + ii] = h;
+    }
+    tile[to + r * 8][ti] = h;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ii = i0 + to + r * 8, oo = o0 + ti;
+    if (oo < sg.out && ii < sg.in) sg.Wt[ii * sg.out_k + oo] = tile[ti][to + r * 8];
+  }
+}
+
+__global__ __launch_bounds__(256) void opt_step_kernel(const OptDesc* __restrict__ op, float* __restrict__ p,
                                                        const float* __restrict__ g,
                                                        float* __restrict__ m, float* __restrict__ v,
                                                        float lr, float bc1, float bc2, float gscale,
                                                        int first) {
+  const OptDesc& o = *op;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < o.total; idx += gridDim.x * blockDim.x) {
     float gr = g[idx] * gscale;
     if (o.maximize) gr = -gr;
@@ -583,6 +660,15 @@ __global__ __launch_bounds__(256) void opt_step_kernel(OptDesc o, float* __restr
   }
 }
 
+int opt_tiled_blocks(const OptDesc& o) {
+  int nb = 0;
+  for (int s = 0; s < o.nseg; ++s) {
+    const OptSeg& sg = o.seg[s];
+    nb += sg.kind == 1 ? ((sg.out + 31) / 32) * ((sg.in + 31) / 32) : (sg.len + 1023) / 1024;
+  }
+  return nb < 1 ? 1 : nb;
+}
+
 template <int MT>
 int set_lds(int bytes) {
   RX_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_step_kernel<MT>),
@@ -606,7 +692,7 @@ int rx_opt_desc_size() { return (int)sizeof(OptDesc); }
 
 // One or more training steps over rows [first_row, first_row + nsteps * batch) of the epoch
 // permutation. Per step: fused fwd/bwd kernel -> (optional) gradient all-reduce -> optimizer.
-int rx_mlp_train_steps(const MlpDesc* d, const OptDesc* o, int mt, float* params, float* grads,
+int rx_mlp_train_steps(const MlpDesc* d, const MlpDesc* d_dev, const OptDesc* o, const OptDesc* o_dev, int mt, float* params, float* grads,
                        float* m, float* v, const u16* feats, const float* labels, const int* perm,
                        int n_rows, int batch, int first_step, int nsteps, const float* lrs,
                        const float* bc1s, const float* bc2s, float gscale, int opt_first_step,
@@ -619,26 +705,26 @@ int rx_mlp_train_steps(const MlpDesc* d, const OptDesc* o, int mt, float* params
     if (rc) return rc;
     lds_set[mt] = d->lds_bytes;
   }
-  const int opt_blocks = (o->total + 255) / 256 < 1024 ? (o->total + 255) / 256 : 1024;
+  const int opt_blocks = opt_tiled_blocks(*o);
   for (int s = 0; s < nsteps; ++s) {
     const int step = first_step + s;
     const int row0 = step * batch;
     const int nvalid = n_rows - row0 < batch ? n_rows - row0 : batch;
     if (nvalid <= 0) break;
     if (mt == 2)
-      hipLaunchKernelGGL(mlp_train_step_kernel<2>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+      hipLaunchKernelGGL(mlp_train_step_kernel<2>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, d_dev,
                          params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
     else if (mt == 4)
-      hipLaunchKernelGGL(mlp_train_step_kernel<4>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+      hipLaunchKernelGGL(mlp_train_step_kernel<4>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, d_dev,
                          params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
     else
-      hipLaunchKernelGGL(mlp_train_step_kernel<8>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+      hipLaunchKernelGGL(mlp_train_step_kernel<8>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, d_dev,
                          params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
     if (allreduce) {
       int rc = allreduce(grads, o->total, ar_ctx, stream);
       if (rc) return rc;
     }
-    hipLaunchKernelGGL(opt_step_kernel, dim3(opt_blocks), dim3(256), 0, stream, *o, params, grads, m, v,
+    hipLaunchKernelGGL(opt_tiled_kernel, dim3(opt_blocks), dim3(256), 0, stream, o_dev, params, grads, m, v,
                        lrs[s], bc1s[s], bc2s[s], gscale, (opt_first_step && s == 0) ? 1 : 0);
   }
   return (int)hipGetLastError();
@@ -646,7 +732,7 @@ int rx_mlp_train_steps(const MlpDesc* d, const OptDesc* o, int mt, float* params
 
 // Single pieces of a step for callers that interleave their own collective between the
 // backward and the optimizer (torch.distributed fallback path).
-int rx_mlp_fwdbwd(const MlpDesc* d, int mt, const float* params, float* grads, const u16* feats,
+int rx_mlp_fwdbwd(const MlpDesc* d, const MlpDesc* d_dev, int mt, const float* params, float* grads, const u16* feats,
                   const float* labels, const int* perm, int n_rows, int batch, int step,
                   float* scratch, double* metrics, hipStream_t stream) {
   static int lds_set[9] = {0};
@@ -660,26 +746,26 @@ int rx_mlp_fwdbwd(const MlpDesc* d, int mt, const float* params, float* grads, c
   const int nvalid = n_rows - row0 < batch ? n_rows - row0 : batch;
   if (nvalid <= 0) return 0;
   if (mt == 2)
-    hipLaunchKernelGGL(mlp_train_step_kernel<2>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+    hipLaunchKernelGGL(mlp_train_step_kernel<2>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, d_dev,
                        params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
   else if (mt == 4)
-    hipLaunchKernelGGL(mlp_train_step_kernel<4>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+    hipLaunchKernelGGL(mlp_train_step_kernel<4>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, d_dev,
                        params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
   else
-    hipLaunchKernelGGL(mlp_train_step_kernel<8>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, *d,
+    hipLaunchKernelGGL(mlp_train_step_kernel<8>, dim3(1), dim3(RX_THREADS), d->lds_bytes, stream, d_dev,
                        params, grads, feats, labels, perm, row0, nvalid, scratch, metrics);
   return (int)hipGetLastError();
 }
 
-int rx_opt_step(const OptDesc* o, float* params, const float* grads, float* m, float* v, float lr,
+int rx_opt_step(const OptDesc* o, const OptDesc* o_dev, float* params, const float* grads, float* m, float* v, float lr,
                 float bc1, float bc2, float gscale, int first, hipStream_t stream) {
-  const int opt_blocks = (o->total + 255) / 256 < 1024 ? (o->total + 255) / 256 : 1024;
-  hipLaunchKernelGGL(opt_step_kernel, dim3(opt_blocks), dim3(256), 0, stream, *o, params, grads, m, v,
+  const int opt_blocks = opt_tiled_blocks(*o);
+  hipLaunchKernelGGL(opt_tiled_kernel, dim3(opt_blocks), dim3(256), 0, stream, o_dev, params, grads, m, v,
                      lr, bc1, bc2, gscale, first);
   return (int)hipGetLastError();
 }
 
-int rx_mlp_eval(const MlpDesc* d, int mt, const float* params, const u16* feats, const float* labels,
+int rx_mlp_eval(const MlpDesc* d, const MlpDesc* d_dev, int mt, const float* params, const u16* feats, const float* labels,
                 int n_rows, int batch, double* metrics, hipStream_t stream) {
   static int lds_set[9] = {0};
   if (mt != 2 && mt != 4 && mt != 8) return -1;
@@ -691,24 +777,25 @@ int rx_mlp_eval(const MlpDesc* d, int mt, const float* params, const u16* feats,
   const int nb = (n_rows + batch - 1) / batch;
   if (nb <= 0) return 0;
   if (mt == 2)
-    hipLaunchKernelGGL(mlp_eval_kernel<2>, dim3(nb), dim3(RX_THREADS), d->lds_bytes, stream, *d, params,
+    hipLaunchKernelGGL(mlp_eval_kernel<2>, dim3(nb), dim3(RX_THREADS), d->lds_bytes, stream, d_dev, params,
                        feats, labels, n_rows, batch, metrics, nullptr);
   else if (mt == 4)
-    hipLaunchKernelGGL(mlp_eval_kernel<4>, dim3(nb), dim3(RX_THREADS), d->lds_bytes, stream, *d, params,
+    hipLaunchKernelGGL(mlp_eval_kernel<4>, dim3(nb), dim3(RX_THREADS), d->lds_bytes, stream, d_dev, params,
                        feats, labels, n_rows, batch, metrics, nullptr);
   else
-    hipLaunchKernelGGL(mlp_eval_kernel<8>, dim3(nb), dim3(RX_THREADS), d->lds_bytes, stream, *d, params,
+    hipLaunchKernelGGL(mlp_eval_kernel<8>, dim3(nb), dim3(RX_THREADS), d->lds_bytes, stream, d_dev, params,
                        feats, labels, n_rows, batch, metrics, nullptr);
   return (int)hipGetLastError();
 }
 
 // Refresh the bf16 images from the fp32 master weights (initialisation / after load).
-int rx_mlp_refresh_images(const OptDesc* o, const float* params, hipStream_t stream);
+int rx_mlp_refresh_images(const OptDesc* o, const OptDesc* o_dev, const float* params, hipStream_t stream);
 
 }  // extern "C"
 
 namespace {
-__global__ void refresh_kernel(OptDesc o, const float* __restrict__ p) {
+__global__ void refresh_kernel(const OptDesc* __restrict__ op, const float* __restrict__ p) {
+  const OptDesc& o = *op;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < o.total; idx += gridDim.x * blockDim.x) {
     for (int s = 0; s < o.nseg; ++s) {
       const OptSeg& sg = o.seg[s];
@@ -727,8 +814,8 @@ __global__ void refresh_kernel(OptDesc o, const float* __restrict__ p) {
 }
 }  // namespace
 
-extern "C" int rx_mlp_refresh_images(const OptDesc* o, const float* params, hipStream_t stream) {
+extern "C" int rx_mlp_refresh_images(const OptDesc* o, const OptDesc* o_dev, const float* params, hipStream_t stream) {
   const int blocks = (o->total + 255) / 256 < 1024 ? (o->total + 255) / 256 : 1024;
-  hipLaunchKernelGGL(refresh_kernel, dim3(blocks), dim3(256), 0, stream, *o, params);
+  hipLaunchKernelGGL(refresh_kernel, dim3(blocks), dim3(256), 0, stream, o_dev, params);
   return (int)hipGetLastError();
 }

@@ -88,12 +88,12 @@ def lib():
     L.rx_mlp_desc_size.restype = i
     L.rx_opt_desc_size.restype = i
     L.rx_ingest_args_size.restype = i
-    L.rx_mlp_train_steps.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, vp, vp, vp,
-                                     f, i, vp, vp, vp, vp, vp]
-    L.rx_mlp_fwdbwd.argtypes = [vp, i, vp, vp, vp, vp, vp, i, i, i, vp, vp, vp]
-    L.rx_opt_step.argtypes = [vp, vp, vp, vp, vp, f, f, f, f, i, vp]
-    L.rx_mlp_eval.argtypes = [vp, i, vp, vp, vp, i, i, vp, vp]
-    L.rx_mlp_refresh_images.argtypes = [vp, vp, vp]
+    L.rx_mlp_train_steps.argtypes = [vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, vp,
+                                     vp, vp, f, i, vp, vp, vp, vp, vp]
+    L.rx_mlp_fwdbwd.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, i, i, i, vp, vp, vp]
+    L.rx_opt_step.argtypes = [vp, vp, vp, vp, vp, vp, f, f, f, f, i, vp]
+    L.rx_mlp_eval.argtypes = [vp, vp, i, vp, vp, vp, i, i, vp, vp]
+    L.rx_mlp_refresh_images.argtypes = [vp, vp, vp, vp]
     L.rx_arrow_ingest.argtypes = [vp, vp, vp]
     L.rx_gather_rows.argtypes = [vp, vp, vp, ll, i, vp]
     for fn in ("rx_mlp_train_steps", "rx_mlp_fwdbwd", "rx_opt_step", "rx_mlp_eval",

@@ -191,8 +191,26 @@ class FusedMLPTrainer:
         o.nesterov, o.maximize = int(cfg.get("nesterov", False)), int(cfg.get("maximize", False))
         self.opt = o
         self.lds_bytes = lds
-        _hip.check(self.lib.rx_mlp_refresh_images(ctypes.byref(o), ctypes.c_void_p(self.params.data_ptr()),
-                                                   _hip.stream_ptr(dev)), "refresh_images")
+        # descriptors live in device memory: the kernels index them with runtime layer ids
+        self._desc_buf = torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8).to(dev)
+        self._opt_buf = torch.frombuffer(bytearray(bytes(o)), dtype=torch.uint8).to(dev)
+        self._dd = ctypes.c_void_p(self._desc_buf.data_ptr())
+        self._od = ctypes.c_void_p(self._opt_buf.data_ptr())
+        self.refresh_images()
+
+    def refresh_images(self):
+        """Rebuild the bf16 W/Wt images from the fp32 master parameters."""
+        _hip.check(self.lib.rx_mlp_refresh_images(ctypes.byref(self.opt), self._od,
+                                                   ctypes.c_void_p(self.params.data_ptr()),
+                                                   _hip.stream_ptr(self.device)), "refresh_images")
+
+    def opt_step(self, lr: float, bc1: float, bc2: float, gscale: float = 1.0, first: bool = False):
+        pp = ctypes.c_void_p
+        _hip.check(self.lib.rx_opt_step(ctypes.byref(self.opt), self._od, pp(self.params.data_ptr()),
+                                        pp(self.grads.data_ptr()), pp(self.m.data_ptr()),
+                                        pp(self.v.data_ptr()), ctypes.c_float(lr), ctypes.c_float(bc1),
+                                        ctypes.c_float(bc2), ctypes.c_float(gscale), int(first),
+                                        _hip.stream_ptr(self.device)), "rx_opt_step")
 
     # ----------------------------------------------------------------------- running ------
     def _lr(self, t: int) -> float:
@@ -221,7 +239,7 @@ class FusedMLPTrainer:
         gscale = 1.0 / world_size
         if allreduce is None:
             rc = self.lib.rx_mlp_train_steps(
-                ctypes.byref(self.desc), ctypes.byref(self.opt), self.mt, pp(self.params.data_ptr()),
+                ctypes.byref(self.desc), self._dd, ctypes.byref(self.opt), self._od, self.mt, pp(self.params.data_ptr()),
                 pp(self.grads.data_ptr()), pp(self.m.data_ptr()), pp(self.v.data_ptr()),
                 pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, 0, nsteps,
                 lrs, bc1, bc2, ctypes.c_float(gscale), int(self.step_count == 0), pp(self.scratch.data_ptr()),
@@ -230,12 +248,12 @@ class FusedMLPTrainer:
         else:
             for s in range(nsteps):
                 rc = self.lib.rx_mlp_fwdbwd(
-                    ctypes.byref(self.desc), self.mt, pp(self.params.data_ptr()), pp(self.grads.data_ptr()),
+                    ctypes.byref(self.desc), self._dd, self.mt, pp(self.params.data_ptr()), pp(self.grads.data_ptr()),
                     pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, s,
                     pp(self.scratch.data_ptr()), pp(self.metrics.data_ptr()), stream)
                 _hip.check(rc, "rx_mlp_fwdbwd")
                 allreduce(self.grads)
-                rc = self.lib.rx_opt_step(ctypes.byref(self.opt), pp(self.params.data_ptr()),
+                rc = self.lib.rx_opt_step(ctypes.byref(self.opt), self._od, pp(self.params.data_ptr()),
                                           pp(self.grads.data_ptr()), pp(self.m.data_ptr()),
                                           pp(self.v.data_ptr()), ctypes.c_float(lrs[s]),
                                           ctypes.c_float(bc1[s]), ctypes.c_float(bc2[s]),
@@ -251,7 +269,7 @@ class FusedMLPTrainer:
         pp = ctypes.c_void_p
         self.metrics.zero_()
         rc = self.lib.rx_mlp_fwdbwd(
-            ctypes.byref(self.desc), self.mt, pp(self.params.data_ptr()), pp(self.grads.data_ptr()),
+            ctypes.byref(self.desc), self._dd, self.mt, pp(self.params.data_ptr()), pp(self.grads.data_ptr()),
             pp(feats.data_ptr()), pp(labels.data_ptr()),
             pp(perm.data_ptr()) if perm is not None else pp(0), n_rows, self.batch, step,
             pp(self.scratch.data_ptr()), pp(self.metrics.data_ptr()), _hip.stream_ptr(self.device))
@@ -269,7 +287,7 @@ class FusedMLPTrainer:
     def evaluate(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int) -> Dict[str, float]:
         self.metrics.zero_()
         pp = ctypes.c_void_p
-        rc = self.lib.rx_mlp_eval(ctypes.byref(self.desc), self.mt, pp(self.params.data_ptr()),
+        rc = self.lib.rx_mlp_eval(ctypes.byref(self.desc), self._dd, self.mt, pp(self.params.data_ptr()),
                                   pp(feats.data_ptr()), pp(labels.data_ptr()), n_rows, self.batch,
                                   pp(self.metrics.data_ptr()), _hip.stream_ptr(self.device))
         _hip.check(rc, "rx_mlp_eval")

@@ -66,6 +66,49 @@ def to_timestamp(v, fmt: Optional[str] = None):
     if pa.types.is_date(t):
         return pc.cast(v, pa.timestamp("s"))
     if _is_str(t):
+        chunks = v.chunks if isinstance(v, pa.ChunkedArray) else [v]
+        key = (tuple((c.buffers()[2].address if c.buffers()[2] is not None else 0, c.offset, len(c))
+                     for c in chunks), fmt)
+        hit = _ts_cache_get(key, v)
+        if hit is not None:
+            return hit
+        out = _parse_ts(v, fmt)
+        _ts_cache_put(key, v, out)
+        return out
+    raise TypeError(f"cannot cast {t} to timestamp")
+
+
+# One parsed-timestamp cache entry per thread: the NYC ETL calls 7 datetime functions on the
+# same string column of a partition; parse it once (common-subexpression elimination).
+import threading as _threading  # noqa: E402
+
+_ts_tls = _threading.local()
+
+
+def _ts_cache_get(key, v):
+    # the entry holds a reference to the source array, so its buffer addresses stay valid
+    ent = getattr(_ts_tls, "ent", None)
+    if ent is not None and ent[0] == key:
+        return ent[2]
+    return None
+
+
+def _ts_cache_put(key, v, out):
+    _ts_tls.ent = (key, v, out)
+
+
+def _parse_ts(v, fmt):
+    if fmt is None:
+        # fast path: "YYYY-MM-DD HH:MM:SS[ UTC]" — parse the first 19 code units directly
+        blen = pc.binary_length(v)
+        shape_ok = pc.or_(pc.equal(blen, 19), pc.and_(pc.equal(blen, 23), pc.ends_with(v, " UTC")))
+        if pc.all(pc.fill_null(shape_ok, True)).as_py():
+            try:
+                # Arrow's ISO-8601 cast: ~10x faster than strptime on this shape
+                return pc.utf8_slice_codeunits(v, 0, 19).cast(pa.timestamp("s"))
+            except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+                pass
+    if True:
         s = pc.utf8_trim_whitespace(v)
         # strip a trailing zone id (" UTC", "Z", "+00:00"): the session time zone is UTC
         s = pc.replace_substring_regex(s, pattern=r"(\s*UTC|Z|\+00:?00)$", replacement="")
@@ -76,7 +119,6 @@ def to_timestamp(v, fmt: Optional[str] = None):
             parsed = pc.strptime(s, format=f, unit="s", error_is_null=True)
             out = parsed if out is None else pc.coalesce(out, parsed)
         return out
-    raise TypeError(f"cannot cast {t} to timestamp")
 
 
 def _spark_type_coerce(a, b):

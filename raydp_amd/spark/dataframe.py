@@ -293,14 +293,28 @@ class DataFrame:
     def filter(self, condition):
         if isinstance(condition, str):
             raise NotImplementedError("SQL string predicates are not supported; use Columns")
-        e = condition._expr
+        src = self._src()
+        preds = [condition._expr]
+        # CombineFilters: consecutive filters become one pass with an AND-ed predicate
+        if isinstance(src, P.MapPlan) and getattr(src, "filter_preds", None) is not None:
+            preds = src.filter_preds + preds
+            src = src.child
 
-        def fn(t, i):
-            mask = e.eval(t)
-            if isinstance(mask, pa.Scalar):
-                return t if mask.as_py() else t.slice(0, 0)
+        def fn(t, i, preds=preds):
+            mask = None
+            for e in preds:
+                m = e.eval(t)
+                if isinstance(m, pa.Scalar):
+                    if not m.as_py():
+                        return t.slice(0, 0)
+                    continue
+                mask = m if mask is None else pc.and_kleene(mask, m)
+            if mask is None:
+                return t
             return t.filter(mask, null_selection_behavior="drop")
-        return self._map(fn, "filter")
+        node = P.MapPlan(src, fn, "filter")
+        node.filter_preds = preds
+        return self._with(node)
 
     where = filter
 

@@ -150,7 +150,8 @@ def spark_partition_id():
 # ---------------------------------------------------------------------- datetime ---------
 def _dt(name, f):
     def builder(c):
-        return _fn(name, [c], lambda a, b: pc.cast(f(_to_ts(as_array(a[0], b.num_rows))),
+        return _fn(name, [c], lambda a, b: pc.cast(f(_to_ts(
+            a[0] if not isinstance(a[0], pa.Scalar) else as_array(a[0], b.num_rows))),
                                                    pa.int32()))
     builder.__name__ = name
     return builder

@@ -78,7 +78,10 @@ class DataFrameReader:
         src = CsvSource(path, header=self._flag("header"), infer_schema=self._flag("inferschema"),
                         sep=self._options.get("sep", self._options.get("delimiter", ",")),
                         schema=_to_arrow_schema(schema) if schema is not None else None,
-                        max_partition_bytes=mpb, null_value=self._options.get("nullvalue"))
+                        max_partition_bytes=mpb, null_value=self._options.get("nullvalue"),
+                        parallelism=self._session._default_parallelism(),
+                        open_cost_bytes=int(self._session.conf.get(
+                            "spark.sql.files.openCostInBytes", str(4 << 20))))
         return DataFrame(P.SourcePlan(src), self._session)
 
     def parquet(self, *paths):

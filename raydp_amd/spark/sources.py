@@ -108,14 +108,19 @@ def _downcast_ints(t: pa.Table) -> pa.Table:
 
 class CsvSource(Source):
     def __init__(self, path, header=True, infer_schema=False, sep=",", schema=None,
-                 max_partition_bytes=128 * 1024 * 1024, null_value=None):
+                 max_partition_bytes=128 * 1024 * 1024, null_value=None, parallelism=1,
+                 open_cost_bytes=4 * 1024 * 1024):
         self.files = _expand_paths(path)
         self.header, self.sep = header, sep
         self.null_value = null_value
         self.splits = []
+        # Spark's FilePartition sizing: maxSplitBytes = min(maxPartitionBytes,
+        # max(openCostInBytes, totalBytes / defaultParallelism))
+        total = sum(os.path.getsize(f) + open_cost_bytes for f in self.files)
+        split_bytes = min(max_partition_bytes, max(open_cost_bytes, total // max(1, parallelism)))
         for f in self.files:
             size = os.path.getsize(f)
-            nsplit = max(1, int(np.ceil(size / max_partition_bytes)))
+            nsplit = max(1, int(np.ceil(size / split_bytes)))
             b = np.linspace(0, size, nsplit + 1).astype(np.int64)
             for j in range(nsplit):
                 self.splits.append((f, int(b[j]), int(b[j + 1])))
@@ -186,7 +191,8 @@ class CsvSource(Source):
         if not data.strip():
             return self._schema.empty_table()
         t = pacsv.read_csv(io.BytesIO(data),
-                           read_options=pacsv.ReadOptions(column_names=names, use_threads=True),
+                           read_options=pacsv.ReadOptions(column_names=names, use_threads=True,
+                                                          block_size=max(1 << 20, len(data) + 1)),
                            parse_options=pacsv.ParseOptions(delimiter=self.sep),
                            convert_options=conv)
         return t

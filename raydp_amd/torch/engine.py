@@ -95,11 +95,7 @@ class FusedMLPEngine:
         if self.world > 1:
             import torch.distributed as dist
             dist.broadcast(self.trainer.params, 0)
-            from raydp_amd.ops import _hip
-            import ctypes
-            _hip.check(self.trainer.lib.rx_mlp_refresh_images(
-                ctypes.byref(self.trainer.opt), ctypes.c_void_p(self.trainer.params.data_ptr()),
-                _hip.stream_ptr(device)), "refresh")
+            self.trainer.refresh_images()
         self.drop_last = bool(config.get("drop_last", False))
         self.shuffle = bool(config.get("shuffle", True))
         self.gen = torch.Generator(device=device)

@@ -14,6 +14,7 @@ instead of being silently dropped (:163).
 import copy
 import inspect
 import os
+import time
 import tempfile
 from typing import Any, Callable, Dict, List, NoReturn, Optional, Union
 
@@ -28,6 +29,9 @@ from raydp_amd.train import session
 from raydp_amd.train.checkpoint import Checkpoint, TorchCheckpoint
 from raydp_amd.train.config import FailureConfig, RunConfig, ScalingConfig
 from raydp_amd.train.trainer import TorchTrainer
+
+# wall-clock phase marks of the last fit in this process (bench / profiling)
+LAST_TIMINGS = {}
 
 
 def _make_lr_schedule(opt_template: torch.optim.Optimizer, creator, config):
@@ -157,7 +161,10 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         else:
             sched = config["lr_scheduler_creator"](optimizer, config) if config["lr_scheduler_creator"] else None
             engine = TorchLoopEngine(model, optimizer, loss, metrics, device, config, sched)
+        t_load0 = time.perf_counter()
         engine.load(train_ds, eval_ds, config)
+        LAST_TIMINGS["ingest"] = time.perf_counter() - t_load0
+        t_train0 = time.perf_counter()
         config.setdefault("_engine_name", engine.name)
         for epoch in range(config["num_epochs"]):
             train_res, train_loss = engine.train_epoch()
@@ -166,6 +173,8 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             if eval_ds is not None:
                 eval_res, test_loss = engine.evaluate_epoch()
                 session.report(dict(epoch=epoch, eval_res=eval_res, test_loss=test_loss))
+        LAST_TIMINGS["train"] = time.perf_counter() - t_train0
+        t_ck0 = time.perf_counter()
         states = engine.state_dict()
         states = {k: v.detach().cpu() for k, v in states.items()}
         with tempfile.TemporaryDirectory() as temp_checkpoint_dir:
@@ -174,6 +183,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                 torch.save(states, os.path.join(temp_checkpoint_dir, "model.pt"))
                 checkpoint = Checkpoint.from_directory(temp_checkpoint_dir)
             session.report({}, checkpoint=checkpoint)
+        LAST_TIMINGS["checkpoint"] = time.perf_counter() - t_ck0
 
     # ------------------------------------------------------------------------- driver -----
     def fit(self, train_ds, evaluate_ds=None, max_retries=3) -> NoReturn:
@@ -226,6 +236,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
     def fit_on_spark(self, train_df: DF, evaluate_df: OPTIONAL_DF = None, max_retries=3,
                      fs_directory: Optional[str] = None, compression: Optional[str] = None,
                      stop_spark_after_conversion=False):
+        t_conv0 = time.perf_counter()
         super().fit_on_spark(train_df, evaluate_df)
         train_df = self._check_and_convert(train_df)
         evaluate_ds = None
@@ -249,6 +260,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             if evaluate_df is not None:
                 evaluate_df = self._check_and_convert(evaluate_df)
                 evaluate_ds = spark_dataframe_to_ray_dataset(evaluate_df, owner=owner)
+        LAST_TIMINGS["etl_and_conversion"] = time.perf_counter() - t_conv0
         if stop_spark_after_conversion:
             from raydp_amd.context import stop_spark
             stop_spark(cleanup_data=False)
