@@ -40,6 +40,7 @@ struct MlpLayer {
   int xt_off;        // LDS byte offset of XT_l
   int stat_off;      // float offset of (mean, invstd) pairs for this layer's outputs in LDS
   int r_off;         // float offset of the saved pre-BN values in the scratch buffer
+  int pr_off;        // float offset of [bias|gamma|beta|run_mean|run_var] (x out_n) in LDS
 };
 
 struct MlpDesc {
@@ -51,6 +52,9 @@ struct MlpDesc {
   int out_dim;
   int feat_k;        // row stride of the bf16 feature matrix
   MlpLayer layer[RX_MAXL];
+  unsigned long long* stamps;  // optional: per-phase s_memtime stamps (profiling builds/tests)
+  int pr_lds_off;    // LDS byte offset of the per-column parameter block
+  int pr_total;      // floats in that block
 };
 
 namespace {
@@ -135,7 +139,8 @@ __device__ void layer_forward(const MlpDesc& d, int l, char* smem, const float* 
     if (n < ntiles) {
       const int c = n * 16 + lr;
       const bool colok = c < ly.out;
-      const float bias = (colok && ly.b_off >= 0) ? P[ly.b_off + c] : 0.f;
+      const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off) + ly.pr_off;
+      const float bias = pr[c];
       const bool act_first = ly.bn != 2;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -170,8 +175,9 @@ __device__ void layer_forward(const MlpDesc& d, int l, char* smem, const float* 
             stats[ly.stat_off + 2 * c] = mean;
             stats[ly.stat_off + 2 * c + 1] = invstd;
             const float unb = nvalid > 1 ? var * (float)nvalid / (float)(nvalid - 1) : var;
-            ly.run_mean[c] = (1.f - ly.momentum) * ly.run_mean[c] + ly.momentum * mean;
-            ly.run_var[c] = (1.f - ly.momentum) * ly.run_var[c] + ly.momentum * unb;
+            float* prw = reinterpret_cast<float*>(smem + d.pr_lds_off) + ly.pr_off;
+            prw[3 * ly.out_n + c] = (1.f - ly.momentum) * prw[3 * ly.out_n + c] + ly.momentum * mean;
+            prw[4 * ly.out_n + c] = (1.f - ly.momentum) * prw[4 * ly.out_n + c] + ly.momentum * unb;
           }
           // save the BN input for the backward pass (thread-private slots)
 #pragma unroll
@@ -180,11 +186,11 @@ __device__ void layer_forward(const MlpDesc& d, int l, char* smem, const float* 
             for (int r = 0; r < 4; ++r)
               scratch[ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c] = acc[j * MT + mt][r];
         } else {
-          mean = colok ? ly.run_mean[c] : 0.f;
-          invstd = colok ? rsqrtf(ly.run_var[c] + ly.eps) : 0.f;
+          mean = colok ? pr[3 * ly.out_n + c] : 0.f;
+          invstd = colok ? rsqrtf(pr[4 * ly.out_n + c] + ly.eps) : 0.f;
         }
-        const float gam = (colok && ly.g_off >= 0) ? P[ly.g_off + c] : 1.f;
-        const float bet = (colok && ly.be_off >= 0) ? P[ly.be_off + c] : 0.f;
+        const float gam = pr[ly.out_n + c];
+        const float bet = pr[2 * ly.out_n + c];
         const bool act_after = ly.bn == 2;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
@@ -211,6 +217,8 @@ __device__ void layer_forward(const MlpDesc& d, int l, char* smem, const float* 
         // loss, metrics and dL/dy (mean reduction over nvalid * out_dim elements)
         float lsum = 0.f, asum = 0.f, ssum = 0.f, gsum = 0.f;
         const float inv_n = 1.f / (float)(nvalid * ly.out);
+        const int lcode = d.loss;
+        const float beta = d.beta;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -223,21 +231,10 @@ __device__ void layer_forward(const MlpDesc& d, int l, char* smem, const float* 
               const float ae = fabsf(e);
               asum += ae;
               ssum += e * e;
-              if (d.loss == 0) {
-                lsum += e * e;
-                g = 2.f * e;
-              } else if (d.loss == 1) {
-                if (ae < d.beta) {
-                  lsum += 0.5f * e * e / d.beta;
-                  g = e / d.beta;
-                } else {
-                  lsum += ae - 0.5f * d.beta;
-                  g = e > 0.f ? 1.f : -1.f;
-                }
-              } else {
-                lsum += ae;
-                g = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
-              }
+              const float sgn = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+              const bool quad = ae < beta;
+              lsum += quad ? 0.5f * e * e / beta : ae - 0.5f * beta;  // smooth-L1 term
+              g = lcode == 0 ? 2.f * e : (lcode == 1 && quad ? e / beta : sgn);
               g *= inv_n;
             }
             acc[j * MT + mt][r] = g;  // acc now holds G_{L-1}
@@ -246,6 +243,8 @@ __device__ void layer_forward(const MlpDesc& d, int l, char* smem, const float* 
         lsum = rx_wavesum(lsum);
         asum = rx_wavesum(asum);
         ssum = rx_wavesum(ssum);
+        if (lcode == 0) lsum = ssum;
+        else if (lcode == 2) lsum = asum;
         if (lane == 0) {
           atomicAdd(&metrics[0], (double)(lsum * inv_n));
           atomicAdd(&metrics[1], (double)asum);
@@ -319,27 +318,36 @@ __device__ void layer_backward(const MlpDesc& d, int l, char* smem, const float*
   const u16* XT = reinterpret_cast<const u16*>(smem + ly.xt_off);
   float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
 
-  // ---- wgrad: dW[o][i] = sum_b G[b][o] X[b][i]  (A = GT, B = XT, K = Bpad) ----
+  // ---- wgrad, computed transposed: dW^T[i][o] = sum_b X[b][i] G[b][o]  (A = XT, B = GT) ----
+  // each lane then holds 4 consecutive i of one o = 16 contiguous bytes of dW[o][:] ->
+  // one dwordx4 store instead of four dword stores (the step is store-queue bound here)
   {
     const int mo_tiles = ly.out_n >> 4, ni_tiles = ly.in_n >> 4;
     const int ntile = mo_tiles * ni_tiles;
+    const bool vec = ((ly.w_off | ly.in) & 3) == 0;
     for (int t = wave; t < ntile; t += RX_NW) {
       const int mo = t / ni_tiles, ni = t % ni_tiles;
       f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k0 = 0; k0 < T::BP; k0 += 32) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(GT + (mo * 16 + lr) * XS + k0 + 8 * lg);
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(XT + (ni * 16 + lr) * XS + k0 + 8 * lg);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(XT + (ni * 16 + lr) * XS + k0 + 8 * lg);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(GT + (mo * 16 + lr) * XS + k0 + 8 * lg);
         a4 = rx_mfma16(a, b, a4);
       }
-      const int i = ni * 16 + lr;
+      const int o = mo * 16 + lr, i0 = ni * 16 + lg * 4;
+      if (o < ly.out) {
+        float* dst = Gr + ly.w_off + o * ly.in + i0;
+        if (vec && i0 + 3 < ly.in) {
+          *reinterpret_cast<f32x4*>(dst) = a4;
+        } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = mo * 16 + lg * 4 + r;
-        if (o < ly.out && i < ly.in) Gr[ly.w_off + o * ly.in + i] = a4[r];
+          for (int r = 0; r < 4; ++r)
+            if (i0 + r < ly.in) dst[r] = a4[r];
+        }
       }
     }
   }
+  if (d.stamps != nullptr && threadIdx.x == 0) d.stamps[20 + 4 * l] = __builtin_amdgcn_s_memtime();
   if (l == 0) return;
 
   // ---- dgrad: dX[b][i] = sum_o G[b][o] W[o][i]  (A = R, B = Wt, K = out_k) ----
@@ -356,7 +364,9 @@ __device__ void layer_backward(const MlpDesc& d, int l, char* smem, const float*
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
+  if (d.stamps != nullptr && threadIdx.x == 0) d.stamps[21 + 4 * l] = __builtin_amdgcn_s_memtime();
   __syncthreads();  // all reads of G_l (R, GT) are done; they are overwritten with G_{l-1}
+  if (d.stamps != nullptr && threadIdx.x == 0) d.stamps[22 + 4 * l] = __builtin_amdgcn_s_memtime();
 
   // ---- post-op backward of layer l-1 (BN / act), producing G_{l-1} ----
 #pragma unroll
@@ -387,8 +397,9 @@ __device__ void layer_backward(const MlpDesc& d, int l, char* smem, const float*
     } else {
       const float mean = colok ? stats[pv.stat_off + 2 * c] : 0.f;
       const float invstd = colok ? stats[pv.stat_off + 2 * c + 1] : 0.f;
-      const float gam = (colok && pv.g_off >= 0) ? P[pv.g_off + c] : 1.f;
-      const float bet = (colok && pv.be_off >= 0) ? P[pv.be_off + c] : 0.f;
+      const float* ppr = reinterpret_cast<const float*>(smem + d.pr_lds_off) + pv.pr_off;
+      const float gam = ppr[pv.out_n + c];
+      const float bet = ppr[2 * pv.out_n + c];
       float xh[MT * 4], s[MT * 4];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -445,6 +456,7 @@ __device__ void layer_backward(const MlpDesc& d, int l, char* smem, const float*
       *reinterpret_cast<uint2*>(GT + c * XS + mt * 16 + lg * 4) = pk;
     }
   }
+  if (d.stamps != nullptr && threadIdx.x == 0) d.stamps[23 + 4 * l] = __builtin_amdgcn_s_memtime();
   // zero the K tail [out_n, out_k) of G_{l-1} in R for the next dgrad
   const int kpad = pv.out_k - pv.out_n;
   if (kpad > 0) {
@@ -454,6 +466,59 @@ __device__ void layer_backward(const MlpDesc& d, int l, char* smem, const float*
     }
   }
   __syncthreads();
+}
+
+// Stage every layer's per-column parameters (bias, BN gamma/beta, running mean/var) into LDS
+// with ONE burst of independent loads per thread (column c = threadIdx.x of every layer,
+// address-clamped so no load sits behind a per-element branch). Saves two dependent
+// cross-XCD round trips per layer in the epilogues.
+__device__ void load_params(const MlpDesc& d, char* smem, const float* __restrict__ P) {
+  float* pr = reinterpret_cast<float*>(smem + d.pr_lds_off);
+  const int c = threadIdx.x;
+  float v[RX_MAXL][5];
+#pragma unroll
+  for (int l = 0; l < RX_MAXL; ++l) {
+    if (l < d.L) {
+      const MlpLayer& ly = d.layer[l];
+      const bool ok = c < ly.out;
+      const int cc = ok ? c : 0;
+      const float b = P[ly.b_off >= 0 ? ly.b_off + cc : 0];
+      const float g = P[ly.g_off >= 0 ? ly.g_off + cc : 0];
+      const float be = P[ly.be_off >= 0 ? ly.be_off + cc : 0];
+      const float* rmp = ly.run_mean ? ly.run_mean : P;
+      const float* rvp = ly.run_var ? ly.run_var : P;
+      const float rm = rmp[ly.run_mean ? cc : 0];
+      const float rv = rvp[ly.run_var ? cc : 0];
+      v[l][0] = (ok && ly.b_off >= 0) ? b : 0.f;
+      v[l][1] = (ok && ly.g_off >= 0) ? g : 1.f;
+      v[l][2] = (ok && ly.be_off >= 0) ? be : 0.f;
+      v[l][3] = (ok && ly.run_mean) ? rm : 0.f;
+      v[l][4] = (ok && ly.run_var) ? rv : 1.f;
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < RX_MAXL; ++l) {
+    if (l < d.L) {
+      const MlpLayer& ly = d.layer[l];
+      if (c < ly.out_n) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) pr[ly.pr_off + k * ly.out_n + c] = v[l][k];
+      }
+    }
+  }
+}
+
+// write the updated BatchNorm running statistics back (once per step, after the forward)
+__device__ void store_running_stats(const MlpDesc& d, char* smem) {
+  const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off);
+  const int c = threadIdx.x;
+  for (int l = 0; l < d.L; ++l) {
+    const MlpLayer& ly = d.layer[l];
+    if (ly.run_mean != nullptr && c < ly.out) {
+      ly.run_mean[c] = pr[ly.pr_off + 3 * ly.out_n + c];
+      ly.run_var[c] = pr[ly.pr_off + 4 * ly.out_n + c];
+    }
+  }
 }
 
 // load the batch's feature rows (gathered through the epoch permutation) into R and XT_0
@@ -491,13 +556,30 @@ __global__ __launch_bounds__(RX_THREADS) void mlp_train_step_kernel(
   const MlpDesc& d = *dp;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int rowidx[Tile<MT>::BP];
+  unsigned long long* st = d.stamps;
+  int si = 0;
+#define RX_STAMP()                                                        \
+  do {                                                                    \
+    if (st != nullptr && threadIdx.x == 0) st[si] = __builtin_amdgcn_s_memtime(); \
+    ++si;                                                                 \
+  } while (0)
+  RX_STAMP();
   for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS)
     rowidx[i] = i < nvalid ? (perm ? perm[row0 + i] : row0 + i) : 0;
+  load_params(d, smem, P);
   __syncthreads();
   load_inputs<MT>(d, smem, feats, rowidx, nvalid, true);
-  for (int l = 0; l < d.L; ++l)
+  RX_STAMP();
+  for (int l = 0; l < d.L; ++l) {
     layer_forward<MT, true>(d, l, smem, P, Gr, labels, rowidx, nvalid, scratch, metrics);
-  for (int l = d.L - 1; l >= 0; --l) layer_backward<MT>(d, l, smem, P, Gr, nvalid, scratch);
+    RX_STAMP();
+  }
+  store_running_stats(d, smem);
+  for (int l = d.L - 1; l >= 0; --l) {
+    layer_backward<MT>(d, l, smem, P, Gr, nvalid, scratch);
+    RX_STAMP();
+  }
+#undef RX_STAMP
 }
 
 template <int MT>
@@ -511,6 +593,7 @@ __global__ __launch_bounds__(RX_THREADS) void mlp_eval_kernel(
   const int row0 = blockIdx.x * batch;
   const int nvalid = min(batch, n_rows - row0);
   for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS) rowidx[i] = i < nvalid ? row0 + i : 0;
+  load_params(d, smem, P);
   __syncthreads();
   load_inputs<MT>(d, smem, feats, rowidx, nvalid, false);
   for (int l = 0; l < d.L; ++l) {
@@ -525,7 +608,7 @@ __global__ __launch_bounds__(RX_THREADS) void mlp_eval_kernel(
 // optimizer: fused Adam / AdamW / SGD(momentum, nesterov) over the flat parameter vector,
 // refreshing the bf16 W / Wt images of every Linear weight in the same pass.
 // ------------------------------------------------------------------------------------------
-#define RX_MAXSEG (3 * RX_MAXL)
+#define RX_MAXSEG (4 * RX_MAXL)
 struct OptSeg {
   int start, len, kind;  // kind 1: linear weight (needs bf16 images)
   int out, in, in_k, out_k;
@@ -612,51 +695,6 @@ __global__ __launch_bounds__(256) void opt_tiled_kernel(const OptDesc* __restric
   for (int r = 0; r < 4; ++r) {
     const int ii = i0 + to + r * 8, oo = o0 + ti;
     if (oo < sg.out && ii < sg.in) sg.Wt[ii * sg.out_k + oo] = tile[ti][to + r * 8];
-  }
-}
-
-__global__ __launch_bounds__(256) void opt_step_kernel(const OptDesc* __restrict__ op, float* __restrict__ p,
-                                                       const float* __restrict__ g,
-                                                       float* __restrict__ m, float* __restrict__ v,
-                                                       float lr, float bc1, float bc2, float gscale,
-                                                       int first) {
-  const OptDesc& o = *op;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < o.total; idx += gridDim.x * blockDim.x) {
-    float gr = g[idx] * gscale;
-    if (o.maximize) gr = -gr;
-    float pv = p[idx];
-    if (o.algo == 2) {
-      if (o.wd != 0.f) gr += o.wd * pv;
-      if (o.momentum != 0.f) {
-        float b = first ? gr : o.momentum * m[idx] + (1.f - o.dampening) * gr;
-        m[idx] = b;
-        gr = o.nesterov ? gr + o.momentum * b : b;
-      }
-      pv -= lr * gr;
-    } else {
-      if (o.algo == 1) pv *= (1.f - lr * o.wd);
-      else if (o.wd != 0.f) gr += o.wd * pv;
-      const float mm = o.b1 * m[idx] + (1.f - o.b1) * gr;
-      const float vv = o.b2 * v[idx] + (1.f - o.b2) * gr * gr;
-      m[idx] = mm;
-      v[idx] = vv;
-      const float denom = sqrtf(vv) / sqrtf(bc2) + o.eps;
-      pv -= (lr / bc1) * mm / denom;
-    }
-    p[idx] = pv;
-    for (int s = 0; s < o.nseg; ++s) {
-      const OptSeg& sg = o.seg[s];
-      if (idx >= sg.start && idx < sg.start + sg.len) {
-        if (sg.kind == 1) {
-          const int q = idx - sg.start;
-          const int oo = q / sg.in, ii = q - oo * sg.in;
-          const u16 h = rx_f2bf(pv);
-          sg.W[oo * sg.in_k + ii] = h;
-          sg.Wt[ii * sg.out_k + oo] = h;
-        }
-        break;
-      }
-    }
   }
 }
 

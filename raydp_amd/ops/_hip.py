@@ -9,7 +9,7 @@ import ctypes
 from raydp_amd.native import loader
 
 MAXL = 8
-MAXSEG = 3 * MAXL
+MAXSEG = 4 * MAXL
 MAXCOLS = 64
 
 
@@ -25,6 +25,7 @@ class MlpLayer(ctypes.Structure):
         ("run_mean", ctypes.c_void_p), ("run_var", ctypes.c_void_p),
         ("eps", ctypes.c_float), ("momentum", ctypes.c_float),
         ("xt_off", ctypes.c_int), ("stat_off", ctypes.c_int), ("r_off", ctypes.c_int),
+        ("pr_off", ctypes.c_int),
     ]
 
 
@@ -37,6 +38,8 @@ class MlpDesc(ctypes.Structure):
         ("loss", ctypes.c_int), ("beta", ctypes.c_float),
         ("out_dim", ctypes.c_int), ("feat_k", ctypes.c_int),
         ("layer", MlpLayer * MAXL),
+        ("stamps", ctypes.c_void_p),
+        ("pr_lds_off", ctypes.c_int), ("pr_total", ctypes.c_int),
     ]
 
 

@@ -118,7 +118,23 @@ class FusedMLPTrainer:
         d.stats_lds_off = alloc(stat_total * 4)
         scratch_off = 0
         stat_off = 0
+        pr_total = 0
         nseg = 0
+
+        def vseg(start, n):
+            # bias / BN gamma+beta vectors: plain element-wise optimizer segments
+            nonlocal nseg
+            sg = o.seg[nseg]
+            sg.start, sg.len, sg.kind = start, n, 0
+            nseg += 1
+
+        def pad4():
+            # every flat segment starts 16-B aligned (vectorised gradient stores)
+            nonlocal off
+            if off % 4:
+                flat.append(torch.zeros(4 - off % 4))
+                off += 4 - off % 4
+
         for li, (ly, dm) in enumerate(zip(spec.layers, dims)):
             i, oo, in_k, out_k, in_n, out_n = dm
             lin = ly.linear
@@ -129,6 +145,7 @@ class FusedMLPTrainer:
             self.W_img.append(W)
             self.Wt_img.append(Wt)
             x.W, x.Wt = W.data_ptr(), Wt.data_ptr()
+            pad4()
             x.w_off = off
             flat.append(lin.weight.detach().reshape(-1).float())
             seg = o.seg[nseg]
@@ -139,9 +156,11 @@ class FusedMLPTrainer:
             self.layout.append(("weight", lin, off, oo * i))
             off += oo * i
             if lin.bias is not None:
+                pad4()
                 x.b_off = off
                 flat.append(lin.bias.detach().reshape(-1).float())
                 self.layout.append(("bias", lin, off, oo))
+                vseg(off, oo)
                 off += oo
             else:
                 x.b_off = -1
@@ -150,14 +169,15 @@ class FusedMLPTrainer:
             if ly.bn:
                 bn = ly.bn_module
                 if bn.affine:
+                    pad4()
                     x.g_off = off
                     flat.append(bn.weight.detach().reshape(-1).float())
                     self.layout.append(("gamma", bn, off, oo))
-                    off += oo
-                    x.be_off = off
+                    x.be_off = off + oo
                     flat.append(bn.bias.detach().reshape(-1).float())
-                    self.layout.append(("beta", bn, off, oo))
-                    off += oo
+                    self.layout.append(("beta", bn, off + oo, oo))
+                    vseg(off, 2 * oo)
+                    off += 2 * oo
                 rm = bn.running_mean.detach().to(dev, torch.float32).clone()
                 rv = bn.running_var.detach().to(dev, torch.float32).clone()
                 self.run_bufs.append((bn, rm, rv))
@@ -168,6 +188,10 @@ class FusedMLPTrainer:
             stat_off += 2 * out_n
             x.r_off = scratch_off
             scratch_off += bp * out_n
+            x.pr_off = pr_total
+            pr_total += 5 * out_n
+        d.pr_lds_off = alloc(pr_total * 4)
+        d.pr_total = pr_total
         d.lds_bytes = lds
         d.max_k, d.max_n = max_k, max_n
         d.loss, d.beta = self.loss_code, self.beta
