@@ -53,6 +53,12 @@ def is_initialized() -> bool:
     return _node is not None
 
 
+def address() -> Optional[str]:
+    """Address other processes use to reach this node (None before ``init``)."""
+    n = _node
+    return None if n is None else getattr(n, "address", None)
+
+
 def current_node():
     return _node
 

@@ -126,3 +126,32 @@ def ray_dataset_to_spark_dataframe(spark, arrow_schema, blocks: List[ObjectRef],
 def read_spark_parquet(path: str) -> Dataset:
     from raydp_amd.data import dataset as D
     return D.read_parquet(path, file_extensions=["parquet"])
+
+
+def _convert_for_estimator(est, train_df, evaluate_df=None, fs_directory: Optional[str] = None,
+                           compression: Optional[str] = None, stop_spark_after_conversion: bool = False,
+                           parallelism: Optional[int] = None):
+    """Shared ``fit_on_spark`` conversion of the estimators (reference: the identical blocks in
+    ``python/raydp/tf/estimator.py:272-304`` and ``xgboost/estimator.py:83-116``): via a
+    parquet directory when ``fs_directory`` is given, else through the object store."""
+    train_df = est._check_and_convert(train_df)
+    evaluate_ds = None
+    if fs_directory is not None:
+        app_id = train_df.sparkSession.sparkContext.applicationId
+        path = fs_directory.rstrip("/") + f"/{app_id}"
+        train_df.write.parquet(path + "/train", compression=compression)
+        train_ds = read_spark_parquet(path + "/train")
+        if evaluate_df is not None:
+            evaluate_df = est._check_and_convert(evaluate_df)
+            evaluate_df.write.parquet(path + "/test", compression=compression)
+            evaluate_ds = read_spark_parquet(path + "/test")
+    else:
+        owner = get_raydp_master_owner(train_df.sparkSession) if stop_spark_after_conversion else None
+        train_ds = spark_dataframe_to_ray_dataset(train_df, parallelism=parallelism, owner=owner)
+        if evaluate_df is not None:
+            evaluate_df = est._check_and_convert(evaluate_df)
+            evaluate_ds = spark_dataframe_to_ray_dataset(evaluate_df, parallelism=parallelism, owner=owner)
+    if stop_spark_after_conversion:
+        from raydp_amd.context import stop_spark
+        stop_spark(cleanup_data=False)
+    return train_ds, evaluate_ds

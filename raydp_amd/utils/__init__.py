@@ -29,6 +29,9 @@ __all__ = [
 ]
 
 
+# runtime "memory" resources are accounted in bytes (Ray >= 2 semantics)
+MEMORY_RESOURCE_UNIT_BYTES = 1
+
 def get_node_ip_address() -> str:
     """IP of this node as seen by peers; loopback when the host name does not resolve."""
     env = os.environ.get("RAYDP_NODE_IP")

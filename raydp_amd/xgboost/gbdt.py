@@ -1,0 +1,558 @@
+"""Histogram gradient-boosted trees on torch tensors (the engine behind ``XGBoostEstimator``).
+
+The reference delegates to xgboost-ray (``python/raydp/xgboost/estimator.py:54-81``: an
+``XGBoostTrainer`` whose workers run XGBoost's ``hist`` method and all-reduce gradient
+histograms over Rabit). XGBoost is not installed here, so this module implements the same
+algorithm natively:
+
+* features are quantised once into ``max_bin`` quantile bins (bin 0 = missing), cut points
+  agreed across workers from an all-gathered sample;
+* trees grow level-wise to ``max_depth``; each level builds one (node, feature, bin) histogram
+  of (gradient, hessian) with a single ``scatter_add`` over the binned matrix, all-reduces it
+  (``torch.distributed`` – RCCL on MI355X, gloo on CPU) exactly like Rabit's histogram
+  all-reduce, and evaluates every split with XGBoost's gain
+  ``G_L²/(H_L+λ) + G_R²/(H_R+λ) − G²/(H+λ)`` including the learned default direction for
+  missing values, ``min_child_weight`` and ``gamma`` pruning;
+* leaves get ``−η·G/(H+λ)`` (clipped by ``max_delta_step``); prediction walks all trees in a
+  vectorised loop (``x < split_cond`` goes left, XGBoost's convention).
+
+Supported objectives: ``reg:squarederror``, ``reg:logistic``, ``binary:logistic``,
+``binary:logitraw``, ``count:poisson``, ``multi:softmax``, ``multi:softprob``.
+"""
+import json
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+DEFAULTS = {"eta": 0.3, "max_depth": 6, "lambda": 1.0, "alpha": 0.0, "gamma": 0.0, "min_child_weight": 1.0,
+            "max_bin": 256, "objective": "reg:squarederror", "subsample": 1.0, "colsample_bytree": 1.0,
+            "max_delta_step": 0.0, "num_class": 1, "seed": 0, "base_score": None}
+_ALIASES = {"learning_rate": "eta", "reg_lambda": "lambda", "reg_alpha": "alpha", "min_split_loss": "gamma"}
+
+
+def normalize_params(params: Optional[Dict]) -> Dict:
+    p = dict(DEFAULTS)
+    for k, v in (params or {}).items():
+        p[_ALIASES.get(k, k)] = v
+    if p["objective"].startswith("multi:") and int(p["num_class"]) < 2:
+        raise ValueError("multi-class objectives need num_class >= 2")
+    return p
+
+
+class DMatrix:
+    """Feature matrix + label (subset of ``xgboost.DMatrix``)."""
+
+    def __init__(self, data, label=None, weight=None, feature_names: Optional[Sequence[str]] = None,
+                 missing: float = float("nan")):
+        import pandas as pd
+        if isinstance(data, pd.DataFrame):
+            feature_names = feature_names or [str(c) for c in data.columns]
+            data = data.to_numpy(dtype=np.float32, na_value=np.nan)
+        x = torch.as_tensor(np.asarray(data, dtype=np.float32))
+        if x.dim() == 1:
+            x = x[:, None]
+        if not math.isnan(missing):
+            x = torch.where(x == missing, torch.full_like(x, float("nan")), x)
+        self.data = x
+        self.label = None if label is None else torch.as_tensor(np.asarray(label, dtype=np.float32)).reshape(-1)
+        self.weight = None if weight is None else torch.as_tensor(np.asarray(weight, dtype=np.float32)).reshape(-1)
+        self.feature_names = list(feature_names) if feature_names else [f"f{i}" for i in range(x.shape[1])]
+
+    def num_row(self):
+        return self.data.shape[0]
+
+    def num_col(self):
+        return self.data.shape[1]
+
+    def get_label(self):
+        return None if self.label is None else self.label.numpy()
+
+
+# --------------------------------------------------------------------------- objectives ----
+def _grad_hess(obj: str, margin: torch.Tensor, y: torch.Tensor, p: Dict):
+    if obj == "reg:squarederror":
+        return margin - y, torch.ones_like(margin)
+    if obj in ("reg:logistic", "binary:logistic", "binary:logitraw"):
+        pr = torch.sigmoid(margin)
+        return pr - y, torch.clamp(pr * (1 - pr), min=1e-16)
+    if obj == "count:poisson":
+        mds = float(p["max_delta_step"]) or 0.7
+        return torch.exp(margin) - y, torch.exp(margin + mds)
+    if obj.startswith("multi:"):
+        k = int(p["num_class"])
+        pr = torch.softmax(margin, dim=1)
+        oh = torch.nn.functional.one_hot(y.long(), k).to(pr.dtype)
+        return pr - oh, torch.clamp(2.0 * pr * (1 - pr), min=1e-16)
+    raise ValueError(f"unsupported objective {obj}")
+
+
+def _transform(obj: str, margin: torch.Tensor) -> torch.Tensor:
+    if obj in ("reg:logistic", "binary:logistic"):
+        return torch.sigmoid(margin)
+    if obj == "count:poisson":
+        return torch.exp(margin)
+    if obj == "multi:softprob":
+        return torch.softmax(margin, dim=1)
+    if obj == "multi:softmax":
+        return margin.argmax(dim=1).to(margin.dtype)
+    return margin
+
+
+def _base_margin(obj: str, y: torch.Tensor, base_score, world) -> float:
+    if obj.startswith("multi:"):
+        return 0.0
+    if base_score is None:
+        s = torch.tensor([float(y.sum()), float(y.numel())], dtype=torch.float64)
+        world.allreduce(s)
+        base_score = float(s[0] / max(float(s[1]), 1.0))
+        if obj in ("reg:logistic", "binary:logistic", "binary:logitraw"):
+            base_score = min(max(base_score, 1e-6), 1 - 1e-6)
+        if obj == "count:poisson":
+            base_score = max(base_score, 1e-6)
+    if obj in ("reg:logistic", "binary:logistic", "binary:logitraw"):
+        return math.log(base_score / (1 - base_score))
+    if obj == "count:poisson":
+        return math.log(base_score)
+    return float(base_score)
+
+
+def eval_metric(name: str, obj: str, margin: torch.Tensor, y: torch.Tensor, world) -> float:
+    """Globally reduced metric (sum/count all-reduced across workers)."""
+    pred = _transform(obj if obj != "multi:softmax" else "multi:softprob", margin)
+    if name == "rmse":
+        s = ((pred - y) ** 2).sum()
+    elif name == "mae":
+        s = (pred - y).abs().sum()
+    elif name == "logloss":
+        pr = pred.clamp(1e-7, 1 - 1e-7)
+        s = -(y * pr.log() + (1 - y) * (1 - pr).log()).sum()
+    elif name == "error":
+        s = ((pred > 0.5).to(y.dtype) != y).sum()
+    elif name == "mlogloss":
+        s = -pred.clamp_min(1e-7).log().gather(1, y.long()[:, None]).sum()
+    elif name == "merror":
+        s = (pred.argmax(1) != y.long()).sum()
+    elif name == "poisson-nloglik":
+        s = (pred - y * pred.clamp_min(1e-16).log() + torch.lgamma(y + 1)).sum()
+    else:
+        raise ValueError(f"unsupported eval_metric {name}")
+    t = torch.tensor([float(s), float(y.shape[0])], dtype=torch.float64)
+    world.allreduce(t)
+    v = float(t[0] / max(float(t[1]), 1.0))
+    return math.sqrt(v) if name == "rmse" else v
+
+
+def default_metric(obj: str) -> str:
+    return {"reg:squarederror": "rmse", "reg:logistic": "rmse", "binary:logistic": "logloss",
+            "binary:logitraw": "logloss", "count:poisson": "poisson-nloglik", "multi:softmax": "mlogloss",
+            "multi:softprob": "mlogloss"}[obj]
+
+
+# ------------------------------------------------------------------------- collectives ----
+class World:
+    """All-reduce / all-gather over ``torch.distributed`` when a process group is up."""
+
+    def __init__(self):
+        import torch.distributed as dist
+        self.dist = dist if dist.is_available() and dist.is_initialized() else None
+        self.size = self.dist.get_world_size() if self.dist else 1
+
+    def allreduce(self, t: torch.Tensor):
+        if self.dist is not None and self.size > 1:
+            dev = t.device
+            if self.dist.get_backend() == "nccl" and dev.type != "cuda":
+                c = t.cuda()
+                self.dist.all_reduce(c)
+                t.copy_(c.to(dev))
+            else:
+                self.dist.all_reduce(t)
+        return t
+
+    def allgather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        if self.dist is None or self.size == 1:
+            return t
+        n = torch.tensor([t.shape[0]], dtype=torch.int64)
+        ns = [torch.zeros_like(n) for _ in range(self.size)]
+        self.dist.all_gather(ns, n)
+        m = int(max(int(x) for x in ns))
+        pad = torch.full((m, t.shape[1]), float("nan"), dtype=t.dtype)
+        pad[:t.shape[0]] = t
+        outs = [torch.empty_like(pad) for _ in range(self.size)]
+        self.dist.all_gather(outs, pad)
+        return torch.cat([o[:int(k)] for o, k in zip(outs, ns)])
+
+
+# ---------------------------------------------------------------------------- binning ----
+def compute_cuts(x: torch.Tensor, max_bin: int, world: World, sample: int = 200_000, seed: int = 0) -> List[torch.Tensor]:
+    """Per-feature cut points from (all-gathered) quantiles; identical on every worker."""
+    g = torch.Generator().manual_seed(seed)
+    xs = x if x.shape[0] <= sample else x[torch.randperm(x.shape[0], generator=g)[:sample]]
+    xs = world.allgather_rows(xs.float().cpu())
+    qs = torch.linspace(0, 1, max_bin - 1, dtype=torch.float64)[1:-1]
+    cuts = []
+    for f in range(xs.shape[1]):
+        col = xs[:, f].double()
+        col = col[~torch.isnan(col)]
+        if col.numel() == 0:
+            cuts.append(torch.empty(0))
+            continue
+        u = torch.unique(col)
+        if u.numel() <= max_bin - 2:
+            # all distinct values: cut between neighbours so every value gets its own bin
+            c = (u[1:] + u[:-1]) / 2 if u.numel() > 1 else u[:0]
+            c = torch.cat([c, u[-1:] + torch.clamp(u[-1:].abs() * 1e-6, min=1e-6)])
+        else:
+            c = torch.unique(torch.quantile(col, qs))
+            c = torch.cat([c, u[-1:] + torch.clamp(u[-1:].abs() * 1e-6, min=1e-6)])
+        cuts.append(c.float())
+    return cuts
+
+
+def bin_matrix(x: torch.Tensor, cuts: List[torch.Tensor]) -> torch.Tensor:
+    """uint8/int16 bins: 0 = missing, 1 + #cuts <= x otherwise."""
+    n, f = x.shape
+    out = torch.empty((n, f), dtype=torch.int16, device=x.device)
+    for j in range(f):
+        col = x[:, j]
+        c = cuts[j].to(x.device)
+        b = torch.searchsorted(c, col.contiguous(), right=True) + 1
+        out[:, j] = torch.where(torch.isnan(col), torch.zeros_like(b), b).to(torch.int16)
+    return out
+
+
+# ------------------------------------------------------------------------------- trees ----
+class Tree:
+    """Flat arrays; node 0 is the root. ``feature < 0`` marks a leaf holding ``value``."""
+
+    def __init__(self):
+        self.feature: List[int] = []
+        self.cond: List[float] = []
+        self.left: List[int] = []
+        self.right: List[int] = []
+        self.default_left: List[bool] = []
+        self.value: List[float] = []
+        self.gain: List[float] = []
+        self.cover: List[float] = []
+
+    def add(self, value=0.0, cover=0.0) -> int:
+        self.feature.append(-1)
+        self.cond.append(0.0)
+        self.left.append(-1)
+        self.right.append(-1)
+        self.default_left.append(True)
+        self.value.append(value)
+        self.gain.append(0.0)
+        self.cover.append(cover)
+        return len(self.feature) - 1
+
+    def to_json(self) -> Dict:
+        return {k: getattr(self, k) for k in ("feature", "cond", "left", "right", "default_left", "value",
+                                              "gain", "cover")}
+
+    @classmethod
+    def from_json(cls, d: Dict) -> "Tree":
+        t = cls()
+        for k, v in d.items():
+            setattr(t, k, list(v))
+        return t
+
+    def tensors(self, device):
+        return (torch.tensor(self.feature, dtype=torch.long, device=device),
+                torch.tensor(self.cond, dtype=torch.float32, device=device),
+                torch.tensor(self.left, dtype=torch.long, device=device),
+                torch.tensor(self.right, dtype=torch.long, device=device),
+                torch.tensor(self.default_left, dtype=torch.bool, device=device),
+                torch.tensor(self.value, dtype=torch.float32, device=device))
+
+    def predict(self, x: torch.Tensor) -> torch.Tensor:
+        feat, cond, left, right, dleft, value = self.tensors(x.device)
+        node = torch.zeros(x.shape[0], dtype=torch.long, device=x.device)
+        for _ in range(64):
+            f = feat[node]
+            active = f >= 0
+            if not bool(active.any()):
+                break
+            v = x.gather(1, f.clamp_min(0)[:, None])[:, 0]
+            go_left = torch.where(torch.isnan(v), dleft[node], v < cond[node])
+            nxt = torch.where(go_left, left[node], right[node])
+            node = torch.where(active, nxt, node)
+        return value[node]
+
+    def dump(self, names: Sequence[str]) -> str:
+        lines = []
+
+        def rec(i, depth):
+            pad = "\t" * depth
+            if self.feature[i] < 0:
+                lines.append(f"{pad}{i}:leaf={self.value[i]:.6g}")
+                return
+            miss = self.left[i] if self.default_left[i] else self.right[i]
+            lines.append(f"{pad}{i}:[{names[self.feature[i]]}<{self.cond[i]:.6g}] yes={self.left[i]},"
+                         f"no={self.right[i]},missing={miss}")
+            rec(self.left[i], depth + 1)
+            rec(self.right[i], depth + 1)
+        rec(0, 0)
+        return "\n".join(lines) + "\n"
+
+
+def _soft(g, alpha):
+    if alpha <= 0:
+        return g
+    return torch.sign(g) * torch.clamp(g.abs() - alpha, min=0.0)
+
+
+def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: torch.Tensor, p: Dict,
+              world: World, feat_mask: Optional[torch.Tensor] = None) -> Tuple[Tree, torch.Tensor]:
+    """One tree on binned data; returns the tree and each row's leaf value (for margin update)."""
+    dev = bins.device
+    n, F = bins.shape
+    B = int(max(c.numel() for c in cuts) + 2) if cuts else 2
+    lam, alpha, gamma = float(p["lambda"]), float(p["alpha"]), float(p["gamma"])
+    mcw, eta, mds = float(p["min_child_weight"]), float(p["eta"]), float(p["max_delta_step"])
+    tree = Tree()
+    tree.add()
+    pos = torch.zeros(n, dtype=torch.long, device=dev)     # index into the current level's node list
+    level = [0]                                            # tree node ids of this level
+    leaf_of_row = torch.zeros(n, dtype=torch.long, device=dev)
+    feat_off = (torch.arange(F, device=dev) * B)[None, :]
+    bins_l = bins.long()
+    gh = torch.stack([g, h], 1).double()
+    ncuts = torch.tensor([c.numel() for c in cuts], device=dev)
+    for depth in range(int(p["max_depth"]) + 1):
+        K = len(level)
+        act = pos >= 0
+        idx = (pos.clamp_min(0)[:, None] * (F * B) + feat_off + bins_l)
+        hist = torch.zeros(K * F * B, 2, dtype=torch.float64, device=dev)
+        sel = idx[act].reshape(-1)
+        hist.index_add_(0, sel, gh[act].repeat_interleave(F, dim=0))
+        world.allreduce(hist)
+        hist = hist.view(K, F, B, 2)
+        tot = hist[:, 0, :, :].sum(1)                         # (K, 2) node totals
+        G, H = tot[:, 0], tot[:, 1]
+        for k, nid in enumerate(level):
+            tree.cover[nid] = float(H[k])
+            w = -_soft(G[k], alpha) / (H[k] + lam)
+            if mds > 0:
+                w = torch.clamp(w, -mds, mds)
+            tree.value[nid] = float(w) * eta
+        if depth == int(p["max_depth"]):
+            break
+        miss = hist[:, :, 0, :]                                # (K, F, 2)
+        cum = hist[:, :, 1:, :].cumsum(2)                      # bins 1..t go left
+        parent = (_soft(G, alpha) ** 2 / (H + lam))[:, None, None]
+        best_gain = torch.full((K,), -1.0, dtype=torch.float64, device=dev)
+        best = torch.zeros((K, 3), dtype=torch.long, device=dev)   # feature, threshold bin, default_left
+        for dl in (1, 0):
+            L = cum + (miss[:, :, None, :] if dl else 0)
+            R = tot[:, None, None, :] - L
+            gain = (_soft(L[..., 0], alpha) ** 2 / (L[..., 1] + lam) + _soft(R[..., 0], alpha) ** 2 / (R[..., 1] + lam)
+                    - parent)
+            valid = (L[..., 1] >= mcw) & (R[..., 1] >= mcw)
+            tpos = torch.arange(cum.shape[2], device=dev)[None, None, :]
+            valid &= tpos < ncuts[None, :, None]                 # threshold must be a real cut
+            if feat_mask is not None:
+                valid &= feat_mask[None, :, None]
+            gain = torch.where(valid, gain, torch.full_like(gain, -1.0))
+            flat = gain.reshape(K, -1)
+            gbest, arg = flat.max(1)
+            better = gbest > best_gain
+            best_gain = torch.where(better, gbest, best_gain)
+            f_b = torch.stack([arg // cum.shape[2], arg % cum.shape[2], torch.full_like(arg, dl)], 1)
+            best = torch.where(better[:, None], f_b, best)
+        new_level, remap = [], torch.full((K,), -1, dtype=torch.long, device=dev)
+        split_feat = torch.full((K,), -1, dtype=torch.long, device=dev)
+        split_bin = torch.zeros((K,), dtype=torch.long, device=dev)
+        split_dl = torch.zeros((K,), dtype=torch.bool, device=dev)
+        bg, bb = best_gain.cpu(), best.cpu()
+        for k, nid in enumerate(level):
+            if float(bg[k]) <= max(gamma, 1e-6):
+                continue
+            f, t, dl = int(bb[k, 0]), int(bb[k, 1]), bool(bb[k, 2])
+            tree.feature[nid] = f
+            tree.cond[nid] = float(cuts[f][t])                  # bins <= t+1  <=>  x < cuts[t]
+            tree.default_left[nid] = dl
+            tree.gain[nid] = float(bg[k])
+            tree.left[nid] = tree.add()
+            tree.right[nid] = tree.add()
+            remap[k] = len(new_level)
+            new_level += [tree.left[nid], tree.right[nid]]
+            split_feat[k], split_bin[k], split_dl[k] = f, t + 1, dl
+        # rows in nodes that became leaves keep their leaf id; others move down
+        cur = pos.clamp_min(0)
+        node_ids = torch.tensor(level, dtype=torch.long, device=dev)
+        leaf_rows = act & (remap[cur] < 0)
+        leaf_of_row = torch.where(leaf_rows, node_ids[cur], leaf_of_row)
+        if not new_level:
+            pos = torch.full_like(pos, -1)
+            level = []
+            break
+        f = split_feat[cur]
+        b = bins_l.gather(1, f.clamp_min(0)[:, None])[:, 0]
+        go_left = torch.where(b == 0, split_dl[cur], b <= split_bin[cur])
+        child = remap[cur] + (~go_left).long()
+        pos = torch.where(act & (remap[cur] >= 0), child, torch.full_like(pos, -1))
+        level = new_level
+    if level:
+        node_ids = torch.tensor(level, dtype=torch.long, device=dev)
+        act = pos >= 0
+        leaf_of_row = torch.where(act, node_ids[pos.clamp_min(0)], leaf_of_row)
+    values = torch.tensor(tree.value, dtype=torch.float32, device=dev)
+    return tree, values[leaf_of_row]
+
+
+# ----------------------------------------------------------------------------- booster ----
+class Booster:
+    """Trained ensemble (subset of ``xgboost.Booster``)."""
+
+    def __init__(self, params: Optional[Dict] = None, model_file: Optional[str] = None):
+        self.params = normalize_params(params)
+        self.trees: List[List[Tree]] = []        # per round, one tree per output group
+        self.base_margin = 0.0
+        self.feature_names: Optional[List[str]] = None
+        self.evals_result: Dict = {}
+        if model_file is not None:
+            self.load_model(model_file)
+
+    @property
+    def num_group(self) -> int:
+        return int(self.params["num_class"]) if self.params["objective"].startswith("multi:") else 1
+
+    def num_boosted_rounds(self) -> int:
+        return len(self.trees)
+
+    def num_features(self) -> int:
+        return len(self.feature_names or [])
+
+    def _margin(self, x: torch.Tensor, iteration_range=None) -> torch.Tensor:
+        lo, hi = iteration_range if iteration_range else (0, len(self.trees))
+        k = self.num_group
+        m = torch.full((x.shape[0], k), self.base_margin, dtype=torch.float32, device=x.device)
+        for rnd in self.trees[lo:hi]:
+            for j, t in enumerate(rnd):
+                m[:, j] += t.predict(x)
+        return m if k > 1 else m[:, 0]
+
+    def predict(self, data, output_margin: bool = False, iteration_range=None):
+        x = data.data if isinstance(data, DMatrix) else torch.as_tensor(np.asarray(data, dtype=np.float32))
+        if x.dim() == 1:
+            x = x[None, :]
+        m = self._margin(x, iteration_range)
+        out = m if output_margin else _transform(self.params["objective"], m)
+        return out.cpu().numpy()
+
+    def inplace_predict(self, data, iteration_range=None, predict_type: str = "value"):
+        import pandas as pd
+        if isinstance(data, pd.DataFrame):
+            data = data.to_numpy(dtype=np.float32, na_value=np.nan)
+        return self.predict(np.asarray(data, dtype=np.float32), output_margin=predict_type == "margin",
+                            iteration_range=iteration_range)
+
+    def get_dump(self, with_stats: bool = False) -> List[str]:
+        names = self.feature_names or [f"f{i}" for i in range(1000)]
+        return [t.dump(names) for rnd in self.trees for t in rnd]
+
+    def get_score(self, importance_type: str = "weight") -> Dict[str, float]:
+        names = self.feature_names or []
+        acc: Dict[str, List[float]] = {}
+        for rnd in self.trees:
+            for t in rnd:
+                for f, gn, cv in zip(t.feature, t.gain, t.cover):
+                    if f >= 0:
+                        v = {"weight": 1.0, "gain": gn, "total_gain": gn, "cover": cv, "total_cover": cv}[importance_type]
+                        acc.setdefault(names[f] if f < len(names) else f"f{f}", []).append(v)
+        if importance_type in ("gain", "cover"):
+            return {k: float(np.mean(v)) for k, v in acc.items()}
+        return {k: float(np.sum(v)) for k, v in acc.items()}
+
+    def save_model(self, fname: str):
+        with open(fname, "w") as f:
+            json.dump(self.to_json(), f)
+
+    def to_json(self) -> Dict:
+        return {"format": "raydp-gbdt-1", "params": self.params, "base_margin": self.base_margin,
+                "feature_names": self.feature_names, "trees": [[t.to_json() for t in rnd] for rnd in self.trees]}
+
+    def load_model(self, fname: str):
+        with open(fname) as f:
+            d = json.load(f)
+        self.params = normalize_params(d["params"])
+        self.base_margin = float(d["base_margin"])
+        self.feature_names = d.get("feature_names")
+        self.trees = [[Tree.from_json(t) for t in rnd] for rnd in d["trees"]]
+        return self
+
+    def save_raw(self) -> bytes:
+        return json.dumps(self.to_json()).encode()
+
+
+def train(params: Dict, dtrain: DMatrix, num_boost_round: int = 10, evals: Sequence = (),
+          evals_result: Optional[Dict] = None, device: Optional[str] = None, verbose_eval: bool = False,
+          callback=None) -> Booster:
+    """Boost ``num_boost_round`` rounds; histograms all-reduced when a process group is up."""
+    p = normalize_params(params)
+    if "num_boost_round" in (params or {}):
+        num_boost_round = int(params["num_boost_round"])
+    world = World()
+    dev = torch.device(device) if device else (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+    obj = p["objective"]
+    k = int(p["num_class"]) if obj.startswith("multi:") else 1
+    x = dtrain.data
+    y = dtrain.label.to(dev)
+    cuts = compute_cuts(x, int(p["max_bin"]), world, seed=int(p["seed"]))
+    bins = bin_matrix(x.to(dev), cuts)
+    bst = Booster(p)
+    bst.feature_names = dtrain.feature_names
+    bst.base_margin = _base_margin(obj, dtrain.label, p["base_score"], world)
+    margin = torch.full((x.shape[0], k), bst.base_margin, dtype=torch.float32, device=dev)
+    if k == 1:
+        margin = margin[:, 0]
+    ev = [(d.data.to(dev), d.label.to(dev), name) for d, name in evals]
+    ev_margin = [torch.full((d[0].shape[0], k) if k > 1 else (d[0].shape[0],), bst.base_margin, device=dev)
+                 for d in ev]
+    metrics = p.get("eval_metric") or default_metric(obj)
+    metrics = [metrics] if isinstance(metrics, str) else list(metrics)
+    res = evals_result if evals_result is not None else {}
+    for _, _, name in ev:
+        res.setdefault(name, {m: [] for m in metrics})
+    gen = torch.Generator(device="cpu").manual_seed(int(p["seed"]))
+    for rnd in range(num_boost_round):
+        g, h = _grad_hess(obj, margin, y, p)
+        if dtrain.weight is not None:
+            w = dtrain.weight.to(dev)
+            g, h = (g * w[:, None], h * w[:, None]) if k > 1 else (g * w, h * w)
+        if float(p["subsample"]) < 1.0:
+            keep = (torch.rand(x.shape[0], generator=gen) < float(p["subsample"])).to(dev)
+            keep = keep[:, None] if k > 1 else keep
+            g, h = g * keep, h * keep
+        fmask = None
+        if float(p["colsample_bytree"]) < 1.0:
+            nf = max(1, int(round(float(p["colsample_bytree"]) * x.shape[1])))
+            fmask = torch.zeros(x.shape[1], dtype=torch.bool)
+            fmask[torch.randperm(x.shape[1], generator=gen)[:nf]] = True
+            fmask = fmask.to(dev)
+        rtrees = []
+        for j in range(k):
+            gj, hj = (g[:, j], h[:, j]) if k > 1 else (g, h)
+            tree, leaf_vals = grow_tree(bins, cuts, gj, hj, p, world, fmask)
+            rtrees.append(tree)
+            if k > 1:
+                margin[:, j] += leaf_vals
+            else:
+                margin += leaf_vals
+            for i, (xe, _, _) in enumerate(ev):
+                if k > 1:
+                    ev_margin[i][:, j] += tree.predict(xe)
+                else:
+                    ev_margin[i] += tree.predict(xe)
+        bst.trees.append(rtrees)
+        for i, (_, ye, name) in enumerate(ev):
+            for m in metrics:
+                res[name][m].append(eval_metric(m, obj, ev_margin[i], ye, world))
+        if verbose_eval and ev:
+            print(f"[{rnd}] " + "\t".join(f"{n}-{m}:{res[n][m][-1]:.5f}" for _, _, n in ev for m in metrics))
+        if callback is not None:
+            callback(rnd, bst, res)
+    bst.evals_result = res
+    return bst
