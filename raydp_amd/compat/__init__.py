@@ -62,6 +62,14 @@ def install_ray():
     client = _mod("ray.util.client")
     client.ray = types.SimpleNamespace(is_connected=lambda: False)
     util.client = client
+    state = importlib.import_module("raydp_amd.runtime.state")
+    sys.modules["ray.util.state"] = state
+    util.state = state
+    from raydp_amd.runtime.actors import ActorDiedError
+    exc = _mod("ray.exceptions", RayActorError=ActorDiedError, ActorDiedError=ActorDiedError,
+               ObjectLostError=runtime.objects.ObjectLostError, RayTaskError=Exception)
+    ray.exceptions = exc
+    ray.actor = _mod("ray.actor", ActorHandle=api.ActorHandle, ActorClass=api.ActorClass)
     cu = _mod("ray.cluster_utils", Cluster=Cluster)
     ray.cluster_utils = cu
     ray.train = train

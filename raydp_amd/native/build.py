@@ -26,14 +26,23 @@ def _hip_sources():
 
 def _runtime_sources():
     d = os.path.join(CSRC, "runtime")
-    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".cc"))
+    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".cc") and f not in _EXE_SOURCES)
+
+
+_EXE_SOURCES = {"supervisor.cc"}
 
 
 LIBS = {
     "exec_kernels": dict(kind="cpu", sources=lambda: [os.path.join(CSRC, "exec", "exec_kernels.cc")]),
     "raydp_runtime": dict(kind="cpu", sources=_runtime_sources, libs=["-lpthread", "-lrt", "-ldl"]),
     "hipkernels": dict(kind="hip", sources=_hip_sources),
+    # executable: the per-node actor supervisor (csrc/runtime/supervisor.cc)
+    "raydp_supervisor": dict(kind="exe", sources=lambda: [os.path.join(CSRC, "runtime", "supervisor.cc")]),
 }
+
+
+def out_path(name: str) -> str:
+    return os.path.join(HERE, name if LIBS[name]["kind"] == "exe" else f"lib{name}.so")
 
 
 def _run(cmd):
@@ -58,12 +67,15 @@ def _newer(out, srcs):
 def build_one(name: str, force: bool = False) -> str:
     spec = LIBS[name]
     srcs = spec["sources"]()
-    out = os.path.join(HERE, f"lib{name}.so")
+    out = out_path(name)
     if not force and _newer(out, srcs):
         return out
     tmp = out + f".tmp{os.getpid()}"
     inc = ["-I", os.path.join(CSRC, "common"), "-I", CSRC]
-    if spec["kind"] == "cpu":
+    if spec["kind"] == "exe":
+        cxx = shutil.which("g++") or "c++"
+        _run([cxx, "-O2", "-std=c++17", "-Wall"] + inc + srcs + ["-o", tmp])
+    elif spec["kind"] == "cpu":
         cxx = shutil.which("g++") or "c++"
         cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-function"] + \
             inc + srcs + ["-o", tmp] + spec.get("libs", [])

@@ -36,5 +36,17 @@ def load(name: str, build_if_missing: bool = True):
         return lib
 
 
+def executable(name: str, build_if_missing: bool = True) -> str:
+    """Path of an in-tree native executable (built on first use)."""
+    from raydp_amd.native import build
+    path = build.out_path(name)
+    with _lock:
+        if build_if_missing and not build._newer(path, build.LIBS[name]["sources"]()):
+            build.build_one(name)
+    if not os.path.exists(path):
+        raise ImportError(f"native executable {path} is not built")
+    return path
+
+
 def is_built(name: str) -> bool:
     return os.path.exists(lib_path(name))

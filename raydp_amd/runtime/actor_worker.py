@@ -1,0 +1,136 @@
+"""Entry point of an actor process (``python -m raydp_amd.runtime.actor_worker``).
+
+Started by the native supervisor with ``RAYDP_ACTOR_ID`` / ``RAYDP_SESSION_DIR`` /
+``RAYDP_STORE_PATH`` / ``RAYDP_NODE_ID`` / ``RAYDP_SUPERVISOR_SOCK`` in its environment. It
+attaches to the node (object store + supervisor), rebuilds the actor instance from the spec
+file the creator wrote (so a supervisor restart re-runs the constructor, Ray's actor-restart
+semantics), then serves method calls on a Unix-domain socket:
+
+    request  = frame(dumps((call_id, method, args, kwargs)))
+    reply    = frame(dumps((call_id, ok, value_or_(exception, traceback))))
+
+Calls run on a pool of ``max_concurrency`` threads (1 = strictly sequential, Ray's default for
+actors). ``__ray_terminate__`` exits cleanly (status 0: never restarted). A constructor
+failure is written to ``<id>.err`` and the process exits 0 so it is not restarted.
+"""
+import os
+import socket
+import struct
+import sys
+import threading
+import traceback
+from concurrent.futures import ThreadPoolExecutor
+
+
+def _recv_exact(conn, n):
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = conn.recv(n - len(buf))
+        if not chunk:
+            raise ConnectionError
+        buf += chunk
+    return bytes(buf)
+
+
+def send_frame(conn, lock, data: bytes):
+    with lock:
+        conn.sendall(struct.pack("<Q", len(data)) + data)
+
+
+def recv_frame(conn) -> bytes:
+    (n,) = struct.unpack("<Q", _recv_exact(conn, 8))
+    return _recv_exact(conn, n)
+
+
+class _Exit(BaseException):
+    pass
+
+
+def actor_paths(session_dir: str, actor_id: str):
+    d = os.path.join(session_dir, "actors")
+    return (os.path.join(d, f"{actor_id}.spec"), os.path.join(d, f"{actor_id}.sock"),
+            os.path.join(d, f"{actor_id}.err"))
+
+
+def main() -> int:
+    aid = os.environ["RAYDP_ACTOR_ID"]
+    sdir = os.environ["RAYDP_SESSION_DIR"]
+    from raydp_amd.runtime import core
+    core.attach_from_env()
+    from raydp_amd.runtime import serialization as S
+    spec_path, sock_path, err_path = actor_paths(sdir, aid)
+    import cloudpickle
+    with open(spec_path, "rb") as f:
+        cls, args, kwargs, opts = cloudpickle.load(f)
+    os.environ["RAYDP_ACTOR_NAME"] = opts.get("name") or ""
+    try:
+        instance = cls(*args, **kwargs)
+    except BaseException as e:  # noqa: BLE001
+        with open(err_path + ".tmp", "wb") as f:
+            try:
+                cloudpickle.dump((e, traceback.format_exc()), f)
+            except Exception:  # unpicklable exception
+                cloudpickle.dump((RuntimeError(repr(e)), traceback.format_exc()), f)
+        os.replace(err_path + ".tmp", err_path)
+        return 0
+    pool = ThreadPoolExecutor(max_workers=int(opts.get("max_concurrency") or 1),
+                              thread_name_prefix=f"actor-{aid[:6]}")
+    tmp = sock_path + ".tmp"
+    for p in (tmp,):
+        if os.path.exists(p):
+            os.unlink(p)
+    srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    srv.bind(tmp)
+    srv.listen(64)
+    os.replace(tmp, sock_path)     # the socket appears atomically once we can accept
+    exiting = threading.Event()
+
+    def run_call(conn, lock, call_id, method, a, k):
+        if method == "__ray_terminate__":
+            send_frame(conn, lock, S.dumps((call_id, True, None)))
+            exiting.set()
+            os._exit(0)
+        try:
+            if method == "__ray_ready__":
+                v = True
+            elif method == "__ray_call__":   # run an arbitrary fn(instance, *args)
+                v = a[0](instance, *a[1:], **k)
+            else:
+                v = getattr(instance, method)(*a, **k)
+            payload = S.dumps((call_id, True, v))
+        except SystemExit as e:
+            send_frame(conn, lock, S.dumps((call_id, True, None)))
+            os._exit(int(e.code or 0))
+        except BaseException as e:  # noqa: BLE001
+            tb = traceback.format_exc()
+            try:
+                payload = S.dumps((call_id, False, (e, tb)))
+            except Exception:  # noqa: BLE001
+                payload = S.dumps((call_id, False, (RuntimeError(repr(e)), tb)))
+        try:
+            send_frame(conn, lock, payload)
+        except OSError:
+            pass
+
+    def serve(conn):
+        lock = threading.Lock()
+        try:
+            while True:
+                call_id, method, a, k = S.loads(recv_frame(conn))
+                pool.submit(run_call, conn, lock, call_id, method, a, k)
+        except (ConnectionError, OSError, EOFError):
+            pass
+        finally:
+            try:
+                conn.close()
+            except OSError:
+                pass
+
+    while not exiting.is_set():
+        conn, _ = srv.accept()
+        threading.Thread(target=serve, args=(conn,), daemon=True).start()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

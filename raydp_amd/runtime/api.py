@@ -11,6 +11,7 @@ semantics used by RayDP (``raydp-executor-<id>``, ``<app>_SPARK_MASTER``).
 """
 import concurrent.futures as cf
 import inspect
+import os
 import threading
 import uuid
 from typing import Any, Dict, List, Optional
@@ -119,12 +120,24 @@ class ActorMethod:
         return self
 
 
+class ActorID(str):
+    """Actor id (``ray.ActorID``-like: ``.hex()``)."""
+
+    def hex(self):
+        return str(self)
+
+
 class ActorHandle:
     def __init__(self, impl, name=None, namespace=None):
         self._impl = impl
         self._actor_name = name
         self._namespace = namespace
-        self._actor_id = uuid.uuid4().hex
+        self._actor_id = ActorID(getattr(impl, "actor_id", None) or uuid.uuid4().hex)
+
+    def __reduce__(self):
+        if getattr(self._impl, "sock_path", None) is None:
+            raise TypeError("in-process (thread) actor handles cannot leave their process")
+        return (_attach_handle, (self._actor_id, self._actor_name, self._namespace))
 
     def __getattr__(self, item):
         if item.startswith("_"):
@@ -192,12 +205,80 @@ class ActorClass:
                     if self._opts.get("get_if_exists"):
                         return _named[(ns, name)]
                     raise ValueError(f"actor name {name!r} already taken in namespace {ns!r}")
-        impl = _ThreadActor(self._cls, args, kwargs, self._opts)
+        if name and _named_file(ns, name) is not None and os.path.exists(_named_file(ns, name)):
+            existing = _lookup_named_file(ns, name)
+            if existing is not None and not existing._impl.dead:
+                if self._opts.get("get_if_exists"):
+                    return existing
+                raise ValueError(f"actor name {name!r} already taken in namespace {ns!r}")
+        if _isolation(self._opts) == "process":
+            impl = core.current_node().actors.create(self._cls, args, kwargs, self._opts, name, ns)
+        else:
+            impl = _ThreadActor(self._cls, args, kwargs, self._opts)
         h = ActorHandle(impl, name, ns)
         if name:
             with _registry_lock:
                 _named[(ns, name)] = h
+            if getattr(impl, "sock_path", None) is not None:
+                _write_named_file(ns, name, impl.actor_id)
         return h
+
+
+def _isolation(opts) -> str:
+    iso = opts.get("isolation") or os.environ.get("RAYDP_ACTOR_ISOLATION", "process")
+    if iso not in ("process", "thread"):
+        raise ValueError(f"isolation must be 'process' or 'thread', got {iso!r}")
+    return iso
+
+
+def _named_file(ns, name):
+    n = core.current_node()
+    if n is None or not n.session_dir:
+        return None
+    safe = "".join(c if c.isalnum() or c in "-_." else "_" for c in f"{ns}__{name}")
+    return os.path.join(n.session_dir, "named", safe)
+
+
+def _write_named_file(ns, name, actor_id):
+    p = _named_file(ns, name)
+    os.makedirs(os.path.dirname(p), exist_ok=True)
+    with open(p + ".tmp", "w") as f:
+        f.write(actor_id)
+    os.replace(p + ".tmp", p)
+
+
+def _remove_named_file(ns, name):
+    p = _named_file(ns, name)
+    if p is not None and os.path.exists(p):
+        try:
+            os.unlink(p)
+        except OSError:
+            pass
+
+
+def _lookup_named_file(ns, name) -> Optional["ActorHandle"]:
+    p = _named_file(ns, name)
+    if p is None or not os.path.exists(p):
+        return None
+    with open(p) as f:
+        aid = f.read().strip()
+    return _attach_handle(aid, name, ns)
+
+
+def _attach_handle(actor_id, name=None, namespace=None) -> "ActorHandle":
+    """Handle to an existing process actor (possibly created by another process)."""
+    if not core.is_initialized():
+        core.init()
+    mgr = core.current_node().actors
+    with mgr._lock:
+        impl = mgr.actors.get(actor_id)
+    if impl is None:
+        from raydp_amd.runtime.actors import ProcessActor
+        impl = ProcessActor(mgr, actor_id, name, namespace or "default", {}, owned=False)
+        with mgr._lock:
+            mgr.actors[actor_id] = impl
+        _ = mgr.supervisor  # subscribe to death events
+    return ActorHandle(impl, name, namespace)
 
 
 def remote(*args, **kwargs):
@@ -220,6 +301,8 @@ def get_actor(name: str, namespace: Optional[str] = None) -> ActorHandle:
     ns = namespace or core.get_runtime_context().namespace
     with _registry_lock:
         h = _named.get((ns, name))
+    if h is None:
+        h = _lookup_named_file(ns, name)
     if h is None:
         from raydp_amd.spark.executor_registry import lookup_executor
         h = lookup_executor(name)
@@ -247,10 +330,14 @@ def list_named():
 
 def kill(actor: ActorHandle, no_restart: bool = True):
     actor._kill(no_restart)
-    with _registry_lock:
-        for k, v in list(_named.items()):
-            if v is actor:
-                _named.pop(k)
+    if no_restart:
+        with _registry_lock:
+            for k, v in list(_named.items()):
+                if v is actor or v._actor_id == actor._actor_id:
+                    _named.pop(k)
+                    _remove_named_file(*k)
+        if actor._actor_name:
+            _remove_named_file(actor._namespace or core.get_runtime_context().namespace, actor._actor_name)
 
 
 def wait(refs: List[ObjectRef], num_returns: int = 1, timeout: Optional[float] = None,

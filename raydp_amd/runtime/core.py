@@ -68,6 +68,52 @@ def current_node_store():
     return None if n is None else n.store
 
 
+_stores_lock = threading.Lock()
+_attached_stores: Dict[str, object] = {}
+
+
+def store_for(node_id: Optional[str], path: Optional[str] = None):
+    """Object store of ``node_id`` as seen from this process (attaching by path if needed).
+
+    Returns None when that node's arena no longer exists (node removed)."""
+    n = _node
+    if n is None:
+        return None
+    if node_id is None or node_id == n.store.node_id:
+        return n.store
+    vn = n.cluster.nodes.get(node_id) if n.cluster is not None else None
+    if vn is not None:
+        return vn.store if vn.alive else None
+    if not path and n.session_dir:
+        f = os.path.join(n.session_dir, "nodes", node_id)
+        if os.path.exists(f):
+            with open(f) as fh:
+                path = fh.read().strip()
+    with _stores_lock:
+        st = _attached_stores.get(node_id)
+        if st is None and path:
+            if not os.path.exists(path):
+                return None
+            from raydp_amd.runtime.store import attach_store
+            try:
+                st = attach_store(path, node_id)
+            except OSError:
+                return None
+            _attached_stores[node_id] = st
+        return st
+
+
+def attach_from_env():
+    """Worker-process mode: join the node described by ``RAYDP_*`` environment variables."""
+    global _node
+    with _lock:
+        if _node is None:
+            from raydp_amd.runtime.node import Node
+            _node = Node.attach(os.environ["RAYDP_SESSION_DIR"], os.environ["RAYDP_STORE_PATH"],
+                                os.environ["RAYDP_NODE_ID"], os.environ.get("RAYDP_NAMESPACE"))
+        return _node
+
+
 def init(address=None, num_cpus=None, num_gpus=None, resources=None, object_store_memory=None,
          namespace=None, include_dashboard=False, ignore_reinit_error=True, logging_level=None,
          job_config=None, **kwargs):
@@ -78,6 +124,11 @@ def init(address=None, num_cpus=None, num_gpus=None, resources=None, object_stor
                 return _node.info()
             raise RuntimeError("runtime already initialized")
         from raydp_amd.runtime.node import Node
+        if os.environ.get("RAYDP_SESSION_DIR") and os.environ.get("RAYDP_STORE_PATH"):
+            # inside an actor process: join the existing node instead of starting one
+            _node = Node.attach(os.environ["RAYDP_SESSION_DIR"], os.environ["RAYDP_STORE_PATH"],
+                                os.environ["RAYDP_NODE_ID"], os.environ.get("RAYDP_NAMESPACE"))
+            return _node.info()
         _node = Node.create(address=address, num_cpus=num_cpus, num_gpus=num_gpus,
                             resources=resources, object_store_memory=object_store_memory,
                             namespace=namespace)
@@ -93,6 +144,10 @@ def shutdown():
         n.shutdown()
     with _lock:
         _pending.clear()
+    with _stores_lock:
+        for st in _attached_stores.values():
+            st.close()
+        _attached_stores.clear()
 
 
 def get_runtime_context() -> RuntimeContext:

@@ -134,6 +134,27 @@ class Node:
         self.store = None
         self.supervisor = None
         self.actors = None
+        self.attached = False
+
+    @classmethod
+    def attach(cls, session_dir: str, store_path: str, node_id: str, namespace=None) -> "Node":
+        """A worker process's view of an existing node (its store arena, supervisor, session)."""
+        from raydp_amd.runtime.actors import ActorManager
+        from raydp_amd.runtime.store import attach_store
+        n = cls(namespace)
+        n.attached = True
+        n.node_id = os.environ.get("RAYDP_HEAD_NODE_ID", node_id)
+        n.session_dir = session_dir
+        n.store = attach_store(store_path, node_id)
+        import json
+        res_file = os.path.join(session_dir, "node_resources.json")
+        res = {"CPU": float(os.cpu_count() or 1)}
+        if os.path.exists(res_file):
+            with open(res_file) as f:
+                res = json.load(f)
+        n.cluster.add(VirtualNode(node_id, res, n.store))
+        n.actors = ActorManager(n)
+        return n
 
     @classmethod
     def create(cls, address=None, num_cpus=None, num_gpus=None, resources=None,
@@ -147,6 +168,10 @@ class Node:
         head = VirtualNode(n.node_id, _default_resources(num_cpus, num_gpus, memory, resources),
                            n.store)
         n.cluster.add(head)
+        n._record_store(n.store)
+        import json
+        with open(os.path.join(n.session_dir, "node_resources.json"), "w") as f:
+            json.dump(head.total, f)
         from raydp_amd.runtime.actors import ActorManager
         n.actors = ActorManager(n)
         return n
@@ -158,7 +183,14 @@ class Node:
         store = open_store(nid, object_store_memory, self.session_dir)
         vn = VirtualNode(nid, _default_resources(num_cpus, num_gpus, memory or (2 << 30), resources), store)
         self.cluster.add(vn)
+        self._record_store(store)
         return vn
+
+    def _record_store(self, store):
+        d = os.path.join(self.session_dir, "nodes")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, store.node_id), "w") as f:
+            f.write(store.path)
 
     def remove_virtual_node(self, node_id: str):
         vn = self.cluster.nodes[node_id]
@@ -167,6 +199,10 @@ class Node:
             self.actors.on_node_removed(node_id)
         if vn.store is not None and vn.store is not self.store:
             vn.store.destroy()
+            try:
+                os.unlink(os.path.join(self.session_dir, "nodes", node_id))
+            except OSError:
+                pass
 
     def info(self):
         return {"node_id": self.node_id, "address": self.address, "session_dir": self.session_dir,
@@ -175,8 +211,14 @@ class Node:
     def shutdown(self):
         if self.actors is not None:
             self.actors.shutdown()
+        if self.attached:
+            self.store.close()
+            return
         for vn in list(self.cluster.nodes.values()):
             if vn.store is not None:
                 vn.store.destroy()
         from raydp_amd.runtime import pgroup as pg
         pg._reset()
+        if self.session_dir and not os.environ.get("RAYDP_KEEP_SESSION_DIR"):
+            import shutil
+            shutil.rmtree(self.session_dir, ignore_errors=True)

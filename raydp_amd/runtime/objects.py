@@ -79,8 +79,11 @@ def put(value: Any, _owner: str = "driver", _lineage=None) -> ObjectRef:
     return ref
 
 
-def put_with_id(oid: str, value: Any):
-    store = _store()
+def put_with_id(oid: str, value: Any, node_id: Optional[str] = None):
+    from raydp_amd.runtime.core import store_for
+    store = store_for(node_id) if node_id is not None else _store()
+    if store is None:
+        store = _store()
     if store is not None:
         store.put(oid, value)
     else:
@@ -89,7 +92,8 @@ def put_with_id(oid: str, value: Any):
 
 
 def contains(ref: ObjectRef) -> bool:
-    store = _store()
+    from raydp_amd.runtime.core import store_for
+    store = store_for(ref.node_id) if ref.node_id is not None else _store()
     if store is not None and store.contains(ref.id):
         return True
     with _local_lock:
@@ -105,7 +109,8 @@ def get(ref, timeout: Optional[float] = None):
     pending = core.pending_result(ref)
     if pending is not None:
         return pending.result(timeout)
-    store = _store()
+    from raydp_amd.runtime.core import store_for
+    store = store_for(ref.node_id) if ref.node_id is not None else _store()
     if store is not None:
         found, value = store.get(ref.id)
         if found:
@@ -117,6 +122,8 @@ def get(ref, timeout: Optional[float] = None):
         # reconstruct from lineage (re-run the producing task) and re-seal under the same id
         value = ref._lineage()
         put_with_id(ref.id, value)
+        st = _store()
+        ref.node_id = st.node_id if st is not None else None
         return value
     raise ObjectLostError(f"object {ref.id} is lost and has no lineage to reconstruct it")
 
@@ -124,8 +131,9 @@ def get(ref, timeout: Optional[float] = None):
 def free(refs):
     if isinstance(refs, ObjectRef):
         refs = [refs]
-    store = _store()
+    from raydp_amd.runtime.core import store_for
     for r in refs:
+        store = store_for(r.node_id) if r.node_id is not None else _store()
         if store is not None:
             store.delete(r.id)
         with _local_lock:

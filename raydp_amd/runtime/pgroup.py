@@ -86,6 +86,14 @@ def get_placement_group(name: str) -> PlacementGroup:
     raise ValueError(f"placement group {name} not found")
 
 
+def get_placement_group_by_id(pg_id: str) -> PlacementGroup:
+    with _lock:
+        g = _groups.get(pg_id)
+    if g is None or g.state == "REMOVED":
+        raise ValueError(f"placement group {pg_id} not found")
+    return g
+
+
 def placement_group_table(pg: Optional[PlacementGroup] = None):
     with _lock:
         items = {k: {"placement_group_id": k, "name": g.name, "strategy": g.strategy,

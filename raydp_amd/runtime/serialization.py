@@ -1,0 +1,171 @@
+"""Cross-process serialization with Arrow data passed through the shared-memory store.
+
+``dumps`` is cloudpickle with a ``reducer_override``: every ``pyarrow.Table``/``RecordBatch``
+above a small threshold is written once into the node's object store (Arrow IPC straight into
+the arena) and pickled as a 32-byte id; ``loads`` maps it back zero-copy. Tables that were
+themselves read from the store are passed by their existing id without a copy. This is how
+task closures (plans holding materialised partitions), task results and actor-call arguments
+move between the driver and actor processes (Ray does the same with plasma-backed
+``ObjectRef`` arguments; reference: Arrow blocks in ``python/raydp/spark/dataset.py:54-84``).
+
+Ownership: ``transfer=True`` objects are deleted by the (single) consumer right after it maps
+them (the mapping pins the memory, so the bytes stay valid for as long as the table lives);
+with ``transfer=False`` the producer keeps the ids (``Payload.oids``) and frees them after
+all consumers are done (broadcast of one stage closure to many executors).
+"""
+import io
+import threading
+import uuid
+import weakref
+from typing import Any, List, Optional, Tuple
+
+import cloudpickle
+import pyarrow as pa
+
+THRESHOLD = 64 * 1024
+_views_lock = threading.Lock()
+_views = {}   # id(table) -> (weakref(table), oid): tables mapped from the store
+
+
+def remember_view(table, oid: str):
+    try:
+        r = weakref.ref(table, lambda _r, k=id(table): _forget(k))
+    except TypeError:
+        return
+    with _views_lock:
+        _views[id(table)] = (r, oid)
+
+
+def _forget(k):
+    with _views_lock:
+        _views.pop(k, None)
+
+
+def _view_oid(table) -> Optional[str]:
+    with _views_lock:
+        e = _views.get(id(table))
+    if e is not None and e[0]() is table:
+        return e[1]
+    return None
+
+
+def _store():
+    from raydp_amd.runtime import core
+    return core.current_node_store()
+
+
+def _store_of(node_id: str, path: str):
+    from raydp_amd.runtime import core
+    st = core.store_for(node_id, path)
+    if st is None:
+        from raydp_amd.runtime.objects import ObjectLostError
+        raise ObjectLostError(f"object store of node {node_id} is gone")
+    return st
+
+
+def _adopt(st, v, node_id: str, path: str, oid: str):
+    """Make ``v`` (a view of store object ``oid``) its owner: the object is deleted when the
+    view is collected (deferred by the store while other processes still pin it)."""
+    remember_view(v, (node_id, path, oid))
+    weakref.finalize(v, _delete_quietly, st, oid)
+    return v
+
+
+def _delete_quietly(st, oid):
+    try:
+        if st._h is not None:
+            st.delete(oid)
+    except Exception:  # noqa: BLE001
+        pass
+
+
+def _load_owned(node_id: str, path: str, oid: str):
+    """Consumer side of a transferred table: map zero-copy and take ownership of the entry."""
+    st = _store_of(node_id, path)
+    found, v = st.get(oid)
+    if not found:
+        raise RuntimeError(f"transferred object {oid} missing from the store")
+    if isinstance(v, pa.Table):
+        return _adopt(st, v, node_id, path, oid)
+    st.delete(oid)
+    return v
+
+
+def share_table(t: pa.Table) -> pa.Table:
+    """Copy ``t`` into the node's store once and return the owning zero-copy view: later
+    pickles of the view travel as a reference (used for driver-side source tables)."""
+    st = _store()
+    if st is None or not isinstance(t, pa.Table) or _view_oid(t) is not None:
+        return t
+    oid = uuid.uuid4().hex
+    st.put(oid, t)
+    found, v = st.get(oid)
+    return _adopt(st, v, st.node_id, st.path, oid)
+
+
+def _load_shared(node_id: str, path: str, oid: str):
+    st = _store_of(node_id, path)
+    found, v = st.get(oid)
+    if not found:
+        raise RuntimeError(f"shared object {oid} missing from the store")
+    remember_view(v, (node_id, path, oid))
+    return v
+
+
+class _Pickler(cloudpickle.CloudPickler):
+    def __init__(self, f, transfer: bool):
+        super().__init__(f, protocol=5)
+        self.transfer = transfer
+        self.oids: List[str] = []
+        self.store = _store()
+
+    def reducer_override(self, obj):
+        if self.store is not None and isinstance(obj, (pa.Table, pa.RecordBatch)) and obj.nbytes >= THRESHOLD:
+            existing = _view_oid(obj)
+            if existing is not None:
+                return _load_shared, existing
+            oid = uuid.uuid4().hex
+            self.store.put(oid, obj)
+            key = (self.store.node_id, self.store.path, oid)
+            if self.transfer:
+                return _load_owned, key
+            self.oids.append(oid)
+            return _load_shared, key
+        return super().reducer_override(obj)
+
+
+class Payload:
+    __slots__ = ("data", "oids")
+
+    def __init__(self, data: bytes, oids: List[str]):
+        self.data, self.oids = data, oids
+
+    def free(self):
+        st = _store()
+        if st is not None:
+            for o in self.oids:
+                st.delete(o)
+        self.oids = []
+
+
+def dumps(obj: Any, transfer: bool = True) -> bytes:
+    f = io.BytesIO()
+    p = _Pickler(f, transfer)
+    p.dump(obj)
+    if not transfer and p.oids:
+        raise ValueError("use dumps_shared() for broadcast payloads")
+    return f.getvalue()
+
+
+def dumps_shared(obj: Any) -> Payload:
+    f = io.BytesIO()
+    p = _Pickler(f, transfer=False)
+    p.dump(obj)
+    return Payload(f.getvalue(), p.oids)
+
+
+def loads(data) -> Any:
+    return cloudpickle.loads(data)
+
+
+_ = Tuple

@@ -222,6 +222,15 @@ class WidePlan(Plan):
     def is_wide(self):
         return True
 
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st.pop("_lock", None)
+        return st
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+        self._lock = threading.Lock()
+
     def materialize(self, scheduler):
         with self._lock:
             if self._out is None:
@@ -313,7 +322,8 @@ class RepartitionPlan(WidePlan):
 
         pieces = scheduler.map(split, range(self.child.num_partitions()))
         schema = self.child.schema
-        return [concat([p[j] for p in pieces], schema) for j in range(n)]
+        # reduce side runs as tasks too: executors read the map outputs from the store
+        return scheduler.map(lambda j: concat([p[j] for p in pieces], schema), range(n))
 
 
 class CoalescePlan(Plan):

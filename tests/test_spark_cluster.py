@@ -1,0 +1,247 @@
+"""Spark-on-runtime cluster behaviour (port of the reference's
+python/raydp/tests/test_spark_cluster.py and test_spark_master_memory.py).
+
+Executors are real actor processes under the native supervisor; multi-node cases use the
+virtual-node cluster (ray.cluster_utils.Cluster equivalent) with one store arena per node."""
+import os
+import time
+
+import pyarrow
+import pytest
+
+import raydp  # noqa: F401  (installs the ray / pyspark facades when those are absent)
+import ray
+import raydp.utils as utils
+from ray.cluster_utils import Cluster
+from ray.util.placement_group import placement_group_table
+
+
+@pytest.fixture
+def local_rt():
+    ray.shutdown()
+    ray.init(num_cpus=6)
+    yield
+    raydp.stop_spark()
+    ray.shutdown()
+
+
+def test_spark(spark_on_ray_small):
+    assert spark_on_ray_small.range(0, 10).count() == 10
+
+
+def test_executors_are_processes(spark_on_ray_2_executors):
+    from raydp_amd.spark.session import SparkSession
+    backend = SparkSession.getActiveSession()._cluster
+    infos = ray.get([e.handle.info.remote() for e in backend.alive_executors()])
+    assert len({i["pid"] for i in infos}) == 2 and os.getpid() not in {i["pid"] for i in infos}
+    assert ray.get_actor("raydp-executor-0") is not None
+    assert ray.get_actor("test2_SPARK_MASTER") is not None
+
+
+def test_legacy_spark_on_fractional_cpu():
+    cluster = Cluster(initialize_head=True, head_node_args={"num_cpus": 2})
+    spark = raydp.init_spark(app_name="test_cpu_fraction", num_executors=1, executor_cores=3,
+                             executor_memory="500M", configs={"spark.ray.actor.resource.cpu": "0.1"})
+    assert spark.range(0, 10).count() == 10
+    raydp.stop_spark()
+    cluster.shutdown()
+
+
+def test_spark_executor_on_fractional_cpu():
+    cluster = Cluster(initialize_head=True, head_node_args={"num_cpus": 2})
+    spark = raydp.init_spark(app_name="test_cpu_fraction", num_executors=1, executor_cores=3,
+                             executor_memory="500M",
+                             configs={"spark.ray.raydp_spark_executor.actor.resource.cpu": "0.1"})
+    assert spark.range(0, 10).count() == 10
+    raydp.stop_spark()
+    cluster.shutdown()
+
+
+def test_spark_executor_node_affinity():
+    cluster = Cluster(initialize_head=True, head_node_args={"num_cpus": 1})
+    node = cluster.add_node(num_cpus=2, resources={"spark_executor": 10})
+    spark = raydp.init_spark(app_name="test_executor_node_affinity", num_executors=1, executor_cores=2,
+                             executor_memory="500M",
+                             configs={"spark.ray.raydp_spark_executor.actor.resource.spark_executor": "1"})
+    assert spark.range(0, 10).count() == 10
+    from ray.util.state import list_actors
+    ex = [a for a in list_actors() if a.name == "raydp-executor-0"][0]
+    assert ex.node_id == node.node_id and ex.required_resources["spark_executor"] == 1
+    raydp.stop_spark()
+    cluster.shutdown()
+
+
+def test_spark_remote(local_rt):
+    @ray.remote
+    class SparkRemote:
+        def __init__(self):
+            import raydp as rdp
+            self.spark = rdp.init_spark(app_name="test_spark_remote", num_executors=1, executor_cores=1,
+                                        executor_memory="500MB")
+
+        def run(self):
+            return self.spark.range(0, 100).count()
+
+        def stop(self):
+            import raydp as rdp
+            self.spark.stop()
+            rdp.stop_spark()
+
+    driver = SparkRemote.remote()
+    assert ray.get(driver.run.remote()) == 100
+    ray.get(driver.stop.remote())
+
+
+def test_spark_driver_and_executor_hostname(spark_on_ray_small):
+    conf = spark_on_ray_small.conf
+    ip = ray.util.get_node_ip_address()
+    assert conf.get("spark.driver.host") == ip
+    assert conf.get("spark.driver.bindAddress") == ip
+
+
+def test_ray_dataset_roundtrip():
+    cluster = Cluster(initialize_head=True, head_node_args={"num_cpus": 6})
+    spark = raydp.init_spark(app_name="test_ray_dataset_roundtrip", num_executors=2, executor_cores=1,
+                             executor_memory="500M")
+    spark_df = spark.createDataFrame([(1, "a"), (2, "b"), (3, "c")], ["one", "two"])
+    rows = [(r.one, r.two) for r in spark_df.take(3)]
+    ds = ray.data.from_spark(spark_df)
+    values = [(r["one"], r["two"]) for r in ds.take(6)]
+    assert values == rows
+    block_refs = [b for bundle in ds.iter_internal_ref_bundles() for b, _ in bundle.blocks]
+    df = raydp.spark.dataset.ray_dataset_to_spark_dataframe(spark, ds.schema(), block_refs)
+    assert [(r.one, r.two) for r in df.take(3)] == values
+    raydp.stop_spark()
+    cluster.shutdown()
+
+
+def test_ray_dataset_to_spark(spark_on_ray_2_executors):
+    spark = spark_on_ray_2_executors
+    n = 5
+    ds = ray.data.from_arrow(pyarrow.Table.from_pydict({"value": list(range(n))}))
+    values = [r["value"] for r in ds.take(n)]
+    refs = [b for bundle in ds.iter_internal_ref_bundles() for b, _ in bundle.blocks]
+    df = raydp.spark.dataset.ray_dataset_to_spark_dataframe(spark, ds.schema(), refs)
+    assert [r.value for r in df.take(n)] == values
+    ds2 = ray.data.from_items([{"id": i} for i in range(n)])
+    ids = [r["id"] for r in ds2.take(n)]
+    refs2 = [b for bundle in ds2.iter_internal_ref_bundles() for b, _ in bundle.blocks]
+    df2 = raydp.spark.dataset.ray_dataset_to_spark_dataframe(spark, ds2.schema(), refs2)
+    assert [r.id for r in df2.take(n)] == ids
+
+
+def test_placement_group(local_rt):
+    for strategy in ["PACK", "STRICT_PACK", "SPREAD", "STRICT_SPREAD"]:
+        spark = raydp.init_spark(f"test_strategy_{strategy}_1", 1, 1, "500M", placement_group_strategy=strategy)
+        assert spark.range(0, 10, numPartitions=10).count() == 10
+        raydp.stop_spark()
+        pg = ray.util.placement_group([{"CPU": 1, "memory": utils.parse_memory_size("500M")}], strategy=strategy)
+        ray.get(pg.ready())
+        spark = raydp.init_spark(f"test_bundle_{strategy}_2", 1, 1, "500M", placement_group=pg,
+                                 placement_group_bundle_indexes=[0])
+        assert spark.range(0, 10, numPartitions=10).count() == 10
+        from ray.util.state import list_actors
+        ex = [a for a in list_actors() if a.name == "raydp-executor-0" and a.state == "ALIVE"][0]
+        assert ex.placement_group_id == pg.id.hex()
+        raydp.stop_spark()
+        spark = raydp.init_spark(f"test_bundle_{strategy}_3", 1, 1, "500M", placement_group=pg)
+        assert spark.range(0, 10, numPartitions=10).count() == 10
+        raydp.stop_spark()
+        ray.util.remove_placement_group(pg)
+    assert len([p for p in placement_group_table().values() if p["state"] != "REMOVED"]) == 0
+
+
+def test_reconstruction():
+    """Remove the node holding converted partitions; every block is still gettable."""
+    cluster = Cluster(initialize_head=True, head_node_args={"num_cpus": 1})
+    node_to_kill = cluster.add_node(num_cpus=1, object_store_memory=10 ** 8)
+    spark = raydp.init_spark("a", 2, 1, "500m", fault_tolerant_mode=True)
+    df = spark.range(100000)
+    ds = raydp.spark.from_spark_recoverable(df)
+    locations = {r.node_id for bundle in ds.iter_internal_ref_bundles() for r, _ in bundle.blocks}
+    assert node_to_kill.node_id in locations   # one executor (and its partitions) lives there
+    cluster.add_node(num_cpus=1, object_store_memory=10 ** 8)
+    cluster.remove_node(node_to_kill)           # arena destroyed, executor relocated
+    cluster.add_node(num_cpus=1, object_store_memory=10 ** 8)
+    total = 0
+    for bundle in ds.iter_internal_ref_bundles():
+        for block_ref, _ in bundle.blocks:
+            total += ray.get(block_ref).num_rows
+    assert total == 100000
+    assert ds.count() == 100000
+    raydp.stop_spark()
+    cluster.shutdown()
+
+
+def test_executor_killed_tasks_retried(spark_on_ray_2_executors):
+    """An executor process dying mid-job: its tasks rerun and the supervisor restarts it."""
+    spark = spark_on_ray_2_executors
+    from raydp_amd.spark.session import SparkSession
+    backend = SparkSession.getActiveSession()._cluster
+    ex = backend.alive_executors()[0]
+    pid = ray.get(ex.handle.info.remote())["pid"]
+    os.kill(pid, 9)
+    assert spark.range(0, 1000, numPartitions=8).count() == 1000
+    info = ray.get(ex.handle.info.remote())
+    assert info["pid"] != pid and info["restart_count"] >= 1
+
+
+def test_recoverable_survives_gc():
+    cluster = Cluster(initialize_head=True, head_node_args={"num_cpus": 6})
+    spark = raydp.init_spark("test_gc", 1, 1, "500M")
+    df = spark.range(1000)
+    ds = raydp.spark.from_spark_recoverable(df)
+    import gc
+    gc.collect()
+    time.sleep(0.2)
+    assert ds.count() == 1000
+    raydp.stop_spark()
+    cluster.shutdown()
+
+
+def test_release_spark_recoverable():
+    cluster = Cluster(initialize_head=True, head_node_args={"num_cpus": 6})
+    spark = raydp.init_spark("test_release", 1, 1, "500M")
+    df = spark.range(100)
+    ds = raydp.spark.from_spark_recoverable(df)
+    from raydp.spark.dataset import _recoverable_rdd_ids
+    backend = spark._cluster
+    rdd_id = _recoverable_rdd_ids[df]
+    assert backend.is_persisted(rdd_id)
+    assert ds.count() == 100
+    raydp.spark.release_spark_recoverable(df)
+    assert not backend.is_persisted(rdd_id)
+    assert df not in _recoverable_rdd_ids
+    raydp.stop_spark()
+    cluster.shutdown()
+
+
+def test_dynamic_allocation(local_rt):
+    spark = raydp.init_spark("dyn", 1, 1, "200M", configs={
+        "spark.dynamicAllocation.enabled": "true", "spark.dynamicAllocation.initialExecutors": "1",
+        "spark.dynamicAllocation.maxExecutors": "3"})
+    backend = spark._cluster
+    assert len(backend.alive_executors()) == 1
+    backend.request_total_executors(5)          # capped at maxExecutors
+    assert len(backend.alive_executors()) == 3
+    assert spark.range(0, 300, numPartitions=6).count() == 300
+    backend.request_total_executors(1)
+    assert len(backend.alive_executors()) == 1
+    assert spark.range(0, 30).count() == 30
+
+
+def test_spark_master_memory_custom():
+    cluster = Cluster(initialize_head=True, head_node_args={"num_cpus": 2, "resources": {"master": 10}})
+    custom_memory = 100 * 1024 * 1024
+    app = "test_spark_master_memory_custom"
+    spark = raydp.init_spark(app_name=app, num_executors=1, executor_cores=1, executor_memory="500M",
+                             configs={"spark.ray.raydp_spark_master.actor.resource.memory": str(custom_memory),
+                                      "spark.ray.raydp_spark_master.actor.resource.master": "1"})
+    assert spark.createDataFrame([(1, 2)], ["a", "b"]).count() == 1
+    actor = ray.get_actor(f"{app}_SPARK_MASTER")
+    from ray.util.state import list_actors
+    st = list_actors(filters=[("actor_id", "=", actor._actor_id.hex())], detail=True)[0]
+    assert st.required_resources["memory"] == custom_memory
+    assert st.required_resources["master"] == 1
+    raydp.stop_spark()
+    cluster.shutdown()
