@@ -136,8 +136,8 @@ def main():
     make_csv(main_csv, args.steps * BATCH, 2000 + rank)
 
     runtime.init(num_cpus=int(os.environ.get("RAYDP_BENCH_CPUS", "4")))
-    spark = context.init_spark(f"nyc-bench-r{rank}", 1, int(os.environ.get("RAYDP_BENCH_CPUS", "4")),
-                               "2G")
+    # one single-core executor process per CPU: Arrow ETL scales without sharing a GIL
+    spark = context.init_spark(f"nyc-bench-r{rank}", int(os.environ.get("RAYDP_BENCH_CPUS", "4")), 1, "1G")
     spark.conf.set("spark.sql.session.timeZone", "UTC")
     storage = os.path.join(tmp, "results")
 

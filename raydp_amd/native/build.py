@@ -21,7 +21,11 @@ ARCH = os.environ.get("RAYDP_GPU_ARCH", "gfx950")
 
 def _hip_sources():
     d = os.path.join(CSRC, "hip")
-    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".hip"))
+    c = os.path.join(CSRC, "comm")
+    srcs = sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".hip"))
+    if os.path.isdir(c):
+        srcs += sorted(os.path.join(c, f) for f in os.listdir(c) if f.endswith(".cc"))
+    return srcs
 
 
 def _runtime_sources():
@@ -89,7 +93,7 @@ def build_one(name: str, force: bool = False) -> str:
                 _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                       "-munsafe-fp-atomics", "-c", s, "-o", o] + inc)
                 objs.append(o)
-            _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", tmp])
+            _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", tmp, "-ldl"])
     os.replace(tmp, out)
     return out
 

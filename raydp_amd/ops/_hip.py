@@ -99,8 +99,14 @@ def lib():
     L.rx_mlp_refresh_images.argtypes = [vp, vp, vp, vp]
     L.rx_arrow_ingest.argtypes = [vp, vp, vp]
     L.rx_gather_rows.argtypes = [vp, vp, vp, ll, i, vp]
+    L.rx_comm_available.restype = i
+    L.rx_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.rx_comm_allreduce.argtypes = [vp, i, vp, vp]
+    L.rx_comm_broadcast.argtypes = [vp, i, i, vp, vp]
+    L.rx_comm_destroy.argtypes = [vp]
     for fn in ("rx_mlp_train_steps", "rx_mlp_fwdbwd", "rx_opt_step", "rx_mlp_eval",
-               "rx_mlp_refresh_images", "rx_arrow_ingest", "rx_gather_rows"):
+               "rx_mlp_refresh_images", "rx_arrow_ingest", "rx_gather_rows", "rx_comm_unique_id",
+               "rx_comm_allreduce", "rx_comm_broadcast", "rx_comm_destroy"):
         getattr(L, fn).restype = i
     for name, cls in (("rx_mlp_desc_size", MlpDesc), ("rx_opt_desc_size", OptDesc),
                       ("rx_ingest_args_size", IngestArgs)):

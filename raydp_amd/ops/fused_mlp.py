@@ -242,9 +242,15 @@ class FusedMLPTrainer:
 
     def train_epoch(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int,
                     perm: Optional[torch.Tensor], allreduce: Optional[Callable] = None,
-                    world_size: int = 1, drop_last: bool = False) -> Dict[str, float]:
-        """Run one epoch; ``allreduce(grads)`` (sum) is called between backward and step."""
+                    world_size: int = 1, drop_last: bool = False, comm=None,
+                    max_steps: Optional[int] = None) -> Dict[str, float]:
+        """Run one epoch. Multi-GPU: ``comm`` (a :class:`raydp_amd.ops.comm.NativeComm`) puts
+        the gradient all-reduce inside the native step loop; otherwise ``allreduce(grads)``
+        (sum) is called from Python between backward and step. ``max_steps`` caps the step
+        count (ranks agree on it so every collective is matched)."""
         nsteps = n_rows // self.batch if drop_last else -(-n_rows // self.batch)
+        if max_steps is not None:
+            nsteps = min(nsteps, int(max_steps))
         self.metrics.zero_()
         if nsteps == 0:
             return self._read_metrics()
@@ -261,13 +267,15 @@ class FusedMLPTrainer:
         pp = ctypes.c_void_p
         perm_p = pp(perm.data_ptr()) if perm is not None else pp(0)
         gscale = 1.0 / world_size
-        if allreduce is None:
+        if comm is not None or allreduce is None:
+            ar_fn = comm.fn_ptr if comm is not None else pp(0)
+            ar_ctx = pp(comm.ctx) if comm is not None else pp(0)
             rc = self.lib.rx_mlp_train_steps(
                 ctypes.byref(self.desc), self._dd, ctypes.byref(self.opt), self._od, self.mt, pp(self.params.data_ptr()),
                 pp(self.grads.data_ptr()), pp(self.m.data_ptr()), pp(self.v.data_ptr()),
                 pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, 0, nsteps,
                 lrs, bc1, bc2, ctypes.c_float(gscale), int(self.step_count == 0), pp(self.scratch.data_ptr()),
-                pp(self.metrics.data_ptr()), stream, pp(0), pp(0))
+                pp(self.metrics.data_ptr()), stream, ar_fn, ar_ctx)
             _hip.check(rc, "rx_mlp_train_steps")
         else:
             for s in range(nsteps):

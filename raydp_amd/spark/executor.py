@@ -32,6 +32,19 @@ class RayDPExecutor:
         self.tasks_run = 0
         from raydp_amd.runtime import core
         self._node = core.current_node()
+        self._warm_up()
+
+    @staticmethod
+    def _warm_up():
+        """Import the task-side engine and load the native kernels while the executor starts
+        (executors start in parallel), so the first stage does not pay for it."""
+        import numpy as np
+        import pyarrow as pa
+        import pyarrow.compute  # noqa: F401
+        import pyarrow.csv  # noqa: F401
+        from raydp_amd.spark import functions, sources, wide  # noqa: F401
+        from raydp_amd.spark.plan import hash_columns
+        hash_columns(pa.table({"k": np.arange(4)}), ["k"])
 
     # ------------------------------------------------------------------ info ------------
     def ping(self):

@@ -122,14 +122,23 @@ class FusedMLPEngine:
         perm = None
         if self.shuffle:
             perm = torch.randperm(t.n, device=self.device, generator=self.gen).to(torch.int32)
-        ar = None
+        ar, comm, max_steps = None, None, None
         if self.world > 1:
             import torch.distributed as dist
-
-            def ar(g):
-                dist.all_reduce(g)
+            from raydp_amd.ops.comm import NativeComm
+            # every rank must run the same number of steps (matched collectives)
+            b = self.trainer.batch
+            mine = t.n // b if self.drop_last else -(-t.n // b)
+            s = torch.tensor([mine], device=self.device, dtype=torch.int64)
+            dist.all_reduce(s, op=dist.ReduceOp.MIN)
+            max_steps = int(s.item())
+            comm = NativeComm.from_process_group() if dist.get_backend() == "nccl" else None
+            if comm is None:
+                def ar(g):
+                    dist.all_reduce(g)
         m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, allreduce=ar,
-                                     world_size=self.world, drop_last=self.drop_last)
+                                     world_size=self.world, drop_last=self.drop_last, comm=comm,
+                                     max_steps=max_steps)
         self.trainer.note_steps(self.trainer.steps_in_epoch)
         return self._res(m), m["loss"]
 

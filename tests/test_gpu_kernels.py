@@ -256,3 +256,39 @@ def test_estimator_uses_fused_engine_on_gpu():
     finally:
         raydp_amd.stop_spark()
         runtime.shutdown()
+
+
+def test_native_rccl_comm_in_step_loop():
+    """The C++ step loop with the RCCL all-reduce enqueued per step (world 1 here) gives the
+    same training trajectory as the loop without a communicator."""
+    import torch.distributed as dist
+    from raydp_amd.models.mlp_spec import extract_mlp_spec
+    from raydp_amd.ops.comm import NativeComm, reset_cache
+    from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+    from raydp_amd.train.trainer import _free_port
+    dev = torch.device("cuda")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        comm = NativeComm.from_process_group()
+        assert comm is not None and comm.world == 1
+        x = torch.arange(1000, dtype=torch.float32, device=dev)
+        comm.allreduce_(x)
+        torch.cuda.synchronize()
+        assert torch.equal(x, torch.arange(1000, dtype=torch.float32, device=dev))
+        torch.manual_seed(0)
+        model = NYC()
+        X = torch.randn(640, 20)
+        Y = torch.randn(640, 1)
+        runs = []
+        for use in (False, True):
+            m2 = copy.deepcopy(model)
+            tr = FusedMLPTrainer(extract_mlp_spec(m2), optimizer_config(torch.optim.Adam(m2.parameters(), lr=1e-3)),
+                                 loss_code(nn.MSELoss()), 64, dev)
+            feats = torch.zeros(640, tr.feat_k, dtype=torch.bfloat16)
+            feats[:, :20] = X.to(torch.bfloat16)
+            tr.train_epoch(feats.to(dev), Y.to(dev), 640, None, comm=comm if use else None, max_steps=8)
+            runs.append(tr.params.clone())
+        assert torch.equal(runs[0], runs[1])
+    finally:
+        reset_cache()
+        dist.destroy_process_group()
