@@ -1,0 +1,617 @@
+// Fused MLP training step for CDNA4 (gfx950) -- device code shared by the ahead-of-time
+// build (fused_mlp.hip, runtime descriptor) and the per-model specialised build that
+// raydp_amd/ops/mlp_jit.py generates (every dimension and offset a compile-time constant).
+//
+// Forward + loss + backward of a [Linear -> act -> BatchNorm1d]* -> Linear network runs in ONE
+// workgroup, bf16 MFMA (v_mfma_f32_16x16x32_bf16) with fp32 accumulation. The reference
+// workloads (NYC_Model in examples/pytorch_nyctaxi.py:69-92, batch 64; the stroke tutorial MLPs;
+// DLRM's MLP towers) are ~6 MFLOP per step: the step is latency bound, so the whole dependency
+// chain (10 GEMMs, 4 BatchNorm reductions, loss) stays in one CU with every activation resident
+// in LDS, and column reductions stay inside a wave (each wave owns whole 16-column tiles).
+//
+// Layouts (bf16 LDS matrices carry a +16 B row pad: ds_read_b128 of 16 rows at one column
+// then hits 16 distinct 16-B slots of the 256-B bank row -> conflict free):
+//   R  [Bpad][max_k]    row-major activations (fwd A operand) / gradients (dgrad A operand)
+//   GT [max_n][Bpad]    transposed gradient (wgrad A operand)
+//   XT_l [in_n][Bpad]   transposed layer inputs saved for wgrad (wgrad B operand)
+// Weights come from one global bf16 image buffer written by the optimizer kernel:
+//   W_l  [out_n][in_k] at w_img   (fwd B operand, K = in contiguous)
+//   Wt_l [in_n][out_k] at wt_img  (dgrad B operand, K = out contiguous)
+//
+// Descriptor access is generic over a "descriptor" type D and "layer" types: at run time they
+// are the MlpDesc / MlpLayer structs below read from device memory; in a specialised build
+// they are empty structs whose fields are static constexpr members, so `ly.out` etc. are
+// compile-time constants and the compiler schedules each layer with full knowledge.
+#pragma once
+#include "rx_common.h"
+
+#define RX_MAXL 8
+#define RX_NW 8          // waves per workgroup
+#define RX_THREADS (RX_NW * RX_WAVE)
+
+struct MlpLayer {
+  int in, out;
+  int in_k, out_k;   // K padding (multiple of 32)
+  int in_n, out_n;   // N padding (multiple of 16)
+  int w_img, wt_img; // element offsets of W_l / Wt_l in the bf16 image buffer
+  int w_off, b_off;  // offsets into the flat fp32 parameter / gradient vectors
+  int act;           // 0 identity, 1 relu
+  int bn;            // 0 none, 1 act->bn, 2 bn->act
+  int g_off, be_off; // BN affine params (-1: not affine)
+  int rs_off;        // float offset of [running_mean | running_var] in the stats buffer (-1: none)
+  int pad_;
+  float eps, momentum;
+  int xt_off;        // LDS byte offset of XT_l
+  int stat_off;      // float offset of (mean, invstd) pairs for this layer's outputs in LDS
+  int r_off;         // float offset of the saved pre-BN values in the scratch buffer
+  int pr_off;        // float offset of [bias|gamma|beta|run_mean|run_var] (x out_n) in LDS
+};
+
+struct MlpDesc {
+  int L;
+  int r_lds_off, gt_lds_off, stats_lds_off, lds_bytes;
+  int max_k, max_n;
+  int loss;          // 0 mse, 1 smooth_l1, 2 l1
+  float beta;        // smooth_l1 beta
+  int out_dim;
+  int feat_k;        // row stride of the bf16 feature matrix
+  MlpLayer layer[RX_MAXL];
+  int pr_lds_off;    // LDS byte offset of the per-column parameter block
+  int pr_total;      // floats in that block
+};
+
+// run-time descriptor: loops over layers are ordinary loops
+struct DynCfg {
+  __device__ static const MlpDesc& desc(const MlpDesc* dp) { return *dp; }
+  template <class F>
+  __device__ static void fwd_layers(const MlpDesc& d, F&& f) {
+    for (int l = 0; l < d.L; ++l) f(d.layer[l], d.layer[l + 1 < d.L ? l + 1 : l], l, l == d.L - 1);
+  }
+  template <class F>
+  __device__ static void bwd_layers(const MlpDesc& d, F&& f) {
+    for (int l = d.L - 1; l >= 0; --l) f(d.layer[l], d.layer[l > 0 ? l - 1 : 0], l);
+  }
+  // unrolled visit (register arrays indexed by l stay in registers)
+  template <class F>
+  __device__ static void each_layer(const MlpDesc& d, F&& f) {
+#pragma unroll
+    for (int l = 0; l < RX_MAXL; ++l)
+      if (l < d.L) f(d.layer[l], l);
+  }
+  __device__ static const MlpLayer& first(const MlpDesc& d) { return d.layer[0]; }
+};
+
+
+template <int MT>
+struct Tile {
+  static constexpr int BP = MT * 16;         // padded batch rows
+  static constexpr int NTW = 16 / MT;        // max output n-tiles per wave (64 acc regs)
+  static constexpr int XS = BP + 8;          // stride (elements) of transposed matrices
+};
+
+__device__ __forceinline__ float act_fwd(int act, float z) { return act == 1 ? fmaxf(z, 0.f) : z; }
+
+// C[Bpad x 16-col tile n] += A (LDS, row-major, K contiguous) x Bt (global bf16, [n][K]).
+// The weight fragments of up to KC k-steps are fetched in ONE burst of unconditional
+// (address-clamped) 16-B loads before any MFMA consumes them, so a layer costs one global
+// round trip per 16-column tile instead of one per 32-deep k-step: the step is latency bound
+// and the weights arrive from the Infinity Cache / another XCD's L2 after each optimizer step.
+template <int MT>
+__device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
+                                          const RX_GLOBAL u16* __restrict__ Brow, int K, int lg) {
+  constexpr int KC = 8;
+  const int nks = K >> 5;
+  for (int kc = 0; kc < nks; kc += KC) {
+    bf16x8 bfr[KC];
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      const int ks = min(kc + s, nks - 1);
+      bfr[s] = *reinterpret_cast<const RX_GLOBAL bf16x8*>(Brow + ks * 32 + 8 * lg);
+    }
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      if (kc + s < nks) {
+        const int k0 = (kc + s) * 32 + 8 * lg;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(Arow + mt * 16 * RS + k0);
+          acc[mt] = rx_mfma16(a, bfr[s], acc[mt]);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// forward of layer l for the rows of this workgroup. Leaves y (the layer output after
+// act/BN) in R (row-major) and in XT_{l+1}; for the last layer computes loss, metrics and
+// writes dL/dy into R/GT as G_{L-1}.
+// ------------------------------------------------------------------------------------------
+template <int MT, bool TRAIN, class D, class LY, class NX>
+__device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX& nx, bool last, char* smem,
+                                              const u16* __restrict__ img, const float* __restrict__ P,
+                              float* __restrict__ Gr, const float* __restrict__ labels,
+                              const int* __restrict__ rowidx, int nvalid, float* __restrict__ scratch,
+                              double* __restrict__ metrics) {
+  using T = Tile<MT>;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int RS = d.max_k + 8;
+  u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
+  u16* GT = reinterpret_cast<u16*>(smem + d.gt_lds_off);
+  float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
+  const int ntiles = ly.out_n >> 4;
+
+  f32x4 acc[T::NTW * MT];
+#pragma unroll
+  for (int j = 0; j < T::NTW; ++j) {
+    f32x4 part[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int n = wave + j * RX_NW;
+    if (n < ntiles) gemm_tile<MT>(part, R + lr * RS, RS, rx_g(img) + ly.w_img + (n * 16 + lr) * ly.in_k, ly.in_k, lg);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
+  }
+
+  // ---- epilogue in registers, in place on acc: bias, act, BN, loss ----
+#pragma unroll
+  for (int j = 0; j < T::NTW; ++j) {
+    const int n = wave + j * RX_NW;
+    if (n < ntiles) {
+      const int c = n * 16 + lr;
+      const bool colok = c < ly.out;
+      const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off) + ly.pr_off;
+      const float bias = pr[c];
+      const bool act_first = ly.bn != 2;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z = acc[j * MT + mt][r] + bias;
+          acc[j * MT + mt][r] = act_first ? act_fwd(ly.act, z) : z;
+        }
+      if (ly.bn != 0) {
+        float mean, invstd;
+        if (TRAIN) {
+          float s = 0.f;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              s += (mt * 16 + lg * 4 + r < nvalid) ? acc[j * MT + mt][r] : 0.f;
+          s = rx_colsum16(s);
+          mean = s / (float)nvalid;
+          float v = 0.f;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float dv = acc[j * MT + mt][r] - mean;
+              v += (mt * 16 + lg * 4 + r < nvalid) ? dv * dv : 0.f;
+            }
+          v = rx_colsum16(v);
+          const float var = v / (float)nvalid;
+          invstd = rsqrtf(var + ly.eps);
+          if (colok && lg == 0) {
+            stats[ly.stat_off + 2 * c] = mean;
+            stats[ly.stat_off + 2 * c + 1] = invstd;
+            const float unb = nvalid > 1 ? var * (float)nvalid / (float)(nvalid - 1) : var;
+            float* prw = reinterpret_cast<float*>(smem + d.pr_lds_off) + ly.pr_off;
+            prw[3 * ly.out_n + c] = (1.f - ly.momentum) * prw[3 * ly.out_n + c] + ly.momentum * mean;
+            prw[4 * ly.out_n + c] = (1.f - ly.momentum) * prw[4 * ly.out_n + c] + ly.momentum * unb;
+          }
+          // save the BN input for the backward pass (thread-private slots)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              scratch[ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c] = acc[j * MT + mt][r];
+        } else {
+          mean = colok ? pr[3 * ly.out_n + c] : 0.f;
+          invstd = colok ? rsqrtf(pr[4 * ly.out_n + c] + ly.eps) : 0.f;
+        }
+        const float gam = pr[ly.out_n + c];
+        const float bet = pr[2 * ly.out_n + c];
+        const bool act_after = ly.bn == 2;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float t = (acc[j * MT + mt][r] - mean) * invstd * gam + bet;
+            acc[j * MT + mt][r] = act_after ? act_fwd(ly.act, t) : t;
+          }
+      } else if (TRAIN && !last) {
+        // ReLU mask source for the backward pass
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            scratch[ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c] = colok ? acc[j * MT + mt][r] : 0.f;
+      }
+      // padded rows / columns carry exact zeros through every GEMM
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (!colok || mt * 16 + lg * 4 + r >= nvalid) acc[j * MT + mt][r] = 0.f;
+      if (last) {
+        // loss, metrics and dL/dy (mean reduction over nvalid * out_dim elements)
+        float lsum = 0.f, asum = 0.f, ssum = 0.f, gsum = 0.f;
+        const float inv_n = 1.f / (float)(nvalid * ly.out);
+        const int lcode = d.loss;
+        const float beta = d.beta;
+        // labels of all padded rows, loaded back to back (padded rows read row 0)
+        const int cl = colok ? c : 0;
+        float tl[MT * 4];
+#pragma unroll
+        for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = mt * 16 + lg * 4 + r;
+            float g = 0.f;
+            if (colok && row < nvalid) {
+              const float t = tl[mt * 4 + r];
+              const float e = acc[j * MT + mt][r] - t;
+              const float ae = fabsf(e);
+              asum += ae;
+              ssum += e * e;
+              const float sgn = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+              const bool quad = ae < beta;
+              lsum += quad ? 0.5f * e * e / beta : ae - 0.5f * beta;  // smooth-L1 term
+              g = lcode == 0 ? 2.f * e : (lcode == 1 && quad ? e / beta : sgn);
+              g *= inv_n;
+            }
+            acc[j * MT + mt][r] = g;  // acc now holds G_{L-1}
+            gsum += g;
+          }
+        lsum = rx_wavesum(lsum);
+        asum = rx_wavesum(asum);
+        ssum = rx_wavesum(ssum);
+        if (lcode == 0) lsum = ssum;
+        else if (lcode == 2) lsum = asum;
+        if (lane == 0) {
+          atomicAdd(&metrics[0], (double)(lsum * inv_n));
+          atomicAdd(&metrics[1], (double)asum);
+          atomicAdd(&metrics[2], (double)ssum);
+          if (n == 0) {
+            atomicAdd(&metrics[3], (double)(nvalid * ly.out));
+            atomicAdd(&metrics[4], 1.0);
+          }
+        }
+        if (TRAIN) {
+          gsum = rx_colsum16(gsum);
+          if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum;
+        }
+      }
+    }
+  }
+  __syncthreads();  // every wave finished reading R for this layer
+  if (last && !TRAIN) return;
+
+  // ---- publish y (or G_{L-1}) as bf16: row-major into R, transposed into XT_{l+1} / GT ----
+  const int XS = T::XS;
+  u16* dstT = last ? GT : reinterpret_cast<u16*>(smem + nx.xt_off);
+  const int tstride = last ? (T::BP + 8) : XS;
+#pragma unroll
+  for (int j = 0; j < T::NTW; ++j) {
+    const int n = wave + j * RX_NW;
+    if (n < ntiles) {
+      const int c = n * 16 + lr;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        u16 h[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          h[r] = rx_f2bf(acc[j * MT + mt][r]);
+          R[(mt * 16 + lg * 4 + r) * RS + c] = h[r];
+        }
+        if (TRAIN || !last) {
+          uint2 pk;
+          pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+          pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+          *reinterpret_cast<uint2*>(dstT + c * tstride + mt * 16 + lg * 4) = pk;
+        }
+      }
+    }
+  }
+  // zero the K padding columns [out_n, out_k) of R so the next GEMM's K tail is exact
+  const int kpad = (last ? ly.out_k : nx.in_k) - ly.out_n;
+  if (kpad > 0) {
+    for (int idx = threadIdx.x; idx < T::BP * kpad; idx += RX_THREADS) {
+      const int row = idx / kpad, cc = ly.out_n + idx % kpad;
+      R[row * RS + cc] = 0;
+    }
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------
+// backward of layer l: G_l is in R (row-major) and GT (transposed).
+// ------------------------------------------------------------------------------------------
+template <int MT, class D, class LY, class PV>
+__device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const PV& pv, int l, char* smem,
+                                               const u16* __restrict__ img, const float* __restrict__ P,
+                                               float* __restrict__ Gr, int nvalid, const float* __restrict__ scratch,
+                                               unsigned long long* __restrict__ stamps) {
+  using T = Tile<MT>;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int RS = d.max_k + 8;
+  const int XS = T::XS;
+  u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
+  u16* GT = reinterpret_cast<u16*>(smem + d.gt_lds_off);
+  const u16* XT = reinterpret_cast<const u16*>(smem + ly.xt_off);
+  float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
+
+  // ---- wgrad, computed transposed: dW^T[i][o] = sum_b X[b][i] G[b][o]  (A = XT, B = GT) ----
+  // each lane then holds 4 consecutive i of one o = 16 contiguous bytes of dW[o][:] ->
+  // one dwordx4 store instead of four dword stores (the step is store-queue bound here)
+  {
+    const int mo_tiles = ly.out_n >> 4, ni_tiles = ly.in_n >> 4;
+    const int ntile = mo_tiles * ni_tiles;
+    const bool vec = ((ly.w_off | ly.in) & 3) == 0;
+    for (int t = wave; t < ntile; t += RX_NW) {
+      const int mo = t / ni_tiles, ni = t % ni_tiles;
+      f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < T::BP; k0 += 32) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(XT + (ni * 16 + lr) * XS + k0 + 8 * lg);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(GT + (mo * 16 + lr) * XS + k0 + 8 * lg);
+        a4 = rx_mfma16(a, b, a4);
+      }
+      const int o = mo * 16 + lr, i0 = ni * 16 + lg * 4;
+      if (o < ly.out) {
+        float* dst = Gr + ly.w_off + o * ly.in + i0;
+        if (vec && i0 + 3 < ly.in) {
+          *reinterpret_cast<f32x4*>(dst) = a4;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (i0 + r < ly.in) dst[r] = a4[r];
+        }
+      }
+    }
+  }
+  if (stamps != nullptr && threadIdx.x == 0) rx_g(stamps)[20 + 4 * l] = __builtin_amdgcn_s_memtime();
+  if (l == 0) return;
+
+  // ---- dgrad: dX[b][i] = sum_o G[b][o] W[o][i]  (A = R, B = Wt, K = out_k) ----
+  // pv (layer l-1) owns the post-ops between layer l-1 and l
+  const int ntiles = ly.in_n >> 4;
+  f32x4 acc[T::NTW * MT];
+#pragma unroll
+  for (int j = 0; j < T::NTW; ++j) {
+    f32x4 part[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int n = wave + j * RX_NW;
+    if (n < ntiles) gemm_tile<MT>(part, R + lr * RS, RS, rx_g(img) + ly.wt_img + (n * 16 + lr) * ly.out_k, ly.out_k, lg);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
+  }
+  if (stamps != nullptr && threadIdx.x == 0) rx_g(stamps)[21 + 4 * l] = __builtin_amdgcn_s_memtime();
+  __syncthreads();  // all reads of G_l (R, GT) are done; they are overwritten with G_{l-1}
+  if (stamps != nullptr && threadIdx.x == 0) rx_g(stamps)[22 + 4 * l] = __builtin_amdgcn_s_memtime();
+
+  // ---- post-op backward of layer l-1 (BN / act), producing G_{l-1} ----
+#pragma unroll
+  for (int j = 0; j < T::NTW; ++j) {
+    const int n = wave + j * RX_NW;
+    if (n >= ntiles) continue;
+    const int c = n * 16 + lr;
+    const bool colok = c < pv.out;
+    // The forward saved this layer's BN input / activation (fp32) for every padded row and
+    // column: issue all loads back to back, unconditionally (a load under a per-element
+    // branch is waited for on its own -> one dependent L2 round trip per element).
+    const RX_GLOBAL float* sp = rx_g(scratch) + pv.r_off + c;
+    float sv[MT * 4], g[MT * 4];
+#pragma unroll
+    for (int q = 0; q < MT * 4; ++q) sv[q] = sp[((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n];
+#pragma unroll
+    for (int q = 0; q < MT * 4; ++q) {
+      const int row = (q >> 2) * 16 + lg * 4 + (q & 3);
+      g[q] = (row < nvalid && colok) ? acc[j * MT + (q >> 2)][q & 3] : 0.f;
+    }
+    if (pv.bn == 0) {
+      if (pv.act == 1) {
+#pragma unroll
+        for (int q = 0; q < MT * 4; ++q) g[q] = sv[q] > 0.f ? g[q] : 0.f;
+      }
+    } else {
+      const float mean = colok ? stats[pv.stat_off + 2 * c] : 0.f;
+      const float invstd = colok ? stats[pv.stat_off + 2 * c + 1] : 0.f;
+      const float* ppr = reinterpret_cast<const float*>(smem + d.pr_lds_off) + pv.pr_off;
+      const float gam = ppr[pv.out_n + c];
+      const float bet = ppr[2 * pv.out_n + c];
+      const bool relu_after = pv.bn == 2 && pv.act == 1;
+      const bool relu_before = pv.bn == 1 && pv.act == 1;
+      float xh[MT * 4];
+#pragma unroll
+      for (int q = 0; q < MT * 4; ++q) {
+        xh[q] = (sv[q] - mean) * invstd;
+        g[q] = (relu_after && !(xh[q] * gam + bet > 0.f)) ? 0.f : g[q];
+      }
+      float sg = 0.f, sgx = 0.f;
+#pragma unroll
+      for (int q = 0; q < MT * 4; ++q) {
+        sg += g[q];
+        sgx += g[q] * xh[q];
+      }
+      sg = rx_colsum16(sg);
+      sgx = rx_colsum16(sgx);
+      if (colok && lg == 0) {
+        if (pv.g_off >= 0) Gr[pv.g_off + c] = sgx;
+        if (pv.be_off >= 0) Gr[pv.be_off + c] = sg;
+      }
+      const float inv_n = 1.f / (float)nvalid;
+      const float k1 = gam * invstd;
+#pragma unroll
+      for (int q = 0; q < MT * 4; ++q) {
+        const int row = (q >> 2) * 16 + lg * 4 + (q & 3);
+        float dz = k1 * (g[q] - sg * inv_n - xh[q] * sgx * inv_n);
+        dz = (relu_before && !(sv[q] > 0.f)) ? 0.f : dz;
+        g[q] = (row < nvalid && colok) ? dz : 0.f;
+      }
+    }
+    // bias grad of layer l-1
+    float bs = 0.f;
+#pragma unroll
+    for (int q = 0; q < MT * 4; ++q) bs += g[q];
+    bs = rx_colsum16(bs);
+    if (colok && lg == 0 && pv.b_off >= 0) Gr[pv.b_off + c] = bs;
+    // publish G_{l-1}
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      u16 h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        h[r] = rx_f2bf(g[mt * 4 + r]);
+        R[(mt * 16 + lg * 4 + r) * RS + c] = h[r];
+      }
+      uint2 pk;
+      pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+      pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+      *reinterpret_cast<uint2*>(GT + c * XS + mt * 16 + lg * 4) = pk;
+    }
+  }
+  if (stamps != nullptr && threadIdx.x == 0) rx_g(stamps)[23 + 4 * l] = __builtin_amdgcn_s_memtime();
+  // zero the K tail [out_n, out_k) of G_{l-1} in R for the next dgrad
+  const int kpad = pv.out_k - pv.out_n;
+  if (kpad > 0) {
+    for (int idx = threadIdx.x; idx < T::BP * kpad; idx += RX_THREADS) {
+      const int row = idx / kpad, cc = pv.out_n + idx % kpad;
+      R[row * RS + cc] = 0;
+    }
+  }
+  __syncthreads();
+}
+
+
+// Stage every layer's per-column parameters (bias, BN gamma/beta, running mean/var) into LDS
+// with ONE burst of independent loads per thread (column c = threadIdx.x of every layer,
+// address-clamped so no load sits behind a per-element branch).
+template <class C, class D>
+__device__ __forceinline__ void load_params(const D& d, char* smem, const float* __restrict__ P,
+                                            const float* __restrict__ rstats) {
+  float* pr = reinterpret_cast<float*>(smem + d.pr_lds_off);
+  const int c = threadIdx.x;
+  float v[RX_MAXL][5];
+  C::each_layer(d, [&](const auto& ly, int l) {
+    const bool ok = c < ly.out;
+    const int cc = ok ? c : 0;
+    const float b = rx_g(P)[ly.b_off >= 0 ? ly.b_off + cc : 0];
+    const float g = rx_g(P)[ly.g_off >= 0 ? ly.g_off + cc : 0];
+    const float be = rx_g(P)[ly.be_off >= 0 ? ly.be_off + cc : 0];
+    const float rm = rx_g(rstats)[ly.rs_off >= 0 ? ly.rs_off + cc : 0];
+    const float rv = rx_g(rstats)[ly.rs_off >= 0 ? ly.rs_off + ly.out + cc : 0];
+    v[l][0] = (ok && ly.b_off >= 0) ? b : 0.f;
+    v[l][1] = (ok && ly.g_off >= 0) ? g : 1.f;
+    v[l][2] = (ok && ly.be_off >= 0) ? be : 0.f;
+    v[l][3] = (ok && ly.rs_off >= 0) ? rm : 0.f;
+    v[l][4] = (ok && ly.rs_off >= 0) ? rv : 1.f;
+  });
+  C::each_layer(d, [&](const auto& ly, int l) {
+    if (c < ly.out_n) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) pr[ly.pr_off + k * ly.out_n + c] = v[l][k];
+    }
+  });
+}
+
+// write the updated BatchNorm running statistics back (once per step, after the forward)
+template <class C, class D>
+__device__ __forceinline__ void store_running_stats(const D& d, char* smem, float* __restrict__ rstats) {
+  const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off);
+  const int c = threadIdx.x;
+  C::each_layer(d, [&](const auto& ly, int) {
+    if (ly.rs_off >= 0 && c < ly.out) {
+      rx_g(rstats)[ly.rs_off + c] = pr[ly.pr_off + 3 * ly.out_n + c];
+      rx_g(rstats)[ly.rs_off + ly.out + c] = pr[ly.pr_off + 4 * ly.out_n + c];
+    }
+  });
+}
+
+// load the batch's feature rows (gathered through the epoch permutation) into R and XT_0
+template <int MT, class D, class L0>
+__device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem, const u16* __restrict__ feats,
+                                            const int* __restrict__ rowidx, int nvalid, bool need_t) {
+  using T = Tile<MT>;
+  const int RS = d.max_k + 8;
+  u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
+  u16* XT = reinterpret_cast<u16*>(smem + l0.xt_off);
+  const int in_n = l0.in_n;
+  const int chunks = d.feat_k >> 3;  // 8 bf16 per 16-B chunk
+  for (int idx = threadIdx.x; idx < T::BP * chunks; idx += RX_THREADS) {
+    const int row = idx / chunks, ch = idx % chunks;
+    u32x4 v = *reinterpret_cast<const RX_GLOBAL u32x4*>(rx_g(feats) + (size_t)rowidx[row] * d.feat_k + ch * 8);
+    if (row >= nvalid) v = u32x4{0u, 0u, 0u, 0u};
+    *reinterpret_cast<u32x4*>(R + row * RS + ch * 8) = v;
+    if (need_t) {
+      const u16* h = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = ch * 8 + e;
+        if (k < in_n) XT[k * T::XS + row] = h[e];
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// One training step (forward, loss, backward -> gradients in Gr) for rows
+// perm[row0 .. row0 + nvalid) of the epoch.
+template <class C, int MT>
+__device__ __forceinline__ void mlp_train_step_body(
+    const MlpDesc* __restrict__ dp, const u16* __restrict__ img, float* __restrict__ rstats,
+    const float* __restrict__ P, float* __restrict__ Gr, const u16* __restrict__ feats,
+    const float* __restrict__ labels, const int* __restrict__ perm, int row0, int nvalid,
+    float* __restrict__ scratch, double* __restrict__ metrics, unsigned long long* __restrict__ stamps,
+    char* smem, int* rowidx) {
+  auto&& d = C::desc(dp);
+  RX_GLOBAL unsigned long long* st = rx_g(stamps);
+  int si = 0;
+#define RX_STAMP()                                                        \
+  do {                                                                    \
+    if (st != nullptr && threadIdx.x == 0) st[si] = __builtin_amdgcn_s_memtime(); \
+    ++si;                                                                 \
+  } while (0)
+  RX_STAMP();
+  for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS)
+    rowidx[i] = i < nvalid ? (perm ? rx_g(perm)[row0 + i] : row0 + i) : (perm ? rx_g(perm)[row0] : row0);
+  load_params<C>(d, smem, P, rstats);
+  __syncthreads();
+  load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, true);
+  RX_STAMP();
+  C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
+    layer_forward<MT, true>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics);
+    RX_STAMP();
+  });
+  store_running_stats<C>(d, smem, rstats);
+  C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
+    layer_backward<MT>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, stamps);
+    RX_STAMP();
+  });
+#undef RX_STAMP
+}
+
+// Evaluation: forward + loss metrics only; one workgroup per batch.
+template <class C, int MT>
+__device__ __forceinline__ void mlp_eval_body(const MlpDesc* __restrict__ dp, const u16* __restrict__ img,
+                                              const float* __restrict__ rstats, const float* __restrict__ P,
+                                              const u16* __restrict__ feats, const float* __restrict__ labels,
+                                              int n_rows, int batch, double* __restrict__ metrics, char* smem,
+                                              int* rowidx) {
+  auto&& d = C::desc(dp);
+  const int row0 = blockIdx.x * batch;
+  const int nvalid = min(batch, n_rows - row0);
+  for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS) rowidx[i] = i < nvalid ? row0 + i : row0;
+  load_params<C>(d, smem, P, rstats);
+  __syncthreads();
+  load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, false);
+  C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
+    layer_forward<MT, false>(d, ly, nx, last, smem, img, P, nullptr, labels, rowidx, nvalid, nullptr, metrics);
+  });
+}

@@ -5,9 +5,20 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
 #define RX_WAVE 64
+
+// Pointers read out of a descriptor in memory are "generic" to the compiler, so every access
+// through them becomes a flat_* instruction -- and a flat load is waited for with vmcnt(0) AND
+// lgkmcnt(0), serialising everything around it. Casting them to the global address space
+// restores global_load/global_store with counted waits.
+#define RX_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ RX_GLOBAL T* rx_g(T* p) {
+  return (RX_GLOBAL T*)p;
+}
 
 // round-to-nearest-even fp32 -> bf16 bits
 __device__ __forceinline__ u16 rx_f2bf(float f) {

@@ -18,11 +18,11 @@ class MlpLayer(ctypes.Structure):
         ("in_", ctypes.c_int), ("out", ctypes.c_int),
         ("in_k", ctypes.c_int), ("out_k", ctypes.c_int),
         ("in_n", ctypes.c_int), ("out_n", ctypes.c_int),
-        ("W", ctypes.c_void_p), ("Wt", ctypes.c_void_p),
+        ("w_img", ctypes.c_int), ("wt_img", ctypes.c_int),
         ("w_off", ctypes.c_int), ("b_off", ctypes.c_int),
         ("act", ctypes.c_int), ("bn", ctypes.c_int),
         ("g_off", ctypes.c_int), ("be_off", ctypes.c_int),
-        ("run_mean", ctypes.c_void_p), ("run_var", ctypes.c_void_p),
+        ("rs_off", ctypes.c_int), ("pad_", ctypes.c_int),
         ("eps", ctypes.c_float), ("momentum", ctypes.c_float),
         ("xt_off", ctypes.c_int), ("stat_off", ctypes.c_int), ("r_off", ctypes.c_int),
         ("pr_off", ctypes.c_int),
@@ -38,9 +38,14 @@ class MlpDesc(ctypes.Structure):
         ("loss", ctypes.c_int), ("beta", ctypes.c_float),
         ("out_dim", ctypes.c_int), ("feat_k", ctypes.c_int),
         ("layer", MlpLayer * MAXL),
-        ("stamps", ctypes.c_void_p),
         ("pr_lds_off", ctypes.c_int), ("pr_total", ctypes.c_int),
     ]
+
+
+class StepBufs(ctypes.Structure):
+    """Device buffers of one fused model (csrc/hip/fused_mlp.hip StepBufs)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("d_dev", "img", "rstats", "params", "grads", "scratch",
+                                               "metrics", "stamps", "jit_step", "jit_eval")]
 
 
 class OptSeg(ctypes.Structure):
@@ -91,11 +96,16 @@ def lib():
     L.rx_mlp_desc_size.restype = i
     L.rx_opt_desc_size.restype = i
     L.rx_ingest_args_size.restype = i
-    L.rx_mlp_train_steps.argtypes = [vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, i, i, i, i, vp,
-                                     vp, vp, f, i, vp, vp, vp, vp, vp]
-    L.rx_mlp_fwdbwd.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, i, i, i, vp, vp, vp]
+    L.rx_step_bufs_size.restype = i
+    # (desc, bufs, opt, opt_dev, mt, m, v, feats, labels, perm, n_rows, batch, first_step, nsteps,
+    #  lrs, bc1s, bc2s, gscale, opt_first, stream, allreduce_fn, ar_ctx)
+    L.rx_mlp_train_steps.argtypes = [vp, vp, vp, vp, i, vp, vp, vp, vp, vp, i, i, i, i, vp, vp, vp, f, i,
+                                     vp, vp, vp]
+    L.rx_mlp_fwdbwd.argtypes = [vp, vp, i, vp, vp, vp, i, i, i, vp]
     L.rx_opt_step.argtypes = [vp, vp, vp, vp, vp, vp, f, f, f, f, i, vp]
-    L.rx_mlp_eval.argtypes = [vp, vp, i, vp, vp, vp, i, i, vp, vp]
+    L.rx_mlp_eval.argtypes = [vp, vp, i, vp, vp, i, i, vp]
+    L.rx_jit_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(vp), i]
+    L.rx_jit_load.restype = i
     L.rx_mlp_refresh_images.argtypes = [vp, vp, vp, vp]
     L.rx_arrow_ingest.argtypes = [vp, vp, vp]
     L.rx_gather_rows.argtypes = [vp, vp, vp, ll, i, vp]
@@ -109,7 +119,7 @@ def lib():
                "rx_comm_allreduce", "rx_comm_broadcast", "rx_comm_destroy"):
         getattr(L, fn).restype = i
     for name, cls in (("rx_mlp_desc_size", MlpDesc), ("rx_opt_desc_size", OptDesc),
-                      ("rx_ingest_args_size", IngestArgs)):
+                      ("rx_ingest_args_size", IngestArgs), ("rx_step_bufs_size", StepBufs)):
         got = getattr(L, name)()
         if got != ctypes.sizeof(cls):
             raise RuntimeError(f"ABI mismatch for {cls.__name__}: C {got} vs ctypes {ctypes.sizeof(cls)}")

@@ -59,6 +59,13 @@ def optimizer_config(opt) -> Optional[dict]:
     return None
 
 
+def jit_enabled() -> bool:
+    """Per-model specialised step kernels (``raydp_amd.ops.mlp_jit``); RAYDP_MLP_JIT=0 turns
+    them off (the ahead-of-time run-time-descriptor kernel is used instead)."""
+    import os
+    return os.environ.get("RAYDP_MLP_JIT", "1") != "0"
+
+
 def pick_mt(batch: int) -> Optional[int]:
     for mt in (2, 4, 8):
         if batch <= mt * 16:
@@ -101,8 +108,10 @@ class FusedMLPTrainer:
             max_n = max(max_n, _ru(oo, 16))
             if _ru(oo, 16) // 16 > ntw * 8 or _ru(i, 16) // 16 > ntw * 8:
                 raise ValueError("layer too wide for this batch size in the fused trainer")
-        self.W_img, self.Wt_img = [], []
         self.run_bufs = []
+        img_off = 0       # bf16 elements: W_l [out_n][in_k] then Wt_l [in_n][out_k], per layer
+        rs_total = 0      # fp32 running statistics [mean | var] per BN layer
+        rs_init = []
         xs = bp + 8
         lds = 0
 
@@ -120,6 +129,7 @@ class FusedMLPTrainer:
         stat_off = 0
         pr_total = 0
         nseg = 0
+        seg_images = []
 
         def vseg(start, n):
             # bias / BN gamma+beta vectors: plain element-wise optimizer segments
@@ -140,18 +150,17 @@ class FusedMLPTrainer:
             lin = ly.linear
             x = d.layer[li]
             x.in_, x.out, x.in_k, x.out_k, x.in_n, x.out_n = i, oo, in_k, out_k, in_n, out_n
-            W = torch.zeros(out_n, in_k, dtype=torch.bfloat16, device=dev)
-            Wt = torch.zeros(in_n, out_k, dtype=torch.bfloat16, device=dev)
-            self.W_img.append(W)
-            self.Wt_img.append(Wt)
-            x.W, x.Wt = W.data_ptr(), Wt.data_ptr()
+            x.w_img = img_off
+            img_off += _ru(out_n * in_k, 8)
+            x.wt_img = img_off
+            img_off += _ru(in_n * out_k, 8)
             pad4()
             x.w_off = off
             flat.append(lin.weight.detach().reshape(-1).float())
             seg = o.seg[nseg]
             seg.start, seg.len, seg.kind = off, oo * i, 1
             seg.out, seg.in_, seg.in_k, seg.out_k = oo, i, in_k, out_k
-            seg.W, seg.Wt = W.data_ptr(), Wt.data_ptr()
+            seg_images.append((nseg, x.w_img, x.wt_img))
             nseg += 1
             self.layout.append(("weight", lin, off, oo * i))
             off += oo * i
@@ -166,6 +175,7 @@ class FusedMLPTrainer:
                 x.b_off = -1
             x.act, x.bn = ly.act, ly.bn
             x.g_off = x.be_off = -1
+            x.rs_off = -1
             if ly.bn:
                 bn = ly.bn_module
                 if bn.affine:
@@ -178,11 +188,11 @@ class FusedMLPTrainer:
                     self.layout.append(("beta", bn, off + oo, oo))
                     vseg(off, 2 * oo)
                     off += 2 * oo
-                rm = bn.running_mean.detach().to(dev, torch.float32).clone()
-                rv = bn.running_var.detach().to(dev, torch.float32).clone()
-                self.run_bufs.append((bn, rm, rv))
-                x.run_mean, x.run_var = rm.data_ptr(), rv.data_ptr()
-                x.eps, x.momentum = float(bn.eps), float(bn.momentum)
+                if bn.running_mean is not None:
+                    x.rs_off = rs_total
+                    rs_init.append((bn, rs_total, oo))
+                    rs_total += 2 * oo
+                x.eps, x.momentum = float(bn.eps), float(bn.momentum if bn.momentum is not None else 0.1)
             x.xt_off = alloc(in_n * xs * 2)
             x.stat_off = stat_off
             stat_off += 2 * out_n
@@ -208,6 +218,15 @@ class FusedMLPTrainer:
         self.v = torch.zeros_like(self.params)
         self.scratch = torch.zeros(max(1, scratch_off), dtype=torch.float32, device=dev)
         self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
+        self.img = torch.zeros(max(8, img_off), dtype=torch.bfloat16, device=dev)
+        self.rstats = torch.zeros(max(1, rs_total), dtype=torch.float32, device=dev)
+        for bn, ro, n_ in rs_init:
+            self.rstats[ro:ro + n_] = bn.running_mean.detach().to(dev, torch.float32)
+            self.rstats[ro + n_:ro + 2 * n_] = bn.running_var.detach().to(dev, torch.float32)
+            self.run_bufs.append((bn, self.rstats[ro:ro + n_], self.rstats[ro + n_:ro + 2 * n_]))
+        base = self.img.data_ptr()
+        for si, wi, wti in seg_images:
+            o.seg[si].W, o.seg[si].Wt = base + 2 * wi, base + 2 * wti
         cfg = self.cfg
         o.nseg, o.total, o.algo = nseg, total, cfg["algo"]
         o.b1, o.b2, o.eps = cfg.get("b1", 0.9), cfg.get("b2", 0.999), cfg.get("eps", 1e-8)
@@ -220,6 +239,15 @@ class FusedMLPTrainer:
         self._opt_buf = torch.frombuffer(bytearray(bytes(o)), dtype=torch.uint8).to(dev)
         self._dd = ctypes.c_void_p(self._desc_buf.data_ptr())
         self._od = ctypes.c_void_p(self._opt_buf.data_ptr())
+        b = _hip.StepBufs()
+        b.d_dev, b.img, b.rstats = self._desc_buf.data_ptr(), self.img.data_ptr(), self.rstats.data_ptr()
+        b.params, b.grads = self.params.data_ptr(), self.grads.data_ptr()
+        b.scratch, b.metrics = self.scratch.data_ptr(), self.metrics.data_ptr()
+        self.bufs = b
+        self.jit = None
+        if jit_enabled():
+            from raydp_amd.ops import mlp_jit
+            self.jit = mlp_jit.load_specialized(self)
         self.refresh_images()
 
     def refresh_images(self):
@@ -271,18 +299,16 @@ class FusedMLPTrainer:
             ar_fn = comm.fn_ptr if comm is not None else pp(0)
             ar_ctx = pp(comm.ctx) if comm is not None else pp(0)
             rc = self.lib.rx_mlp_train_steps(
-                ctypes.byref(self.desc), self._dd, ctypes.byref(self.opt), self._od, self.mt, pp(self.params.data_ptr()),
-                pp(self.grads.data_ptr()), pp(self.m.data_ptr()), pp(self.v.data_ptr()),
+                ctypes.byref(self.desc), ctypes.byref(self.bufs), ctypes.byref(self.opt), self._od, self.mt,
+                pp(self.m.data_ptr()), pp(self.v.data_ptr()),
                 pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, 0, nsteps,
-                lrs, bc1, bc2, ctypes.c_float(gscale), int(self.step_count == 0), pp(self.scratch.data_ptr()),
-                pp(self.metrics.data_ptr()), stream, ar_fn, ar_ctx)
+                lrs, bc1, bc2, ctypes.c_float(gscale), int(self.step_count == 0), stream, ar_fn, ar_ctx)
             _hip.check(rc, "rx_mlp_train_steps")
         else:
             for s in range(nsteps):
                 rc = self.lib.rx_mlp_fwdbwd(
-                    ctypes.byref(self.desc), self._dd, self.mt, pp(self.params.data_ptr()), pp(self.grads.data_ptr()),
-                    pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, s,
-                    pp(self.scratch.data_ptr()), pp(self.metrics.data_ptr()), stream)
+                    ctypes.byref(self.desc), ctypes.byref(self.bufs), self.mt,
+                    pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, s, stream)
                 _hip.check(rc, "rx_mlp_fwdbwd")
                 allreduce(self.grads)
                 rc = self.lib.rx_opt_step(ctypes.byref(self.opt), self._od, pp(self.params.data_ptr()),
@@ -301,10 +327,10 @@ class FusedMLPTrainer:
         pp = ctypes.c_void_p
         self.metrics.zero_()
         rc = self.lib.rx_mlp_fwdbwd(
-            ctypes.byref(self.desc), self._dd, self.mt, pp(self.params.data_ptr()), pp(self.grads.data_ptr()),
+            ctypes.byref(self.desc), ctypes.byref(self.bufs), self.mt,
             pp(feats.data_ptr()), pp(labels.data_ptr()),
             pp(perm.data_ptr()) if perm is not None else pp(0), n_rows, self.batch, step,
-            pp(self.scratch.data_ptr()), pp(self.metrics.data_ptr()), _hip.stream_ptr(self.device))
+            _hip.stream_ptr(self.device))
         _hip.check(rc, "rx_mlp_fwdbwd")
         return self.grads
 
@@ -319,9 +345,9 @@ class FusedMLPTrainer:
     def evaluate(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int) -> Dict[str, float]:
         self.metrics.zero_()
         pp = ctypes.c_void_p
-        rc = self.lib.rx_mlp_eval(ctypes.byref(self.desc), self._dd, self.mt, pp(self.params.data_ptr()),
+        rc = self.lib.rx_mlp_eval(ctypes.byref(self.desc), ctypes.byref(self.bufs), self.mt,
                                   pp(feats.data_ptr()), pp(labels.data_ptr()), n_rows, self.batch,
-                                  pp(self.metrics.data_ptr()), _hip.stream_ptr(self.device))
+                                  _hip.stream_ptr(self.device))
         _hip.check(rc, "rx_mlp_eval")
         return self._read_metrics()
 

@@ -1,0 +1,144 @@
+"""Per-model specialised fused-MLP step kernels.
+
+``FusedMLPTrainer`` describes its network with an ``MlpDesc`` (layer dims, paddings, LDS and
+buffer offsets, loss). The ahead-of-time kernel reads that descriptor from device memory at
+run time; this module instead *generates* a translation unit in which every one of those
+numbers is a compile-time constant (empty structs with ``static constexpr`` members, consumed
+by the same device code in ``csrc/hip/mlp_core.h``), compiles it for gfx950 with
+``hipcc --genco`` and loads the code object with ``hipModuleLoad``. With the layer loop
+unrolled and all offsets known, the compiler schedules each layer's loads, MFMAs and
+epilogue as straight-line code (no descriptor loads, no dead branches, exact trip counts).
+
+Code objects are cached by content hash under ``raydp_amd/native/jit/`` (in-tree, so a cache
+warmed by ``__graft_entry__.build()`` travels with the repository); a cold cache costs one
+hipcc run (~10-20 s) per distinct model/loss/batch-size.
+"""
+import ctypes
+import hashlib
+import os
+import subprocess
+import threading
+from typing import Optional
+
+from raydp_amd.ops import _hip
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
+CSRC_HIP = os.path.join(ROOT, "csrc", "hip")
+CACHE = os.environ.get("RAYDP_JIT_CACHE", os.path.join(ROOT, "raydp_amd", "native", "jit"))
+ARCH = os.environ.get("RAYDP_GPU_ARCH", "gfx950")
+_lock = threading.Lock()
+_loaded = {}
+
+_LAYER_INT = ("in_", "out", "in_k", "out_k", "in_n", "out_n", "w_img", "wt_img", "w_off", "b_off", "act", "bn",
+              "g_off", "be_off", "rs_off", "xt_off", "stat_off", "r_off", "pr_off")
+_DESC_INT = ("L", "r_lds_off", "gt_lds_off", "stats_lds_off", "lds_bytes", "max_k", "max_n", "loss", "out_dim",
+             "feat_k", "pr_lds_off", "pr_total")
+
+
+def _f(x: float) -> str:
+    return repr(float(x)) + "f" if "e" in repr(float(x)) or "." in repr(float(x)) else f"{float(x)}f"
+
+
+def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
+    L = desc.L
+    out = ['#include "mlp_core.h"', "", "namespace {", "", "struct JD {"]
+    for k in _DESC_INT:
+        out.append(f"  static constexpr int {k} = {int(getattr(desc, k))};")
+    out.append(f"  static constexpr float beta = {_f(desc.beta)};")
+    out.append("};")
+    for li in range(L):
+        ly = desc.layer[li]
+        out.append(f"struct JL{li} {{")
+        for k in _LAYER_INT:
+            out.append(f"  static constexpr int {k.rstrip('_')} = {int(getattr(ly, k))};")
+        out.append(f"  static constexpr float eps = {_f(ly.eps)};")
+        out.append(f"  static constexpr float momentum = {_f(ly.momentum)};")
+        out.append("};")
+    fwd = "; ".join(f"f(JL{li}{{}}, JL{min(li + 1, L - 1)}{{}}, {li}, {'true' if li == L - 1 else 'false'})"
+                    for li in range(L))
+    bwd = "; ".join(f"f(JL{li}{{}}, JL{max(li - 1, 0)}{{}}, {li})" for li in range(L - 1, -1, -1))
+    each = "; ".join(f"f(JL{li}{{}}, {li})" for li in range(L))
+    out += [
+        "struct JitCfg {",
+        "  __device__ static JD desc(const MlpDesc*) { return {}; }",
+        f"  template <class F> __device__ static void fwd_layers(const JD&, F&& f) {{ {fwd}; }}",
+        f"  template <class F> __device__ static void bwd_layers(const JD&, F&& f) {{ {bwd}; }}",
+        f"  template <class F> __device__ static void each_layer(const JD&, F&& f) {{ {each}; }}",
+        "  __device__ static JL0 first(const JD&) { return {}; }",
+        "};",
+        "}  // namespace",
+        "",
+        f"#define RX_MT {mt}",
+        'extern "C" __global__ __launch_bounds__(RX_THREADS) void rx_jit_step(',
+        "    const MlpDesc* __restrict__ dp, const u16* __restrict__ img, float* __restrict__ rstats,",
+        "    const float* __restrict__ P, float* __restrict__ Gr, const u16* __restrict__ feats,",
+        "    const float* __restrict__ labels, const int* __restrict__ perm, int row0, int nvalid,",
+        "    float* __restrict__ scratch, double* __restrict__ metrics, unsigned long long* __restrict__ stamps) {",
+        "  extern __shared__ __attribute__((aligned(16))) char smem[];",
+        "  __shared__ int rowidx[Tile<RX_MT>::BP];",
+        "  mlp_train_step_body<JitCfg, RX_MT>(dp, img, rstats, P, Gr, feats, labels, perm, row0, nvalid, scratch,",
+        "                                     metrics, stamps, smem, rowidx);",
+        "}",
+        'extern "C" __global__ __launch_bounds__(RX_THREADS) void rx_jit_eval(',
+        "    const MlpDesc* __restrict__ dp, const u16* __restrict__ img, const float* __restrict__ rstats,",
+        "    const float* __restrict__ P, const u16* __restrict__ feats, const float* __restrict__ labels,",
+        "    int n_rows, int batch, double* __restrict__ metrics) {",
+        "  extern __shared__ __attribute__((aligned(16))) char smem[];",
+        "  __shared__ int rowidx[Tile<RX_MT>::BP];",
+        "  mlp_eval_body<JitCfg, RX_MT>(dp, img, rstats, P, feats, labels, n_rows, batch, metrics, smem, rowidx);",
+        "}",
+    ]
+    return "\n".join(out) + "\n"
+
+
+def _hipcc() -> str:
+    return os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+
+
+def _key(src: str) -> str:
+    h = hashlib.sha256(src.encode())
+    for f in ("mlp_core.h", "rx_common.h"):
+        with open(os.path.join(CSRC_HIP, f), "rb") as fh:
+            h.update(fh.read())
+    h.update(ARCH.encode())
+    return h.hexdigest()[:24]
+
+
+def compile_source(src: str) -> str:
+    """Compile (or find in the cache) the code object for ``src``; returns its path."""
+    key = _key(src)
+    path = os.path.join(CACHE, f"mlp_{key}.hsaco")
+    if os.path.exists(path):
+        return path
+    os.makedirs(CACHE, exist_ok=True)
+    cpp = os.path.join(CACHE, f"mlp_{key}.hip")
+    with open(cpp, "w") as f:
+        f.write(src)
+    tmp = path + f".tmp{os.getpid()}"
+    cmd = [_hipcc(), "--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-munsafe-fp-atomics",
+           "-I", CSRC_HIP, cpp, "-o", tmp]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"specialised kernel build failed:\n{' '.join(cmd)}\n{r.stdout[-4000:]}")
+    os.replace(tmp, path)
+    return path
+
+
+def compile_for(trainer) -> str:
+    return compile_source(generate_source(trainer.desc, trainer.mt))
+
+
+def load_specialized(trainer) -> Optional[str]:
+    """Compile/load the specialised kernels for ``trainer`` and plug them into its buffers."""
+    path = compile_for(trainer)
+    with _lock:
+        fns = _loaded.get(path)
+        if fns is None:
+            step, ev = ctypes.c_void_p(), ctypes.c_void_p()
+            _hip.check(_hip.lib().rx_jit_load(path.encode(), ctypes.byref(step), ctypes.byref(ev),
+                                              int(trainer.desc.lds_bytes)), "rx_jit_load")
+            fns = (step.value, ev.value)
+            _loaded[path] = fns
+    trainer.bufs.jit_step, trainer.bufs.jit_eval = fns
+    return path

@@ -18,8 +18,7 @@ model = NYC()
 tr = FusedMLPTrainer(extract_mlp_spec(model), optimizer_config(torch.optim.Adam(model.parameters())),
                      loss_code(nn.SmoothL1Loss()), 64, dev)
 stamps = torch.zeros(64, dtype=torch.int64, device=dev)
-tr.desc.stamps = stamps.data_ptr()
-tr._desc_buf.copy_(torch.frombuffer(bytearray(bytes(tr.desc)), dtype=torch.uint8).to(dev))
+tr.bufs.stamps = stamps.data_ptr()
 n = 64 * 200
 feats = torch.zeros(n, tr.feat_k, dtype=torch.bfloat16, device=dev)
 feats[:, :20] = torch.randn(n, 20, device=dev).to(torch.bfloat16)
