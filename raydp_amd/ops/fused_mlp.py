@@ -75,8 +75,12 @@ def pick_mt(batch: int) -> Optional[int]:
 
 class FusedMLPTrainer:
     def __init__(self, spec: MlpSpec, opt_cfg: dict, loss: tuple, batch_size: int,
-                 device: torch.device, lr_schedule: Optional[Callable[[int], float]] = None):
-        self.spec, self.cfg, self.device = spec, opt_cfg, torch.device(device)
+                 device: torch.device, lr_schedule: Optional[Callable[[int], float]] = None,
+                 layout_only: bool = False):
+        # layout_only: build the descriptors on the host (no GPU needed) -- used to warm the
+        # specialised-kernel cache at build time
+        self.layout_only = layout_only
+        self.spec, self.cfg, self.device = spec, opt_cfg, torch.device("cpu" if layout_only else device)
         self.batch = int(batch_size)
         self.mt = pick_mt(self.batch)
         if self.mt is None:
@@ -245,6 +249,8 @@ class FusedMLPTrainer:
         b.scratch, b.metrics = self.scratch.data_ptr(), self.metrics.data_ptr()
         self.bufs = b
         self.jit = None
+        if self.layout_only:
+            return
         if jit_enabled():
             from raydp_amd.ops import mlp_jit
             self.jit = mlp_jit.load_specialized(self)

@@ -142,3 +142,12 @@ def load_specialized(trainer) -> Optional[str]:
             _loaded[path] = fns
     trainer.bufs.jit_step, trainer.bufs.jit_eval = fns
     return path
+
+
+def precompile(model, optimizer, loss, batch_size: int) -> str:
+    """Warm the code-object cache for one model/optimizer/loss/batch on a host without a GPU."""
+    from raydp_amd.models.mlp_spec import extract_mlp_spec
+    from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+    tr = FusedMLPTrainer(extract_mlp_spec(model), optimizer_config(optimizer), loss_code(loss), batch_size,
+                         None, layout_only=True)
+    return compile_for(tr)
