@@ -187,7 +187,7 @@ class DataFrame:
 
     @property
     def rdd(self):
-        return _RDD(self)
+        return _df_rdd(self)
 
     @property
     def write(self):
@@ -671,23 +671,17 @@ class DataFrame:
         return self.count()
 
 
-class _RDD:
-    """Minimal ``df.rdd`` view (partition count, row iteration)."""
+def _df_rdd(df: "DataFrame"):
+    """``df.rdd``: an RDD of Row objects whose partitions are the DataFrame's partitions."""
+    from raydp_amd.spark.rdd import RDD
+    plan = df._src()
+    P.prepare(plan, df._session._scheduler_or_default())
+    names = plan.schema.names
 
-    def __init__(self, df: DataFrame):
-        self._df = df
-
-    def getNumPartitions(self) -> int:
-        return self._df._src().num_partitions()
-
-    def collect(self):
-        return self._df.collect()
-
-    def count(self):
-        return self._df.count()
-
-    def map(self, f):
-        return [f(r) for r in self._df.collect()]
-
-    def id(self):
-        return self._df._id
+    def rows(i):
+        t = plan.compute(i)
+        cols = [c.to_pylist() for c in t.columns]
+        return [Row._make(names, vals) for vals in zip(*cols)] if cols else []
+    r = RDD(df._session, plan.num_partitions(), rows, "dataframe")
+    r._id_str = df._id
+    return r

@@ -56,7 +56,7 @@ def spark_dataframe_to_ray_dataset(df: DataFrame, parallelism: Optional[int] = N
 def from_spark_recoverable(df: DataFrame, storage_level=StorageLevel.MEMORY_AND_DISK,
                            parallelism: Optional[int] = None) -> Dataset:
     original = df
-    if parallelism is not None and parallelism != df.rdd.getNumPartitions():
+    if parallelism is not None and parallelism != df._src().num_partitions():
         df = df.repartition(parallelism)
     backend = df.sparkSession._cluster
     if backend is not None:

@@ -378,13 +378,12 @@ def sort_table(t: pa.Table, sort_keys) -> pa.Table:
         return t
     tmp = t
     keys = []
-    null_first = None
     for j, (e, asc, nulls_first) in enumerate(sort_keys):
         name = f"__sk{j}"
         from raydp_amd.spark.column import as_array
         tmp = tmp.append_column(name, as_array(e.eval(t), t.num_rows))
-        keys.append((name, "ascending" if asc else "descending"))
-        null_first = nulls_first if null_first is None else null_first
-    idx = pc.sort_indices(tmp, sort_keys=keys,
-                          null_placement="at_start" if null_first else "at_end")
+        # Spark default: nulls first for ascending, last for descending
+        nf = asc if nulls_first is None else nulls_first
+        keys.append((name, "ascending" if asc else "descending", "at_start" if nf else "at_end"))
+    idx = pc.sort_indices(tmp, sort_keys=keys)
     return t.take(idx)

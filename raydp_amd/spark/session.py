@@ -91,7 +91,22 @@ class SparkContext:
         self._session.stop()
 
     def parallelize(self, data, numSlices=None):
-        return self._session.createDataFrame([(x,) for x in data], ["value"])
+        from raydp_amd.spark.rdd import RDD
+        data = list(data)
+        n = max(1, int(numSlices or self.defaultParallelism))
+        n = min(n, max(1, len(data)))
+        bounds = [len(data) * k // n for k in range(n + 1)]
+        parts = [data[bounds[k]:bounds[k + 1]] for k in range(n)]
+        return RDD(self._session, n, lambda i: parts[i], "parallelize")
+
+    def range(self, start, end=None, step=1, numSlices=None):
+        if end is None:
+            start, end = 0, start
+        return self.parallelize(range(start, end, step), numSlices)
+
+    def emptyRDD(self):
+        from raydp_amd.spark.rdd import RDD
+        return RDD(self._session, 1, lambda i: [], "empty")
 
 
 def _to_arrow_schema(schema) -> pa.Schema:
@@ -299,56 +314,71 @@ class SparkSession:
         return DataFrame(P.SourcePlan(RangeSource(start, end, step, n)), self)
 
     def createDataFrame(self, data, schema=None, samplingRatio=None, verifySchema=True) -> DataFrame:
+        from raydp_amd.spark.rdd import RDD, RDDSource
+        if isinstance(data, RDD):
+            src = RDDSource(data, schema, rows_to_table)
+            src.schema()   # resolved on the driver, shipped with the plan
+            return DataFrame(P.SourcePlan(src), self)
         table = self._to_table(data, schema)
         n = self._default_parallelism()
         n = max(1, min(n, table.num_rows)) if table.num_rows else 1
-        return DataFrame(P.SourcePlan(TableSource(split_table(table, n), table.schema)), self)
+        parts = split_table(table, n)
+        if getattr(self._scheduler, "remote", False):
+            # executors are processes: place the source partitions in the object store once
+            from raydp_amd.runtime.serialization import share_table
+            parts = [share_table(t) for t in parts]
+        return DataFrame(P.SourcePlan(TableSource(parts, table.schema)), self)
 
     def _to_table(self, data, schema) -> pa.Table:
-        import pandas as pd
-        if isinstance(data, pa.Table):
-            return data if schema is None else data.cast(_to_arrow_schema(schema))
-        if isinstance(data, pd.DataFrame):
-            t = pa.Table.from_pandas(data, preserve_index=False)
-            if schema is not None:
-                target = _to_arrow_schema(schema) if not isinstance(schema, (list, tuple)) else None
-                if target is not None:
-                    t = t.rename_columns(target.names).cast(target)
-                else:
-                    t = t.rename_columns(list(schema))
-            return t
-        rows = list(data)
-        names = None
-        target = None
-        if isinstance(schema, (list, tuple)):
-            names = list(schema)
-        elif schema is not None:
-            target = _to_arrow_schema(schema)
-            names = target.names
-        if rows and isinstance(rows[0], dict):
-            names = names or list(rows[0].keys())
-            cols = {k: [r.get(k) for r in rows] for k in names}
-        elif rows and isinstance(rows[0], Row) and rows[0].__fields__:
-            names = names or list(rows[0].__fields__)
-            cols = {k: [r[j] for r in rows] for j, k in enumerate(names)}
-        else:
-            rows = [r if isinstance(r, (tuple, list)) else (r,) for r in rows]
-            width = len(rows[0]) if rows else (len(names) if names else 0)
-            names = names or [f"_{j + 1}" for j in range(width)]
-            cols = {k: [r[j] for r in rows] for j, k in enumerate(names)}
-        if target is not None:
-            arrays = [pa.array(cols[f.name], type=f.type) for f in target]
-            return pa.Table.from_arrays(arrays, schema=target)
-        arrays = []
-        for k in names:
-            vals = cols[k]
-            ty = None
-            for v in vals:
-                ty = _infer_value_type(v)
-                if ty is not None:
-                    break
-            arrays.append(pa.array(vals, type=ty))
-        return pa.Table.from_arrays(arrays, names=names)
+        return rows_to_table(data, schema)
+
+
+def rows_to_table(data, schema) -> pa.Table:
+    """Python rows / dicts / Row objects / pandas frame -> Arrow table (createDataFrame)."""
+    import pandas as pd
+    if isinstance(data, pa.Table):
+        return data if schema is None else data.cast(_to_arrow_schema(schema))
+    if isinstance(data, pd.DataFrame):
+        t = pa.Table.from_pandas(data, preserve_index=False)
+        if schema is not None:
+            target = _to_arrow_schema(schema) if not isinstance(schema, (list, tuple)) else None
+            if target is not None:
+                t = t.rename_columns(target.names).cast(target)
+            else:
+                t = t.rename_columns(list(schema))
+        return t
+    rows = list(data)
+    names = None
+    target = None
+    if isinstance(schema, (list, tuple)):
+        names = list(schema)
+    elif schema is not None:
+        target = _to_arrow_schema(schema)
+        names = target.names
+    if rows and isinstance(rows[0], dict):
+        names = names or list(rows[0].keys())
+        cols = {k: [r.get(k) for r in rows] for k in names}
+    elif rows and isinstance(rows[0], Row) and rows[0].__fields__:
+        names = names or list(rows[0].__fields__)
+        cols = {k: [r[j] for r in rows] for j, k in enumerate(names)}
+    else:
+        rows = [r if isinstance(r, (tuple, list)) else (r,) for r in rows]
+        width = len(rows[0]) if rows else (len(names) if names else 0)
+        names = names or [f"_{j + 1}" for j in range(width)]
+        cols = {k: [r[j] for r in rows] for j, k in enumerate(names)}
+    if target is not None:
+        arrays = [pa.array(cols[f.name], type=f.type) for f in target]
+        return pa.Table.from_arrays(arrays, schema=target)
+    arrays = []
+    for k in names:
+        vals = cols[k]
+        ty = None
+        for v in vals:
+            ty = _infer_value_type(v)
+            if ty is not None:
+                break
+        arrays.append(pa.array(vals, type=ty))
+    return pa.Table.from_arrays(arrays, names=names)
 
 
 class _UDFRegistration:

@@ -1,0 +1,70 @@
+"""TorchEstimator on Spark data (port of the reference's tests/test_torch.py and
+tests/test_torch_sequential.py). CPU path: gloo workers spawned by the trainer."""
+import os
+import shutil
+
+import pytest
+import torch
+
+import raydp  # noqa: F401
+import pyspark.pandas as ps
+from raydp.torch import TorchEstimator
+from raydp.utils import random_split
+
+
+@pytest.mark.parametrize("use_fs_directory", [True, False])
+def test_torch_estimator(spark_on_ray_small, use_fs_directory, tmp_path):
+    _ = spark_on_ray_small
+    df = ps.range(0, 100000)
+    df["x"] = df["id"] + 100
+    df["y"] = df["id"] + 1000
+    df["z"] = df["x"] * 3 + df["y"] * 4 + 5
+    df = df.astype("float")
+    train_df, test_df = random_split(df, [0.7, 0.3])
+
+    class LinearModel(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.linear = torch.nn.Linear(2, 1)
+
+        def forward(self, x):
+            return self.linear(x)
+
+    model = LinearModel()
+    optimizer = torch.optim.Adam(model.parameters())
+    loss = torch.nn.MSELoss()
+
+    def lr_scheduler_creator(optimizer, config):
+        return torch.optim.lr_scheduler.MultiStepLR(optimizer, milestones=[150, 250, 350], gamma=0.1)
+
+    estimator = TorchEstimator(num_workers=2, model=model, optimizer=optimizer, loss=loss,
+                               lr_scheduler_creator=lr_scheduler_creator, feature_columns=["x", "y"],
+                               feature_types=torch.float, label_column="z", label_type=torch.float,
+                               batch_size=1000, num_epochs=2, use_gpu=False)
+    if use_fs_directory:
+        d = str(tmp_path / "test_torch")
+        estimator.fit_on_spark(train_df, test_df, fs_directory="file://" + d)
+    else:
+        estimator.fit_on_spark(train_df, test_df)
+    model = estimator.get_model()
+    result = model(torch.Tensor([[0, 0], [1, 1]]))
+    assert result.shape == (2, 1)
+    hist = estimator.results.metrics_history
+    assert any("train_loss" in h for h in hist)
+
+
+def test_torch_estimator_sequential(spark_on_ray_small):
+    customers = [(1, "James", 21, 6), (2, "Liz", 25, 8), (3, "John", 31, 6), (4, "Jennifer", 45, 7),
+                 (5, "Robert", 41, 5), (6, "Sandra", 45, 8)]
+    df = spark_on_ray_small.createDataFrame(customers, ["cID", "name", "age", "grade"])
+    model = torch.nn.Sequential(torch.nn.Linear(1, 2), torch.nn.Linear(2, 1))
+    optimizer = torch.optim.Adam(model.parameters())
+    loss = torch.nn.MSELoss()
+    estimator = TorchEstimator(model=model, optimizer=optimizer, loss=loss, num_workers=3, num_epochs=5,
+                               feature_columns=["age"], feature_types=torch.float, label_column="grade",
+                               label_type=torch.float, batch_size=1)
+    estimator.fit_on_spark(df)
+    assert estimator.get_model()(torch.tensor([[30.0]])).shape == (1, 1)
+
+
+_ = (os, shutil)
