@@ -86,6 +86,17 @@ def install_ray():
          FailureConfig=train.FailureConfig, CheckpointConfig=train.CheckpointConfig)
     sys.modules["ray.air.session"] = importlib.import_module("raydp_amd.train.session")
     _mod("ray.job_config", JobConfig=api.JobConfig)
+    hvd = importlib.import_module("raydp_amd.hvd")
+    train.horovod = _mod("ray.train.horovod", HorovodTrainer=hvd.HorovodTrainer)
+
+
+def install_horovod():
+    if not _missing("horovod"):
+        return
+    hvd = importlib.import_module("raydp_amd.hvd")
+    top = _mod("horovod", __version__="0.28.1-raydp-amd")
+    top.torch = hvd
+    sys.modules["horovod.torch"] = hvd
 
 
 def install_pyspark():
@@ -112,3 +123,4 @@ def install_pyspark():
 def install():
     install_ray()
     install_pyspark()
+    install_horovod()

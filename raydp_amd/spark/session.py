@@ -203,9 +203,30 @@ class Builder:
                 for k, v in self._options.items():
                     _active_session.conf.set(k, v)
                 return _active_session
-            s = SparkSession(dict(self._options))
+            opts = dict(_submit_conf())
+            opts.update(self._options)
+            master = opts.get("spark.master", "")
+            if master == "ray" or master.startswith("ray://"):
+                # "--master ray" (raydp-submit / RayCoarseGrainedSchedulerBackend.scala:81-117):
+                # bring up the runtime and the executor cluster for this application
+                from raydp_amd.context import init_spark
+                return init_spark(opts.get("spark.app.name", "raydp-app"),
+                                  int(opts.get("spark.executor.instances", "1")),
+                                  int(opts.get("spark.executor.cores", "1")),
+                                  opts.get("spark.executor.memory", "1g"),
+                                  enable_hive=opts.get("spark.sql.catalogImplementation") == "hive",
+                                  configs={k: v for k, v in opts.items() if k != "spark.master"})
+            s = SparkSession(opts)
             _active_session = s
             return s
+
+
+def _submit_conf() -> Dict[str, str]:
+    """Spark confs handed over by ``raydp-submit`` (RAYDP_SUBMIT_CONF, JSON)."""
+    import json
+    import os
+    raw = os.environ.get("RAYDP_SUBMIT_CONF")
+    return json.loads(raw) if raw else {}
 
 
 class SparkSession:
