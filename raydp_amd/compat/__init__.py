@@ -75,9 +75,7 @@ def install_ray():
     ray.train = train
     sys.modules["ray.train"] = train
     from raydp_amd.train import trainer as _tr
-    torch_mod = _mod("ray.train.torch", TorchTrainer=_tr.TorchTrainer,
-                     prepare_model=_tr.prepare_model, TorchCheckpoint=train.TorchCheckpoint)
-    train.torch = torch_mod
+    sys.modules["ray.train.torch"] = train.torch
     air = _mod("ray.air", session=importlib.import_module("raydp_amd.train.session"),
                ScalingConfig=train.ScalingConfig, RunConfig=train.RunConfig,
                FailureConfig=train.FailureConfig, CheckpointConfig=train.CheckpointConfig)
@@ -88,6 +86,22 @@ def install_ray():
     _mod("ray.job_config", JobConfig=api.JobConfig)
     hvd = importlib.import_module("raydp_amd.hvd")
     train.horovod = _mod("ray.train.horovod", HorovodTrainer=hvd.HorovodTrainer)
+    from raydp_amd.train import legacy
+    train.Trainer = legacy.Trainer
+    train.TrainingCallback = legacy.TrainingCallback
+    train.get_dataset_shard = importlib.import_module("raydp_amd.train.session").get_dataset_shard
+    train.report = importlib.import_module("raydp_amd.train.session").report
+
+
+def install_xgboost():
+    """``xgboost`` / ``xgboost_ray`` facades over the native GBDT (only when absent)."""
+    from raydp_amd.xgboost import gbdt, ray_api
+    if _missing("xgboost"):
+        _mod("xgboost", DMatrix=gbdt.DMatrix, Booster=gbdt.Booster, train=gbdt.train,
+             __version__="2.0.0-raydp-amd")
+    if _missing("xgboost_ray"):
+        _mod("xgboost_ray", RayDMatrix=ray_api.RayDMatrix, RayParams=ray_api.RayParams, train=ray_api.train,
+             predict=ray_api.predict)
 
 
 def install_horovod():
@@ -124,3 +138,35 @@ def install():
     install_ray()
     install_pyspark()
     install_horovod()
+    install_xgboost()
+
+
+class _LazyFacades:
+    """Meta-path hook: install the facades the first time user code imports one of the
+    faked top-level packages (keeps worker processes from importing torch at start-up)."""
+    _names = {"ray", "pyspark", "horovod", "xgboost", "xgboost_ray"}
+
+    def find_spec(self, fullname, path=None, target=None):
+        if fullname.split(".")[0] in self._names:
+            sys.meta_path[:] = [f for f in sys.meta_path if f is not self]
+            install()
+            if fullname in sys.modules:
+                import importlib.machinery
+                return importlib.machinery.ModuleSpec(fullname, _Preloaded(sys.modules[fullname]))
+        return None
+
+
+class _Preloaded:
+    def __init__(self, mod):
+        self.mod = mod
+
+    def create_module(self, spec):
+        return self.mod
+
+    def exec_module(self, module):
+        pass
+
+
+def install_lazy():
+    if not any(isinstance(f, _LazyFacades) for f in sys.meta_path):
+        sys.meta_path.insert(0, _LazyFacades())

@@ -1,0 +1,70 @@
+"""Legacy ``Dataset.to_torch`` iterable: ``(features, label)`` mini-batches as torch tensors.
+
+Feature layout rules (Ray Data 1.x contract the reference estimator relies on,
+``python/raydp/torch/estimator.py:300-330``): ``feature_columns`` as a list of names ->
+one ``[B, F]`` tensor (one dtype); a list of lists -> a list of ``[B, F_i]`` tensors; a dict
+name -> list -> a dict of tensors. Columns are converted with one numpy stack per batch; the
+label is ``[B, 1]`` when ``unsqueeze_label_tensor``.
+"""
+from typing import Any, List, Optional
+
+import numpy as np
+
+
+def _np_dtype(tdt):
+    import torch
+    if tdt is None:
+        return np.float32
+    return torch.empty((), dtype=tdt).numpy().dtype
+
+
+class TorchBatchIterable:
+    def __init__(self, ds, label_column, feature_columns, label_dtype, feature_dtypes, batch_size, drop_last,
+                 unsqueeze_label, device="cpu"):
+        self.ds = ds
+        self.label_column = label_column
+        self.feature_columns = feature_columns
+        self.label_dtype = label_dtype
+        self.feature_dtypes = feature_dtypes
+        self.batch_size = int(batch_size)
+        self.drop_last = drop_last
+        self.unsqueeze_label = unsqueeze_label
+        self.device = device
+
+    def _cols(self, t, names: List[str], dtype) -> Any:
+        import torch
+        nd = _np_dtype(dtype)
+        arr = np.stack([t.column(c).to_numpy(zero_copy_only=False).astype(nd, copy=False) for c in names], axis=1)
+        return torch.from_numpy(np.ascontiguousarray(arr)).to(self.device)
+
+    def _features(self, t):
+        fc = self.feature_columns
+        if fc is None:
+            fc = [c for c in t.column_names if c != self.label_column]
+        fd = self.feature_dtypes
+        if isinstance(fc, dict):
+            return {k: self._cols(t, v if isinstance(v, list) else [v], fd.get(k) if isinstance(fd, dict) else fd)
+                    for k, v in fc.items()}
+        if fc and isinstance(fc[0], (list, tuple)):
+            dts = fd if isinstance(fd, (list, tuple)) else [fd] * len(fc)
+            return [self._cols(t, list(names), dt) for names, dt in zip(fc, dts)]
+        if isinstance(fd, (list, tuple)):
+            return [self._cols(t, [c], dt) for c, dt in zip(fc, fd)]
+        return self._cols(t, list(fc), fd)
+
+    def __iter__(self):
+        import torch
+        for t in self.ds.iter_batches(self.batch_size, "pyarrow", self.drop_last):
+            feats = self._features(t)
+            label: Optional[torch.Tensor] = None
+            if self.label_column is not None:
+                nd = _np_dtype(self.label_dtype)
+                lab = t.column(self.label_column).to_numpy(zero_copy_only=False).astype(nd, copy=False)
+                label = torch.from_numpy(np.ascontiguousarray(lab)).to(self.device)
+                if self.unsqueeze_label:
+                    label = label.unsqueeze(1)
+            yield feats, label
+
+    def __len__(self):
+        n = self.ds.count()
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)

@@ -57,6 +57,11 @@ def main() -> int:
     sdir = os.environ["RAYDP_SESSION_DIR"]
     from raydp_amd.runtime import core
     core.attach_from_env()
+    try:   # same ray / pyspark / horovod facades as the driver, installed on first import
+        from raydp_amd import compat
+        compat.install_lazy()
+    except Exception:  # noqa: BLE001
+        pass
     from raydp_amd.runtime import serialization as S
     spec_path, sock_path, err_path = actor_paths(sdir, aid)
     import cloudpickle

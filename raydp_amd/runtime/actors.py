@@ -278,6 +278,9 @@ class ActorManager:
         ra, rk = _resolve_args(args, kwargs)
         clean = {k: v for k, v in opts.items() if k not in ("scheduling_strategy", "placement_group")}
         a.opts = dict(opts, _class_name=getattr(cls, "__name__", str(cls)))
+        a.gpu_ids = self._take_gpus(vnode, res.get("GPU", 0.0))
+        if a.gpu_ids:
+            a.opts["_gpu_ids"] = a.gpu_ids
         with open(a.spec_path + ".tmp", "wb") as f:
             cloudpickle.dump((cls, ra, rk, clean), f)
         os.replace(a.spec_path + ".tmp", a.spec_path)
@@ -318,11 +321,25 @@ class ActorManager:
             vn.acquire(req)
             return vn, req, None, None
 
+    @staticmethod
+    def _take_gpus(vnode, n: float):
+        """Whole-GPU assignment: the actor sees exactly these devices (HIP_VISIBLE_DEVICES)."""
+        import math
+        if vnode is None or not n:
+            return []
+        if not hasattr(vnode, "gpu_free"):
+            vnode.gpu_free = list(range(int(vnode.total.get("GPU", 0))))
+        k = max(1, int(math.ceil(n)))
+        ids, vnode.gpu_free = vnode.gpu_free[:k], vnode.gpu_free[k:]
+        return ids
+
     def release(self, a: ProcessActor):
         with self._lock:
             if getattr(a, "_released", False):
                 return
             a._released = True
+        if getattr(a, "gpu_ids", None) and a.vnode is not None:
+            a.vnode.gpu_free = sorted(set(getattr(a.vnode, "gpu_free", [])) | set(a.gpu_ids))
         cl = self.node.cluster
         with cl.lock:
             if a.pg is not None:

@@ -10,3 +10,5 @@ __all__ = ["Checkpoint", "TorchCheckpoint", "CheckpointConfig", "FailureConfig",
            "ScalingConfig", "get_checkpoint", "get_context", "get_dataset_shard", "get_device",
            "get_local_rank", "get_world_rank", "get_world_size", "report", "DataParallelTrainer",
            "Result", "TorchTrainer", "TrainingFailedError", "prepare_model"]
+
+from raydp_amd.train import torch  # noqa: E402,F401  (ray.train.torch)

@@ -230,43 +230,91 @@ class DataParallelTrainer:
                 dist.destroy_process_group()
 
     def _run_spawned(self, world, use_gpu, storage, reporter):
-        import multiprocessing as mp
+        """Worker group of ``world`` process actors (one per rank, GPUs assigned by the
+        runtime), joined into one ``torch.distributed`` group (RCCL when they own GPUs)."""
         import cloudpickle
-        ctx = mp.get_context("spawn")
-        queue = ctx.Queue()
+        from raydp_amd import runtime
+        from raydp_amd.runtime import pgroup
+        res = dict(self.scaling.resources_per_worker or {})
+        cpus = float(res.pop("CPU", 1))
+        gpus = float(res.pop("GPU", 1 if use_gpu else 0)) if use_gpu else 0.0
+        bundle = {"CPU": cpus}
+        if gpus:
+            bundle["GPU"] = gpus
+        bundle.update(res)
+        strategy = self.scaling.placement_strategy if isinstance(self.scaling.placement_strategy, str) else "PACK"
+        pg = pgroup.placement_group([dict(bundle) for _ in range(world)], strategy=strategy)
         port = _free_port()
-        procs = []
-        for r in range(world):
-            shards = _shard(self.datasets, r, world)
-            for ds in shards.values():
-                if hasattr(ds, "materialize"):
-                    ds.materialize()
-            payload = cloudpickle.dumps((self.fn, self.config, shards, use_gpu, storage, "raydp"))
-            p = ctx.Process(target=_worker_entry, args=(r, world, port, payload, queue), daemon=True)
-            p.start()
-            procs.append(p)
-        done = set()
-        error = None
-        while len(done) < world and error is None:
-            try:
-                kind, rank, a, b = queue.get(timeout=1.0)
-            except Exception:  # noqa: BLE001 - queue.Empty
-                dead = [p for p in procs if not p.is_alive() and p.exitcode not in (0, None)]
-                if dead:
-                    error = f"worker process exited with code {dead[0].exitcode}"
-                continue
-            if kind == "report":
-                reporter(rank, a, b)
-            elif kind == "done":
-                done.add(rank)
-            elif kind == "error":
-                error = a
-        for p in procs:
-            if error is not None and p.is_alive():
-                p.terminate()
-            p.join(timeout=30)
-        if error is not None:
-            raise _WorkerFailure(error)
+        cls = runtime.remote(_TrainWorker)
+        workers = []
+        try:
+            for r in range(world):
+                opts = {"num_cpus": cpus, "num_gpus": gpus, "placement_group": pg,
+                        "placement_group_bundle_index": r, "max_concurrency": 2}
+                if res:
+                    opts["resources"] = res
+                workers.append(cls.options(**opts).remote(r, world, storage, use_gpu))
+            runtime.get([w.setup.remote("127.0.0.1", port) for w in workers])
+            refs = []
+            for r, w in enumerate(workers):
+                shards = _shard(self.datasets, r, world)
+                payload = cloudpickle.dumps((self.fn, self.config, shards, self.resume))
+                refs.append(w.run.remote(payload))
+            outs, error = [None] * world, None
+            for r, ref in enumerate(refs):
+                try:
+                    outs[r] = runtime.get(ref)
+                except Exception:  # noqa: BLE001 - a rank failed (user error or lost process)
+                    error = traceback.format_exc()
+                    break
+            if error is not None:
+                raise _WorkerFailure(error)
+            for r, reports in enumerate(outs):
+                for metrics, ckpt in reports:
+                    reporter(r, metrics, ckpt)
+        finally:
+            for w in workers:
+                try:
+                    runtime.kill(w, no_restart=True)
+                except Exception:  # noqa: BLE001
+                    pass
+            pgroup.remove_placement_group(pg)
+
+
+class _TrainWorker:
+    """One rank of a spawned worker group (a process actor)."""
+
+    def __init__(self, rank: int, world: int, storage: str, use_gpu: bool):
+        self.rank, self.world, self.storage, self.use_gpu = rank, world, storage, use_gpu
+
+    def setup(self, addr: str, port: int):
+        import torch
+        self.device = torch.device("cpu")
+        if self.use_gpu and torch.cuda.is_available():
+            torch.cuda.set_device(0)     # the runtime exposes exactly this worker's GPU(s)
+            self.device = torch.device("cuda", 0)
+        os.environ.update({"RANK": str(self.rank), "WORLD_SIZE": str(self.world), "LOCAL_RANK": "0",
+                           "MASTER_ADDR": addr, "MASTER_PORT": str(port)})
+        _init_dist("nccl" if self.device.type == "cuda" else "gloo", self.rank, self.world, addr, port)
+        return True
+
+    def run(self, payload: bytes):
+        import cloudpickle
+        fn, config, shards, resume = cloudpickle.loads(payload)
+        reports = []
+
+        def reporter(r, metrics, ckpt):
+            reports.append((metrics, ckpt))
+        ctx = S.TrainContext(self.rank, self.world, 0, 1, self.rank, self.device, "raydp", self.storage)
+        S._set_session(S._Session(ctx, shards, reporter, self.storage, resume))
+        try:
+            fn(config) if _accepts_arg(fn) else fn()
+        finally:
+            S._set_session(None)
+            import torch.distributed as dist
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        return reports
 
 
 class _WorkerFailure(Exception):

@@ -1,0 +1,22 @@
+"""The ported examples run end to end on CPU (reference: examples/*.py)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+EX = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples")
+
+
+@pytest.mark.parametrize("script,args,expect", [
+    ("pytorch_nyctaxi.py", [], "_training_iteration"),
+    ("raytrain_nyctaxi.py", [], "final"),
+    ("horovod_nyctaxi.py", ["--epochs", "1"], "'epoch': 1"),
+    ("xgboost_ray_nyctaxi.py", [], "Final validation rmse"),
+])
+def test_example_runs(script, args, expect):
+    env = dict(os.environ, NYC_EPOCHS="1")
+    r = subprocess.run([sys.executable, os.path.join(EX, script)] + args, cwd=EX, env=env, timeout=400,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert expect in r.stdout, r.stdout[-3000:]
