@@ -120,6 +120,10 @@ class _Pickler(cloudpickle.CloudPickler):
         self.store = _store()
 
     def reducer_override(self, obj):
+        if isinstance(obj, (pa.Table, pa.RecordBatch)) and (self.store is None or obj.nbytes < THRESHOLD):
+            # small tables travel inline as Arrow IPC: unlike Arrow's own pickling, IPC writes
+            # only the sliced range of each buffer (a slice must not drag its parent along)
+            return _from_ipc, (_to_ipc(obj), isinstance(obj, pa.RecordBatch))
         if self.store is not None and isinstance(obj, (pa.Table, pa.RecordBatch)) and obj.nbytes >= THRESHOLD:
             existing = _view_oid(obj)
             if existing is not None:
@@ -132,6 +136,23 @@ class _Pickler(cloudpickle.CloudPickler):
             self.oids.append(oid)
             return _load_shared, key
         return super().reducer_override(obj)
+
+
+def _to_ipc(obj) -> bytes:
+    sink = pa.BufferOutputStream()
+    with pa.ipc.new_stream(sink, obj.schema) as w:
+        if isinstance(obj, pa.RecordBatch):
+            w.write_batch(obj)
+        else:
+            w.write_table(obj)
+    return sink.getvalue().to_pybytes()
+
+
+def _from_ipc(data: bytes, batch: bool = False):
+    t = pa.ipc.open_stream(pa.py_buffer(data)).read_all()
+    if batch:
+        return t.combine_chunks().to_batches()[0] if t.num_rows else pa.RecordBatch.from_pylist([], t.schema)
+    return t
 
 
 class Payload:

@@ -36,6 +36,7 @@ logger = logging.getLogger(__name__)
 EXECUTOR_RESOURCE_PREFIX = "spark.ray.raydp_spark_executor.actor.resource."
 LEGACY_ACTOR_CPU = "spark.ray.actor.resource.cpu"
 MASTER_SUFFIX = "_SPARK_MASTER"
+_TRACE = bool(__import__("os").environ.get("RAYDP_TRACE_STAGES"))
 
 
 class ExecutorInfo:
@@ -68,23 +69,48 @@ class ExecutorTaskScheduler(P.TaskScheduler):
         indices = list(indices)
         if not indices:
             return []
+        t0 = time.perf_counter()
+        payload, key = self._stage_payload(fn)
+        t1 = time.perf_counter()
+        try:
+            return self._dispatch(lambda ex, i: ex.handle.run_task.remote(key, i), indices)
+        finally:
+            self._free_payload(payload, key)
+            if _TRACE:
+                logger.warning("stage: %d tasks, payload %d B (%d store objs), pickle %.3fs, run %.3fs",
+                               len(indices), len(payload.data), len(payload.oids), t1 - t0,
+                               time.perf_counter() - t1)
+
+    @staticmethod
+    def _stage_payload(fn):
+        """Pickle the stage function once and seal it in the object store: each task call
+        then carries only its id, and an executor maps + unpickles it once per stage."""
+        import uuid
+        from raydp_amd.runtime import core
         from raydp_amd.runtime import serialization as S
         payload = S.dumps_shared(fn)
-        try:
-            return self._dispatch(lambda ex, i: ex.handle.run_task.remote(payload.data, i), indices)
-        finally:
-            payload.free()
+        st = core.current_node_store()
+        oid = uuid.uuid4().hex
+        st.put(oid, payload.data)
+        return payload, (st.node_id, st.path, oid)
+
+    @staticmethod
+    def _free_payload(payload, key):
+        from raydp_amd.runtime import core
+        payload.free()
+        st = core.current_node_store()
+        if st is not None:
+            st.delete(key[2])
 
     def persist(self, fn, rdd_id: str, indices) -> List[tuple]:
-        from raydp_amd.runtime import serialization as S
         indices = list(indices)
-        payload = S.dumps_shared(fn)
+        payload, key = self._stage_payload(fn)
         out = []
         try:
-            res = self._dispatch(lambda ex, i: ex.handle.persist_partitions.remote(payload.data, rdd_id, [i]),
+            res = self._dispatch(lambda ex, i: ex.handle.persist_partitions.remote(key, rdd_id, [i]),
                                  indices, tag=True)
         finally:
-            payload.free()
+            self._free_payload(payload, key)
         for ex_id, lst in res:
             for (i, oid, node_id, path, rows) in lst:
                 out.append((i, oid, node_id, path, rows, ex_id))

@@ -18,7 +18,7 @@ import pyarrow.compute as pc
 
 from raydp_amd.spark import plan as P
 from raydp_amd.spark import wide as W
-from raydp_amd.spark.column import (AggExpr, Alias, ColRef, Column, Func, Lit, SortOrder,
+from raydp_amd.spark.column import (AggExpr, Alias, ColRef, Column, Expr, Func, Lit, SortOrder,
                                     WindowExpr, _to_expr, as_array)
 from raydp_amd.spark.row import Row
 from raydp_amd.spark.types import StructType, from_arrow_schema
@@ -253,12 +253,28 @@ class DataFrame:
         return self._map(lambda t, i: _eval_projection(t, exprs), "project")
 
     def selectExpr(self, *exprs):
-        return self.select(*[e.strip() for e in exprs])
+        from raydp_amd.spark.functions import expr
+        out = []
+        for e in exprs:
+            e = e.strip()
+            out.append(e if e == "*" or e.replace("_", "").isalnum() else expr(e))
+        return self.select(*out)
+
+    def where(self, condition):
+        return self.filter(condition)
 
     def withColumn(self, colName: str, col: Column):
         e = col._expr
         if isinstance(e, WindowExpr):
             return self._with(W.WindowPlan(self._src(), colName, e.fn, e.args, e.window))
+        e, hoisted = _hoist_windows(e)
+        if hoisted:
+            # window functions nested in an expression (e.g. row_number().over(w) - 1): compute
+            # each as a temporary column first, then the outer expression, then drop them
+            df = self
+            for tmp, we in hoisted:
+                df = df._with(W.WindowPlan(df._src(), tmp, we.fn, we.args, we.window))
+            return df.withColumn(colName, Column(e)).drop(*[t for t, _ in hoisted])
         names = self.columns
 
         def fn(t, i):
@@ -292,7 +308,8 @@ class DataFrame:
 
     def filter(self, condition):
         if isinstance(condition, str):
-            raise NotImplementedError("SQL string predicates are not supported; use Columns")
+            from raydp_amd.spark.sqlexpr import parse
+            condition = parse(condition)
         src = self._src()
         preds = [condition._expr]
         # CombineFilters: consecutive filters become one pass with an AND-ed predicate
@@ -685,3 +702,33 @@ def _df_rdd(df: "DataFrame"):
     r = RDD(df._session, plan.num_partitions(), rows, "dataframe")
     r._id_str = df._id
     return r
+
+
+def _hoist_windows(e):
+    """Replace every nested WindowExpr in ``e`` by a temporary column reference."""
+    import copy
+    import uuid
+    found = []
+
+    def walk(x):
+        if isinstance(x, WindowExpr):
+            name = f"__win_{uuid.uuid4().hex[:8]}"
+            found.append((name, x))
+            return ColRef(name)
+        if isinstance(x, Expr):
+            y = copy.copy(x)
+            for k, v in vars(x).items():
+                nv = walk(v) if isinstance(v, (Expr, list, tuple)) else v
+                if nv is not v:
+                    setattr(y, k, nv)
+            return y
+        if isinstance(x, (list, tuple)):
+            out = [walk(v) if isinstance(v, (Expr, list, tuple)) else v for v in x]
+            if any(a is not b for a, b in zip(out, x)):
+                return type(x)(out) if isinstance(x, tuple) else out
+            return x
+        return x
+    if isinstance(e, WindowExpr):
+        return e, []
+    ne = walk(e)
+    return (ne, found) if found else (e, [])

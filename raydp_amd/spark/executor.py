@@ -57,13 +57,25 @@ class RayDPExecutor:
                 "restart_count": int(os.environ.get("RAYDP_ACTOR_RESTART_COUNT", "0"))}
 
     # ------------------------------------------------------------------ tasks -----------
-    def _fn(self, payload: bytes):
-        key = hashlib.blake2b(payload, digest_size=16).hexdigest()
+    def _fn(self, payload):
+        """Stage function from a store key ``(node_id, path, oid)`` (or raw pickled bytes)."""
+        if isinstance(payload, (bytes, bytearray)):
+            key = hashlib.blake2b(payload, digest_size=16).hexdigest()
+        else:
+            key = payload[2]
         with self._lock:
             fn = self._fns.get(key)
         if fn is None:
             from raydp_amd.runtime import serialization as S
-            fn = S.loads(payload)
+            if isinstance(payload, (bytes, bytearray)):
+                fn = S.loads(payload)
+            else:
+                from raydp_amd.runtime import core
+                st = core.store_for(payload[0], payload[1])
+                buf = st.get_buffer(payload[2]) if st is not None else None
+                if buf is None:
+                    raise RuntimeError("stage payload missing from the object store")
+                fn = S.loads(memoryview(buf))
             with self._lock:
                 self._fns[key] = fn
                 self._fn_order.append(key)

@@ -32,10 +32,12 @@ def lit(value) -> Column:
 
 
 def expr(s: str) -> Column:
+    """Parse a Spark SQL expression string (raydp_amd.spark.sqlexpr)."""
     s = s.strip()
     if s.replace("_", "").isalnum():
         return col(s)
-    raise NotImplementedError("SQL expression strings are limited to column names")
+    from raydp_amd.spark.sqlexpr import parse
+    return parse(s)
 
 
 def _fn(name, cols, impl, display=None):

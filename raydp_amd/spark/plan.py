@@ -225,11 +225,27 @@ class WidePlan(Plan):
     def __getstate__(self):
         st = dict(self.__dict__)
         st.pop("_lock", None)
+        if self._out is not None:
+            # a finished stage ships only its outputs: the lineage below it stays on the
+            # driver (otherwise every later stage would re-ship every upstream result)
+            st["_schema"] = self.schema
+            for k, v in list(st.items()):
+                if isinstance(v, Plan) or (isinstance(v, (list, tuple)) and v and isinstance(v[0], Plan)):
+                    st[k] = None
+            st["_cut"] = True
         return st
 
     def __setstate__(self, st):
         self.__dict__.update(st)
         self._lock = threading.Lock()
+
+    def empty(self):
+        if getattr(self, "_cut", False):
+            return self._schema.empty_table()
+        return self._empty()
+
+    def _empty(self):
+        raise NotImplementedError
 
     def materialize(self, scheduler):
         with self._lock:
@@ -296,7 +312,7 @@ class RepartitionPlan(WidePlan):
     def num_partitions(self):
         return self.n
 
-    def empty(self):
+    def _empty(self):
         return self.child.empty()
 
     def execute(self, scheduler):
@@ -360,7 +376,7 @@ class SortPlan(WidePlan):
     def num_partitions(self):
         return max(1, self.n_out)
 
-    def empty(self):
+    def _empty(self):
         return self.child.empty()
 
     def execute(self, scheduler):

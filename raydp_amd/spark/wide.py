@@ -62,7 +62,7 @@ class JoinPlan(WidePlan):
             names.append(c)
         return out
 
-    def empty(self):
+    def _empty(self):
         return self._join(self.left.empty(), self.right.empty())
 
     def execute(self, scheduler):
@@ -152,7 +152,7 @@ class AggregatePlan(WidePlan):
     def num_partitions(self):
         return self.n
 
-    def empty(self):
+    def _empty(self):
         t = aggregate_table(self.child.empty(), self.keys, self.aggs)
         return t.slice(0, 0)
 
@@ -181,7 +181,7 @@ class DistinctPlan(WidePlan):
     def num_partitions(self):
         return self.n
 
-    def empty(self):
+    def _empty(self):
         return self.child.empty()
 
     def _dedup(self, t: pa.Table) -> pa.Table:
@@ -263,7 +263,7 @@ class WindowPlan(WidePlan):
             vals = pa.array(vals.astype(np.int32))
         return st.append_column(self.out_name, vals)
 
-    def empty(self):
+    def _empty(self):
         return self._apply(self.child.empty())
 
     def execute(self, scheduler):
