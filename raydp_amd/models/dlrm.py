@@ -1,0 +1,68 @@
+"""DLRM (Naumov et al.; reference: the ``Dlrm`` model of examples/pytorch_dlrm.ipynb cell 9)
+re-designed for MI355X: the 26 embedding tables are one fused parameter gathered by a HIP
+kernel straight into the interaction input, the dot interaction runs on MFMA
+(``raydp_amd.ops.dlrm_ops``), and the MLP towers are plain Linear+ReLU (hipBLASLt GEMMs).
+
+Same constructor and ``forward(*inputs)`` contract as the reference, so it drops into
+``TorchEstimator`` with ``feature_columns = ['_c1', ..., '_c39']``: the first
+``num_numerical_features`` inputs are float columns, the rest integer category ids.
+"""
+import math
+from typing import Optional, Sequence
+
+import torch
+import torch.nn as nn
+
+from raydp_amd.ops.dlrm_ops import FusedEmbeddings, dot_interaction
+
+
+class TorchMlp(nn.Module):
+    def __init__(self, input_dim: int, sizes: Sequence[int]):
+        super().__init__()
+        layers = []
+        for out_dim in sizes:
+            layers += [nn.Linear(input_dim, out_dim), nn.ReLU(inplace=True)]
+            input_dim = out_dim
+        self.layers = nn.Sequential(*layers)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.normal_(m.weight, 0.0, math.sqrt(2.0 / (m.in_features + m.out_features)))
+                nn.init.normal_(m.bias, 0.0, math.sqrt(1.0 / m.out_features))
+
+    @property
+    def weights(self):
+        return [m.weight for m in self.layers if isinstance(m, nn.Linear)]
+
+    def forward(self, x):
+        return self.layers(x)
+
+
+class Dlrm(nn.Module):
+    def __init__(self, num_numerical_features: int, categorical_feature_sizes: Sequence[int],
+                 bottom_mlp_sizes: Sequence[int], top_mlp_sizes: Sequence[int], embedding_dim: int = 32,
+                 fused_embedding_sgd_lr: Optional[float] = None):
+        super().__init__()
+        if embedding_dim != bottom_mlp_sizes[-1]:
+            raise ValueError("The last bottom MLP layer must have same size as embedding.")
+        self.num_numerical_features = num_numerical_features
+        self.embedding_dim = embedding_dim
+        self.bottom_mlp = TorchMlp(num_numerical_features, bottom_mlp_sizes)
+        self.embeddings = FusedEmbeddings(categorical_feature_sizes, embedding_dim, fused_embedding_sgd_lr)
+        f = len(categorical_feature_sizes) + 1
+        self.num_interactions = embedding_dim + f * (f - 1) // 2 + 1
+        self.top_mlp = TorchMlp(self.num_interactions, top_mlp_sizes[:-1])
+        self.out = nn.Linear(top_mlp_sizes[-2], top_mlp_sizes[-1])
+        with torch.no_grad():   # the zero-pad column of the interaction never contributes
+            self.top_mlp.weights[0][:, -1].zero_()
+
+    def forward(self, *inputs):
+        ntab = len(self.embeddings.table_sizes)
+        if len(inputs) == 2 and inputs[0].dim() == 2 and inputs[0].shape[1] == self.num_numerical_features \
+                and inputs[1].dim() == 2 and inputs[1].shape[1] == ntab and ntab + self.num_numerical_features != 2:
+            dense, cats = inputs      # (dense [B, 13], categorical ids [B, 26])
+        else:
+            dense = torch.cat(inputs[:self.num_numerical_features], dim=1).float()
+            cats = torch.cat(inputs[self.num_numerical_features:], dim=1)
+        mlp_out = self.bottom_mlp(dense.float())
+        X = self.embeddings(mlp_out, cats.long())
+        return self.out(self.top_mlp(dot_interaction(X)))

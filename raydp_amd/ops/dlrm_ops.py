@@ -1,0 +1,143 @@
+"""DLRM operators: fused multi-table embedding lookup and the dot interaction.
+
+On a GPU both run the gfx950 kernels of ``csrc/hip/dlrm.hip`` (``rx_emb_gather`` /
+``rx_emb_sgd`` / ``rx_dot_interaction_fwd|bwd``) and fail loudly if the library is missing; on
+the CPU they use the equivalent PyTorch expressions (for tests and CPU-only hosts).
+"""
+import ctypes
+import math
+from typing import Optional, Sequence
+
+import torch
+import torch.nn as nn
+
+from raydp_amd.ops import _hip
+
+_bound = False
+
+
+def _lib():
+    global _bound
+    L = _hip.lib()
+    if not _bound:
+        vp, i, f, ll = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_longlong
+        L.rx_emb_gather.argtypes = [vp, vp, vp, vp, i, i, i, i, ll, vp]
+        L.rx_emb_sgd.argtypes = [vp, vp, vp, vp, i, i, i, i, f, ll, vp]
+        L.rx_dot_interaction_fwd.argtypes = [vp, vp, i, i, i, vp]
+        L.rx_dot_interaction_bwd.argtypes = [vp, vp, vp, i, i, i, vp]
+        for n in ("rx_emb_gather", "rx_emb_sgd", "rx_dot_interaction_fwd", "rx_dot_interaction_bwd"):
+            getattr(L, n).restype = i
+        _bound = True
+    return L
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def tril_indices(F: int):
+    rows = [i for i in range(F) for _ in range(i)]
+    cols = [j for i in range(F) for j in range(i)]
+    return torch.tensor(rows), torch.tensor(cols)
+
+
+def dot_interaction_reference(X: torch.Tensor) -> torch.Tensor:
+    """[B, F, D] -> [B, D + F(F-1)/2 + 1]: bottom row, strict lower triangle of X X^T, zero pad."""
+    B, F, D = X.shape
+    Z = torch.bmm(X, X.transpose(1, 2))
+    r, c = tril_indices(F)
+    flat = Z[:, r.to(X.device), c.to(X.device)]
+    return torch.cat([X[:, 0], flat, torch.zeros(B, 1, dtype=X.dtype, device=X.device)], dim=1)
+
+
+class _DotInteraction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X):
+        X = X.contiguous().float()
+        B, F, D = X.shape
+        out = torch.empty(B, D + F * (F - 1) // 2 + 1, dtype=torch.float32, device=X.device)
+        _hip.check(_lib().rx_dot_interaction_fwd(_p(X), _p(out), B, F, D, _hip.stream_ptr(X.device)),
+                   "rx_dot_interaction_fwd")
+        ctx.save_for_backward(X)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (X,) = ctx.saved_tensors
+        B, F, D = X.shape
+        g = g.contiguous().float()
+        dX = torch.empty_like(X)
+        _hip.check(_lib().rx_dot_interaction_bwd(_p(X), _p(g), _p(dX), B, F, D, _hip.stream_ptr(X.device)),
+                   "rx_dot_interaction_bwd")
+        return dX
+
+
+def dot_interaction(X: torch.Tensor) -> torch.Tensor:
+    if X.is_cuda:
+        if X.shape[1] > 32 or X.shape[2] not in (32, 64, 128):
+            raise ValueError("HIP dot interaction supports F <= 32 and D in {32, 64, 128}")
+        return _DotInteraction.apply(X)
+    return dot_interaction_reference(X)
+
+
+class _EmbedConcat(torch.autograd.Function):
+    """X = [mlp_out; W[offs + idx]] ([B, 1 + T, D]); weight gradient sparse (or fused SGD)."""
+
+    @staticmethod
+    def forward(ctx, mlp_out, weight, offsets, idx, fused_lr):
+        B, T = idx.shape
+        D = weight.shape[1]
+        X = torch.empty(B, T + 1, D, dtype=torch.float32, device=weight.device)
+        X[:, 0] = mlp_out
+        idx = idx.contiguous().long()
+        _hip.check(_lib().rx_emb_gather(_p(weight), _p(offsets), _p(idx), _p(X), B, T, D, T + 1, weight.shape[0],
+                                        _hip.stream_ptr(weight.device)), "rx_emb_gather")
+        ctx.save_for_backward(weight, offsets, idx)
+        ctx.fused_lr = fused_lr
+        return X
+
+    @staticmethod
+    def backward(ctx, dX):
+        weight, offsets, idx = ctx.saved_tensors
+        B, T = idx.shape
+        D = weight.shape[1]
+        dX = dX.contiguous()
+        d_mlp = dX[:, 0]
+        if ctx.fused_lr is not None:
+            _hip.check(_lib().rx_emb_sgd(_p(weight), _p(offsets), _p(idx), _p(dX), B, T, D, T + 1,
+                                         ctypes.c_float(ctx.fused_lr), weight.shape[0],
+                                         _hip.stream_ptr(weight.device)), "rx_emb_sgd")
+            return d_mlp, None, None, None, None
+        rows = (idx + offsets.view(1, -1)).reshape(-1)
+        grad = torch.sparse_coo_tensor(rows.unsqueeze(0), dX[:, 1:].reshape(-1, D), weight.shape)
+        return d_mlp, grad, None, None, None
+
+
+class FusedEmbeddings(nn.Module):
+    """All categorical tables in one [sum(rows), D] parameter (row offsets per table)."""
+
+    def __init__(self, table_sizes: Sequence[int], dim: int, fused_sgd_lr: Optional[float] = None):
+        super().__init__()
+        self.table_sizes = [int(s) for s in table_sizes]
+        self.dim = dim
+        total = sum(self.table_sizes)
+        self.weight = nn.Parameter(torch.empty(total, dim))
+        offs = [0]
+        for s in self.table_sizes[:-1]:
+            offs.append(offs[-1] + s)
+        self.register_buffer("offsets", torch.tensor(offs, dtype=torch.int64))
+        self.fused_sgd_lr = fused_sgd_lr
+        with torch.no_grad():
+            for o, s in zip(offs, self.table_sizes):   # reference init: U(-sqrt(1/n), sqrt(1/n))
+                self.weight[o:o + s].uniform_(-math.sqrt(1.0 / s), math.sqrt(1.0 / s))
+
+    def table(self, t: int) -> torch.Tensor:
+        o = int(self.offsets[t])
+        return self.weight[o:o + self.table_sizes[t]]
+
+    def forward(self, mlp_out: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+        if self.weight.is_cuda:
+            return _EmbedConcat.apply(mlp_out.float(), self.weight, self.offsets, idx, self.fused_sgd_lr)
+        rows = idx.long() + self.offsets.view(1, -1)
+        emb = nn.functional.embedding(rows, self.weight, sparse=True)
+        return torch.cat([mlp_out.unsqueeze(1).float(), emb], dim=1)
