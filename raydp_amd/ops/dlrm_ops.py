@@ -122,6 +122,7 @@ class FusedEmbeddings(nn.Module):
         self.dim = dim
         total = sum(self.table_sizes)
         self.weight = nn.Parameter(torch.empty(total, dim))
+        self.weight._raydp_sparse_grad = fused_sgd_lr is None   # DDP: reduce as sparse rows
         offs = [0]
         for s in self.table_sizes[:-1]:
             offs.append(offs[-1] + s)

@@ -50,9 +50,22 @@ class DistributedDataParallel(nn.Module):
         self.world = dist.get_world_size(process_group)
         self.broadcast_buffers = broadcast_buffers
         cap = float(os.environ.get("RAYDP_DDP_BUCKET_MB", bucket_cap_mb or 32.0)) * (1 << 20)
-        params = [p for p in module.parameters() if p.requires_grad]
+        sparse_ids = set()
+        for m in module.modules():
+            if isinstance(m, (nn.Embedding, nn.EmbeddingBag)) and m.sparse:
+                sparse_ids.add(id(m.weight))
+        params, self.sparse_params = [], []
+        for p in module.parameters():
+            if not p.requires_grad or getattr(p, "_raydp_model_parallel", False):
+                continue   # sharded tables (raydp_amd.parallel.embedding_mp) are not replicated
+            if id(p) in sparse_ids or getattr(p, "_raydp_sparse_grad", False):
+                self.sparse_params.append(p)
+            else:
+                params.append(p)
         with torch.no_grad():
             for t in list(module.parameters()) + list(module.buffers()):
+                if getattr(t, "_raydp_model_parallel", False):
+                    continue
                 dist.broadcast(t.data, 0, group=process_group)
         # reverse order ~= gradient production order
         self.buckets: List[_Bucket] = []
@@ -71,8 +84,39 @@ class DistributedDataParallel(nn.Module):
             for pi, p in enumerate(b.params):
                 self._where[p] = (bi, pi)
                 p.register_post_accumulate_grad_hook(self._make_hook(p))
+        for p in self.sparse_params:
+            p.register_post_accumulate_grad_hook(self._sparse_hook)
         self._finalize_queued = False
         self.require_backward_grad_sync = True
+
+    def _sparse_hook(self, param):
+        if self.require_backward_grad_sync and not self._finalize_queued:
+            self._finalize_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+
+    def _reduce_sparse(self, p):
+        """Sum a sparse (embedding-row) gradient over ranks without densifying it."""
+        g = p.grad
+        if g is None:
+            g = torch.sparse_coo_tensor(torch.zeros(1, 0, dtype=torch.long, device=p.device),
+                                        torch.zeros(0, *p.shape[1:], dtype=p.dtype, device=p.device), p.shape)
+        g = g.coalesce()
+        idx, val = g.indices(), g.values()
+        n = torch.tensor([idx.shape[1]], device=p.device)
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(ns, n, group=self.pg)
+        m = int(max(int(x) for x in ns))
+        pi = torch.zeros(idx.shape[0], m, dtype=idx.dtype, device=p.device)
+        pv = torch.zeros((m,) + tuple(val.shape[1:]), dtype=val.dtype, device=p.device)
+        pi[:, :idx.shape[1]] = idx
+        pv[:val.shape[0]] = val
+        gi = [torch.empty_like(pi) for _ in range(self.world)]
+        gv = [torch.empty_like(pv) for _ in range(self.world)]
+        dist.all_gather(gi, pi, group=self.pg)
+        dist.all_gather(gv, pv, group=self.pg)
+        ai = torch.cat([x[:, :int(k)] for x, k in zip(gi, ns)], dim=1)
+        av = torch.cat([x[:int(k)] for x, k in zip(gv, ns)], dim=0) / self.world
+        p.grad = torch.sparse_coo_tensor(ai, av, p.shape).coalesce()
 
     def _make_hook(self, p):
         def hook(param):
@@ -92,6 +136,8 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._finalize_queued = False
+        for p in self.sparse_params:
+            self._reduce_sparse(p)
         for b in self.buckets:
             if b.pending != 0:
                 # parameters unused in this forward: reduce the zeros they contributed
