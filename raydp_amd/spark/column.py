@@ -127,9 +127,9 @@ def _spark_type_coerce(a, b):
     tb = b.type if hasattr(b, "type") else None
     if ta is not None and tb is not None:
         if _is_str(ta) and (pa.types.is_integer(tb) or pa.types.is_floating(tb)):
-            a = pc.cast(a, pa.float64(), safe=False)
+            a = pc.cast(_numeric_or_null(a) if not isinstance(a, pa.Scalar) else a, pa.float64(), safe=False)
         elif _is_str(tb) and (pa.types.is_integer(ta) or pa.types.is_floating(ta)):
-            b = pc.cast(b, pa.float64(), safe=False)
+            b = pc.cast(_numeric_or_null(b) if not isinstance(b, pa.Scalar) else b, pa.float64(), safe=False)
         elif pa.types.is_timestamp(ta) and _is_str(tb):
             b = to_timestamp(b if isinstance(b, (pa.Array, pa.ChunkedArray)) else pa.array([b.as_py()]))[0] \
                 if isinstance(b, pa.Scalar) else to_timestamp(b)
@@ -333,6 +333,19 @@ class Alias(Expr):
         return self.alias
 
 
+_NUMERIC_RE = r"^\s*[-+]?((\d+\.?\d*|\.\d+)([eE][-+]?\d+)?|[Nn]a[Nn]|[Ii]nf(inity)?)\s*$"
+
+
+def _numeric_or_null(v):
+    """String array with every non-numeric entry replaced by NULL (trimmed)."""
+    try:
+        pc.cast(v, pa.float64())
+        return v
+    except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+        ok = pc.match_substring_regex(v, _NUMERIC_RE)
+        return pc.utf8_trim_whitespace(pc.if_else(ok, v, pa.scalar(None, v.type)))
+
+
 class Cast(Expr):
     def __init__(self, child: Expr, to: DataType):
         self.child, self.to = child, to
@@ -347,8 +360,13 @@ class Cast(Expr):
             return to_timestamp(v if not isinstance(v, pa.Scalar) else pa.array([v.as_py()]))
         if pa.types.is_integer(t) and hasattr(v, "type") and pa.types.is_floating(v.type):
             return pc.cast(pc.trunc(v), t, safe=False)
-        if pa.types.is_integer(t) and hasattr(v, "type") and _is_str(v.type):
-            return pc.cast(pc.trunc(pc.cast(v, pa.float64(), safe=False)), t, safe=False)
+        if hasattr(v, "type") and _is_str(v.type) and (pa.types.is_integer(t) or pa.types.is_floating(t)
+                                                        or pa.types.is_decimal(t)):
+            # Spark (non-ANSI) casts unparsable strings to NULL instead of failing
+            v = _numeric_or_null(v)
+            if pa.types.is_integer(t):
+                return pc.cast(pc.trunc(pc.cast(v, pa.float64(), safe=False)), t, safe=False)
+            return pc.cast(v, t, safe=False)
         if _is_str(t) and hasattr(v, "type") and pa.types.is_boolean(v.type):
             return pc.if_else(v, "true", "false")
         return pc.cast(v, t, safe=False)

@@ -144,8 +144,10 @@ class CsvSource(Source):
             head = head[:cut + 1]
         first_nl = head.find(b"\n")
         self._header_line = head[:first_nl + 1] if self.header else b""
-        conv = pacsv.ConvertOptions(strings_can_be_null=True) if infer else pacsv.ConvertOptions(
-            column_types=None)
+        # Spark's CSV null token is the empty string only ("N/A", "NULL", ... stay values)
+        nulls = [self.null_value] if self.null_value else [""]
+        conv = pacsv.ConvertOptions(strings_can_be_null=True, null_values=nulls) if infer else \
+            pacsv.ConvertOptions(column_types=None, null_values=nulls)
         t = pacsv.read_csv(io.BytesIO(head), read_options=self._read_opts(),
                            parse_options=pacsv.ParseOptions(delimiter=self.sep),
                            convert_options=conv)
@@ -187,7 +189,7 @@ class CsvSource(Source):
         names = self._schema.names
         conv = pacsv.ConvertOptions(column_types={f.name: f.type for f in self._schema},
                                     strings_can_be_null=True,
-                                    null_values=[self.null_value] if self.null_value else None)
+                                    null_values=[self.null_value] if self.null_value else [""])
         if not data.strip():
             return self._schema.empty_table()
         t = pacsv.read_csv(io.BytesIO(data),
