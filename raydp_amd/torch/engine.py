@@ -8,7 +8,9 @@
   loss is MSE/SmoothL1/L1, the optimizer Adam/AdamW/SGD and the metrics are MAE/MSE.
 * ``TorchLoopEngine`` — any other model. Still device-resident (data ingested once, batches are
   device slices of a permuted index), loss and metrics accumulated on the device and read once
-  per epoch; DDP via ``raydp_amd.parallel.ddp`` when ``world_size > 1``.
+  per epoch; DDP via ``raydp_amd.parallel.ddp`` when ``world_size > 1``. On one GPU the whole
+  step (gather, fwd, loss, metrics, bwd, optimizer) is replayed from a captured HIP graph
+  (``raydp_amd/torch/graphs.py``).
 
 Both report the reference's per-epoch dicts ``{epoch, train_res, train_loss}`` and
 ``{epoch, eval_res, test_loss}`` (``python/raydp/torch/estimator.py:245-253``).
@@ -176,6 +178,17 @@ class TorchLoopEngine:
         self.shuffle = bool(config.get("shuffle", True))
         self.gen = torch.Generator(device=device)
         self.gen.manual_seed(1234 + session.get_world_rank())
+        self.graphed = None
+        from raydp_amd.torch import graphs
+        if graphs.graphs_requested():
+            why = graphs.supported(self)
+            if why is None:
+                self.metrics.to(device)
+                self.graphed = graphs.GraphedTrainLoop(self)
+                self.name = "torch_loop_hipgraph"
+            self.graph_status = why or "enabled"
+        else:
+            self.graph_status = "disabled (RAYDP_TORCH_GRAPHS=0)"
 
     def load(self, train_ds, eval_ds, config):
         fc, ft = config["feature_columns"], config["feature_types"]
@@ -198,7 +211,15 @@ class TorchLoopEngine:
                 lab = data.labels[s:s + self.batch]
             yield (feats if data.multi else feats[0]), lab
 
+    def _reset_metrics(self):
+        if self.graphed is not None:
+            self.metrics.zero_()   # captured updates keep pointing at this storage
+        else:
+            self.metrics.reset()
+
     def train_epoch(self):
+        if self.graphed is not None:
+            return self.graphed.train_epoch()
         self.model.train()
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         nb = 0
@@ -214,7 +235,7 @@ class TorchLoopEngine:
                 self.scheduler.step()
             nb += 1
         res = self.metrics.compute()
-        self.metrics.reset()
+        self._reset_metrics()
         return res, (total / max(nb, 1)).item()
 
     @torch.no_grad()
@@ -228,7 +249,7 @@ class TorchLoopEngine:
             self.metrics.update(outputs, targets)
             nb += 1
         res = self.metrics.compute()
-        self.metrics.reset()
+        self._reset_metrics()
         return res, (total / max(nb, 1)).item()
 
     def state_dict(self):

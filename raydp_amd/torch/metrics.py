@@ -31,6 +31,12 @@ class Metric:
     def compute(self):
         raise NotImplementedError
 
+    def zero_(self):
+        """Reset in place (keeps tensor storage: required when ``update`` is graph-captured)."""
+        for v in vars(self).values():
+            if isinstance(v, torch.Tensor):
+                v.zero_()
+
 
 class _SumCount(Metric):
     def reset(self):
@@ -133,3 +139,17 @@ class TorchMetric:
     def reset(self):
         for m in self._metrics.values():
             m.reset()
+
+    def graph_safe(self) -> bool:
+        """True if every metric is a built-in device-state metric (updates can be captured)."""
+        return all(isinstance(m, Metric) and type(m).__name__ in _BUILTIN for m in self._metrics.values())
+
+    def to(self, device):
+        for m in self._metrics.values():
+            if isinstance(m, Metric):
+                m.to(device)
+        return self
+
+    def zero_(self):
+        for m in self._metrics.values():
+            m.zero_()
