@@ -122,9 +122,15 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local)
+    # modulo: lets a rehearsal put several ranks on a 1-GPU box (RAYDP_BENCH_BACKEND=gloo)
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("RAYDP_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     import raydp  # noqa: F401 - API facade
     from raydp_amd import context, runtime
@@ -180,6 +186,7 @@ def main():
                        "global_batch": BATCH * world, "seq_len": None,
                        "parallelism": f"dp{world}", "per_gpu_batch": BATCH, "epochs": 1,
                        "engine": engine,
+                       "allreduce": res.metrics_history[0].get("allreduce") if res.metrics_history else None,
                        "timed_region": "csv read+ETL+from_spark+shuffle+HBM ingest+train+checkpoint",
                        "final_train_loss": res.metrics_history[0].get("train_loss")
                        if res.metrics_history else None,

@@ -1,0 +1,49 @@
+// MI355X configuration keys seen by native code: the C++ mirror of the spark.ray.mi355x.*
+// entries of raydp_amd/utils/config.py (tests/test_config.py checks the two agree).
+//
+// Native code runs in processes without a Spark session (actor workers, trainer ranks), so
+// it reads the environment variable each key maps to; the Python side exports those
+// variables for workers (config.env_for_workers).
+#pragma once
+#include <stdlib.h>
+#include <string.h>
+
+namespace rx_config {
+
+struct Key {
+  const char* key;
+  const char* env;
+  const char* default_value;
+};
+
+constexpr Key kKeys[] = {
+    {"spark.ray.mi355x.allreduce", "RAYDP_ALLREDUCE", "auto"},
+    {"spark.ray.mi355x.allreduce.timeout_s", "RAYDP_ALLREDUCE_TIMEOUT_S", "30"},
+    {"spark.ray.mi355x.fused", "RAYDP_FUSED", "auto"},
+    {"spark.ray.mi355x.hip_graphs", "RAYDP_TORCH_GRAPHS", "1"},
+    {"spark.ray.mi355x.mlp_jit", "RAYDP_MLP_JIT", "1"},
+    {"spark.ray.mi355x.ddp.bucket_mb", "RAYDP_DDP_BUCKET_MB", "32"},
+    {"spark.ray.mi355x.object_store_bytes", "RAYDP_OBJECT_STORE_BYTES", "0"},
+    {"spark.ray.mi355x.trace", "RAYDP_TRACE", ""},
+    {"spark.ray.mi355x.roctx", "RAYDP_ROCTX", "0"},
+    {"spark.ray.mi355x.log_dir", "RAYDP_LOG_DIR", ""},
+    {"spark.ray.mi355x.opt_xcd_affine", "RAYDP_OPT_XCD_AFFINE", "1"},
+    {"spark.ray.mi355x.xg_opt_stride", "RAYDP_XG_OPT_STRIDE", "1"},
+};
+
+// Value of a key: its environment variable when set and non-empty, else the default.
+inline const char* get(const char* key) {
+  for (const Key& k : kKeys)
+    if (strcmp(k.key, key) == 0) {
+      const char* v = getenv(k.env);
+      return (v && v[0]) ? v : k.default_value;
+    }
+  return nullptr;
+}
+
+inline long get_int(const char* key, long fallback) {
+  const char* v = get(key);
+  return (v && v[0]) ? strtol(v, nullptr, 10) : fallback;
+}
+
+}  // namespace rx_config

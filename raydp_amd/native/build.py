@@ -24,7 +24,7 @@ def _hip_sources():
     c = os.path.join(CSRC, "comm")
     srcs = sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".hip"))
     if os.path.isdir(c):
-        srcs += sorted(os.path.join(c, f) for f in os.listdir(c) if f.endswith(".cc"))
+        srcs += sorted(os.path.join(c, f) for f in os.listdir(c) if f.endswith((".cc", ".hip")))
     return srcs
 
 

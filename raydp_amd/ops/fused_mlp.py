@@ -277,11 +277,13 @@ class FusedMLPTrainer:
     def train_epoch(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int,
                     perm: Optional[torch.Tensor], allreduce: Optional[Callable] = None,
                     world_size: int = 1, drop_last: bool = False, comm=None,
-                    max_steps: Optional[int] = None) -> Dict[str, float]:
+                    max_steps: Optional[int] = None, xg=None) -> Dict[str, float]:
         """Run one epoch. Multi-GPU: ``comm`` (a :class:`raydp_amd.ops.comm.NativeComm`) puts
         the gradient all-reduce inside the native step loop; otherwise ``allreduce(grads)``
-        (sum) is called from Python between backward and step. ``max_steps`` caps the step
-        count (ranks agree on it so every collective is matched)."""
+        (sum) is called from Python between backward and step. ``xg`` (a
+        :class:`raydp_amd.ops.comm.XgmiComm`) instead fuses a one-shot xGMI all-reduce into the
+        optimizer kernel. ``max_steps`` caps the step count (ranks agree on it so every
+        collective is matched)."""
         nsteps = n_rows // self.batch if drop_last else -(-n_rows // self.batch)
         if max_steps is not None:
             nsteps = min(nsteps, int(max_steps))
@@ -301,7 +303,14 @@ class FusedMLPTrainer:
         pp = ctypes.c_void_p
         perm_p = pp(perm.data_ptr()) if perm is not None else pp(0)
         gscale = 1.0 / world_size
-        if comm is not None or allreduce is None:
+        if xg is not None:
+            rc = self.lib.rx_mlp_train_steps_xg(
+                ctypes.byref(self.desc), ctypes.byref(self.bufs), ctypes.byref(self.opt), self._od, self.mt,
+                pp(self.m.data_ptr()), pp(self.v.data_ptr()),
+                pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, 0, nsteps,
+                lrs, bc1, bc2, ctypes.c_float(gscale), int(self.step_count == 0), stream, pp(xg.ctx))
+            _hip.check(rc, "rx_mlp_train_steps_xg")
+        elif comm is not None or allreduce is None:
             ar_fn = comm.fn_ptr if comm is not None else pp(0)
             ar_ctx = pp(comm.ctx) if comm is not None else pp(0)
             rc = self.lib.rx_mlp_train_steps(
@@ -325,7 +334,10 @@ class FusedMLPTrainer:
                 _hip.check(rc, "rx_opt_step")
         self.step_count += nsteps
         self.steps_in_epoch = nsteps
-        return self._read_metrics()
+        out = self._read_metrics()
+        if xg is not None:
+            xg.check()
+        return out
 
     def forward_backward(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int,
                          perm: Optional[torch.Tensor] = None, step: int = 0) -> torch.Tensor:

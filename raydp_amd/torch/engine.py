@@ -124,7 +124,7 @@ class FusedMLPEngine:
         perm = None
         if self.shuffle:
             perm = torch.randperm(t.n, device=self.device, generator=self.gen).to(torch.int32)
-        ar, comm, max_steps = None, None, None
+        ar, comm, max_steps, xg = None, None, None, None
         if self.world > 1:
             import torch.distributed as dist
             from raydp_amd.ops.comm import NativeComm
@@ -134,13 +134,18 @@ class FusedMLPEngine:
             s = torch.tensor([mine], device=self.device, dtype=torch.int64)
             dist.all_reduce(s, op=dist.ReduceOp.MIN)
             max_steps = int(s.item())
-            comm = NativeComm.from_process_group() if dist.get_backend() == "nccl" else None
-            if comm is None:
+            xg = _xgmi_for(self.trainer)
+            comm = None
+            if xg is None:
+                comm = NativeComm.from_process_group() if dist.get_backend() == "nccl" else None
+            self.allreduce_kind = "xgmi_oneshot" if xg is not None else (
+                "rccl_native" if comm is not None else f"torch.distributed:{dist.get_backend()}")
+            if comm is None and xg is None:
                 def ar(g):
                     dist.all_reduce(g)
         m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, allreduce=ar,
                                      world_size=self.world, drop_last=self.drop_last, comm=comm,
-                                     max_steps=max_steps)
+                                     max_steps=max_steps, xg=xg if self.world > 1 else None)
         self.trainer.note_steps(self.trainer.steps_in_epoch)
         return self._res(m), m["loss"]
 
@@ -152,6 +157,24 @@ class FusedMLPEngine:
     def state_dict(self):
         self.trainer.write_back()
         return self.model.state_dict()
+
+
+def _xgmi_for(trainer):
+    """The one-shot xGMI communicator for this trainer's gradient, or None (RCCL instead).
+
+    ``RAYDP_ALLREDUCE`` / ``spark.ray.mi355x.allreduce``: ``auto`` (default: xGMI when every
+    rank of the group maps its peers and passes the self-test), ``xgmi`` (same, but failing
+    the setup is an error), ``rccl`` (never)."""
+    import torch.distributed as dist
+    from raydp_amd.ops.comm import XgmiComm
+    from raydp_amd.utils.config import get as conf_get
+    mode = conf_get("spark.ray.mi355x.allreduce")
+    if mode == "rccl" or not torch.cuda.is_available():
+        return None
+    xg = XgmiComm.create(trainer.opt.total, timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
+    if xg is None and mode == "xgmi":
+        raise RuntimeError("spark.ray.mi355x.allreduce=xgmi but the xGMI peer mapping is unavailable")
+    return xg
 
 
 class TorchLoopEngine:

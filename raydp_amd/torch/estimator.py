@@ -169,7 +169,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         for epoch in range(config["num_epochs"]):
             train_res, train_loss = engine.train_epoch()
             session.report(dict(epoch=epoch, train_res=train_res, train_loss=train_loss,
-                                engine=engine.name))
+                                engine=engine.name, allreduce=getattr(engine, "allreduce_kind", None)))
             if eval_ds is not None:
                 eval_res, test_loss = engine.evaluate_epoch()
                 session.report(dict(epoch=epoch, eval_res=eval_res, test_loss=test_loss))
