@@ -3,6 +3,10 @@
 * ``libexec_kernels.so``  — CPU shuffle/hash kernels (g++).
 * ``libraydp_runtime.so`` — shared-memory object store + actor supervisor + framed IPC (g++).
 * ``libhipkernels.so``    — CDNA4 HIP kernels for gfx950 (hipcc ``--offload-arch=gfx950``).
+* ``raydp_supervisor`` / ``raydp_appmaster`` / ``raydp_shuffle_service`` — native services (g++).
+
+``RAYDP_SANITIZE=address,undefined`` (or ``thread``) builds the host-side C++ with that
+sanitizer into a separate ``sanitize/`` directory (``scripts/sanitize_runtime.sh``).
 
 Usage: ``python -m raydp_amd.native.build [name ...]``.
 """
@@ -40,8 +44,11 @@ LIBS = {
     "exec_kernels": dict(kind="cpu", sources=lambda: [os.path.join(CSRC, "exec", "exec_kernels.cc")]),
     "raydp_runtime": dict(kind="cpu", sources=_runtime_sources, libs=["-lpthread", "-lrt", "-ldl"]),
     "hipkernels": dict(kind="hip", sources=_hip_sources),
-    # executable: the per-node actor supervisor (csrc/runtime/supervisor.cc)
+    # executables: the per-node actor supervisor, the application master (native control
+    # plane) and the per-node external shuffle-block service
     "raydp_supervisor": dict(kind="exe", sources=lambda: [os.path.join(CSRC, "runtime", "supervisor.cc")]),
+    "raydp_appmaster": dict(kind="exe", sources=lambda: [os.path.join(CSRC, "control", "app_master.cc")]),
+    "raydp_shuffle_service": dict(kind="exe", sources=lambda: [os.path.join(CSRC, "exec", "shuffle_service.cc")]),
 }
 
 
@@ -61,7 +68,7 @@ def _newer(out, srcs):
         return False
     t = os.path.getmtime(out)
     deps = list(srcs)
-    for d in ("common", "hip", "runtime", "exec", "comm"):
+    for d in ("common", "hip", "runtime", "exec", "comm", "control"):
         p = os.path.join(CSRC, d)
         if os.path.isdir(p):
             deps += [os.path.join(p, f) for f in os.listdir(p) if f.endswith((".h", ".hpp", ".cuh"))]

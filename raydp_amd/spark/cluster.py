@@ -1,8 +1,12 @@
 """Cluster backend of a Spark-on-runtime application (driver side).
 
-Roles of the reference's JVM control plane, collapsed into one driver-side object:
+The application's control state lives in the native app master (``csrc/control/app_master.cc``,
+client ``raydp_amd.spark.appmaster``): application registration, executor ids, the
+registration / restart-remap protocol, the executor caps, dynamic-allocation targets, the
+per-node shuffle services and the RecacheRDD relay. This object is the driver half around it:
 
-* **app master** (``RayAppMaster.scala``): launches executor actors with their resources
+* **executor launcher** (``RayExecutorUtils.createExecutorActor``): carries out the master's
+  launch orders — executor actors with their resources
   (``spark.ray.raydp_spark_executor.actor.resource.*``, the legacy
   ``spark.ray.actor.resource.cpu``, ``spark.executor.memory``), spreads them round-robin over
   the placement-group bundles named by ``spark.ray.placement_group`` /
@@ -10,7 +14,7 @@ Roles of the reference's JVM control plane, collapsed into one driver-side objec
   limit (``RayExecutorUtils.java:58``) and answers dynamic-allocation requests
   (``requestTotalExecutors`` / ``killExecutors``: ``RayCoarseGrainedSchedulerBackend.scala:
   278-301``);
-* **scheduler backend**: ``ExecutorTaskScheduler`` ships stage tasks to the executor
+* **scheduler backend** (``RayCoarseGrainedSchedulerBackend``): ``ExecutorTaskScheduler`` ships stage tasks to the executor
   processes with at most ``cores`` tasks in flight per executor, and resubmits the tasks of a
   lost executor (``spark.task.maxFailures``);
 * **object-store writer** (``ObjectStoreWriter.scala:164-216``): ``prepare_recoverable``
@@ -178,11 +182,11 @@ class ClusterBackend:
         self._recoverable: Dict[str, dict] = {}
         self._lock = threading.RLock()
         self._executors: Dict[str, ExecutorInfo] = {}
-        self._next_id = 0
-        self._bundle_rr = 0
         self.master = None
+        self.appmaster = None
         self._master_url = None
         self._started = False
+        self.shuffle_service_enabled = str(conf.get("spark.shuffle.service.enabled", "false")).lower() == "true"
 
     # ---------------------------------------------------------------- lifecycle ----------
     def start(self):
@@ -200,12 +204,76 @@ class ClusterBackend:
             opts["resources"] = res
         self.master = runtime.remote(RayDPSparkMaster).options(**opts).remote(self.app_name, self.conf)
         master_url = self.master.start_up.remote(self.master_resources)
-        self.request_total_executors(self._initial_executors())
+        self._start_appmaster()
         self._master_url = runtime.get(master_url)
         # executors come up in parallel; wait until each answers
         runtime.get([e.handle.ping.remote() for e in self.alive_executors()])
         self._sched = ExecutorTaskScheduler(self)
         self._started = True
+
+    def _start_appmaster(self):
+        """Launch the native app master, register the application and carry out the launch
+        orders of its initial ``schedule()``."""
+        from raydp_amd.runtime import core
+        from raydp_amd.spark.appmaster import AppMasterClient
+        from raydp_amd.utils import get_node_ip_address
+        node = core.current_node()
+        workdir = node.session_dir if node is not None and node.session_dir else __import__("tempfile").mkdtemp()
+        self.appmaster = AppMasterClient.launch(workdir)
+        self.conf["spark.ray.appmaster.socket"] = self.appmaster.sock_path
+        cpu = self.conf.get(EXECUTOR_RESOURCE_PREFIX + "cpu") or self.conf.get(LEGACY_ACTOR_CPU)
+        custom = {k[len(EXECUTOR_RESOURCE_PREFIX):]: float(v) for k, v in self.conf.items()
+                  if k.startswith(EXECUTOR_RESOURCE_PREFIX) and k[len(EXECUTOR_RESOURCE_PREFIX):].lower() != "cpu"}
+        mem = self.conf.get("spark.executor.memory")
+        bundles = []
+        if self.conf.get("spark.ray.placement_group"):
+            from raydp_amd.runtime import pgroup
+            pg = pgroup.get_placement_group_by_id(self.conf["spark.ray.placement_group"])
+            bundles = [int(x) for x in self.conf.get("spark.ray.bundle_indexes", "").split(",") if x != ""] \
+                or list(range(pg.bundle_count))
+        dyn = self.conf.get("spark.dynamicAllocation.enabled", "false").lower() == "true"
+        max_n = self.conf.get("spark.dynamicAllocation.maxExecutors")
+        orders = self.appmaster.register_app(
+            self.app_name, self._initial_executors(), self.cores,
+            int(parse_memory_size(mem) // (1 << 20)) if mem else 1024,
+            float(cpu) if cpu else float(self.cores), custom, bundles, dyn,
+            int(max_n) if max_n is not None else (1 << 30), self.shuffle_service_enabled,
+            self.conf.get("spark.local.dir", ""), get_node_ip_address())
+        self.app_id = self.appmaster.app_id
+        for o in orders:
+            self._launch_executor(o)
+        self.appmaster.subscribe(self._on_master_event)
+
+    def _on_master_event(self, ev):
+        """Driver agent (``RayDPDriverAgent.receive RecacheRDD``): re-materialise a persisted
+        dataset whose blocks an executor lost."""
+        if ev and ev[0] == "recache":
+            try:
+                self.recache(ev[1])
+            except Exception as e:  # noqa: BLE001
+                logger.warning("recache of %s failed: %s", ev[1], e)
+
+    def recache(self, rdd_id: str) -> int:
+        """Recompute the partitions of a recoverable dataset that no live executor holds."""
+        with self._lock:
+            rec = self._recoverable.get(rdd_id)
+        if rec is None or "plan" not in rec:
+            return 0
+        held = {}
+        for e in self.alive_executors():
+            try:
+                from raydp_amd import runtime
+                held.update(runtime.get(e.handle.block_locations.remote(rdd_id)))
+            except Exception:  # noqa: BLE001
+                pass
+        n = rec["plan"].num_partitions()
+        missing = [i for i in range(n) if i not in held]
+        if missing:
+            placed = self._sched.persist(rec["plan"].compute, rdd_id, missing)
+            with self._lock:
+                for (i, _oid, _node, _path, _rows, ex_id) in placed:
+                    rec["locations"][i] = ex_id
+        return len(missing)
 
     def _initial_executors(self) -> int:
         if self.conf.get("spark.dynamicAllocation.enabled", "false").lower() == "true":
@@ -214,40 +282,28 @@ class ClusterBackend:
             return max(int(n), 1)
         return self.num_executors
 
-    def _executor_options(self, executor_id: str) -> dict:
-        cpu = self.conf.get(EXECUTOR_RESOURCE_PREFIX + "cpu") or self.conf.get(LEGACY_ACTOR_CPU)
-        opts = {"name": f"raydp-executor-{executor_id}", "num_cpus": float(cpu) if cpu else float(self.cores),
-                "max_restarts": -1, "max_concurrency": max(2, self.cores)}
-        mem = self.conf.get("spark.executor.memory")
-        if mem:
-            opts["memory"] = float(parse_memory_size(mem))
-        custom = {}
-        for k, v in self.conf.items():
-            if k.startswith(EXECUTOR_RESOURCE_PREFIX):
-                name = k[len(EXECUTOR_RESOURCE_PREFIX):]
-                if name.lower() != "cpu":
-                    custom[name] = float(v)
-        if custom:
-            opts["resources"] = custom
+    def _executor_options(self, order) -> dict:
+        """Actor options of one launch order (``RayExecutorUtils.createExecutorActor``:
+        name, CPU, memory, custom resources, bundle, ``maxRestarts=-1``)."""
+        opts = {"name": f"raydp-executor-{order.executor_id}", "num_cpus": order.cpu,
+                "max_restarts": -1, "max_concurrency": max(2, order.cores)}
+        if self.conf.get("spark.executor.memory"):
+            opts["memory"] = float(order.memory_mb) * (1 << 20)
+        if order.resources:
+            opts["resources"] = dict(order.resources)
         pg_id = self.conf.get("spark.ray.placement_group")
-        if pg_id:
+        if pg_id and order.bundle >= 0:
             from raydp_amd.runtime import pgroup
-            pg = pgroup.get_placement_group_by_id(pg_id)
-            idx = [int(x) for x in self.conf.get("spark.ray.bundle_indexes", "").split(",") if x != ""] \
-                or list(range(pg.bundle_count))
-            opts["placement_group"] = pg
-            opts["placement_group_bundle_index"] = idx[self._bundle_rr % len(idx)]
-            self._bundle_rr += 1
+            opts["placement_group"] = pgroup.get_placement_group_by_id(pg_id)
+            opts["placement_group_bundle_index"] = order.bundle
         return opts
 
-    def _launch_executor(self) -> ExecutorInfo:
+    def _launch_executor(self, order) -> ExecutorInfo:
         from raydp_amd import runtime
         from raydp_amd.spark.executor import RayDPExecutor
         from raydp_amd.spark.executor_registry import register_executor
-        with self._lock:
-            eid = str(self._next_id)
-            self._next_id += 1
-        opts = self._executor_options(eid)
+        eid = order.executor_id
+        opts = self._executor_options(order)
         h = runtime.remote(RayDPExecutor).options(**opts).remote(eid, self.app_id, self.cores, self.conf)
         info = ExecutorInfo(eid, h, self.cores)
         with self._lock:
@@ -257,20 +313,31 @@ class ClusterBackend:
 
     # ------------------------------------------------------------ dynamic allocation ----
     def request_total_executors(self, n: int) -> bool:
-        """``doRequestTotalExecutors``: grow (or shrink) the executor set to ``n``."""
-        max_n = self.conf.get("spark.dynamicAllocation.maxExecutors")
-        if max_n is not None:
-            n = min(n, int(max_n))
+        """``doRequestTotalExecutors``: the master decides how many to add (its caps count
+        restarted executors, ``RayAppMaster.scala:258-303``); surplus executors are killed."""
         alive = self.alive_executors()
-        for _ in range(n - len(alive)):
-            self._launch_executor()
         if n < len(alive):
-            self.kill_executors([e.executor_id for e in alive[n:]])
+            return self.kill_executors([e.executor_id for e in alive[n:]])
+        for o in self.appmaster.request_executors(n):
+            self._launch_executor(o)
         return True
+
+    def _master_ids(self) -> Dict[str, str]:
+        """original (actor-name) executor id -> the id the master currently knows it by."""
+        cur = {}
+        for new, old in sorted(self.appmaster.get_restarted().items(), key=lambda kv: int(kv[0])):
+            cur[old] = new
+            for k, v in list(cur.items()):  # chains of restarts
+                if v == old:
+                    cur[k] = new
+        return cur
 
     def kill_executors(self, ids: List[str]) -> bool:
         from raydp_amd import runtime
         from raydp_amd.spark.executor_registry import unregister_executor
+        if self.appmaster is not None:
+            remap = self._master_ids()
+            self.appmaster.kill_executors([remap.get(i, i) for i in ids])
         for eid in ids:
             with self._lock:
                 info = self._executors.get(eid)
@@ -297,8 +364,11 @@ class ClusterBackend:
         only replace it when the runtime gave up on the actor."""
         if info.handle._impl.dead and info.state == "RUNNING":
             info.state = "LOST"
-            logger.warning("executor %s lost; launching a replacement", info.executor_id)
-            self._launch_executor()
+            logger.warning("executor %s lost; asking the master for a replacement", info.executor_id)
+            if self.appmaster is not None:
+                self.appmaster.executor_lost(self._master_ids().get(info.executor_id, info.executor_id))
+                for o in self.appmaster.request_executors(len(self.alive_executors()) + 1):
+                    self._launch_executor(o)
 
     def master_url(self) -> str:
         if self._master_url:
@@ -320,6 +390,13 @@ class ClusterBackend:
             for rdd in recs:
                 self.release_recoverable(rdd)
         self.kill_executors([e.executor_id for e in self.executors()])
+        if self.appmaster is not None:
+            try:
+                self.appmaster.unregister_app()
+            except OSError:
+                pass
+            self.appmaster.shutdown()
+            self.appmaster = None
         if self.master is not None and cleanup_data:
             try:
                 runtime.kill(self.master, no_restart=True)
@@ -362,9 +439,15 @@ class ClusterBackend:
         return self._sched.map(plan.compute, [i])[0].replace_schema_metadata()
 
     def block_locations(self, rdd_id) -> Dict[int, str]:
+        """partition -> executor (actor-name id), like ``getBlockLocations`` followed by the
+        restarted-executor remap of ``ObjectStoreWriter.scala:179-191``."""
         with self._lock:
             rec = self._recoverable.get(rdd_id)
         return dict(rec.get("locations", {})) if rec else {}
+
+    def restarted_executors(self) -> Dict[str, str]:
+        """new executor id -> original id (``RayAppMaster.getRestartedExecutors``)."""
+        return self.appmaster.get_restarted() if self.appmaster is not None else {}
 
     def release_recoverable(self, rdd_id):
         from raydp_amd import runtime

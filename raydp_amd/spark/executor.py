@@ -33,6 +33,19 @@ class RayDPExecutor:
         from raydp_amd.runtime import core
         self._node = core.current_node()
         self._warm_up()
+        self.registration = None
+        sock = self.conf.get("spark.ray.appmaster.socket")
+        if sock:
+            # registerToAppMaster (+ RequestAddPendingRestartedExecutor after a restart):
+            # the master answers with the id this process now runs as
+            from raydp_amd.spark import shuffle
+            from raydp_amd.spark.appmaster import ExecutorRegistration
+            restarted = int(os.environ.get("RAYDP_ACTOR_RESTART_COUNT", "0")) > 0
+            self.registration = ExecutorRegistration(sock, executor_id, self._node.store.node_id, restarted)
+            self.spark_executor_id = self.registration.executor_id
+            shuffle.set_local_service(self.registration.shuffle_socket)
+        else:
+            self.spark_executor_id = executor_id
 
     @staticmethod
     def _warm_up():
@@ -54,7 +67,9 @@ class RayDPExecutor:
         from raydp_amd.utils import get_node_ip_address
         return {"executor_id": self.executor_id, "pid": os.getpid(), "node_id": self._node.store.node_id,
                 "ip": get_node_ip_address(), "cores": self.cores, "tasks_run": self.tasks_run,
-                "restart_count": int(os.environ.get("RAYDP_ACTOR_RESTART_COUNT", "0"))}
+                "restart_count": int(os.environ.get("RAYDP_ACTOR_RESTART_COUNT", "0")),
+                "spark_executor_id": self.spark_executor_id,
+                "shuffle_service": self.registration.shuffle_socket if self.registration else None}
 
     # ------------------------------------------------------------------ tasks -----------
     def _fn(self, payload):
@@ -119,6 +134,9 @@ class RayDPExecutor:
         with self._lock:
             oid = self._cache.get((rdd_id, index))
         if oid is None:
+            # requestRecacheRDD (RayDPExecutor.scala:289-310): the driver agent re-materialises
+            if self.registration is not None:
+                self.registration.recache(rdd_id)
             return None
         found, t = self._node.store.get(oid)
         return t if found else None

@@ -13,6 +13,7 @@ import pyarrow.compute as pc
 
 from raydp_amd.spark.column import AggExpr, Expr, as_array
 from raydp_amd.spark.plan import Plan, WidePlan, concat, hash_partition, sort_table
+from raydp_amd.spark.shuffle import exchange
 
 _BROADCAST_BYTES = 10 * 1024 * 1024
 
@@ -74,14 +75,13 @@ class JoinPlan(WidePlan):
             self.n = n_left
             return scheduler.map(lambda i: self._join(self.left.compute(i), rt), range(n_left))
         n = self.n
-        lparts = scheduler.map(lambda i: hash_partition(self.left.compute(i), self.lk, n),
-                               range(self.left.num_partitions()))
-        rbuck = [hash_partition(t, self.rk, n) for t in rparts]
         ls, rs = self.left.schema, self.right.schema
+        lsh = exchange(scheduler, self.left.compute, self.left.num_partitions(), self.lk, n, ls)
+        rbuck = [hash_partition(t, self.rk, n) for t in rparts]
 
         def one(j):
-            return self._join(concat([p[j] for p in lparts], ls), concat([p[j] for p in rbuck], rs))
-        return scheduler.map(one, range(n))
+            return self._join(lsh.bucket(j), concat([p[j] for p in rbuck], rs))
+        return _reduce(scheduler, one, n, lsh)
 
 
 _AGG_MAP = {"sum": "sum", "avg": "mean", "min": "min", "max": "max", "count": "count",
@@ -162,11 +162,8 @@ class AggregatePlan(WidePlan):
         if not keys:
             parts = scheduler.map(self.child.compute, range(self.child.num_partitions()))
             return [aggregate_table(concat(parts, schema), [], self.aggs)]
-        pieces = scheduler.map(lambda i: hash_partition(self.child.compute(i), keys, n),
-                               range(self.child.num_partitions()))
-        return scheduler.map(
-            lambda j: aggregate_table(concat([p[j] for p in pieces], schema), keys, self.aggs),
-            range(n))
+        sh = exchange(scheduler, self.child.compute, self.child.num_partitions(), keys, n, schema)
+        return _reduce(scheduler, lambda j: aggregate_table(sh.bucket(j), keys, self.aggs), n, sh)
 
 
 class DistinctPlan(WidePlan):
@@ -198,11 +195,9 @@ class DistinctPlan(WidePlan):
     def execute(self, scheduler):
         keys = self.subset or self.child.schema.names
         n = self.n
-        pieces = scheduler.map(lambda i: hash_partition(self.child.compute(i), keys, n),
-                               range(self.child.num_partitions()))
         schema = self.child.schema
-        return scheduler.map(lambda j: self._dedup(concat([p[j] for p in pieces], schema)),
-                             range(n))
+        sh = exchange(scheduler, self.child.compute, self.child.num_partitions(), keys, n, schema)
+        return _reduce(scheduler, lambda j: self._dedup(sh.bucket(j)), n, sh)
 
 
 class WindowPlan(WidePlan):
@@ -274,10 +269,16 @@ class WindowPlan(WidePlan):
             self.n = 1
             return [self._apply(concat(parts, schema))]
         n = self.n
-        pieces = scheduler.map(lambda i: hash_partition(self.child.compute(i), keys, n),
-                               range(self.child.num_partitions()))
-        return scheduler.map(lambda j: self._apply(concat([p[j] for p in pieces], schema)),
-                             range(n))
+        sh = exchange(scheduler, self.child.compute, self.child.num_partitions(), keys, n, schema)
+        return _reduce(scheduler, lambda j: self._apply(sh.bucket(j)), n, sh)
+
+
+def _reduce(scheduler, fn, n, sh):
+    """Reduce stage of a shuffle; the map outputs are dropped once it has run."""
+    try:
+        return scheduler.map(fn, range(n))
+    finally:
+        sh.release()
 
 
 def _col(name):

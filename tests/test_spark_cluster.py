@@ -245,3 +245,45 @@ def test_spark_master_memory_custom():
     assert st.required_resources["master"] == 1
     raydp.stop_spark()
     cluster.shutdown()
+
+
+def test_restarted_executor_registers_under_a_new_id(spark_on_ray_2_executors):
+    """RayDPExecutor.scala:82-94 + RayAppMaster.scala:192-209: a restarted executor actor keeps
+    its name but asks the master for a new executor id; the master records new -> old."""
+    spark = spark_on_ray_2_executors
+    backend = spark._cluster
+    ex = [e for e in backend.alive_executors() if e.executor_id == "1"][0]
+    before = ray.get(ex.handle.info.remote())
+    assert before["spark_executor_id"] == "1"
+    os.kill(before["pid"], 9)
+    assert spark.range(0, 100, numPartitions=4).count() == 100
+    after = ray.get(ex.handle.info.remote())
+    assert after["pid"] != before["pid"]
+    assert after["spark_executor_id"] not in ("0", "1")
+    assert backend.restarted_executors() == {after["spark_executor_id"]: "1"}
+    info = backend.appmaster.app_info()
+    assert info["executors"][after["spark_executor_id"]]["registered"]
+
+
+def test_external_shuffle_service(local_rt):
+    """spark.shuffle.service.enabled: map outputs go through the per-node native service
+    (RayAppMaster.scala:155-163) and the results equal the in-store shuffle's."""
+    import pandas as pd
+    from raydp_amd.spark import functions as F
+    from raydp_amd.spark import shuffle as S
+    spark = raydp.init_spark("shuf", 2, 1, "200M", configs={"spark.shuffle.service.enabled": "true"})
+    backend = spark._cluster
+    assert backend.shuffle_service_enabled
+    pdf = pd.DataFrame({"k": [i % 7 for i in range(5000)], "v": [float(i) for i in range(5000)]})
+    df = spark.createDataFrame(pdf).repartition(4)
+    got = df.groupBy("k").agg(F.sum("v").alias("s")).toPandas().sort_values("k").reset_index(drop=True)
+    want = pdf.groupby("k", as_index=False)["v"].sum().rename(columns={"v": "s"})
+    assert got["k"].tolist() == want["k"].tolist()
+    assert got["s"].tolist() == pytest.approx(want["s"].tolist())
+    assert df.select("k").distinct().count() == 7
+    services = backend.appmaster.app_info()["shuffle_services"]
+    assert len(services) == 1
+    sock = next(iter(services.values()))
+    assert S.client(sock).list() == []      # map outputs released after the reduce stage
+    infos = ray.get([e.handle.info.remote() for e in backend.alive_executors()])
+    assert {i["shuffle_service"] for i in infos} == {sock}
