@@ -54,6 +54,8 @@
 #include <vector>
 
 #include "frame.h"
+#include "logging.h"
+#include "trace.h"
 
 namespace {
 
@@ -116,11 +118,11 @@ struct AppInfo {  // ApplicationInfo
   bool register_executor(const std::string& id) {
     auto it = executors.find(id);
     if (it == executors.end()) {
-      fprintf(stderr, "[appmaster] register of unknown executor %s\n", id.c_str());
+      rx_log::msg("appmaster", "register of unknown executor %s", id.c_str());
       return false;
     }
     if (it->second.registered) {
-      fprintf(stderr, "[appmaster] executor %s registered twice\n", id.c_str());
+      rx_log::msg("appmaster", "executor %s registered twice", id.c_str());
       return false;
     }
     it->second.registered = true;
@@ -207,7 +209,8 @@ struct Master {
       if (stat(sock.c_str(), &st) == 0) break;
       usleep(2000);
     }
-    fprintf(stderr, "[appmaster] started shuffle service on node %s (pid %d)\n", node.c_str(), (int)pid);
+    rx_log::msg("appmaster", "started shuffle service on node %s (pid %d)", node.c_str(), (int)pid);
+    rx_trace::instant("appmaster", "shuffle service " + node, sock);
     shuffle_services[node] = {pid, sock};
     return sock;
   }
@@ -223,7 +226,8 @@ struct Master {
   void on_disconnected(int conn) {
     for (auto& kv : app.executors)
       if (kv.second.conn == conn) {
-        fprintf(stderr, "[appmaster] executor %s disconnected\n", kv.first.c_str());
+        rx_log::msg("appmaster", "executor %s disconnected", kv.first.c_str());
+        rx_trace::instant("appmaster", "executor disconnected " + kv.first);
         app.kill(kv.first);  // shutdownActor = false: the runtime may restart it
         return;
       }
@@ -279,6 +283,9 @@ struct Master {
         have_app = true;
         restarted.clear();
         app.state = AppState::RUNNING;
+        rx_log::msg("appmaster", "registered application %s (%s), %d executors", app.id.c_str(), d.name.c_str(),
+                    d.num_executors);
+        rx_trace::instant("appmaster", "register application " + app.id, d.name);
         std::vector<std::string> out = {"ok", app.id, master_url()};
         std::vector<std::string> orders;
         for (int i = 0; i < d.num_executors; ++i) request_new_executor(orders);  // schedule()
@@ -303,6 +310,7 @@ struct Master {
           eid = nid;
         }
         if (!app.register_executor(eid)) return reply({"err", "register rejected"});
+        rx_trace::instant("appmaster", "register executor " + eid, a[3] == "1" ? "restarted from " + a[0] : "");
         ExecutorDesc& e = app.executors[eid];
         e.node = a[1];
         e.pid = a[2];

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "frame.h"
+#include "trace.h"
 
 namespace {
 
@@ -127,6 +128,7 @@ struct Service {
           outputs.erase(old);
         }
         outputs[key] = o;
+        rx_trace::instant("shuffle", "map output " + a[0] + "/" + a[1], std::to_string(o.offsets.back()) + " B");
         return reply({"ok"});
       }
       case kFetch: {

@@ -42,6 +42,9 @@
 #include <string>
 #include <vector>
 
+#include "logging.h"
+#include "trace.h"
+
 namespace {
 
 enum Op : uint32_t { kSpawn = 1, kKill = 2, kList = 3, kSubscribe = 4, kShutdown = 5, kPing = 6, kWait = 7, kEvent = 100, kReply = 101 };
@@ -148,7 +151,11 @@ pid_t spawn(Proc& pr) {
     sigprocmask(SIG_SETMASK, &all, nullptr);
     if (!pr.cwd.empty() && chdir(pr.cwd.c_str()) != 0) _exit(126);
     if (!pr.log.empty()) {
-      int fd = open(pr.log.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+      // per-process log file with the ":job_id:" header (logging agent, Agent.java:41-97)
+      std::string job;
+      for (const auto& e : pr.env)
+        if (e.compare(0, 13, "RAYDP_JOB_ID=") == 0) job = e.substr(13);
+      int fd = rx_log::open_file(pr.log.c_str(), job.c_str(), pr.id.c_str(), pr.restarts);
       if (fd >= 0) {
         dup2(fd, 1);
         dup2(fd, 2);
@@ -174,6 +181,7 @@ pid_t spawn(Proc& pr) {
   pr.pid = pid;
   pr.alive = true;
   g_by_pid[pid] = pr.id;
+  rx_trace::instant("actor", "spawn " + pr.id, "pid " + std::to_string(pid) + " restart " + std::to_string(pr.restarts));
   return pid;
 }
 
@@ -195,6 +203,7 @@ void reap() {
     // a clean exit (status 0) is a voluntary actor exit: never restarted
     bool restart = !pr.no_restart && pr.status != 0 && (pr.max_restarts < 0 || pr.restarts < pr.max_restarts);
     broadcast({"died", id, std::to_string(pid), std::to_string(pr.status), restart ? "1" : "0"});
+    rx_trace::instant("actor", "died " + id, "status " + std::to_string(pr.status) + (restart ? " (restarting)" : ""));
     if (restart) {
       pr.restarts += 1;
       if (spawn(pr) > 0) broadcast({"restarted", id, std::to_string(pr.pid), std::to_string(pr.restarts)});

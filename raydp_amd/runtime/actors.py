@@ -86,6 +86,7 @@ class ProcessActor:
                   "RAYDP_HEAD_NODE_ID": node.node_id,
                   "RAYDP_SUPERVISOR_SOCK": self.manager.supervisor.sock_path,
                   "RAYDP_NAMESPACE": self.namespace, "PYTHONPATH": _python_path(),
+                  "RAYDP_JOB_ID": str(getattr(node, "job_id", "") or ""),
                   "RAYDP_NODE_IP": self.vnode.ip if self.vnode is not None else ""})
         gpus = self.opts.get("_gpu_ids")
         if gpus is not None:

@@ -73,11 +73,13 @@ class ExecutorTaskScheduler(P.TaskScheduler):
         indices = list(indices)
         if not indices:
             return []
+        from raydp_amd.utils import tracing
         t0 = time.perf_counter()
         payload, key = self._stage_payload(fn)
         t1 = time.perf_counter()
         try:
-            return self._dispatch(lambda ex, i: ex.handle.run_task.remote(key, i), indices)
+            with tracing.span("stage", cat="etl", tasks=len(indices), payload_bytes=len(payload.data)):
+                return self._dispatch(lambda ex, i: ex.handle.run_task.remote(key, i), indices)
         finally:
             self._free_payload(payload, key)
             if _TRACE:
@@ -108,10 +110,12 @@ class ExecutorTaskScheduler(P.TaskScheduler):
 
     def persist(self, fn, rdd_id: str, indices) -> List[tuple]:
         indices = list(indices)
+        from raydp_amd.utils import tracing
         payload, key = self._stage_payload(fn)
         out = []
         try:
-            res = self._dispatch(lambda ex, i: ex.handle.persist_partitions.remote(key, rdd_id, [i]),
+            with tracing.span("persist stage", cat="etl", tasks=len(indices)):
+                res = self._dispatch(lambda ex, i: ex.handle.persist_partitions.remote(key, rdd_id, [i]),
                                  indices, tag=True)
         finally:
             self._free_payload(payload, key)

@@ -101,7 +101,8 @@ class RayDPExecutor:
     def run_task(self, payload: bytes, index: int):
         fn = self._fn(payload)
         from raydp_amd.spark.plan import _PartitionScope
-        with _PartitionScope(index):
+        from raydp_amd.utils import tracing
+        with tracing.span("task", cat="executor", partition=index), _PartitionScope(index):
             out = fn(index)
         self.tasks_run += 1
         return out
@@ -113,8 +114,10 @@ class RayDPExecutor:
         fn = self._fn(payload)
         st = self._node.store
         out = []
+        from raydp_amd.utils import tracing
         for i in indices:
-            t = fn(i)
+            with tracing.span("task", cat="executor", partition=i, persist=rdd_id):
+                t = fn(i)
             if not isinstance(t, pa.Table):
                 raise TypeError(f"stage produced {type(t)} for a persisted partition")
             t = t.replace_schema_metadata()

@@ -161,28 +161,33 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         else:
             sched = config["lr_scheduler_creator"](optimizer, config) if config["lr_scheduler_creator"] else None
             engine = TorchLoopEngine(model, optimizer, loss, metrics, device, config, sched)
+        from raydp_amd.utils import tracing
         t_load0 = time.perf_counter()
-        engine.load(train_ds, eval_ds, config)
+        with tracing.span("ingest", cat="train", engine=engine.name):
+            engine.load(train_ds, eval_ds, config)
         LAST_TIMINGS["ingest"] = time.perf_counter() - t_load0
         t_train0 = time.perf_counter()
         config.setdefault("_engine_name", engine.name)
         for epoch in range(config["num_epochs"]):
-            train_res, train_loss = engine.train_epoch()
+            with tracing.span("train epoch", cat="train", epoch=epoch):
+                train_res, train_loss = engine.train_epoch()
             session.report(dict(epoch=epoch, train_res=train_res, train_loss=train_loss,
                                 engine=engine.name, allreduce=getattr(engine, "allreduce_kind", None)))
             if eval_ds is not None:
-                eval_res, test_loss = engine.evaluate_epoch()
+                with tracing.span("eval epoch", cat="train", epoch=epoch):
+                    eval_res, test_loss = engine.evaluate_epoch()
                 session.report(dict(epoch=epoch, eval_res=eval_res, test_loss=test_loss))
         LAST_TIMINGS["train"] = time.perf_counter() - t_train0
         t_ck0 = time.perf_counter()
-        states = engine.state_dict()
-        states = {k: v.detach().cpu() for k, v in states.items()}
-        with tempfile.TemporaryDirectory() as temp_checkpoint_dir:
-            checkpoint = None
-            if session.get_world_rank() == 0:
-                torch.save(states, os.path.join(temp_checkpoint_dir, "model.pt"))
-                checkpoint = Checkpoint.from_directory(temp_checkpoint_dir)
-            session.report({}, checkpoint=checkpoint)
+        with tracing.span("checkpoint", cat="train"):
+            states = engine.state_dict()
+            states = {k: v.detach().cpu() for k, v in states.items()}
+            with tempfile.TemporaryDirectory() as temp_checkpoint_dir:
+                checkpoint = None
+                if session.get_world_rank() == 0:
+                    torch.save(states, os.path.join(temp_checkpoint_dir, "model.pt"))
+                    checkpoint = Checkpoint.from_directory(temp_checkpoint_dir)
+                session.report({}, checkpoint=checkpoint)
         LAST_TIMINGS["checkpoint"] = time.perf_counter() - t_ck0
 
     # ------------------------------------------------------------------------- driver -----
@@ -236,30 +241,32 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
     def fit_on_spark(self, train_df: DF, evaluate_df: OPTIONAL_DF = None, max_retries=3,
                      fs_directory: Optional[str] = None, compression: Optional[str] = None,
                      stop_spark_after_conversion=False):
+        from raydp_amd.utils import tracing
         t_conv0 = time.perf_counter()
-        super().fit_on_spark(train_df, evaluate_df)
-        train_df = self._check_and_convert(train_df)
-        evaluate_ds = None
-        if fs_directory is not None:
-            from raydp_amd.spark.dataset import read_spark_parquet
-            app_id = train_df.sparkSession.sparkContext.applicationId
-            path = fs_directory.rstrip("/") + f"/{app_id}"
-            train_df.write.parquet(path + "/train", compression=compression)
-            train_ds = read_spark_parquet(path + "/train")
-            if evaluate_df is not None:
-                evaluate_df = self._check_and_convert(evaluate_df)
-                evaluate_df.write.parquet(path + "/test", compression=compression)
-                evaluate_ds = read_spark_parquet(path + "/test")
-        else:
-            from raydp_amd.spark.dataset import (get_raydp_master_owner,
-                                                 spark_dataframe_to_ray_dataset)
-            owner = None
-            if stop_spark_after_conversion:
-                owner = get_raydp_master_owner(train_df.sparkSession)
-            train_ds = spark_dataframe_to_ray_dataset(train_df, owner=owner)
-            if evaluate_df is not None:
-                evaluate_df = self._check_and_convert(evaluate_df)
-                evaluate_ds = spark_dataframe_to_ray_dataset(evaluate_df, owner=owner)
+        with tracing.span("etl + conversion", cat="etl"):
+            super().fit_on_spark(train_df, evaluate_df)
+            train_df = self._check_and_convert(train_df)
+            evaluate_ds = None
+            if fs_directory is not None:
+                from raydp_amd.spark.dataset import read_spark_parquet
+                app_id = train_df.sparkSession.sparkContext.applicationId
+                path = fs_directory.rstrip("/") + f"/{app_id}"
+                train_df.write.parquet(path + "/train", compression=compression)
+                train_ds = read_spark_parquet(path + "/train")
+                if evaluate_df is not None:
+                    evaluate_df = self._check_and_convert(evaluate_df)
+                    evaluate_df.write.parquet(path + "/test", compression=compression)
+                    evaluate_ds = read_spark_parquet(path + "/test")
+            else:
+                from raydp_amd.spark.dataset import (get_raydp_master_owner,
+                                                     spark_dataframe_to_ray_dataset)
+                owner = None
+                if stop_spark_after_conversion:
+                    owner = get_raydp_master_owner(train_df.sparkSession)
+                train_ds = spark_dataframe_to_ray_dataset(train_df, owner=owner)
+                if evaluate_df is not None:
+                    evaluate_df = self._check_and_convert(evaluate_df)
+                    evaluate_ds = spark_dataframe_to_ray_dataset(evaluate_df, owner=owner)
         LAST_TIMINGS["etl_and_conversion"] = time.perf_counter() - t_conv0
         if stop_spark_after_conversion:
             from raydp_amd.context import stop_spark
