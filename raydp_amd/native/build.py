@@ -5,8 +5,8 @@
 * ``libhipkernels.so``    — CDNA4 HIP kernels for gfx950 (hipcc ``--offload-arch=gfx950``).
 * ``raydp_supervisor`` / ``raydp_appmaster`` / ``raydp_shuffle_service`` — native services (g++).
 
-``RAYDP_SANITIZE=address,undefined`` (or ``thread``) builds the host-side C++ with that
-sanitizer into a separate ``sanitize/`` directory (``scripts/sanitize_runtime.sh``).
+``build_sanitized("asan"|"tsan", dir)`` builds the host-side services and the runtime stress
+test under AddressSanitizer+UBSan or ThreadSanitizer (``scripts/sanitize_runtime.sh``).
 
 Usage: ``python -m raydp_amd.native.build [name ...]``.
 """
@@ -105,6 +105,32 @@ def build_one(name: str, force: bool = False) -> str:
     return out
 
 
+SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+              "tsan": ["-fsanitize=thread"]}
+
+
+def build_sanitized(kind: str, out_dir: str, names=("raydp_supervisor", "raydp_appmaster", "raydp_shuffle_service"),
+                    stress: bool = True) -> dict:
+    """Host C++ (services + the runtime stress test) under a sanitizer, into ``out_dir``
+    (SURVEY.md §5.2). Returns ``{name: path}``."""
+    flags = SANITIZERS[kind]
+    os.makedirs(out_dir, exist_ok=True)
+    cxx = shutil.which("g++") or "c++"
+    inc = ["-I", os.path.join(CSRC, "common"), "-I", CSRC]
+    out = {}
+    for n in names:
+        p = os.path.join(out_dir, n)
+        _run([cxx, "-O1", "-g", "-std=c++17", "-Wall"] + flags + inc + LIBS[n]["sources"]() + ["-o", p])
+        out[n] = p
+    if stress:
+        p = os.path.join(out_dir, "runtime_stress")
+        _run([cxx, "-O1", "-g", "-std=c++17"] + flags + inc +
+             [os.path.join(CSRC, "tests", "runtime_stress.cc"), os.path.join(CSRC, "runtime", "objstore.cc"),
+              "-o", p, "-lpthread", "-lrt"])
+        out["runtime_stress"] = p
+    return out
+
+
 def build_all(names=None, force=False):
     for n in names or LIBS:
         if LIBS[n]["kind"] == "hip" and not os.path.exists(os.path.join(ROCM, "bin", "hipcc")):
@@ -117,4 +143,7 @@ def build_all(names=None, force=False):
 
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("-")]
-    build_all(args or None, force="--force" in sys.argv)
+    if "--sanitize" in sys.argv:  # python -m raydp_amd.native.build --sanitize asan <dir>
+        print(build_sanitized(args[0], args[1]))
+    else:
+        build_all(args or None, force="--force" in sys.argv)

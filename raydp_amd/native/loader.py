@@ -37,7 +37,13 @@ def load(name: str, build_if_missing: bool = True):
 
 
 def executable(name: str, build_if_missing: bool = True) -> str:
-    """Path of an in-tree native executable (built on first use)."""
+    """Path of an in-tree native executable (built on first use).
+
+    ``RAYDP_NATIVE_BIN_DIR`` points at an alternative build of the services (the sanitizer
+    builds of ``scripts/sanitize_runtime.sh``); a binary found there wins."""
+    alt = os.environ.get("RAYDP_NATIVE_BIN_DIR")
+    if alt and os.path.exists(os.path.join(alt, name)):
+        return os.path.join(alt, name)
     from raydp_amd.native import build
     path = build.out_path(name)
     with _lock:
