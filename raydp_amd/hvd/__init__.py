@@ -304,6 +304,10 @@ class _Fusion:
 
     def __init__(self, params: List[torch.nn.Parameter], threshold: int, op, compression, gscale):
         self.op, self.compression, self.gscale = op, compression, gscale
+        self._sum = None
+        if op in (Average, Sum, Adasum):
+            from raydp_amd.ops.comm import BucketAllreduce
+            self._sum = BucketAllreduce()   # one-shot xGMI for small fp32 buckets
         self.buckets: List[List[torch.nn.Parameter]] = []
         cur, cur_bytes = [], 0
         for p in reversed(params):
@@ -335,7 +339,10 @@ class _Fusion:
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in ps]
         flat = torch.cat([g.reshape(-1) for g in grads])
         flat, ctx = self.compression.compress(flat)
-        work = dist.all_reduce(flat, op=_reduce_op(self.op), async_op=True)
+        if self._sum is not None:
+            work = self._sum(flat)
+        else:
+            work = dist.all_reduce(flat, op=_reduce_op(self.op), async_op=True)
         self.pending.append((b, flat, ctx, work))
 
     def finish(self):

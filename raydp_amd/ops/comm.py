@@ -125,7 +125,8 @@ class XgmiComm:
 
     def check(self):
         if self.error():
-            raise RuntimeError("xGMI all-reduce: a peer did not arrive within the timeout")
+            from raydp_amd.exceptions import CollectiveError
+            raise CollectiveError("xGMI all-reduce: a peer did not arrive within the timeout")
 
     def close(self):
         if self.ctx:
@@ -192,3 +193,48 @@ def _agree(ok: bool, group=None) -> bool:
     t = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
     dist.all_reduce(t, group=group)
     return int(t.item()) == 0
+
+
+XG_BUCKET_MAX_BYTES = 1 << 20  # one-shot threshold (<= 1 MB buckets)
+
+
+class _Done:
+    """Completed-work handle for a collective that is already ordered on the compute stream."""
+
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+class BucketAllreduce:
+    """Sum-all-reduce of gradient buckets for the DDP and Horovod wrappers.
+
+    Buckets of at most ``XG_BUCKET_MAX_BYTES`` fp32 go through the one-shot xGMI kernel
+    (stream-ordered, latency-bound sizes); larger ones, other dtypes and non-RCCL groups use
+    ``torch.distributed.all_reduce``. Construct it on every rank at the same point (it runs
+    the collective xGMI set-up)."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        from raydp_amd.utils.config import get as conf_get
+        self.group = group
+        self.xg = None
+        try:
+            if (dist.is_initialized() and dist.get_backend(group) == "nccl" and torch.cuda.is_available()
+                    and conf_get("spark.ray.mi355x.allreduce") != "rccl"):
+                self.xg = XgmiComm.create(XG_BUCKET_MAX_BYTES // 4, group=group,
+                                          timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
+        except Exception:  # noqa: BLE001
+            self.xg = None
+
+    def __call__(self, flat):
+        import torch
+        import torch.distributed as dist
+        if (self.xg is not None and flat.is_cuda and flat.dtype == torch.float32 and flat.is_contiguous()
+                and flat.numel() * 4 <= XG_BUCKET_MAX_BYTES and not torch.cuda.is_current_stream_capturing()):
+            self.xg.allreduce_(flat)
+            return _Done()
+        return dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)

@@ -88,6 +88,8 @@ class DistributedDataParallel(nn.Module):
             p.register_post_accumulate_grad_hook(self._sparse_hook)
         self._finalize_queued = False
         self.require_backward_grad_sync = True
+        from raydp_amd.ops.comm import BucketAllreduce
+        self._allreduce = BucketAllreduce(process_group)
 
     def _sparse_hook(self, param):
         if self.require_backward_grad_sync and not self._finalize_queued:
@@ -131,7 +133,7 @@ class DistributedDataParallel(nn.Module):
                 self._finalize_queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
             if b.pending == 0:
-                b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                b.work = self._allreduce(b.flat)
         return hook
 
     def _finalize(self):
@@ -145,7 +147,7 @@ class DistributedDataParallel(nn.Module):
                     if p.grad is None:
                         off = b.offsets[pi]
                         b.flat[off:off + p.numel()].zero_()
-                b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                b.work = self._allreduce(b.flat)
             b.work.wait()
             b.flat.div_(self.world)
             for pi, p in enumerate(b.params):

@@ -18,6 +18,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
+from raydp_amd.exceptions import AppMasterError
 from raydp_amd.runtime.supervisor import encode, read_frame
 
 (OP_REGISTER_APP, OP_UNREGISTER_APP, OP_REGISTER_EXECUTOR, OP_EXECUTOR_STARTED, OP_REQUEST_EXECUTORS,
@@ -47,10 +48,6 @@ class LaunchOrder:
             k, v = item.rsplit(":", 1)
             res[k] = float(v)
         return cls(kv["id"], float(kv["cpu"]), int(kv["memory_mb"]), int(kv["cores"]), int(kv["bundle"]), res)
-
-
-class AppMasterError(RuntimeError):
-    pass
 
 
 class _Conn:
