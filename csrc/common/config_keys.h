@@ -26,7 +26,6 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.object_store_bytes", "RAYDP_OBJECT_STORE_BYTES", "0"},
     {"spark.ray.mi355x.trace", "RAYDP_TRACE", ""},
     {"spark.ray.mi355x.roctx", "RAYDP_ROCTX", "0"},
-    {"spark.ray.mi355x.log_dir", "RAYDP_LOG_DIR", ""},
     {"spark.ray.mi355x.opt_xcd_affine", "RAYDP_OPT_XCD_AFFINE", "1"},
     {"spark.ray.mi355x.xg_opt_stride", "RAYDP_XG_OPT_STRIDE", "1"},
 };

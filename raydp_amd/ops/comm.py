@@ -223,8 +223,10 @@ class BucketAllreduce:
         self.group = group
         self.xg = None
         try:
-            if (dist.is_initialized() and dist.get_backend(group) == "nccl" and torch.cuda.is_available()
-                    and conf_get("spark.ray.mi355x.allreduce") != "rccl"):
+            # gloo groups qualify too when the tensors are on the GPU (a rehearsal with several
+            # ranks per device): the peer regions are bootstrapped over whatever group is given
+            if (dist.is_initialized() and dist.get_backend(group) in ("nccl", "gloo") and torch.cuda.is_available()
+                    and torch.cuda.is_initialized() and conf_get("spark.ray.mi355x.allreduce") != "rccl"):
                 self.xg = XgmiComm.create(XG_BUCKET_MAX_BYTES // 4, group=group,
                                           timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
         except Exception:  # noqa: BLE001

@@ -63,7 +63,8 @@ def jit_enabled() -> bool:
     """Per-model specialised step kernels (``raydp_amd.ops.mlp_jit``); RAYDP_MLP_JIT=0 turns
     them off (the ahead-of-time run-time-descriptor kernel is used instead)."""
     import os
-    return os.environ.get("RAYDP_MLP_JIT", "1") != "0"
+    from raydp_amd.utils.config import get as conf_get
+    return bool(conf_get("spark.ray.mi355x.mlp_jit"))
 
 
 def pick_mt(batch: int) -> Optional[int]:

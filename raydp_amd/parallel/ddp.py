@@ -49,7 +49,8 @@ class DistributedDataParallel(nn.Module):
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
         self.broadcast_buffers = broadcast_buffers
-        cap = float(os.environ.get("RAYDP_DDP_BUCKET_MB", bucket_cap_mb or 32.0)) * (1 << 20)
+        from raydp_amd.utils.config import get as conf_get
+        cap = float(bucket_cap_mb or conf_get("spark.ray.mi355x.ddp.bucket_mb")) * (1 << 20)
         sparse_ids = set()
         for m in module.modules():
             if isinstance(m, (nn.Embedding, nn.EmbeddingBag)) and m.sparse:

@@ -148,10 +148,18 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         from raydp_amd.torch.engine import FusedMLPEngine, TorchLoopEngine
         engine = None
         fused = None
-        if config.get("fused", True):
+        fused_mode = config.get("fused", None)
+        if fused_mode is None:
+            from raydp_amd.utils.config import get as conf_get
+            fused_mode = conf_get("spark.ray.mi355x.fused")
+        fused_mode = {True: "auto", False: "off"}.get(fused_mode, fused_mode)
+        if fused_mode != "off":
             fused = FusedMLPEngine.applicable(model, optimizer, loss, metrics, device,
                                               config["batch_size"], config["feature_columns"],
                                               config["feature_types"])
+        if fused is None and fused_mode == "on":
+            raise ValueError("spark.ray.mi355x.fused=on but the model / optimizer / loss is not fusable "
+                             "(FusedMLPEngine.applicable)")
         if fused is not None:
             spec, lc, oc = fused
             lr_fn = None
@@ -207,7 +215,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             "shuffle": self._shuffle,
             "evaluate": True,
             "metrics": self._metrics,
-            "fused": self._extra_config.get("fused", True),
+            "fused": self._extra_config.get("fused", None),
         }
         use_gpu = self._extra_config.get("use_gpu")
         if self._resources_per_worker and "GPU" in self._resources_per_worker:

@@ -39,7 +39,8 @@ _SAFE_OPT = _ADAM_LIKE + (torch.optim.SGD,)
 
 
 def graphs_requested() -> bool:
-    return os.environ.get("RAYDP_TORCH_GRAPHS", "1") not in ("0", "false", "False", "")
+    from raydp_amd.utils.config import get as conf_get
+    return bool(conf_get("spark.ray.mi355x.hip_graphs"))
 
 
 def supported(engine) -> Optional[str]:

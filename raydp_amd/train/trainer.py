@@ -247,10 +247,14 @@ class DataParallelTrainer:
         port = _free_port()
         cls = runtime.remote(_TrainWorker)
         workers = []
+        from raydp_amd.utils.config import env_for_workers
+        wenv = env_for_workers()   # spark.ray.mi355x.* settings of the driver's session
         try:
             for r in range(world):
                 opts = {"num_cpus": cpus, "num_gpus": gpus, "placement_group": pg,
                         "placement_group_bundle_index": r, "max_concurrency": 2}
+                if wenv:
+                    opts["runtime_env"] = {"env_vars": dict(wenv)}
                 if res:
                     opts["resources"] = res
                 workers.append(cls.options(**opts).remote(r, world, storage, use_gpu))

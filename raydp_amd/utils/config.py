@@ -142,8 +142,6 @@ register("spark.ray.mi355x.opt_xcd_affine", "bool", True,
 register("spark.ray.mi355x.xg_opt_stride", "int", 1,
          "workgroup stride of the fused reduce+optimizer kernel (1: every XCD pulls peer lines)",
          env="RAYDP_XG_OPT_STRIDE")
-register("spark.ray.mi355x.log_dir", "str", None,
-         "directory of per-process log files (default <session>/logs)", env="RAYDP_LOG_DIR")
 
 
 def _active_conf() -> Optional[Mapping]:
@@ -169,8 +167,8 @@ def _lookup(m, key):
 def lookup(key: str) -> ConfigKey:
     if key in REGISTRY:
         return REGISTRY[key]
-    for k in REGISTRY.values():
-        if k.prefix and key.startswith(k.key):
+    for name, k in REGISTRY.items():
+        if k.prefix and key.startswith(name):
             return k
     raise KeyError(f"unknown configuration key {key!r}")
 
@@ -216,7 +214,7 @@ def validate(conf: Mapping) -> List[str]:
 def env_for_workers(conf: Optional[Mapping] = None) -> Dict[str, str]:
     """Environment that carries every set MI355X key into worker processes."""
     out = {}
-    for k in set(REGISTRY.values()):
+    for k in {id(v): v for v in REGISTRY.values()}.values():
         if not k.env:
             continue
         v = _lookup(conf, k.key) if conf is not None else None

@@ -150,3 +150,47 @@ def test_fused_step_loop_with_xgmi_reduce_matches_gloo_allreduce():
         assert status == "ok", (rank, status)
         assert same, "replicas diverged across ranks"
         assert rel < 1e-4, (rank, rel)
+
+
+def _ddp_main(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    _init(rank, world, port)
+    try:
+        from raydp_amd.ops import comm as C
+        from raydp_amd.parallel.ddp import DistributedDataParallel
+        res = {}
+        for mode in ("auto", "rccl"):   # rccl: BucketAllreduce falls back to dist.all_reduce (gloo here)
+            os.environ["RAYDP_ALLREDUCE"] = mode
+            torch.manual_seed(0)
+            net = torch.nn.Sequential(torch.nn.Linear(20, 64), torch.nn.ReLU(), torch.nn.Linear(64, 1)).cuda()
+            ddp = DistributedDataParallel(net)
+            used = ddp._allreduce.xg is not None
+            opt = torch.optim.SGD(ddp.parameters(), lr=0.05)
+            g = torch.Generator().manual_seed(11 + rank)
+            for _ in range(5):
+                x = torch.randn(32, 20, generator=g).cuda()
+                y = torch.randn(32, 1, generator=g).cuda()
+                opt.zero_grad()
+                torch.nn.functional.mse_loss(ddp(x), y).backward()
+                opt.step()
+            torch.cuda.synchronize()
+            res[mode] = (used, torch.cat([p.detach().reshape(-1) for p in net.parameters()]).cpu())
+        os.environ.pop("RAYDP_ALLREDUCE", None)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, res["auto"][1])
+        same = all(bool(torch.equal(gathered[0], t)) for t in gathered)
+        diff = float((res["auto"][1] - res["rccl"][1]).abs().max())
+        q.put((rank, res["auto"][0], res["rccl"][0], same, diff))
+        dist.barrier()
+        C.reset_cache()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_small_buckets_take_the_xgmi_path():
+    res = _run(_ddp_main)
+    for rank, used_xg, used_fallback, same, diff in res:
+        assert used_xg and not used_fallback, (rank, used_xg, used_fallback)
+        assert same, "DDP replicas diverged"
+        assert diff < 1e-5, (rank, diff)
