@@ -43,6 +43,14 @@ MASTER_SUFFIX = "_SPARK_MASTER"
 _TRACE = bool(__import__("os").environ.get("RAYDP_TRACE_STAGES"))
 
 
+def _seconds(v) -> float:
+    v = str(v).strip().lower()
+    for suf, k in (("ms", 1e-3), ("s", 1.0), ("m", 60.0)):
+        if v.endswith(suf):
+            return float(v[:-len(suf)]) * k
+    return float(v)
+
+
 class ExecutorInfo:
     def __init__(self, executor_id: str, handle, cores: int):
         self.executor_id = executor_id
@@ -50,6 +58,7 @@ class ExecutorInfo:
         self.cores = cores
         self.state = "RUNNING"
         self.launched = time.time()
+        self.node_id: Optional[str] = None   # store node of the executor (locality)
 
     @property
     def alive(self) -> bool:
@@ -68,8 +77,11 @@ class ExecutorTaskScheduler(P.TaskScheduler):
         self.backend = backend
         self.parallelism = max(1, backend.num_executors * backend.cores)
         self.max_failures = int(backend.conf.get("spark.task.maxFailures", "4"))
+        self.locality_wait = _seconds(backend.conf.get("spark.locality.wait", "3s"))
 
-    def map(self, fn, indices):
+    def map(self, fn, indices, prefs=None):
+        """``prefs``: optional ``{partition: node_id}`` locality hints (else taken from the plan
+        when ``fn`` is a plan's ``compute``)."""
         indices = list(indices)
         if not indices:
             return []
@@ -79,7 +91,10 @@ class ExecutorTaskScheduler(P.TaskScheduler):
         t1 = time.perf_counter()
         try:
             with tracing.span("stage", cat="etl", tasks=len(indices), payload_bytes=len(payload.data)):
-                return self._dispatch(lambda ex, i: ex.handle.run_task.remote(key, i), indices)
+                pos_prefs = ({pos: prefs[i] for pos, i in enumerate(indices) if prefs.get(i)}
+                             if prefs is not None else self._prefs(fn, indices))
+                return self._dispatch(lambda ex, i: ex.handle.run_task.remote(key, i), indices,
+                                      prefs=pos_prefs)
         finally:
             self._free_payload(payload, key)
             if _TRACE:
@@ -124,7 +139,40 @@ class ExecutorTaskScheduler(P.TaskScheduler):
                 out.append((i, oid, node_id, path, rows, ex_id))
         return out
 
-    def _dispatch(self, submit, indices, tag=False):
+    @staticmethod
+    def _prefs(fn, indices) -> Dict[int, str]:
+        """Locality hints of a stage whose function is a plan's ``compute``."""
+        plan = getattr(fn, "__self__", None)
+        if not isinstance(plan, P.Plan):
+            return {}
+        out = {}
+        for pos, i in enumerate(indices):
+            n = P.preferred_node(plan, i)
+            if n is not None:
+                out[pos] = n
+        return out
+
+    def _pick(self, todo, execs, load, prefs, t_stage):
+        """Next (task position, executor) under delay scheduling (``spark.locality.wait``): a
+        task with a preferred node waits for a free slot there, up to the wait, unless no
+        executor lives on that node; tasks without a preference take any free slot."""
+        free = [e for e in execs if load[e.executor_id] < e.cores]
+        if not free:
+            return None
+        least = min(free, key=lambda e: load[e.executor_id])
+        expired = time.monotonic() - t_stage >= self.locality_wait
+        for pos in todo:
+            want = prefs.get(pos) if prefs else None
+            if want is None:
+                return pos, least
+            local = [e for e in free if e.node_id == want]
+            if local:
+                return pos, min(local, key=lambda e: load[e.executor_id])
+            if expired or not any(e.node_id == want for e in execs):
+                return pos, least
+        return None
+
+    def _dispatch(self, submit, indices, tag=False, prefs=None):
         from raydp_amd.runtime import core
         from raydp_amd.runtime.actors import ActorDiedError
         results = [None] * len(indices)
@@ -132,15 +180,17 @@ class ExecutorTaskScheduler(P.TaskScheduler):
         inflight: Dict[cf.Future, tuple] = {}
         load: Dict[str, int] = collections.defaultdict(int)
         failures: Dict[int, int] = collections.defaultdict(int)
+        t_stage = time.monotonic()
         while todo or inflight:
             execs = self.backend.alive_executors()
             if not execs and not inflight:
                 raise RuntimeError("no live executors to run tasks")
             while todo and execs:
-                ex = min(execs, key=lambda e: load[e.executor_id])
-                if load[ex.executor_id] >= ex.cores:
+                pick = self._pick(todo, execs, load, prefs, t_stage)
+                if pick is None:
                     break
-                pos = todo.popleft()
+                pos, ex = pick
+                todo.remove(pos)
                 try:
                     ref = submit(ex, indices[pos])
                 except ActorDiedError:
@@ -153,7 +203,8 @@ class ExecutorTaskScheduler(P.TaskScheduler):
             if not inflight:
                 time.sleep(0.01)
                 continue
-            done, _ = cf.wait(list(inflight), return_when=cf.FIRST_COMPLETED)
+            done, _ = cf.wait(list(inflight), return_when=cf.FIRST_COMPLETED,
+                              timeout=self.locality_wait if todo and prefs else None)
             for f in done:
                 pos, ex = inflight.pop(f)
                 load[ex.executor_id] -= 1
@@ -210,8 +261,10 @@ class ClusterBackend:
         master_url = self.master.start_up.remote(self.master_resources)
         self._start_appmaster()
         self._master_url = runtime.get(master_url)
-        # executors come up in parallel; wait until each answers
-        runtime.get([e.handle.ping.remote() for e in self.alive_executors()])
+        # executors come up in parallel; wait until each answers (and learn its node)
+        execs = self.alive_executors()
+        for e, inf in zip(execs, runtime.get([e.handle.info.remote() for e in execs])):
+            e.node_id = inf["node_id"]
         self._sched = ExecutorTaskScheduler(self)
         self._started = True
 

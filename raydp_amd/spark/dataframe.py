@@ -699,7 +699,7 @@ def _df_rdd(df: "DataFrame"):
         t = plan.compute(i)
         cols = [c.to_pylist() for c in t.columns]
         return [Row._make(names, vals) for vals in zip(*cols)] if cols else []
-    r = RDD(df._session, plan.num_partitions(), rows, "dataframe")
+    r = RDD(df._session, plan.num_partitions(), rows, "dataframe", prefs=lambda i: P.preferred_node(plan, i))
     r._id_str = df._id
     return r
 

@@ -120,6 +120,10 @@ def ray_dataset_to_spark_dataframe(spark, arrow_schema, blocks: List[ObjectRef],
         def schema(self):
             return arrow_schema
 
+        def preferred_node(self, i):
+            # RayDatasetRDD / RayObjectRefRDD: run the task where the block lives
+            return getattr(blocks[i], "node_id", None)
+
     return DataFrame(P.SourcePlan(_BlockSource()), spark)
 
 

@@ -112,6 +112,20 @@ class Plan:
         pass
 
 
+def preferred_node(plan: Plan, i: int) -> Optional[str]:
+    """Node holding the input of partition ``i``, following the narrow chain down to its source
+    (``RayDatasetRDD.getPreferredLocations``, ``RayDatasetRDD.scala:35-57``); None if unknown."""
+    p = plan
+    while True:
+        if isinstance(p, SourcePlan):
+            f = getattr(p.source, "preferred_node", None)
+            return f(i) if f is not None else None
+        if isinstance(p, MapPlan):
+            p = p.child
+            continue
+        return None
+
+
 def prepare(plan: Plan, scheduler: TaskScheduler):
     """Materialise every wide operator below ``plan`` bottom-up (stage scheduling)."""
     for c in plan.children():

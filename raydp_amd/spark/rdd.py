@@ -36,11 +36,13 @@ def _portable_hash(x) -> int:
 
 
 class RDD:
-    def __init__(self, session, num_partitions: int, compute: Callable[[int], Iterable], name: str = "rdd"):
+    def __init__(self, session, num_partitions: int, compute: Callable[[int], Iterable], name: str = "rdd",
+                 prefs: Optional[Callable[[int], Optional[str]]] = None):
         self._session = session
         self._n = max(1, int(num_partitions))
         self._compute = compute
         self._name = name
+        self._prefs = prefs   # partition -> node holding its input (narrow lineage only)
         self._cached: Optional[List[list]] = None
         import uuid
         self._id = uuid.uuid4().int & 0x7FFFFFFF
@@ -64,11 +66,15 @@ class RDD:
 
     def _run(self, fn: Callable[[int], Any]) -> list:
         sched = self._session._scheduler_or_default()
+        if self._prefs is not None and self._cached is None and getattr(sched, "remote", False):
+            return sched.map(fn, range(self._n), prefs={i: self._prefs(i) for i in range(self._n)})
         return sched.map(fn, range(self._n))
 
     def _derive(self, fn: Callable[[Iterable, int], Iterable], name: str, n: Optional[int] = None) -> "RDD":
         src = self._part_fn()
-        return RDD(self._session, self._n if n is None else n, lambda i: fn(src(i), i), name)
+        keep = n is None or n == self._n
+        return RDD(self._session, self._n if n is None else n, lambda i: fn(src(i), i), name,
+                   prefs=self._prefs if keep and self._cached is None else None)
 
     # ------------------------------------------------------------------ narrow -----------
     def map(self, f, preservesPartitioning=False) -> "RDD":

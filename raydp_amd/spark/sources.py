@@ -17,6 +17,10 @@ import pyarrow.parquet as pq
 
 
 class Source:
+    def preferred_node(self, i: int):
+        """Node id whose store holds partition ``i``'s input (locality hint), or None."""
+        return None
+
     def num_partitions(self) -> int:
         raise NotImplementedError
 

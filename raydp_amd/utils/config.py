@@ -103,6 +103,9 @@ register("spark.dynamicAllocation.minExecutors", "int", 0, "lower bound under dy
 register("spark.dynamicAllocation.initialExecutors", "int", None, "initial executors under dynamic allocation")
 register("spark.driver.host", "str", None, "driver address (default: node IP)", ref="python/raydp/spark/ray_cluster.py:121-124")
 register("spark.driver.bindAddress", "str", None, "driver bind address (default: node IP)")
+register("spark.locality.wait", "str", "3s",
+         "delay scheduling: how long a task waits for a slot on the node holding its input")
+register("spark.task.maxFailures", "int", 4, "task attempts before a stage fails (executor loss)")
 register("spark.sql.session.timeZone", "str", "UTC", "session time zone of datetime functions")
 for _k, _r in [("spark.ray.raydp_app_master.extraJavaOptions", "python/raydp/spark/ray_cluster_master.py:116-119"),
                ("raydp.executor.extraClassPath", "python/raydp/spark/ray_cluster_master.py:93-95"),

@@ -287,3 +287,28 @@ def test_external_shuffle_service(local_rt):
     assert S.client(sock).list() == []      # map outputs released after the reduce stage
     infos = ray.get([e.handle.info.remote() for e in backend.alive_executors()])
     assert {i["shuffle_service"] for i in infos} == {sock}
+
+
+def test_to_spark_tasks_run_where_blocks_live():
+    """RayDatasetRDD.getPreferredLocations (RayDatasetRDD.scala:35-57): a DataFrame built over
+    dataset blocks schedules each partition's task on an executor of the block's node."""
+    cluster = Cluster(initialize_head=True, head_node_args={"num_cpus": 1})
+    cluster.add_node(num_cpus=1, object_store_memory=10 ** 8)
+    cluster.add_node(num_cpus=1, object_store_memory=10 ** 8)
+    spark = raydp.init_spark("loc", 2, 1, "200M")
+    df = spark.range(0, 4000, numPartitions=8)
+    ds = raydp.spark.from_spark_recoverable(df)
+    refs = [r for bundle in ds.iter_internal_ref_bundles() for r, _ in bundle.blocks]
+    homes = [r.node_id for r in refs]
+    assert len(set(homes)) == 2            # blocks spread over both executors' nodes
+    back = ds.to_spark(spark)
+
+    def where(it):
+        import os as _os
+        rows = list(it)
+        yield (_os.environ.get("RAYDP_NODE_ID"), len(rows))
+    ran = back.rdd.mapPartitions(where).collect()
+    assert [n for n, _ in ran] == homes
+    assert sum(c for _, c in ran) == 4000
+    raydp.stop_spark()
+    cluster.shutdown()
