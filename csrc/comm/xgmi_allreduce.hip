@@ -69,13 +69,13 @@ void* rx_xg_create(int world, int rank, int device, int n, double timeout_s) {
   if (hipMalloc(&err, 64) != hipSuccess || hipMemset(err, 0, 64) != hipSuccess ||
       hipMemset(h->base, 0, h->bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
       hipIpcGetMemHandle(&h->handle, h->base) != hipSuccess) {
-    if (err) hipFree(err);
-    hipFree(h->base);
+    if (err) (void)hipFree(err);
+    (void)hipFree(h->base);
     delete h;
     return nullptr;
   }
   int khz = 100000;
-  hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
   memset(&h->dev, 0, sizeof(h->dev));
   h->dev.world = world;
   h->dev.rank = rank;
@@ -154,12 +154,12 @@ int rx_xg_error(void* ctx) {
 int rx_xg_destroy(void* ctx) {
   XgHost* h = (XgHost*)ctx;
   if (!h) return 0;
-  hipSetDevice(h->device);
-  hipDeviceSynchronize();
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
   for (int p = 0; p < h->dev.world; ++p)
-    if (h->opened[p]) hipIpcCloseMemHandle(h->dev.region[p]);
-  hipFree(h->dev.err);
-  hipFree(h->base);
+    if (h->opened[p]) (void)hipIpcCloseMemHandle(h->dev.region[p]);
+  (void)hipFree(h->dev.err);
+  (void)hipFree(h->base);
   delete h;
   return 0;
 }
