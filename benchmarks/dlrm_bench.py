@@ -1,9 +1,13 @@
-"""DLRM training throughput on one MI355X (synthetic Criteo-shaped batches, random init).
+"""DLRM training throughput on N MI355X (synthetic Criteo-shaped batches, random init).
 
-Model: the reference notebook's configuration (13 dense features, 26 tables, bottom MLP
-512-128-32, top MLP 1024-1024-512-256-1, embedding dim 32), table sizes from the synthetic
-preprocessing vocabulary (or --rows-per-table). Timed region: K full steps (forward, BCE loss,
-backward, SGD incl. sparse embedding update) bracketed by synchronize. Prints one JSON line.
+Model: the reference notebook's configuration (examples/pytorch_dlrm.ipynb cell 9: 13 dense
+features, 26 tables, bottom MLP 512-128-32, top MLP 1024-1024-512-256-1, embedding dim 32),
+``--rows-per-table`` rows per table. One GPU: fused multi-table embedding kernels (optionally
+with the sparse SGD fused into backward). N GPUs (``torchrun --nproc-per-node N``): tables
+sharded table-wise over the ranks with all-to-all of ids and rows (RCCL over xGMI), dense MLPs
+data parallel (bucketed all-reduce); weak scaling, ``--batch`` rows per GPU.
+Timed region: K full steps (forward, BCE loss, backward, all collectives, SGD incl. the sparse
+embedding update) bracketed by barrier + synchronize; the max over ranks. One JSON line.
 """
 import argparse
 import json
@@ -13,53 +17,86 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
+import torch.distributed as dist
 
 from raydp_amd.models.dlrm import Dlrm
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--batch", type=int, default=2048, help="rows per GPU per step")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rows-per-table", type=int, default=100000)
-    ap.add_argument("--fused-sgd", action="store_true", help="apply the embedding SGD inside backward")
+    ap.add_argument("--fused-sgd", action="store_true", help="apply the embedding SGD inside backward (1 GPU)")
     ap.add_argument("--amp", action="store_true", help="bf16 autocast for the MLP towers")
+    ap.add_argument("--model-parallel", action="store_true", help="sharded tables even on 1 GPU")
     args = ap.parse_args()
-    dev = torch.device("cuda")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_i = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_i)
+    dev = torch.device("cuda", dev_i)
+    mp = world > 1 or args.model_parallel
+    if mp:
+        dist.init_process_group(os.environ.get("RAYDP_BENCH_BACKEND", "nccl"), device_id=dev
+                                if os.environ.get("RAYDP_BENCH_BACKEND", "nccl") == "nccl" else None)
     torch.manual_seed(0)
     sizes = [args.rows_per_table] * 26
     lr = 0.01
     model = Dlrm(13, sizes, [512, 128, 32], [1024, 1024, 512, 256, 1], 32,
-                 fused_embedding_sgd_lr=lr if args.fused_sgd else None).to(dev)
+                 fused_embedding_sgd_lr=lr if (args.fused_sgd and not mp) else None, model_parallel=mp).to(dev)
+    net = model
+    if mp:
+        from raydp_amd.parallel.ddp import DistributedDataParallel
+        net = DistributedDataParallel(model)
     opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=lr)
     lossf = torch.nn.BCEWithLogitsLoss()
     n = args.batch * 8
-    dense = torch.randn(n, 13, device=dev)
-    cats = torch.randint(0, args.rows_per_table, (n, 26), device=dev)
-    y = torch.randint(0, 2, (n, 1), device=dev).float()
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    dense = torch.randn(n, 13, device=dev, generator=g)
+    cats = torch.randint(0, args.rows_per_table, (n, 26), device=dev, generator=g)
+    y = torch.randint(0, 2, (n, 1), device=dev, generator=g).float()
 
     def step(i):
         s = (i % 8) * args.batch
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.amp):
-            out = model(dense[s:s + args.batch], cats[s:s + args.batch])
+            out = net(dense[s:s + args.batch], cats[s:s + args.batch])
         loss = lossf(out.float(), y[s:s + args.batch])
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
         return loss
+
+    def barrier():
+        torch.cuda.synchronize()
+        if mp:
+            dist.barrier()
+            torch.cuda.synchronize()
+
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
+    barrier()
     t = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
-    torch.cuda.synchronize()
+    barrier()
     dt = time.perf_counter() - t
-    print(json.dumps({"metric": "DLRM training samples/sec (synthetic Criteo-shaped)", "value": round(args.steps * args.batch / dt, 1),
-                      "unit": "samples/s", "ms_per_step": round(dt * 1e3 / args.steps, 3), "batch": args.batch,
-                      "steps": args.steps, "fused_sgd": args.fused_sgd, "amp": args.amp,
-                      "loss": float(loss), "tables": 26, "rows_per_table": args.rows_per_table}))
+    if mp:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank == 0:
+        print(json.dumps({"metric": "DLRM training samples/sec (synthetic Criteo-shaped)",
+                          "value": round(world * args.steps * args.batch / dt, 1), "unit": "samples/s",
+                          "n_gpus": world, "ms_per_step": round(dt * 1e3 / args.steps, 3),
+                          "per_gpu_batch": args.batch, "steps": args.steps, "warmup": args.warmup,
+                          "embeddings": "table-wise sharded + all-to-all" if mp else "replicated fused",
+                          "fused_sgd": args.fused_sgd and not mp, "amp": args.amp, "loss": float(loss),
+                          "tables": 26, "rows_per_table": args.rows_per_table, "scaling": "weak"}), flush=True)
+    if mp:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -3,6 +3,9 @@ re-designed for MI355X: the 26 embedding tables are one fused parameter gathered
 kernel straight into the interaction input, the dot interaction runs on MFMA
 (``raydp_amd.ops.dlrm_ops``), and the MLP towers are plain Linear+ReLU (hipBLASLt GEMMs).
 
+``model_parallel=True`` shards the tables over the process group instead (table-wise, all-to-all
+exchange) for multi-GPU training.
+
 Same constructor and ``forward(*inputs)`` contract as the reference, so it drops into
 ``TorchEstimator`` with ``feature_columns = ['_c1', ..., '_c39']``: the first
 ``num_numerical_features`` inputs are float columns, the rest integer category ids.
@@ -40,14 +43,21 @@ class TorchMlp(nn.Module):
 class Dlrm(nn.Module):
     def __init__(self, num_numerical_features: int, categorical_feature_sizes: Sequence[int],
                  bottom_mlp_sizes: Sequence[int], top_mlp_sizes: Sequence[int], embedding_dim: int = 32,
-                 fused_embedding_sgd_lr: Optional[float] = None):
+                 fused_embedding_sgd_lr: Optional[float] = None, model_parallel: bool = False,
+                 embedding_group=None):
         super().__init__()
         if embedding_dim != bottom_mlp_sizes[-1]:
             raise ValueError("The last bottom MLP layer must have same size as embedding.")
         self.num_numerical_features = num_numerical_features
         self.embedding_dim = embedding_dim
         self.bottom_mlp = TorchMlp(num_numerical_features, bottom_mlp_sizes)
-        self.embeddings = FusedEmbeddings(categorical_feature_sizes, embedding_dim, fused_embedding_sgd_lr)
+        if model_parallel:
+            # table-wise sharding over the process group, all-to-all of ids / rows
+            # (raydp_amd.parallel.embedding_mp); the MLPs stay data parallel
+            from raydp_amd.parallel.embedding_mp import ShardedEmbeddings
+            self.embeddings = ShardedEmbeddings(categorical_feature_sizes, embedding_dim, group=embedding_group)
+        else:
+            self.embeddings = FusedEmbeddings(categorical_feature_sizes, embedding_dim, fused_embedding_sgd_lr)
         f = len(categorical_feature_sizes) + 1
         self.num_interactions = embedding_dim + f * (f - 1) // 2 + 1
         self.top_mlp = TorchMlp(self.num_interactions, top_mlp_sizes[:-1])

@@ -63,9 +63,16 @@ class DistributedDataParallel(nn.Module):
                 self.sparse_params.append(p)
             else:
                 params.append(p)
+        # rank-local state: tensors flagged model parallel, and everything of a module flagged so
+        # (a buffer's flag would not survive .to(device), the module's does)
+        local_ids = set()
+        for m in module.modules():
+            if getattr(m, "_raydp_model_parallel", False):
+                local_ids.update(id(t) for t in list(m.parameters()) + list(m.buffers()))
+        self._local_ids = local_ids
         with torch.no_grad():
             for t in list(module.parameters()) + list(module.buffers()):
-                if getattr(t, "_raydp_model_parallel", False):
+                if getattr(t, "_raydp_model_parallel", False) or id(t) in local_ids:
                     continue
                 dist.broadcast(t.data, 0, group=process_group)
         # reverse order ~= gradient production order
@@ -163,8 +170,11 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *args, **kw):
         if self.broadcast_buffers and self.world > 1:
             with torch.no_grad():
-                for t in self.module.buffers():
-                    dist.broadcast(t.data, 0, group=self.pg)
+                for m in self.module.modules():   # replicated buffers only (rank-local ones stay)
+                    if getattr(m, "_raydp_model_parallel", False):
+                        continue
+                    for t in m.buffers(recurse=False):
+                        dist.broadcast(t.data, 0, group=self.pg)
         return self.module(*args, **kw)
 
     def state_dict(self, *a, **kw):

@@ -108,6 +108,7 @@ class ShardedEmbeddings(nn.Module):
         self.register_buffer("local_offsets", torch.tensor(offs[:len(local_sizes)], dtype=torch.int64))
         self.weight = nn.Parameter(torch.empty(max(1, sum(local_sizes)), dim))
         self.weight._raydp_model_parallel = True   # owned by this rank only: DDP leaves it alone
+        self._raydp_model_parallel = True          # ... and every buffer of this module (offsets)
         with torch.no_grad():
             for t, o in zip(self.local_tables, offs):
                 s = self.table_sizes[t]

@@ -105,3 +105,49 @@ def test_ddp_reduces_sparse_embedding_grads():
     exp[3] += 2.0   # twice per rank: (2 + 2) / 2
     for r in (0, 1):
         assert torch.allclose(torch.tensor(res[r]), exp)
+
+
+def _dlrm_rank(rank, world, port, q):
+    import torch.distributed as dist
+    from raydp_amd.models.dlrm import Dlrm
+    from raydp_amd.parallel.ddp import DistributedDataParallel
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        sizes = [7, 11, 5, 9]
+        model = Dlrm(3, sizes, [16, 8], [32, 16, 1], 8, model_parallel=True)
+        net = DistributedDataParallel(model)
+        opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=0.1)
+        g = torch.Generator().manual_seed(5 + rank)
+        losses = []
+        for _ in range(3):
+            dense = torch.randn(6, 3, generator=g)
+            cats = torch.stack([torch.randint(0, s, (6,), generator=g) for s in sizes], 1)
+            y = torch.randint(0, 2, (6, 1), generator=g).float()
+            loss = torch.nn.functional.binary_cross_entropy_with_logits(net(dense, cats), y)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(float(loss))
+        dense_params = torch.cat([p.detach().reshape(-1) for n, p in model.named_parameters()
+                                  if not n.startswith("embeddings")])
+        gathered = [None] * world
+        dist.all_gather_object(gathered, dense_params)
+        q.put((rank, all(math.isfinite(x) for x in losses), all(torch.equal(gathered[0], t) for t in gathered),
+               model.embeddings.local_tables))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dlrm_model_parallel_trains_with_ddp():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_dlrm_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+    assert all(r[1] and r[2] for r in res), res
+    assert sorted(t for r in res for t in r[3]) == [0, 1, 2, 3]
