@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rows-per-table", type=int, default=100000)
-    ap.add_argument("--fused-sgd", action="store_true", help="apply the embedding SGD inside backward (1 GPU)")
+    ap.add_argument("--fused-sgd", action="store_true", help="apply the embedding SGD inside backward")
     ap.add_argument("--amp", action="store_true", help="bf16 autocast for the MLP towers")
     ap.add_argument("--model-parallel", action="store_true", help="sharded tables even on 1 GPU")
     args = ap.parse_args()
@@ -46,7 +46,8 @@ def main():
     sizes = [args.rows_per_table] * 26
     lr = 0.01
     model = Dlrm(13, sizes, [512, 128, 32], [1024, 1024, 512, 256, 1], 32,
-                 fused_embedding_sgd_lr=lr if (args.fused_sgd and not mp) else None, model_parallel=mp).to(dev)
+                 fused_embedding_sgd_lr=lr if args.fused_sgd else None, model_parallel=mp,
+                 static_batch=True).to(dev)
     net = model
     if mp:
         from raydp_amd.parallel.ddp import DistributedDataParallel
@@ -93,7 +94,7 @@ def main():
                           "n_gpus": world, "ms_per_step": round(dt * 1e3 / args.steps, 3),
                           "per_gpu_batch": args.batch, "steps": args.steps, "warmup": args.warmup,
                           "embeddings": "table-wise sharded + all-to-all" if mp else "replicated fused",
-                          "fused_sgd": args.fused_sgd and not mp, "amp": args.amp, "loss": float(loss),
+                          "fused_sgd": args.fused_sgd, "amp": args.amp, "loss": float(loss),
                           "tables": 26, "rows_per_table": args.rows_per_table, "scaling": "weak"}), flush=True)
     if mp:
         dist.destroy_process_group()

@@ -24,7 +24,7 @@ constexpr int kMaxF = 32;  // interaction rows (1 + tables), padded
 // X[b][1 + t][:] = W[offsets[t] + idx[b][t]][:]   (one 16-B chunk of D per thread)
 __global__ __launch_bounds__(256) void emb_gather_kernel(const float* __restrict__ W, const long long* __restrict__ offs,
                                                          const long long* __restrict__ idx, float* __restrict__ X,
-                                                         int B, int T, int D, int F, long long total_rows) {
+                                                         int B, int T, int D, int F, long long total_rows, int col0) {
   const int chunks = D >> 2;
   const long long n = (long long)B * T * chunks;
   for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += (long long)gridDim.x * blockDim.x) {
@@ -35,14 +35,15 @@ __global__ __launch_bounds__(256) void emb_gather_kernel(const float* __restrict
     long long row = offs[t] + idx[b * T + t];
     row = row < 0 ? 0 : (row >= total_rows ? total_rows - 1 : row);  // never read out of bounds
     const f32x4 v = *reinterpret_cast<const f32x4*>(W + row * D + 4 * c);
-    *reinterpret_cast<f32x4*>(X + (b * F + 1 + t) * D + 4 * c) = v;
+    *reinterpret_cast<f32x4*>(X + (b * F + col0 + t) * D + 4 * c) = v;
   }
 }
 
 // W[row] -= lr * dX[b][1 + t]   (duplicates accumulate through fp32 atomics)
 __global__ __launch_bounds__(256) void emb_sgd_kernel(float* __restrict__ W, const long long* __restrict__ offs,
                                                       const long long* __restrict__ idx, const float* __restrict__ dX,
-                                                      int B, int T, int D, int F, float lr, long long total_rows) {
+                                                      int B, int T, int D, int F, float lr, long long total_rows,
+                                                      int col0) {
   const long long n = (long long)B * T * D;
   for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += (long long)gridDim.x * blockDim.x) {
     const int d = (int)(g % D);
@@ -51,7 +52,7 @@ __global__ __launch_bounds__(256) void emb_sgd_kernel(float* __restrict__ W, con
     const long long b = bt / T;
     long long row = offs[t] + idx[b * T + t];
     if (row < 0 || row >= total_rows) continue;
-    atomicAdd(W + row * D + d, -lr * dX[(b * F + 1 + t) * D + d]);
+    atomicAdd(W + row * D + d, -lr * dX[(b * F + col0 + t) * D + d]);
   }
 }
 
@@ -179,14 +180,33 @@ int rx_emb_gather(const float* W, const long long* offs, const long long* idx, f
                   long long total_rows, hipStream_t s) {
   if (D % 4 != 0 || F < T + 1) return -1;
   hipLaunchKernelGGL(emb_gather_kernel, dim3(grid_for((long long)B * T * (D / 4))), dim3(256), 0, s, W, offs, idx, X, B,
-                     T, D, F, total_rows);
+                     T, D, F, total_rows, 1);
+  return (int)hipGetLastError();
+}
+
+// Packed variant for the owner side of table-wise sharding: Y[b][t] = W[offs[t] + idx[b][t]]
+// ([B, T, D], no interaction slot) -- the rows an owner returns over all-to-all.
+int rx_emb_gather_rows(const float* W, const long long* offs, const long long* idx, float* Y, int B, int T, int D,
+                       long long total_rows, hipStream_t s) {
+  if (D % 4 != 0) return -1;
+  hipLaunchKernelGGL(emb_gather_kernel, dim3(grid_for((long long)B * T * (D / 4))), dim3(256), 0, s, W, offs, idx, Y, B,
+                     T, D, T, total_rows, 0);
+  return (int)hipGetLastError();
+}
+
+// W[offs[t] + idx[b][t]] -= lr * G[b][t]: the sparse SGD of the owner's local tables, applied
+// straight from the gradient rows that came back over all-to-all.
+int rx_emb_sgd_rows(float* W, const long long* offs, const long long* idx, const float* G, int B, int T, int D,
+                    float lr, long long total_rows, hipStream_t s) {
+  hipLaunchKernelGGL(emb_sgd_kernel, dim3(grid_for((long long)B * T * D)), dim3(256), 0, s, W, offs, idx, G, B, T, D, T,
+                     lr, total_rows, 0);
   return (int)hipGetLastError();
 }
 
 int rx_emb_sgd(float* W, const long long* offs, const long long* idx, const float* dX, int B, int T, int D, int F,
                float lr, long long total_rows, hipStream_t s) {
   hipLaunchKernelGGL(emb_sgd_kernel, dim3(grid_for((long long)B * T * D)), dim3(256), 0, s, W, offs, idx, dX, B, T, D, F,
-                     lr, total_rows);
+                     lr, total_rows, 1);
   return (int)hipGetLastError();
 }
 

@@ -44,7 +44,7 @@ class Dlrm(nn.Module):
     def __init__(self, num_numerical_features: int, categorical_feature_sizes: Sequence[int],
                  bottom_mlp_sizes: Sequence[int], top_mlp_sizes: Sequence[int], embedding_dim: int = 32,
                  fused_embedding_sgd_lr: Optional[float] = None, model_parallel: bool = False,
-                 embedding_group=None):
+                 embedding_group=None, static_batch: bool = False):
         super().__init__()
         if embedding_dim != bottom_mlp_sizes[-1]:
             raise ValueError("The last bottom MLP layer must have same size as embedding.")
@@ -55,7 +55,8 @@ class Dlrm(nn.Module):
             # table-wise sharding over the process group, all-to-all of ids / rows
             # (raydp_amd.parallel.embedding_mp); the MLPs stay data parallel
             from raydp_amd.parallel.embedding_mp import ShardedEmbeddings
-            self.embeddings = ShardedEmbeddings(categorical_feature_sizes, embedding_dim, group=embedding_group)
+            self.embeddings = ShardedEmbeddings(categorical_feature_sizes, embedding_dim, group=embedding_group,
+                                                fused_sgd_lr=fused_embedding_sgd_lr, static_batch=static_batch)
         else:
             self.embeddings = FusedEmbeddings(categorical_feature_sizes, embedding_dim, fused_embedding_sgd_lr)
         f = len(categorical_feature_sizes) + 1

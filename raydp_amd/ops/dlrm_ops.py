@@ -23,9 +23,12 @@ def _lib():
         vp, i, f, ll = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_longlong
         L.rx_emb_gather.argtypes = [vp, vp, vp, vp, i, i, i, i, ll, vp]
         L.rx_emb_sgd.argtypes = [vp, vp, vp, vp, i, i, i, i, f, ll, vp]
+        L.rx_emb_gather_rows.argtypes = [vp, vp, vp, vp, i, i, i, ll, vp]
+        L.rx_emb_sgd_rows.argtypes = [vp, vp, vp, vp, i, i, i, f, ll, vp]
         L.rx_dot_interaction_fwd.argtypes = [vp, vp, i, i, i, vp]
         L.rx_dot_interaction_bwd.argtypes = [vp, vp, vp, i, i, i, vp]
-        for n in ("rx_emb_gather", "rx_emb_sgd", "rx_dot_interaction_fwd", "rx_dot_interaction_bwd"):
+        for n in ("rx_emb_gather", "rx_emb_sgd", "rx_emb_gather_rows", "rx_emb_sgd_rows", "rx_dot_interaction_fwd",
+                  "rx_dot_interaction_bwd"):
             getattr(L, n).restype = i
         _bound = True
     return L
@@ -78,6 +81,34 @@ def dot_interaction(X: torch.Tensor) -> torch.Tensor:
             raise ValueError("HIP dot interaction supports F <= 32 and D in {32, 64, 128}")
         return _DotInteraction.apply(X)
     return dot_interaction_reference(X)
+
+
+def gather_rows(weight: torch.Tensor, offsets: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """``[B, T] ids -> [B, T, D]`` rows ``weight[offsets[t] + idx[b, t]]`` (HIP on GPU)."""
+    B, T = idx.shape
+    D = weight.shape[1]
+    if not weight.is_cuda:
+        return weight[(idx.long() + offsets.view(1, -1)).reshape(-1)].view(B, T, D)
+    idx = idx.contiguous().long()
+    out = torch.empty(B, T, D, dtype=weight.dtype, device=weight.device)
+    if B * T:
+        _hip.check(_lib().rx_emb_gather_rows(_p(weight), _p(offsets), _p(idx), _p(out), B, T, D, weight.shape[0],
+                                             _hip.stream_ptr(weight.device)), "rx_emb_gather_rows")
+    return out
+
+
+def sgd_rows_(weight: torch.Tensor, offsets: torch.Tensor, idx: torch.Tensor, grad_rows: torch.Tensor, lr: float):
+    """In-place sparse SGD ``weight[offsets[t] + idx[b, t]] -= lr * grad_rows[b, t]``."""
+    B, T = idx.shape
+    D = weight.shape[1]
+    if not weight.is_cuda:
+        rows = (idx.long() + offsets.view(1, -1)).reshape(-1)
+        weight.data.index_add_(0, rows, grad_rows.reshape(-1, D), alpha=-lr)
+        return
+    if B * T:
+        _hip.check(_lib().rx_emb_sgd_rows(_p(weight), _p(offsets), _p(idx.contiguous().long()),
+                                          _p(grad_rows.contiguous()), B, T, D, ctypes.c_float(lr), weight.shape[0],
+                                          _hip.stream_ptr(weight.device)), "rx_emb_sgd_rows")
 
 
 class _EmbedConcat(torch.autograd.Function):

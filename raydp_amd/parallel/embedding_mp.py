@@ -46,21 +46,27 @@ class _ShardedLookup(torch.autograd.Function):
         B, T = idx.shape
         D = weight.shape[1]
         dev = weight.device
-        # batch sizes of every rank (ranks may hold different local batch sizes)
-        bs = torch.tensor([B], device=dev)
-        all_b = [torch.zeros_like(bs) for _ in range(world)]
-        dist.all_gather(all_b, bs, group=group)
-        all_b = [int(x) for x in all_b]
+        # batch sizes of every rank (ranks may hold different local batch sizes, unless the
+        # module was built with static_batch: then every rank's B equals this one's)
+        if mod.static_batch:
+            all_b = [B] * world
+        else:
+            bs = torch.tensor([B], device=dev)
+            all_b = [torch.zeros_like(bs) for _ in range(world)]
+            dist.all_gather(all_b, bs, group=group)
+            all_b = [int(x) for x in all_b]
         # 1) ids to owners: for each destination r, my rows' ids of tables r owns ([B, n_r])
         send = torch.cat([idx[:, mod.tables_of[r]].reshape(-1) for r in range(world)]) if T else idx.reshape(-1)
         in_splits = [B * len(mod.tables_of[r]) for r in range(world)]
         out_splits = [all_b[r] * len(mod.local_tables) for r in range(world)]
         recv = torch.empty(sum(out_splits), dtype=idx.dtype, device=dev)
         _a2a(recv, send, out_splits, in_splits, group)
-        # 2) owner-side gather for every source rank
+        # 2) owner-side gather for every source rank (HIP row gather on the GPU)
         nl = len(mod.local_tables)
-        rows = (recv.view(-1, nl) + mod.local_offsets.view(1, -1)).reshape(-1) if nl else recv
-        emb = weight.index_select(0, rows) if nl else torch.empty(0, D, device=dev, dtype=weight.dtype)
+        from raydp_amd.ops.dlrm_ops import gather_rows
+        lidx = recv.view(-1, nl) if nl else recv.view(0, 0)
+        emb = gather_rows(weight, mod.local_offsets, lidx).view(-1, D) if nl else \
+            torch.empty(0, D, device=dev, dtype=weight.dtype)
         # 3) embeddings back to the requesting ranks
         back = torch.empty(sum(in_splits), D, dtype=weight.dtype, device=dev)
         _a2a(back, emb, [s for s in in_splits], [s for s in out_splits], group)
@@ -71,27 +77,37 @@ class _ShardedLookup(torch.autograd.Function):
             if n:
                 out[:, mod.tables_of[r]] = back[off:off + B * n].view(B, n, D)
             off += B * n
-        ctx.save_for_backward(rows)
+        ctx.save_for_backward(lidx, weight)
         ctx.meta = (mod, B, T, D, in_splits, out_splits, weight.shape)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        (rows,) = ctx.saved_tensors
+        lidx, weight = ctx.saved_tensors
         mod, B, T, D, in_splits, out_splits, wshape = ctx.meta
         send = torch.cat([g[:, mod.tables_of[r]].reshape(-1, D) for r in range(mod.world)]) if T else g.reshape(-1, D)
         recv = torch.empty(sum(out_splits), D, dtype=g.dtype, device=g.device)
         _a2a(recv, send, out_splits, in_splits, mod.group)
-        grad = torch.sparse_coo_tensor(rows.unsqueeze(0), recv, wshape) if len(mod.local_tables) else None
-        return grad, None, None
+        nl = len(mod.local_tables)
+        if not nl:
+            return None, None, None
+        if mod.fused_sgd_lr is not None:
+            # apply the rows straight into the owner's tables (no sparse tensor, no optimizer pass)
+            from raydp_amd.ops.dlrm_ops import sgd_rows_
+            sgd_rows_(weight, mod.local_offsets, lidx, recv.view(-1, nl, D), mod.fused_sgd_lr)
+            return None, None, None
+        rows = (lidx + mod.local_offsets.view(1, -1)).reshape(-1)
+        return torch.sparse_coo_tensor(rows.unsqueeze(0), recv, wshape), None, None
 
 
 class ShardedEmbeddings(nn.Module):
     """Drop-in for :class:`raydp_amd.ops.dlrm_ops.FusedEmbeddings` across a process group."""
 
     def __init__(self, table_sizes: Sequence[int], dim: int, group=None, owners: Optional[List[int]] = None,
-                 seed: int = 0):
+                 seed: int = 0, fused_sgd_lr: Optional[float] = None, static_batch: bool = False):
         super().__init__()
+        self.fused_sgd_lr = fused_sgd_lr   # apply SGD to the local tables inside backward
+        self.static_batch = static_batch   # every rank always uses the same local batch size
         import math
         self.group = group
         self.world = dist.get_world_size(group)
@@ -108,6 +124,8 @@ class ShardedEmbeddings(nn.Module):
         self.register_buffer("local_offsets", torch.tensor(offs[:len(local_sizes)], dtype=torch.int64))
         self.weight = nn.Parameter(torch.empty(max(1, sum(local_sizes)), dim))
         self.weight._raydp_model_parallel = True   # owned by this rank only: DDP leaves it alone
+        # with fused_sgd_lr the weight still requires grad (so backward runs the reverse
+        # all-to-all) but its .grad stays None: optimizers skip it
         self._raydp_model_parallel = True          # ... and every buffer of this module (offsets)
         with torch.no_grad():
             for t, o in zip(self.local_tables, offs):

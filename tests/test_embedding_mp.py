@@ -151,3 +151,38 @@ def test_dlrm_model_parallel_trains_with_ddp():
         p.join(timeout=30)
     assert all(r[1] and r[2] for r in res), res
     assert sorted(t for r in res for t in r[3]) == [0, 1, 2, 3]
+
+
+def _fused_rank(rank, world, port, q):
+    import torch.distributed as dist
+    from raydp_amd.parallel.embedding_mp import ShardedEmbeddings
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        B = 5
+        g = torch.Generator().manual_seed(300 + rank)
+        idx = torch.stack([torch.randint(0, s, (B,), generator=g) for s in SIZES], 1)
+        mlp = torch.randn(B, D, generator=g)
+        coef = torch.randn(B, len(SIZES) + 1, D, generator=g)
+        a = ShardedEmbeddings(SIZES, D, static_batch=True)
+        b = ShardedEmbeddings(SIZES, D, fused_sgd_lr=0.5, static_batch=True)
+        (a(mlp, idx) * coef).sum().backward()
+        with torch.no_grad():
+            if a.weight.grad is not None:
+                a.weight.add_(a.weight.grad.coalesce().to_dense(), alpha=-0.5)
+        (b(mlp, idx) * coef).sum().backward()
+        q.put((rank, b.weight.grad is None, bool(torch.allclose(a.weight, b.weight, atol=1e-6))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_fused_sgd_equals_sparse_sgd():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_fused_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+    assert all(r[1] and r[2] for r in res), res
