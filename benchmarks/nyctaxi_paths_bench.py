@@ -64,9 +64,13 @@ def main():
         xg = _xgmi_for(tr) if world > 1 else None
 
         def run(k):
-            nr = k * args.batch
-            tr.train_epoch(feats[:nr], y[:nr], nr, None, world_size=world, xg=xg,
-                           allreduce=(lambda gr: dist.all_reduce(gr)) if world > 1 and xg is None else None)
+            # epochs over the resident 256 batches (the kernel reads rows [0, nr) only)
+            while k > 0:
+                nb = min(k, n // args.batch)
+                nr = nb * args.batch
+                tr.train_epoch(feats, y, nr, None, world_size=world, xg=xg,
+                               allreduce=(lambda gr: dist.all_reduce(gr)) if world > 1 and xg is None else None)
+                k -= nb
         run(args.warmup)
         kind = "fused step + " + ("xgmi_oneshot" if xg is not None else "allreduce" if world > 1 else "none")
     else:

@@ -25,6 +25,28 @@
 #pragma once
 #include "rx_common.h"
 
+// timing experiments only (raydp_amd/ops/mlp_jit.py RAYDP_MLP_EXPERIMENT): drop a store class
+#ifdef RX_EXP_NOSCRATCH
+constexpr bool kExpNoScratch = true;
+#else
+constexpr bool kExpNoScratch = false;
+#endif
+#ifdef RX_EXP_SCRATCHWT
+constexpr bool kExpScratchWt = true;
+#else
+constexpr bool kExpScratchWt = false;
+#endif
+#ifdef RX_EXP_WTSTORE
+constexpr bool kWtStores = true;   // measured: no gain over plain 16-B stores here
+#else
+constexpr bool kWtStores = false;
+#endif
+#ifdef RX_EXP_NOWGRAD
+constexpr bool kExpNoWgrad = true;
+#else
+constexpr bool kExpNoWgrad = false;
+#endif
+
 #define RX_MAXL 8
 #define RX_NW 8          // waves per workgroup
 #define RX_THREADS (RX_NW * RX_WAVE)
@@ -122,6 +144,54 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restric
   }
 }
 
+// The first PK k-steps of a tile's weight fragments, fetched ahead of time (before the work
+// that precedes the GEMM) so their global round trip overlaps that work.
+constexpr int RX_PJ = 2;  // tiles per wave prefetched
+constexpr int RX_PK = 4;  // k-steps per tile prefetched
+__device__ __forceinline__ void gemm_prefetch(bf16x8 (&pre)[RX_PK], const RX_GLOBAL u16* __restrict__ Brow, int K,
+                                              int lg) {
+  const int nks = K >> 5;
+#pragma unroll
+  for (int s = 0; s < RX_PK; ++s) {
+    const int ks = min(s, nks - 1);
+    pre[s] = *reinterpret_cast<const RX_GLOBAL bf16x8*>(Brow + ks * 32 + 8 * lg);
+  }
+}
+
+// Head of this wave's forward weight tiles of layer `ly` (W_l rows, K = in_k).
+template <class LY>
+__device__ __forceinline__ void fwd_prefetch(const LY& ly, const u16* __restrict__ img, bf16x8 (&wpre)[RX_PJ][RX_PK]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int ntiles = ly.out_n >> 4;
+#pragma unroll
+  for (int j = 0; j < RX_PJ; ++j)
+    if (j * RX_NW < ntiles) {
+      const int n = min(wave + j * RX_NW, ntiles - 1);
+      gemm_prefetch(wpre[j], rx_g(img) + ly.w_img + (n * 16 + lr) * ly.in_k, ly.in_k, lg);
+    }
+}
+
+template <int MT>
+__device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
+                                              const RX_GLOBAL u16* __restrict__ Brow, int K, int lg,
+                                              const bf16x8 (&pre)[RX_PK]) {
+  const int nks = K >> 5;
+#pragma unroll
+  for (int s = 0; s < RX_PK; ++s) {
+    if (s < nks) {
+      const int k0 = s * 32 + 8 * lg;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Arow + mt * 16 * RS + k0);
+        acc[mt] = rx_mfma16(a, pre[s], acc[mt]);
+      }
+    }
+  }
+  if (nks > RX_PK)
+    gemm_tile<MT>(acc, Arow + RX_PK * 32, RS, Brow + RX_PK * 32, K - RX_PK * 32, lg);
+}
+
 // ------------------------------------------------------------------------------------------
 // forward of layer l for the rows of this workgroup. Leaves y (the layer output after
 // act/BN) in R (row-major) and in XT_{l+1}; for the last layer computes loss, metrics and
@@ -132,7 +202,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
                                               const u16* __restrict__ img, const float* __restrict__ P,
                               float* __restrict__ Gr, const float* __restrict__ labels,
                               const int* __restrict__ rowidx, int nvalid, float* __restrict__ scratch,
-                              double* __restrict__ metrics) {
+                              double* __restrict__ metrics, bf16x8 (&wpre)[RX_PJ][RX_PK]) {
   using T = Tile<MT>;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lr = lane & 15, lg = lane >> 4;
@@ -149,10 +219,18 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int n = wave + j * RX_NW;
-    if (n < ntiles) gemm_tile<MT>(part, R + lr * RS, RS, rx_g(img) + ly.w_img + (n * 16 + lr) * ly.in_k, ly.in_k, lg);
+    if (n < ntiles) {
+      const RX_GLOBAL u16* Brow = rx_g(img) + ly.w_img + (n * 16 + lr) * ly.in_k;
+      if (j < RX_PJ)
+        gemm_tile_pre<MT>(part, R + lr * RS, RS, Brow, ly.in_k, lg, wpre[j < RX_PJ ? j : 0]);
+      else
+        gemm_tile<MT>(part, R + lr * RS, RS, Brow, ly.in_k, lg);
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
+  // the next layer's weight head travels while this layer's epilogue runs
+  if (!last) fwd_prefetch(nx, img, wpre);
 
   // ---- epilogue in registers, in place on acc: bias, act, BN, loss ----
 #pragma unroll
@@ -206,7 +284,13 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
           for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              scratch[ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c] = acc[j * MT + mt][r];
+              if (!kExpNoScratch) {
+                float* sp = scratch + ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c;
+                if (kExpScratchWt)
+                  __hip_atomic_store(rx_g(sp), acc[j * MT + mt][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else
+                  *sp = acc[j * MT + mt][r];
+              }
         } else {
           mean = colok ? pr[3 * ly.out_n + c] : 0.f;
           invstd = colok ? rsqrtf(pr[4 * ly.out_n + c] + ly.eps) : 0.f;
@@ -346,31 +430,109 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
   const u16* XT = reinterpret_cast<const u16*>(smem + ly.xt_off);
   float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
 
+  // ---- prefetch what the dgrad and the post-op backward read from global memory (the head of
+  // every dgrad weight tile of this wave, and the saved forward values of the post-op) so both
+  // round trips overlap the wgrad below instead of following it. Address-clamped, no
+  // per-element branches; tiles past RX_PJ fetch in the dgrad itself.
+  const int ntiles_d = ly.in_n >> 4;
+  bf16x8 wpre[RX_PJ][RX_PK];
+  float svp[RX_PJ][MT * 4];
+  if (l != 0) {
+#pragma unroll
+    for (int j = 0; j < RX_PJ; ++j) {
+      if (j * RX_NW < ntiles_d) {
+        const int n = min(wave + j * RX_NW, ntiles_d - 1);
+        gemm_prefetch(wpre[j], rx_g(img) + ly.wt_img + (n * 16 + lr) * ly.out_k, ly.out_k, lg);
+        const RX_GLOBAL float* sp = rx_g(scratch) + pv.r_off + n * 16 + lr;
+#pragma unroll
+        for (int q = 0; q < MT * 4; ++q) svp[j][q] = sp[((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n];
+      }
+    }
+  }
+
   // ---- wgrad, computed transposed: dW^T[i][o] = sum_b X[b][i] G[b][o]  (A = XT, B = GT) ----
   // each lane then holds 4 consecutive i of one o = 16 contiguous bytes of dW[o][:] ->
-  // one dwordx4 store instead of four dword stores (the step is store-queue bound here)
+  // one dwordx4 store instead of four dword stores (the step is store-queue bound here).
+  // Register blocking: a wave owns whole rows (or columns) of the tile grid and keeps that
+  // side's fragments in registers while it streams the other side, so every XT / GT fragment
+  // leaves LDS once per wave instead of once per tile (LDS bandwidth bound otherwise).
   {
     const int mo_tiles = ly.out_n >> 4, ni_tiles = ly.in_n >> 4;
-    const int ntile = mo_tiles * ni_tiles;
     const bool vec = ((ly.w_off | ly.in) & 3) == 0;
-    for (int t = wave; t < ntile; t += RX_NW) {
-      const int mo = t / ni_tiles, ni = t % ni_tiles;
-      f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k0 = 0; k0 < T::BP; k0 += 32) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(XT + (ni * 16 + lr) * XS + k0 + 8 * lg);
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(GT + (mo * 16 + lr) * XS + k0 + 8 * lg);
-        a4 = rx_mfma16(a, b, a4);
-      }
+    constexpr int KS = T::BP / 32;
+    constexpr int NB = 4;  // tiles of the cached side per wave (larger grids loop)
+    auto store = [&](int mo, int ni, const f32x4& a4) {
       const int o = mo * 16 + lr, i0 = ni * 16 + lg * 4;
       if (o < ly.out) {
         float* dst = Gr + ly.w_off + o * ly.in + i0;
         if (vec && i0 + 3 < ly.in) {
-          *reinterpret_cast<f32x4*>(dst) = a4;
+          if (!kExpNoWgrad) {
+            if (kWtStores)
+              rx_store16_wt(Gr, (ly.w_off + o * ly.in + i0) * 4, a4);
+            else
+              *reinterpret_cast<f32x4*>(dst) = a4;
+          }
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (i0 + r < ly.in) dst[r] = a4[r];
+        }
+      }
+    };
+    if (ni_tiles >= mo_tiles) {
+      // waves own ni tiles (XT rows cached), GT streamed once per block of NB tiles
+      for (int nb0 = wave; nb0 < ni_tiles; nb0 += RX_NW * NB) {
+        bf16x8 xa[NB][KS];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          const int ni = min(nb0 + q * RX_NW, ni_tiles - 1);
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            xa[q][ks] = *reinterpret_cast<const bf16x8*>(XT + (ni * 16 + lr) * XS + ks * 32 + 8 * lg);
+        }
+        for (int mo = 0; mo < mo_tiles; ++mo) {
+          bf16x8 gb[KS];
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            gb[ks] = *reinterpret_cast<const bf16x8*>(GT + (mo * 16 + lr) * XS + ks * 32 + 8 * lg);
+#pragma unroll
+          for (int q = 0; q < NB; ++q) {
+            const int ni = nb0 + q * RX_NW;
+            if (ni < ni_tiles) {
+              f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int ks = 0; ks < KS; ++ks) a4 = rx_mfma16(xa[q][ks], gb[ks], a4);
+              store(mo, ni, a4);
+            }
+          }
+        }
+      }
+    } else {
+      // waves own mo tiles (GT rows cached), XT streamed
+      for (int mb0 = wave; mb0 < mo_tiles; mb0 += RX_NW * NB) {
+        bf16x8 gb[NB][KS];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          const int mo = min(mb0 + q * RX_NW, mo_tiles - 1);
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            gb[q][ks] = *reinterpret_cast<const bf16x8*>(GT + (mo * 16 + lr) * XS + ks * 32 + 8 * lg);
+        }
+        for (int ni = 0; ni < ni_tiles; ++ni) {
+          bf16x8 xa[KS];
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            xa[ks] = *reinterpret_cast<const bf16x8*>(XT + (ni * 16 + lr) * XS + ks * 32 + 8 * lg);
+#pragma unroll
+          for (int q = 0; q < NB; ++q) {
+            const int mo = mb0 + q * RX_NW;
+            if (mo < mo_tiles) {
+              f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int ks = 0; ks < KS; ++ks) a4 = rx_mfma16(xa[ks], gb[q][ks], a4);
+              store(mo, ni, a4);
+            }
+          }
         }
       }
     }
@@ -388,7 +550,13 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int n = wave + j * RX_NW;
-    if (n < ntiles) gemm_tile<MT>(part, R + lr * RS, RS, rx_g(img) + ly.wt_img + (n * 16 + lr) * ly.out_k, ly.out_k, lg);
+    if (n < ntiles) {
+      const RX_GLOBAL u16* Brow = rx_g(img) + ly.wt_img + (n * 16 + lr) * ly.out_k;
+      if (j < RX_PJ)
+        gemm_tile_pre<MT>(part, R + lr * RS, RS, Brow, ly.out_k, lg, wpre[j < RX_PJ ? j : 0]);
+      else
+        gemm_tile<MT>(part, R + lr * RS, RS, Brow, ly.out_k, lg);
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
@@ -408,8 +576,13 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     // branch is waited for on its own -> one dependent L2 round trip per element).
     const RX_GLOBAL float* sp = rx_g(scratch) + pv.r_off + c;
     float sv[MT * 4], g[MT * 4];
+    if (j < RX_PJ) {
 #pragma unroll
-    for (int q = 0; q < MT * 4; ++q) sv[q] = sp[((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n];
+      for (int q = 0; q < MT * 4; ++q) sv[q] = svp[j < RX_PJ ? j : 0][q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < MT * 4; ++q) sv[q] = sp[((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n];
+    }
 #pragma unroll
     for (int q = 0; q < MT * 4; ++q) {
       const int row = (q >> 2) * 16 + lg * 4 + (q & 3);
@@ -579,6 +752,8 @@ __device__ __forceinline__ void mlp_train_step_body(
     ++si;                                                                 \
   } while (0)
   RX_STAMP();
+  bf16x8 wpre[RX_PJ][RX_PK];
+  fwd_prefetch(C::first(d), img, wpre);
   for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS)
     rowidx[i] = i < nvalid ? (perm ? rx_g(perm)[row0 + i] : row0 + i) : (perm ? rx_g(perm)[row0] : row0);
   load_params<C>(d, smem, P, rstats);
@@ -586,7 +761,7 @@ __device__ __forceinline__ void mlp_train_step_body(
   load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, true);
   RX_STAMP();
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
-    layer_forward<MT, true>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics);
+    layer_forward<MT, true>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre);
     RX_STAMP();
   });
   store_running_stats<C>(d, smem, rstats);
@@ -611,7 +786,10 @@ __device__ __forceinline__ void mlp_eval_body(const MlpDesc* __restrict__ dp, co
   load_params<C>(d, smem, P, rstats);
   __syncthreads();
   load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, false);
+  bf16x8 wpre[RX_PJ][RX_PK];
+  fwd_prefetch(C::first(d), img, wpre);
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
-    layer_forward<MT, false>(d, ly, nx, last, smem, img, P, nullptr, labels, rowidx, nvalid, nullptr, metrics);
+    layer_forward<MT, false>(d, ly, nx, last, smem, img, P, nullptr, labels, rowidx, nvalid, nullptr, metrics,
+                             wpre);
   });
 }

@@ -47,6 +47,14 @@ __device__ __forceinline__ f32x4 rx_mfma16(const bf16x8& a, const bf16x8& b, con
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// 16-B write-through (sc1) store through a buffer descriptor: tens of KB published by one
+// workgroup drain far faster write-through than as plain write-back stores
+// (MI355X_MICROARCH.md "publish-large"). `base` must be wave-uniform.
+__device__ __forceinline__ void rx_store16_wt(float* base, int byte_off, const f32x4& v) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7ffffff0, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, byte_off, 0, 16);
+}
+
 #define RX_CHECK(x)                                                     \
   do {                                                                  \
     hipError_t e_ = (x);                                                \

@@ -285,6 +285,7 @@ class FusedMLPTrainer:
         :class:`raydp_amd.ops.comm.XgmiComm`) instead fuses a one-shot xGMI all-reduce into the
         optimizer kernel. ``max_steps`` caps the step count (ranks agree on it so every
         collective is matched)."""
+        self._check_operands(feats, labels, n_rows, perm)
         nsteps = n_rows // self.batch if drop_last else -(-n_rows // self.batch)
         if max_steps is not None:
             nsteps = min(nsteps, int(max_steps))
@@ -340,9 +341,28 @@ class FusedMLPTrainer:
             xg.check()
         return out
 
+    def _check_operands(self, feats, labels, n_rows, perm=None):
+        """Host-side guard: the kernels index rows [0, n_rows) of feats / labels (through perm)
+        without bounds checks, so a mismatch must never reach the GPU."""
+        def here(t):
+            return t.device.type == self.device.type and (self.device.index is None or t.device.index is None
+                                                          or t.device.index == self.device.index)
+        if not here(feats) or not here(labels):
+            raise ValueError("features / labels must live on the trainer's device")
+        if feats.dtype != torch.bfloat16 or feats.dim() != 2 or feats.shape[1] != self.feat_k or \
+                not feats.is_contiguous():
+            raise ValueError(f"features must be a contiguous bf16 [rows, {self.feat_k}] matrix")
+        if labels.dtype != torch.float32 or not labels.is_contiguous() or labels.numel() < n_rows * self.desc.out_dim:
+            raise ValueError("labels must be contiguous fp32 with n_rows * out_dim elements")
+        if n_rows < 0 or feats.shape[0] < n_rows:
+            raise ValueError(f"n_rows={n_rows} exceeds the {feats.shape[0]} feature rows")
+        if perm is not None and (perm.dtype != torch.int32 or perm.numel() < n_rows or not here(perm)):
+            raise ValueError("perm must be an int32 permutation of n_rows on the trainer's device")
+
     def forward_backward(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int,
                          perm: Optional[torch.Tensor] = None, step: int = 0) -> torch.Tensor:
         """One fused fwd/bwd (no optimizer) — returns the flat fp32 gradient (for tests)."""
+        self._check_operands(feats, labels, n_rows, perm)
         pp = ctypes.c_void_p
         self.metrics.zero_()
         rc = self.lib.rx_mlp_fwdbwd(
@@ -362,6 +382,7 @@ class FusedMLPTrainer:
         return out
 
     def evaluate(self, feats: torch.Tensor, labels: torch.Tensor, n_rows: int) -> Dict[str, float]:
+        self._check_operands(feats, labels, n_rows)
         self.metrics.zero_()
         pp = ctypes.c_void_p
         rc = self.lib.rx_mlp_eval(ctypes.byref(self.desc), ctypes.byref(self.bufs), self.mt,

@@ -65,6 +65,8 @@ def _sink():
     if not p:
         return None
     if _file is None or _file_pid != os.getpid():
+        d = os.path.dirname(os.path.abspath(p))
+        os.makedirs(d, exist_ok=True)
         _file = open(f"{p}.{os.getpid()}.jsonl", "a", buffering=1)
         _file_pid = os.getpid()
     return _file

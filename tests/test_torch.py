@@ -68,3 +68,22 @@ def test_torch_estimator_sequential(spark_on_ray_small):
 
 
 _ = (os, shutil)
+
+
+def test_fused_trainer_rejects_mismatched_operands_on_host():
+    """The fused kernels index rows without bounds checks: shape errors must stop on the host."""
+    import torch.nn as nn
+    from raydp_amd.models.mlp_spec import extract_mlp_spec
+    from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+    m = nn.Sequential(nn.Linear(4, 8), nn.ReLU(), nn.Linear(8, 1))
+    tr = FusedMLPTrainer(extract_mlp_spec(m), optimizer_config(torch.optim.Adam(m.parameters())),
+                         loss_code(nn.MSELoss()), 16, "cpu", layout_only=True)
+    feats = torch.zeros(32, tr.feat_k, dtype=torch.bfloat16)
+    labels = torch.zeros(32, 1)
+    tr._check_operands(feats, labels, 32)
+    with pytest.raises(ValueError):
+        tr._check_operands(feats, labels, 64)          # more rows than the matrix holds
+    with pytest.raises(ValueError):
+        tr._check_operands(feats.float(), labels, 32)  # wrong dtype
+    with pytest.raises(ValueError):
+        tr._check_operands(feats, labels, 32, perm=torch.arange(16, dtype=torch.int32))
