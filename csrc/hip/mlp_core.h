@@ -31,11 +31,25 @@ constexpr bool kExpNoScratch = true;
 #else
 constexpr bool kExpNoScratch = false;
 #endif
-#ifdef RX_EXP_SCRATCHWT
-constexpr bool kExpScratchWt = true;
+// Saved forward values (BN inputs / ReLU mask sources) stay fp32: a bf16 copy halves their
+// bytes but the BN gamma/beta gradients cancel to near zero for some channels, and Adam turns
+// their rounding error into sign flips of the update (measured: 12 % parameter error).
+#ifdef RX_EXP_SCRATCH16
+constexpr bool kScratchBf16 = true;
 #else
-constexpr bool kExpScratchWt = false;
+constexpr bool kScratchBf16 = false;
 #endif
+__device__ __forceinline__ void save_val(float* scratch, int idx, float v) {
+  if (kScratchBf16)
+    reinterpret_cast<u16*>(scratch)[idx] = rx_f2bf(v);
+  else
+    scratch[idx] = v;
+}
+__device__ __forceinline__ float load_val(const float* scratch, int idx) {
+  if (kScratchBf16) return rx_bf2f(rx_g(reinterpret_cast<const u16*>(scratch))[idx]);
+  return rx_g(scratch)[idx];
+}
+
 #ifdef RX_EXP_WTSTORE
 constexpr bool kWtStores = true;   // measured: no gain over plain 16-B stores here
 #else
@@ -67,6 +81,8 @@ struct MlpLayer {
   int stat_off;      // float offset of (mean, invstd) pairs for this layer's outputs in LDS
   int r_off;         // float offset of the saved pre-BN values in the scratch buffer
   int pr_off;        // float offset of [bias|gamma|beta|run_mean|run_var] (x out_n) in LDS
+  int xg_off;        // wgrad_mode 1: bf16 offset of X^T_l [in_n][BP] in the exported activation area
+  int gg_off;        //               bf16 offset of G^T_l [out_n][BP]
 };
 
 struct MlpDesc {
@@ -80,6 +96,9 @@ struct MlpDesc {
   MlpLayer layer[RX_MAXL];
   int pr_lds_off;    // LDS byte offset of the per-column parameter block
   int pr_total;      // floats in that block
+  int act_off;       // float offset (in the gradient buffer) of the exported activation area
+  int wgrad_mode;    // 0: weight gradients computed and stored here; 1: X^T / G^T exported and
+                     //    the optimizer kernel computes dW = X^T G on its own workgroups
 };
 
 // run-time descriptor: loops over layers are ordinary loops
@@ -172,6 +191,19 @@ __device__ __forceinline__ void fwd_prefetch(const LY& ly, const u16* __restrict
     }
 }
 
+// Copy `rows` rows of a transposed bf16 LDS matrix (row stride XS) to global memory packed
+// [rows][BP]: whole 128-B (BP = 64) rows, 16 B per lane. The optimizer kernel computes the
+// weight gradients from these (wgrad_mode 1), so the step kernel's critical chain neither runs
+// the wgrad GEMMs nor stores 4 B of fp32 gradient per weight.
+template <int MT>
+__device__ __forceinline__ void export_rows(const u16* lds, int rows, u16* __restrict__ glob) {
+  constexpr int BP = Tile<MT>::BP, XS = Tile<MT>::XS, CH = BP / 8;
+  for (int idx = threadIdx.x; idx < rows * CH; idx += RX_THREADS) {
+    const int r = idx / CH, c = idx % CH;
+    *reinterpret_cast<RX_GLOBAL u32x4*>(rx_g(glob) + r * BP + c * 8) = *reinterpret_cast<const u32x4*>(lds + r * XS + c * 8);
+  }
+}
+
 template <int MT>
 __device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
                                               const RX_GLOBAL u16* __restrict__ Brow, int K, int lg,
@@ -211,6 +243,9 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   u16* GT = reinterpret_cast<u16*>(smem + d.gt_lds_off);
   float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
   const int ntiles = ly.out_n >> 4;
+  if (TRAIN && d.wgrad_mode == 1)  // X^T_l (published by the previous layer / the input load)
+    export_rows<MT>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n,
+                    reinterpret_cast<u16*>(Gr + d.act_off) + ly.xg_off);
 
   f32x4 acc[T::NTW * MT];
 #pragma unroll
@@ -284,13 +319,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
           for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              if (!kExpNoScratch) {
-                float* sp = scratch + ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c;
-                if (kExpScratchWt)
-                  __hip_atomic_store(rx_g(sp), acc[j * MT + mt][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else
-                  *sp = acc[j * MT + mt][r];
-              }
+              if (!kExpNoScratch) save_val(scratch, ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c, acc[j * MT + mt][r]);
         } else {
           mean = colok ? pr[3 * ly.out_n + c] : 0.f;
           invstd = colok ? rsqrtf(pr[4 * ly.out_n + c] + ly.eps) : 0.f;
@@ -311,7 +340,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            scratch[ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c] = colok ? acc[j * MT + mt][r] : 0.f;
+            save_val(scratch, ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c, colok ? acc[j * MT + mt][r] : 0.f);
       }
       // padded rows / columns carry exact zeros through every GEMM
 #pragma unroll
@@ -443,13 +472,17 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       if (j * RX_NW < ntiles_d) {
         const int n = min(wave + j * RX_NW, ntiles_d - 1);
         gemm_prefetch(wpre[j], rx_g(img) + ly.wt_img + (n * 16 + lr) * ly.out_k, ly.out_k, lg);
-        const RX_GLOBAL float* sp = rx_g(scratch) + pv.r_off + n * 16 + lr;
+        const int sp = pv.r_off + n * 16 + lr;
 #pragma unroll
-        for (int q = 0; q < MT * 4; ++q) svp[j][q] = sp[((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n];
+        for (int q = 0; q < MT * 4; ++q) svp[j][q] = load_val(scratch, sp + ((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n);
       }
     }
   }
 
+  if (d.wgrad_mode == 1) {
+    // G^T_l leaves for the optimizer kernel's wgrad (GT is overwritten with G_{l-1} below)
+    export_rows<MT>(GT, ly.out_n, reinterpret_cast<u16*>(Gr + d.act_off) + ly.gg_off);
+  } else
   // ---- wgrad, computed transposed: dW^T[i][o] = sum_b X[b][i] G[b][o]  (A = XT, B = GT) ----
   // each lane then holds 4 consecutive i of one o = 16 contiguous bytes of dW[o][:] ->
   // one dwordx4 store instead of four dword stores (the step is store-queue bound here).
@@ -574,14 +607,14 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     // The forward saved this layer's BN input / activation (fp32) for every padded row and
     // column: issue all loads back to back, unconditionally (a load under a per-element
     // branch is waited for on its own -> one dependent L2 round trip per element).
-    const RX_GLOBAL float* sp = rx_g(scratch) + pv.r_off + c;
+    const int sp = pv.r_off + c;
     float sv[MT * 4], g[MT * 4];
     if (j < RX_PJ) {
 #pragma unroll
       for (int q = 0; q < MT * 4; ++q) sv[q] = svp[j < RX_PJ ? j : 0][q];
     } else {
 #pragma unroll
-      for (int q = 0; q < MT * 4; ++q) sv[q] = sp[((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n];
+      for (int q = 0; q < MT * 4; ++q) sv[q] = load_val(scratch, sp + ((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n);
     }
 #pragma unroll
     for (int q = 0; q < MT * 4; ++q) {

@@ -25,7 +25,7 @@ class MlpLayer(ctypes.Structure):
         ("rs_off", ctypes.c_int), ("pad_", ctypes.c_int),
         ("eps", ctypes.c_float), ("momentum", ctypes.c_float),
         ("xt_off", ctypes.c_int), ("stat_off", ctypes.c_int), ("r_off", ctypes.c_int),
-        ("pr_off", ctypes.c_int),
+        ("pr_off", ctypes.c_int), ("xg_off", ctypes.c_int), ("gg_off", ctypes.c_int),
     ]
 
 
@@ -39,6 +39,7 @@ class MlpDesc(ctypes.Structure):
         ("out_dim", ctypes.c_int), ("feat_k", ctypes.c_int),
         ("layer", MlpLayer * MAXL),
         ("pr_lds_off", ctypes.c_int), ("pr_total", ctypes.c_int),
+        ("act_off", ctypes.c_int), ("wgrad_mode", ctypes.c_int),
     ]
 
 
@@ -52,6 +53,7 @@ class OptSeg(ctypes.Structure):
     _fields_ = [
         ("start", ctypes.c_int), ("len", ctypes.c_int), ("kind", ctypes.c_int),
         ("out", ctypes.c_int), ("in_", ctypes.c_int), ("in_k", ctypes.c_int), ("out_k", ctypes.c_int),
+        ("in_n", ctypes.c_int), ("out_n", ctypes.c_int), ("xg_off", ctypes.c_int), ("gg_off", ctypes.c_int),
         ("W", ctypes.c_void_p), ("Wt", ctypes.c_void_p),
     ]
 
@@ -63,6 +65,8 @@ class OptDesc(ctypes.Structure):
         ("wd", ctypes.c_float), ("momentum", ctypes.c_float), ("dampening", ctypes.c_float),
         ("nesterov", ctypes.c_int), ("maximize", ctypes.c_int),
         ("seg", OptSeg * MAXSEG),
+        ("act_off", ctypes.c_int), ("act_floats", ctypes.c_int), ("bp", ctypes.c_int),
+        ("wgrad_mode", ctypes.c_int),
     ]
 
 
@@ -103,6 +107,7 @@ def lib():
                                      vp, vp, vp]
     L.rx_mlp_fwdbwd.argtypes = [vp, vp, i, vp, vp, vp, i, i, i, vp]
     L.rx_opt_step.argtypes = [vp, vp, vp, vp, vp, vp, f, f, f, f, i, vp]
+    L.rx_mlp_wgrad.argtypes = [vp, vp, vp, vp]
     L.rx_mlp_eval.argtypes = [vp, vp, i, vp, vp, i, i, vp]
     L.rx_jit_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(vp), i]
     L.rx_jit_load.restype = i

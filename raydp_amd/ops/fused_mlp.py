@@ -67,6 +67,14 @@ def jit_enabled() -> bool:
     return bool(conf_get("spark.ray.mi355x.mlp_jit"))
 
 
+def wgrad_mode() -> int:
+    """Where weight gradients are computed (``spark.ray.mi355x.mlp_wgrad``): ``opt`` (default,
+    1): the step kernel exports X^T / G^T and the optimizer kernel's many workgroups compute
+    dW = X^T G as they update; ``step`` (0): inside the single-workgroup step kernel."""
+    from raydp_amd.utils.config import get as conf_get
+    return 1 if conf_get("spark.ray.mi355x.mlp_wgrad") == "opt" else 0
+
+
 def pick_mt(batch: int) -> Optional[int]:
     for mt in (2, 4, 8):
         if batch <= mt * 16:
@@ -135,6 +143,8 @@ class FusedMLPTrainer:
         pr_total = 0
         nseg = 0
         seg_images = []
+        act = 0           # bf16 elements of the exported X^T_l / G^T_l area (wgrad_mode 1)
+        wmode = wgrad_mode()
 
         def vseg(start, n):
             # bias / BN gamma+beta vectors: plain element-wise optimizer segments
@@ -165,6 +175,11 @@ class FusedMLPTrainer:
             seg = o.seg[nseg]
             seg.start, seg.len, seg.kind = off, oo * i, 1
             seg.out, seg.in_, seg.in_k, seg.out_k = oo, i, in_k, out_k
+            x.xg_off = seg.xg_off = act
+            act += in_n * bp
+            x.gg_off = seg.gg_off = act
+            act += out_n * bp
+            seg.in_n, seg.out_n = in_n, out_n
             seg_images.append((nseg, x.w_img, x.wt_img))
             nseg += 1
             self.layout.append(("weight", lin, off, oo * i))
@@ -217,8 +232,14 @@ class FusedMLPTrainer:
         self.desc = d
         self.feat_k = d.feat_k
         total = off
+        # gradient buffer = [flat gradient (total) | exported activation area]; in xGMI mode the
+        # whole buffer is the exchange slot, so peers read each other's X^T / G^T from it
+        act_off = _ru(total, 4)
+        act_floats = _ru((act + 1) // 2, 4)
+        d.act_off, d.wgrad_mode = act_off, wmode
+        self.total = total
         self.params = torch.cat(flat).to(dev).contiguous()
-        self.grads = torch.zeros_like(self.params)
+        self.grads = torch.zeros(act_off + act_floats, dtype=torch.float32, device=dev)
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
         self.scratch = torch.zeros(max(1, scratch_off), dtype=torch.float32, device=dev)
@@ -237,6 +258,7 @@ class FusedMLPTrainer:
         o.b1, o.b2, o.eps = cfg.get("b1", 0.9), cfg.get("b2", 0.999), cfg.get("eps", 1e-8)
         o.wd, o.momentum, o.dampening = cfg.get("wd", 0.0), cfg.get("momentum", 0.0), cfg.get("dampening", 0.0)
         o.nesterov, o.maximize = int(cfg.get("nesterov", False)), int(cfg.get("maximize", False))
+        o.act_off, o.act_floats, o.bp, o.wgrad_mode = act_off, act_floats, bp, wmode
         self.opt = o
         self.lds_bytes = lds
         # descriptors live in device memory: the kernels index them with runtime layer ids
@@ -327,7 +349,9 @@ class FusedMLPTrainer:
                     ctypes.byref(self.desc), ctypes.byref(self.bufs), self.mt,
                     pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, s, stream)
                 _hip.check(rc, "rx_mlp_fwdbwd")
-                allreduce(self.grads)
+                _hip.check(self.lib.rx_mlp_wgrad(ctypes.byref(self.opt), self._od, ctypes.byref(self.bufs),
+                                                 stream), "rx_mlp_wgrad")
+                allreduce(self.grads[:self.total])
                 rc = self.lib.rx_opt_step(ctypes.byref(self.opt), self._od, pp(self.params.data_ptr()),
                                           pp(self.grads.data_ptr()), pp(self.m.data_ptr()),
                                           pp(self.v.data_ptr()), ctypes.c_float(lrs[s]),
@@ -371,7 +395,9 @@ class FusedMLPTrainer:
             pp(perm.data_ptr()) if perm is not None else pp(0), n_rows, self.batch, step,
             _hip.stream_ptr(self.device))
         _hip.check(rc, "rx_mlp_fwdbwd")
-        return self.grads
+        _hip.check(self.lib.rx_mlp_wgrad(ctypes.byref(self.opt), self._od, ctypes.byref(self.bufs),
+                                         _hip.stream_ptr(self.device)), "rx_mlp_wgrad")
+        return self.grads[:self.total]
 
     def unflatten(self, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
         """Map a flat vector (params/grads) onto ``{module_param_name: tensor}`` by identity."""

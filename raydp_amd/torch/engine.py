@@ -171,7 +171,8 @@ def _xgmi_for(trainer):
     mode = conf_get("spark.ray.mi355x.allreduce")
     if mode == "rccl" or not torch.cuda.is_available():
         return None
-    xg = XgmiComm.create(trainer.opt.total, timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
+    # the exchange slot is the whole gradient buffer (flat gradient + exported activations)
+    xg = XgmiComm.create(trainer.grads.numel(), timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
     if xg is None and mode == "xgmi":
         raise RuntimeError("spark.ray.mi355x.allreduce=xgmi but the xGMI peer mapping is unavailable")
     return xg

@@ -132,6 +132,10 @@ register("spark.ray.mi355x.hip_graphs", "bool", True, "replay torch training ste
          env="RAYDP_TORCH_GRAPHS")
 register("spark.ray.mi355x.mlp_jit", "bool", True, "per-model specialised fused-MLP code objects",
          env="RAYDP_MLP_JIT")
+register("spark.ray.mi355x.mlp_wgrad", "str", "opt",
+         "fused MLP weight gradients: opt (computed by the optimizer kernel's workgroups from exported "
+         "activations) or step (inside the single-workgroup step kernel)", env="RAYDP_MLP_WGRAD",
+         choices=["opt", "step"])
 register("spark.ray.mi355x.ddp.bucket_mb", "float", 32.0,
          "DDP gradient bucket size (xGMI rings are per-link bound: few large buckets)", env="RAYDP_DDP_BUCKET_MB")
 register("spark.ray.mi355x.object_store_bytes", "bytes", "0",

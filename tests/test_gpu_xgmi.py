@@ -95,7 +95,7 @@ def _fused_main(rank, world, port, q):
             labels = torch.randn(n, 1, generator=g)
             feats, labels = feats.to(dev), labels.to(dev)
             if mode == "xgmi":
-                xg = XgmiComm.create(tr.opt.total, timeout_s=20.0)
+                xg = XgmiComm.create(tr.grads.numel(), timeout_s=20.0)
                 if xg is None:
                     q.put((rank, "create failed", None, None))
                     return
