@@ -176,11 +176,28 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         LAST_TIMINGS["ingest"] = time.perf_counter() - t_load0
         t_train0 = time.perf_counter()
         config.setdefault("_engine_name", engine.name)
+        timed = device.type == "cuda"
         for epoch in range(config["num_epochs"]):
+            if timed:   # device-timed epoch (HIP events; no per-step host sync)
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            t_ep = time.perf_counter()
             with tracing.span("train epoch", cat="train", epoch=epoch):
                 train_res, train_loss = engine.train_epoch()
+            wall = time.perf_counter() - t_ep
+            dev_s = None
+            if timed:
+                ev1.record()
+                ev1.synchronize()
+                dev_s = ev0.elapsed_time(ev1) / 1000.0
+            rows = getattr(getattr(engine, "train", None), "n", None)
+            perf = {}
+            if rows:
+                perf = {"train_samples_per_s": rows / max(wall, 1e-9), "train_epoch_wall_s": wall}
+                if dev_s is not None:
+                    perf["train_epoch_device_s"] = dev_s
             session.report(dict(epoch=epoch, train_res=train_res, train_loss=train_loss,
-                                engine=engine.name, allreduce=getattr(engine, "allreduce_kind", None)))
+                                engine=engine.name, allreduce=getattr(engine, "allreduce_kind", None), **perf))
             if eval_ds is not None:
                 with tracing.span("eval epoch", cat="train", epoch=epoch):
                     eval_res, test_loss = engine.evaluate_epoch()

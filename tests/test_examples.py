@@ -14,6 +14,7 @@ EX = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "
     ("horovod_nyctaxi.py", ["--epochs", "1"], "'epoch': 1"),
     ("xgboost_ray_nyctaxi.py", [], "Final validation rmse"),
     ("raydp-submit.py", [], "Pi is roughly"),
+    ("tensorflow_nyctaxi.py", [], "TensorFlow is not installed"),
     ("test_raydp_submit_pyfiles.py", [], "py-files OK"),
     ("random_nyctaxi.py", ["--num-records", "1000", "--output", "/tmp/raydp_random_nyctaxi.csv"], "wrote 1000 rows"),
 ])

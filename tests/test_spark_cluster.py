@@ -312,3 +312,15 @@ def test_to_spark_tasks_run_where_blocks_live():
     assert sum(c for _, c in ran) == 4000
     raydp.stop_spark()
     cluster.shutdown()
+
+
+def test_fault_inject_helpers(spark_on_ray_2_executors):
+    """raydp_amd.runtime.fault_inject: kill an executor by name, wait for its restart, and the
+    application keeps working (tasks retried, restart registered with a new id)."""
+    from raydp_amd.runtime import fault_inject as FI
+    spark = spark_on_ray_2_executors
+    old = FI.kill_executor("0")
+    new = FI.wait_restarted("raydp-executor-0", old)
+    assert new != old
+    assert spark.range(0, 500, numPartitions=5).count() == 500
+    assert "0" in spark._cluster.restarted_executors().values()

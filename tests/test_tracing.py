@@ -28,7 +28,9 @@ def test_trace_covers_etl_runtime_and_training(monkeypatch):
                              label_column="y", batch_size=64, num_epochs=1)
         # optimizer given as a class: the estimator builds it (reference semantics allow creators)
         est._optimizer = lambda m, cfg: torch.optim.SGD(m.parameters(), lr=1e-4)
-        est.fit_on_spark(df)
+        res = est.fit_on_spark(df)
+        first = res.metrics_history[0]
+        assert first["train_samples_per_s"] > 0 and first["train_epoch_wall_s"] > 0
         raydp_amd.stop_spark()
         runtime.shutdown()
     finally:
