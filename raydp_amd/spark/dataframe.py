@@ -347,7 +347,7 @@ class DataFrame:
                 return 1
 
             def empty(self_):
-                return src.empty()
+                return src.schema.empty_table()
 
             def execute(self_, scheduler):
                 out, have = [], 0

@@ -172,7 +172,7 @@ class MapPlan(Plan):
 
     def empty(self):
         with _PartitionScope(0):
-            return self.fn(self.child.empty(), 0)
+            return self.fn(self.child.schema.empty_table(), 0)
 
 
 class UnionPlan(Plan):
@@ -207,7 +207,7 @@ class UnionPlan(Plan):
         return self._conform(self.plans[k].compute(i - int(offs[k])))
 
     def empty(self):
-        return self.plans[0].empty()
+        return self.plans[0].schema.empty_table()
 
 
 class MaterializedPlan(Plan):
@@ -327,7 +327,7 @@ class RepartitionPlan(WidePlan):
         return self.n
 
     def _empty(self):
-        return self.child.empty()
+        return self.child.schema.empty_table()
 
     def execute(self, scheduler):
         n = self.n
@@ -375,7 +375,7 @@ class CoalescePlan(Plan):
         return concat([self.child.compute(int(j)) for j in self.groups[i]], self.child.schema)
 
     def empty(self):
-        return self.child.empty()
+        return self.child.schema.empty_table()
 
 
 class SortPlan(WidePlan):
@@ -391,7 +391,7 @@ class SortPlan(WidePlan):
         return max(1, self.n_out)
 
     def _empty(self):
-        return self.child.empty()
+        return self.child.schema.empty_table()
 
     def execute(self, scheduler):
         parts = scheduler.map(self.child.compute, range(self.child.num_partitions()))

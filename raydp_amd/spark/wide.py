@@ -64,7 +64,7 @@ class JoinPlan(WidePlan):
         return out
 
     def _empty(self):
-        return self._join(self.left.empty(), self.right.empty())
+        return self._join(self.left.schema.empty_table(), self.right.schema.empty_table())
 
     def execute(self, scheduler):
         rparts = scheduler.map(self.right.compute, range(self.right.num_partitions()))
@@ -153,7 +153,7 @@ class AggregatePlan(WidePlan):
         return self.n
 
     def _empty(self):
-        t = aggregate_table(self.child.empty(), self.keys, self.aggs)
+        t = aggregate_table(self.child.schema.empty_table(), self.keys, self.aggs)
         return t.slice(0, 0)
 
     def execute(self, scheduler):
@@ -179,7 +179,7 @@ class DistinctPlan(WidePlan):
         return self.n
 
     def _empty(self):
-        return self.child.empty()
+        return self.child.schema.empty_table()
 
     def _dedup(self, t: pa.Table) -> pa.Table:
         keys = self.subset or t.column_names
@@ -259,7 +259,7 @@ class WindowPlan(WidePlan):
         return st.append_column(self.out_name, vals)
 
     def _empty(self):
-        return self._apply(self.child.empty())
+        return self._apply(self.child.schema.empty_table())
 
     def execute(self, scheduler):
         keys = self.window.partition_cols
