@@ -190,7 +190,8 @@ def main():
                        "timed_region": "csv read+ETL+from_spark+shuffle+HBM ingest+train+checkpoint",
                        "final_train_loss": res.metrics_history[0].get("train_loss")
                        if res.metrics_history else None,
-                       "rank0_breakdown_s": {k: round(v, 4) for k, v in LAST_TIMINGS.items()}},
+                       "rank0_breakdown_s": dict({k: round(v, 4) for k, v in LAST_TIMINGS.items()},
+                                                 other=round(dt - sum(LAST_TIMINGS.values()), 4))},
         }
         print(json.dumps(out), flush=True)
     context.stop_spark()
