@@ -314,15 +314,19 @@ class FusedMLPTrainer:
         self.metrics.zero_()
         if nsteps == 0:
             return self._read_metrics()
+        import numpy as np
         b1, b2 = self.opt.b1, self.opt.b2
-        lrs = (ctypes.c_float * nsteps)()
-        bc1 = (ctypes.c_float * nsteps)()
-        bc2 = (ctypes.c_float * nsteps)()
-        for s in range(nsteps):
-            t = self.step_count + s + 1
-            lrs[s] = self._lr(self.step_count + s)
-            bc1[s] = 1.0 - b1 ** t
-            bc2[s] = 1.0 - b2 ** t
+        # per-step learning rate and Adam bias corrections, vectorised (a Python loop here costs
+        # ~5 us per step of host time in front of the epoch's first launch)
+        t = np.arange(self.step_count + 1, self.step_count + nsteps + 1, dtype=np.float64)
+        if self.lr_schedule is None:
+            lr_np = np.full(nsteps, float(self.cfg["lr"]), dtype=np.float32)
+        else:
+            lr_np = np.array([self._lr(self.step_count + s) for s in range(nsteps)], dtype=np.float32)
+        bc1_np = (1.0 - np.power(float(b1), t)).astype(np.float32)
+        bc2_np = (1.0 - np.power(float(b2), t)).astype(np.float32)
+        fptr = ctypes.POINTER(ctypes.c_float)
+        lrs, bc1, bc2 = (a.ctypes.data_as(fptr) for a in (lr_np, bc1_np, bc2_np))
         stream = _hip.stream_ptr(self.device)
         pp = ctypes.c_void_p
         perm_p = pp(perm.data_ptr()) if perm is not None else pp(0)

@@ -242,7 +242,13 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                                        placement_strategy=self._placement_strategy)
         run_config = RunConfig(failure_config=FailureConfig(max_failures=max_retries),
                                storage_path=self._extra_config.get("storage_path"))
-        if self._shuffle:
+        # The reference shuffles the dataset once before sharding (torch/estimator.py:335-338).
+        # Both engines here draw a fresh device-side permutation of their whole resident shard
+        # every epoch, so when every worker trains on all of its rows (one worker, or SPMD ranks
+        # with local shards) the host-side pass adds nothing but a copy of the data; it stays
+        # where it decides which rows land on which worker.
+        local_only = self._num_workers == 1 or bool(self._extra_config.get("spmd_local_shards"))
+        if self._shuffle and not local_only:
             seed = self._extra_config.get("shuffle_seed")
             train_ds = train_ds.random_shuffle(seed=seed)
             if evaluate_ds:
