@@ -137,9 +137,19 @@ __device__ __forceinline__ float act_fwd(int act, float z) { return act == 1 ? f
 // (address-clamped) 16-B loads before any MFMA consumes them, so a layer costs one global
 // round trip per 16-column tile instead of one per 32-deep k-step: the step is latency bound
 // and the weights arrive from the Infinity Cache / another XCD's L2 after each optimizer step.
-template <int MT>
+// Weight-image load: plain in the launch-per-step loop; sc1 (L2-served) in the persistent epoch
+// kernel, where other workgroups of the same launch rewrite the images every step.
+template <bool PS>
+__device__ __forceinline__ bf16x8 ld_w(const u16* __restrict__ img, int off) {
+  if constexpr (PS)
+    return __builtin_bit_cast(bf16x8, rx_load16_sc1(img, off * 2));
+  else
+    return *reinterpret_cast<const RX_GLOBAL bf16x8*>(rx_g(img) + off);
+}
+
+template <int MT, bool PS>
 __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
-                                          const RX_GLOBAL u16* __restrict__ Brow, int K, int lg) {
+                                          const u16* __restrict__ img, int boff, int K, int lg) {
   constexpr int KC = 8;
   const int nks = K >> 5;
   for (int kc = 0; kc < nks; kc += KC) {
@@ -147,7 +157,7 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restric
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
       const int ks = min(kc + s, nks - 1);
-      bfr[s] = *reinterpret_cast<const RX_GLOBAL bf16x8*>(Brow + ks * 32 + 8 * lg);
+      bfr[s] = ld_w<PS>(img, boff + ks * 32 + 8 * lg);
     }
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
@@ -167,27 +177,28 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restric
 // that precedes the GEMM) so their global round trip overlaps that work.
 constexpr int RX_PJ = 2;  // tiles per wave prefetched
 constexpr int RX_PK = 4;  // k-steps per tile prefetched
-__device__ __forceinline__ void gemm_prefetch(bf16x8 (&pre)[RX_PK], const RX_GLOBAL u16* __restrict__ Brow, int K,
+template <bool PS>
+__device__ __forceinline__ void gemm_prefetch(bf16x8 (&pre)[RX_PK], const u16* __restrict__ img, int boff, int K,
                                               int lg) {
   const int nks = K >> 5;
 #pragma unroll
   for (int s = 0; s < RX_PK; ++s) {
     const int ks = min(s, nks - 1);
-    pre[s] = *reinterpret_cast<const RX_GLOBAL bf16x8*>(Brow + ks * 32 + 8 * lg);
+    pre[s] = ld_w<PS>(img, boff + ks * 32 + 8 * lg);
   }
 }
 
 // Head of this wave's forward weight tiles of layer `ly` (W_l rows, K = in_k).
-template <class LY>
+template <bool PS, class LY>
 __device__ __forceinline__ void fwd_prefetch(const LY& ly, const u16* __restrict__ img, bf16x8 (&wpre)[RX_PJ][RX_PK]) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
   const int lr = lane & 15, lg = lane >> 4;
   const int ntiles = ly.out_n >> 4;
 #pragma unroll
   for (int j = 0; j < RX_PJ; ++j)
     if (j * RX_NW < ntiles) {
       const int n = min(wave + j * RX_NW, ntiles - 1);
-      gemm_prefetch(wpre[j], rx_g(img) + ly.w_img + (n * 16 + lr) * ly.in_k, ly.in_k, lg);
+      gemm_prefetch<PS>(wpre[j], img, ly.w_img + (n * 16 + lr) * ly.in_k, ly.in_k, lg);
     }
 }
 
@@ -195,18 +206,27 @@ __device__ __forceinline__ void fwd_prefetch(const LY& ly, const u16* __restrict
 // [rows][BP]: whole 128-B (BP = 64) rows, 16 B per lane. The optimizer kernel computes the
 // weight gradients from these (wgrad_mode 1), so the step kernel's critical chain neither runs
 // the wgrad GEMMs nor stores 4 B of fp32 gradient per weight.
-template <int MT>
-__device__ __forceinline__ void export_rows(const u16* lds, int rows, u16* __restrict__ glob) {
+// `byte_base`: byte offset of the destination inside the gradient buffer Gr. Persistent (PS) with
+// `wt`: write-through sc1 stores (some optimizer workgroup of the launch sits on another XCD);
+// plain stores otherwise (every reader shares this XCD's L2 and reads it with sc1 loads).
+template <int MT, bool PS>
+__device__ __forceinline__ void export_rows(const u16* lds, int rows, float* __restrict__ Gr, int byte_base,
+                                            bool wt = true) {
   constexpr int BP = Tile<MT>::BP, XS = Tile<MT>::XS, CH = BP / 8;
-  for (int idx = threadIdx.x; idx < rows * CH; idx += RX_THREADS) {
+  for (int idx = rx_tid<PS>(); idx < rows * CH; idx += RX_THREADS) {
     const int r = idx / CH, c = idx % CH;
-    *reinterpret_cast<RX_GLOBAL u32x4*>(rx_g(glob) + r * BP + c * 8) = *reinterpret_cast<const u32x4*>(lds + r * XS + c * 8);
+    const int boff = byte_base + (r * BP + c * 8) * 2;
+    const u32x4 val = *reinterpret_cast<const u32x4*>(lds + r * XS + c * 8);
+    if (PS && wt)
+      rx_store16_sc1(Gr, boff, val);
+    else
+      *reinterpret_cast<RX_GLOBAL u32x4*>(rx_g(reinterpret_cast<char*>(Gr)) + boff) = val;
   }
 }
 
-template <int MT>
+template <int MT, bool PS>
 __device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
-                                              const RX_GLOBAL u16* __restrict__ Brow, int K, int lg,
+                                              const u16* __restrict__ img, int boff, int K, int lg,
                                               const bf16x8 (&pre)[RX_PK]) {
   const int nks = K >> 5;
 #pragma unroll
@@ -221,7 +241,7 @@ __device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __res
     }
   }
   if (nks > RX_PK)
-    gemm_tile<MT>(acc, Arow + RX_PK * 32, RS, Brow + RX_PK * 32, K - RX_PK * 32, lg);
+    gemm_tile<MT, PS>(acc, Arow + RX_PK * 32, RS, img, boff + RX_PK * 32, K - RX_PK * 32, lg);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -229,14 +249,14 @@ __device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __res
 // act/BN) in R (row-major) and in XT_{l+1}; for the last layer computes loss, metrics and
 // writes dL/dy into R/GT as G_{L-1}.
 // ------------------------------------------------------------------------------------------
-template <int MT, bool TRAIN, class D, class LY, class NX>
+template <int MT, bool TRAIN, bool PS, class D, class LY, class NX>
 __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX& nx, bool last, char* smem,
                                               const u16* __restrict__ img, const float* __restrict__ P,
                               float* __restrict__ Gr, const float* __restrict__ labels,
                               const int* __restrict__ rowidx, int nvalid, float* __restrict__ scratch,
-                              double* __restrict__ metrics, bf16x8 (&wpre)[RX_PJ][RX_PK]) {
+                              double* __restrict__ metrics, bf16x8 (&wpre)[RX_PJ][RX_PK], bool ps_wt = true) {
   using T = Tile<MT>;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
   const int lr = lane & 15, lg = lane >> 4;
   const int RS = d.max_k + 8;
   u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
@@ -244,8 +264,8 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
   const int ntiles = ly.out_n >> 4;
   if (TRAIN && d.wgrad_mode == 1)  // X^T_l (published by the previous layer / the input load)
-    export_rows<MT>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n,
-                    reinterpret_cast<u16*>(Gr + d.act_off) + ly.xg_off);
+    export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
+                        ps_wt);
 
   f32x4 acc[T::NTW * MT];
 #pragma unroll
@@ -255,17 +275,17 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int n = wave + j * RX_NW;
     if (n < ntiles) {
-      const RX_GLOBAL u16* Brow = rx_g(img) + ly.w_img + (n * 16 + lr) * ly.in_k;
+      const int boff = ly.w_img + (n * 16 + lr) * ly.in_k;
       if (j < RX_PJ)
-        gemm_tile_pre<MT>(part, R + lr * RS, RS, Brow, ly.in_k, lg, wpre[j < RX_PJ ? j : 0]);
+        gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg, wpre[j < RX_PJ ? j : 0]);
       else
-        gemm_tile<MT>(part, R + lr * RS, RS, Brow, ly.in_k, lg);
+        gemm_tile<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
   // the next layer's weight head travels while this layer's epilogue runs
-  if (!last) fwd_prefetch(nx, img, wpre);
+  if (!last) fwd_prefetch<PS>(nx, img, wpre);
 
   // ---- epilogue in registers, in place on acc: bias, act, BN, loss ----
 #pragma unroll
@@ -433,7 +453,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   // zero the K padding columns [out_n, out_k) of R so the next GEMM's K tail is exact
   const int kpad = (last ? ly.out_k : nx.in_k) - ly.out_n;
   if (kpad > 0) {
-    for (int idx = threadIdx.x; idx < T::BP * kpad; idx += RX_THREADS) {
+    for (int idx = rx_tid<PS>(); idx < T::BP * kpad; idx += RX_THREADS) {
       const int row = idx / kpad, cc = ly.out_n + idx % kpad;
       R[row * RS + cc] = 0;
     }
@@ -444,13 +464,18 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
 // ------------------------------------------------------------------------------------------
 // backward of layer l: G_l is in R (row-major) and GT (transposed).
 // ------------------------------------------------------------------------------------------
-template <int MT, class D, class LY, class PV>
+// PS (persistent epoch kernel): once this layer's dgrad has read its last weight byte and its
+// G^T export has drained, lane 0 publishes flag `sync[32 l] = step + 1` -- the optimizer
+// workgroups of layer l may then compute dW_l and rewrite W_l / Wt_l while the backward goes on.
+template <int MT, bool PS, class D, class LY, class PV>
 __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const PV& pv, int l, char* smem,
                                                const u16* __restrict__ img, const float* __restrict__ P,
                                                float* __restrict__ Gr, int nvalid, const float* __restrict__ scratch,
-                                               unsigned long long* __restrict__ stamps) {
+                                               unsigned long long* __restrict__ stamps,
+                                               unsigned* __restrict__ sync = nullptr, int step = 0,
+                                               bool ps_wt = true) {
   using T = Tile<MT>;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
   const int lr = lane & 15, lg = lane >> 4;
   const int RS = d.max_k + 8;
   const int XS = T::XS;
@@ -471,7 +496,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     for (int j = 0; j < RX_PJ; ++j) {
       if (j * RX_NW < ntiles_d) {
         const int n = min(wave + j * RX_NW, ntiles_d - 1);
-        gemm_prefetch(wpre[j], rx_g(img) + ly.wt_img + (n * 16 + lr) * ly.out_k, ly.out_k, lg);
+        gemm_prefetch<PS>(wpre[j], img, ly.wt_img + (n * 16 + lr) * ly.out_k, ly.out_k, lg);
         const int sp = pv.r_off + n * 16 + lr;
 #pragma unroll
         for (int q = 0; q < MT * 4; ++q) svp[j][q] = load_val(scratch, sp + ((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n);
@@ -481,7 +506,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 
   if (d.wgrad_mode == 1) {
     // G^T_l leaves for the optimizer kernel's wgrad (GT is overwritten with G_{l-1} below)
-    export_rows<MT>(GT, ly.out_n, reinterpret_cast<u16*>(Gr + d.act_off) + ly.gg_off);
+    export_rows<MT, PS>(GT, ly.out_n, Gr, d.act_off * 4 + ly.gg_off * 2, ps_wt);
   } else
   // ---- wgrad, computed transposed: dW^T[i][o] = sum_b X[b][i] G[b][o]  (A = XT, B = GT) ----
   // each lane then holds 4 consecutive i of one o = 16 contiguous bytes of dW[o][:] ->
@@ -570,7 +595,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       }
     }
   }
-  if (stamps != nullptr && threadIdx.x == 0) rx_g(stamps)[20 + 4 * l] = __builtin_amdgcn_s_memtime();
+  if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[20 + 4 * l] = __builtin_amdgcn_s_memtime();
   if (l == 0) return;
 
   // ---- dgrad: dX[b][i] = sum_o G[b][o] W[o][i]  (A = R, B = Wt, K = out_k) ----
@@ -584,18 +609,22 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int n = wave + j * RX_NW;
     if (n < ntiles) {
-      const RX_GLOBAL u16* Brow = rx_g(img) + ly.wt_img + (n * 16 + lr) * ly.out_k;
+      const int boff = ly.wt_img + (n * 16 + lr) * ly.out_k;
       if (j < RX_PJ)
-        gemm_tile_pre<MT>(part, R + lr * RS, RS, Brow, ly.out_k, lg, wpre[j < RX_PJ ? j : 0]);
+        gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg, wpre[j < RX_PJ ? j : 0]);
       else
-        gemm_tile<MT>(part, R + lr * RS, RS, Brow, ly.out_k, lg);
+        gemm_tile<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
-  if (stamps != nullptr && threadIdx.x == 0) rx_g(stamps)[21 + 4 * l] = __builtin_amdgcn_s_memtime();
+  if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[21 + 4 * l] = __builtin_amdgcn_s_memtime();
+  if constexpr (PS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's G^T export drained
   __syncthreads();  // all reads of G_l (R, GT) are done; they are overwritten with G_{l-1}
-  if (stamps != nullptr && threadIdx.x == 0) rx_g(stamps)[22 + 4 * l] = __builtin_amdgcn_s_memtime();
+  if constexpr (PS) {
+    if (rx_tid<PS>() == 0) __hip_atomic_store(sync + 32 * l, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[22 + 4 * l] = __builtin_amdgcn_s_memtime();
 
   // ---- post-op backward of layer l-1 (BN / act), producing G_{l-1} ----
 #pragma unroll
@@ -683,11 +712,11 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       *reinterpret_cast<uint2*>(GT + c * XS + mt * 16 + lg * 4) = pk;
     }
   }
-  if (stamps != nullptr && threadIdx.x == 0) rx_g(stamps)[23 + 4 * l] = __builtin_amdgcn_s_memtime();
+  if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[23 + 4 * l] = __builtin_amdgcn_s_memtime();
   // zero the K tail [out_n, out_k) of G_{l-1} in R for the next dgrad
   const int kpad = pv.out_k - pv.out_n;
   if (kpad > 0) {
-    for (int idx = threadIdx.x; idx < T::BP * kpad; idx += RX_THREADS) {
+    for (int idx = rx_tid<PS>(); idx < T::BP * kpad; idx += RX_THREADS) {
       const int row = idx / kpad, cc = pv.out_n + idx % kpad;
       R[row * RS + cc] = 0;
     }
@@ -697,13 +726,13 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 
 
 // Stage every layer's per-column parameters (bias, BN gamma/beta, running mean/var) into LDS
-// with ONE burst of independent loads per thread (column c = threadIdx.x of every layer,
+// with ONE burst of independent loads per thread (column c = rx_tid() of every layer,
 // address-clamped so no load sits behind a per-element branch).
 template <class C, class D>
 __device__ __forceinline__ void load_params(const D& d, char* smem, const float* __restrict__ P,
                                             const float* __restrict__ rstats) {
   float* pr = reinterpret_cast<float*>(smem + d.pr_lds_off);
-  const int c = threadIdx.x;
+  const int c = rx_tid<false>();
   float v[RX_MAXL][5];
   C::each_layer(d, [&](const auto& ly, int l) {
     const bool ok = c < ly.out;
@@ -731,7 +760,7 @@ __device__ __forceinline__ void load_params(const D& d, char* smem, const float*
 template <class C, class D>
 __device__ __forceinline__ void store_running_stats(const D& d, char* smem, float* __restrict__ rstats) {
   const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off);
-  const int c = threadIdx.x;
+  const int c = rx_tid<false>();
   C::each_layer(d, [&](const auto& ly, int) {
     if (ly.rs_off >= 0 && c < ly.out) {
       rx_g(rstats)[ly.rs_off + c] = pr[ly.pr_off + 3 * ly.out_n + c];
@@ -741,7 +770,7 @@ __device__ __forceinline__ void store_running_stats(const D& d, char* smem, floa
 }
 
 // load the batch's feature rows (gathered through the epoch permutation) into R and XT_0
-template <int MT, class D, class L0>
+template <int MT, bool PS = false, class D, class L0>
 __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem, const u16* __restrict__ feats,
                                             const int* __restrict__ rowidx, int nvalid, bool need_t) {
   using T = Tile<MT>;
@@ -750,7 +779,7 @@ __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem
   u16* XT = reinterpret_cast<u16*>(smem + l0.xt_off);
   const int in_n = l0.in_n;
   const int chunks = d.feat_k >> 3;  // 8 bf16 per 16-B chunk
-  for (int idx = threadIdx.x; idx < T::BP * chunks; idx += RX_THREADS) {
+  for (int idx = rx_tid<PS>(); idx < T::BP * chunks; idx += RX_THREADS) {
     const int row = idx / chunks, ch = idx % chunks;
     u32x4 v = *reinterpret_cast<const RX_GLOBAL u32x4*>(rx_g(feats) + (size_t)rowidx[row] * d.feat_k + ch * 8);
     if (row >= nvalid) v = u32x4{0u, 0u, 0u, 0u};
@@ -781,25 +810,25 @@ __device__ __forceinline__ void mlp_train_step_body(
   int si = 0;
 #define RX_STAMP()                                                        \
   do {                                                                    \
-    if (st != nullptr && threadIdx.x == 0) st[si] = __builtin_amdgcn_s_memtime(); \
+    if (st != nullptr && rx_tid<false>() == 0) st[si] = __builtin_amdgcn_s_memtime(); \
     ++si;                                                                 \
   } while (0)
   RX_STAMP();
   bf16x8 wpre[RX_PJ][RX_PK];
-  fwd_prefetch(C::first(d), img, wpre);
-  for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS)
+  fwd_prefetch<false>(C::first(d), img, wpre);
+  for (int i = rx_tid<false>(); i < Tile<MT>::BP; i += RX_THREADS)
     rowidx[i] = i < nvalid ? (perm ? rx_g(perm)[row0 + i] : row0 + i) : (perm ? rx_g(perm)[row0] : row0);
   load_params<C>(d, smem, P, rstats);
   __syncthreads();
   load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, true);
   RX_STAMP();
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
-    layer_forward<MT, true>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre);
+    layer_forward<MT, true, false>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre);
     RX_STAMP();
   });
   store_running_stats<C>(d, smem, rstats);
   C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
-    layer_backward<MT>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, stamps);
+    layer_backward<MT, false>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, stamps);
     RX_STAMP();
   });
 #undef RX_STAMP
@@ -815,14 +844,14 @@ __device__ __forceinline__ void mlp_eval_body(const MlpDesc* __restrict__ dp, co
   auto&& d = C::desc(dp);
   const int row0 = blockIdx.x * batch;
   const int nvalid = min(batch, n_rows - row0);
-  for (int i = threadIdx.x; i < Tile<MT>::BP; i += RX_THREADS) rowidx[i] = i < nvalid ? row0 + i : row0;
+  for (int i = rx_tid<false>(); i < Tile<MT>::BP; i += RX_THREADS) rowidx[i] = i < nvalid ? row0 + i : row0;
   load_params<C>(d, smem, P, rstats);
   __syncthreads();
   load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, false);
   bf16x8 wpre[RX_PJ][RX_PK];
-  fwd_prefetch(C::first(d), img, wpre);
+  fwd_prefetch<false>(C::first(d), img, wpre);
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
-    layer_forward<MT, false>(d, ly, nx, last, smem, img, P, nullptr, labels, rowidx, nvalid, nullptr, metrics,
+    layer_forward<MT, false, false>(d, ly, nx, last, smem, img, P, nullptr, labels, rowidx, nvalid, nullptr, metrics,
                              wpre);
   });
 }

@@ -20,6 +20,24 @@ __device__ __forceinline__ RX_GLOBAL T* rx_g(T* p) {
   return (RX_GLOBAL T*)p;
 }
 
+// Thread index behind an opaque (volatile) register move. The persistent epoch kernel runs the
+// step body in a loop: with a plain threadIdx.x the compiler hoists every lane-dependent address
+// of every layer out of that loop, keeps them all live across it and spills to scratch. The
+// wave index goes back to an SGPR through readfirstlane (it is wave-uniform).
+// Outside such loops (OPQ = false) it is the plain threadIdx.x.
+template <bool OPQ = true>
+__device__ __forceinline__ int rx_tid() {
+  if constexpr (!OPQ) return (int)threadIdx.x;
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return (int)threadIdx.x + z;
+}
+template <bool OPQ = true>
+__device__ __forceinline__ int rx_wave() {
+  if constexpr (!OPQ) return (int)(threadIdx.x >> 6);
+  return __builtin_amdgcn_readfirstlane(rx_tid<true>() >> 6);
+}
+
 // round-to-nearest-even fp32 -> bf16 bits
 __device__ __forceinline__ u16 rx_f2bf(float f) {
   uint32_t u = __float_as_uint(f);
@@ -53,6 +71,19 @@ __device__ __forceinline__ f32x4 rx_mfma16(const bf16x8& a, const bf16x8& b, con
 __device__ __forceinline__ void rx_store16_wt(float* base, int byte_off, const f32x4& v) {
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7ffffff0, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, byte_off, 0, 16);
+}
+
+// 16-B sc1 load / store through a buffer descriptor (`base` wave-uniform). sc1 loads bypass
+// the CU's L1 and are served by L2, sc1 stores write through: the pair is how workgroups of one
+// persistent launch hand data to each other without acquire/release fences
+// (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility", valid forms).
+__device__ __forceinline__ u32x4 rx_load16_sc1(const void* base, int byte_off) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7ffffff0, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, byte_off, 0, 16);
+}
+__device__ __forceinline__ void rx_store16_sc1(void* base, int byte_off, const u32x4& v) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7ffffff0, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, byte_off, 0, 16);
 }
 
 #define RX_CHECK(x)                                                     \

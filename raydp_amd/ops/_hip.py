@@ -46,7 +46,8 @@ class MlpDesc(ctypes.Structure):
 class StepBufs(ctypes.Structure):
     """Device buffers of one fused model (csrc/hip/fused_mlp.hip StepBufs)."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("d_dev", "img", "rstats", "params", "grads", "scratch",
-                                               "metrics", "stamps", "jit_step", "jit_eval")]
+                                               "metrics", "stamps", "jit_step", "jit_eval",
+                                               "jit_persist")]
 
 
 class OptSeg(ctypes.Structure):
@@ -109,7 +110,16 @@ def lib():
     L.rx_opt_step.argtypes = [vp, vp, vp, vp, vp, vp, f, f, f, f, i, vp]
     L.rx_mlp_wgrad.argtypes = [vp, vp, vp, vp]
     L.rx_mlp_eval.argtypes = [vp, vp, i, vp, vp, i, i, vp]
-    L.rx_jit_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(vp), i]
+    L.rx_jit_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), i]
+    # (desc, bufs, opt, opt_dev, mt, m, v, feats, labels, perm, n_rows, batch, nsteps, sched, opt_first,
+    #  sync, timeout_s, stream)
+    L.rx_mlp_train_persistent.argtypes = [vp, vp, vp, vp, i, vp, vp, vp, vp, vp, i, i, i, vp, i, vp,
+                                          ctypes.c_double, vp]
+    L.rx_mlp_train_persistent.restype = i
+    L.rx_ps_sync_words.restype = i
+    L.rx_ps_err_index.restype = i
+    L.rx_ps_grid_blocks.argtypes = [vp]
+    L.rx_ps_grid_blocks.restype = i
     L.rx_jit_load.restype = i
     L.rx_mlp_refresh_images.argtypes = [vp, vp, vp, vp]
     L.rx_arrow_ingest.argtypes = [vp, vp, vp]

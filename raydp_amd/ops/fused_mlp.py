@@ -75,6 +75,12 @@ def wgrad_mode() -> int:
     return 1 if conf_get("spark.ray.mi355x.mlp_wgrad") == "opt" else 0
 
 
+def persistent_enabled() -> bool:
+    """One-GPU epochs as one persistent launch (``spark.ray.mi355x.mlp_persistent``)."""
+    from raydp_amd.utils.config import get as conf_get
+    return bool(conf_get("spark.ray.mi355x.mlp_persistent"))
+
+
 def pick_mt(batch: int) -> Optional[int]:
     for mt in (2, 4, 8):
         if batch <= mt * 16:
@@ -314,7 +320,6 @@ class FusedMLPTrainer:
         self.metrics.zero_()
         if nsteps == 0:
             return self._read_metrics()
-        import numpy as np
         b1, b2 = self.opt.b1, self.opt.b2
         # per-step learning rate and Adam bias corrections, vectorised (a Python loop here costs
         # ~5 us per step of host time in front of the epoch's first launch)
@@ -331,7 +336,10 @@ class FusedMLPTrainer:
         pp = ctypes.c_void_p
         perm_p = pp(perm.data_ptr()) if perm is not None else pp(0)
         gscale = 1.0 / world_size
-        if xg is not None:
+        if xg is None and comm is None and allreduce is None and world_size == 1 and \
+                self._run_persistent(feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream):
+            pass
+        elif xg is not None:
             rc = self.lib.rx_mlp_train_steps_xg(
                 ctypes.byref(self.desc), ctypes.byref(self.bufs), ctypes.byref(self.opt), self._od, self.mt,
                 pp(self.m.data_ptr()), pp(self.v.data_ptr()),
@@ -368,6 +376,36 @@ class FusedMLPTrainer:
         if xg is not None:
             xg.check()
         return out
+
+    def _run_persistent(self, feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream) -> bool:
+        """The whole epoch as one persistent launch (csrc/hip/mlp_persist.h); False when this
+        model / configuration cannot use it (the caller then runs the launch-per-step loop)."""
+        if self.desc.wgrad_mode != 1 or not persistent_enabled():
+            return False
+        if getattr(self, "_ps_grid", None) is None:
+            self._ps_grid = int(self.lib.rx_ps_grid_blocks(ctypes.byref(self.opt)))
+            self._ps_sync = torch.zeros(int(self.lib.rx_ps_sync_words()), dtype=torch.int32, device=self.device)
+            self._ps_err = int(self.lib.rx_ps_err_index())
+            props = torch.cuda.get_device_properties(self.device)
+            self._ps_ok = self._ps_grid <= int(props.multi_processor_count)
+        if not self._ps_ok:
+            return False
+        sched = torch.from_numpy(np.concatenate([lr_np, bc1_np, bc2_np])).to(self.device)
+        pp = ctypes.c_void_p
+        from raydp_amd.utils.config import get as conf_get
+        timeout = max(5.0, float(conf_get("spark.ray.mi355x.allreduce.timeout_s")))
+        rc = self.lib.rx_mlp_train_persistent(
+            ctypes.byref(self.desc), ctypes.byref(self.bufs), ctypes.byref(self.opt), self._od, self.mt,
+            pp(self.m.data_ptr()), pp(self.v.data_ptr()), pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p,
+            n_rows, self.batch, nsteps, pp(sched.data_ptr()), int(self.step_count == 0),
+            pp(self._ps_sync.data_ptr()), ctypes.c_double(timeout), stream)
+        if rc in (-3, -4):
+            return False
+        _hip.check(rc, "rx_mlp_train_persistent")
+        self._ps_sched = sched   # kept alive until the launch has consumed it
+        if int(self._ps_sync[self._ps_err].item()) != 0:
+            raise RuntimeError("persistent fused-MLP epoch: a workgroup wait timed out (grid not co-resident?)")
+        return True
 
     def _check_operands(self, feats, labels, n_rows, perm=None):
         """Host-side guard: the kernels index rows [0, n_rows) of feats / labels (through perm)

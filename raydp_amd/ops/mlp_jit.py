@@ -42,7 +42,7 @@ def _f(x: float) -> str:
 
 def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
     L = desc.L
-    out = ['#include "mlp_core.h"', "", "namespace {", "", "struct JD {"]
+    out = ['#include "mlp_persist.h"', "", "namespace {", "", "struct JD {"]
     exp = os.environ.get("RAYDP_MLP_EXPERIMENT")   # timing experiments only (wrong numerics)
     if exp:
         out = [f"#define RX_EXP_{e}" for e in exp.split(",")] + out
@@ -91,6 +91,20 @@ def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
         "  __shared__ int rowidx[Tile<RX_MT>::BP];",
         "  mlp_eval_body<JitCfg, RX_MT>(dp, img, rstats, P, feats, labels, n_rows, batch, metrics, smem, rowidx);",
         "}",
+        'extern "C" __global__ __launch_bounds__(RX_THREADS) void rx_jit_persist(',
+        "    const MlpDesc* __restrict__ dp, const OptDesc* __restrict__ od, const u16* __restrict__ img,",
+        "    float* __restrict__ rstats, float* __restrict__ P, float* __restrict__ Gr,",
+        "    const u16* __restrict__ feats, const float* __restrict__ labels, const int* __restrict__ perm,",
+        "    int n_rows, int batch, int nsteps, float* __restrict__ scratch, double* __restrict__ metrics,",
+        "    float* __restrict__ m, float* __restrict__ v, const float* __restrict__ sched, int opt_first,",
+        "    unsigned* __restrict__ sync, unsigned long long ticks, unsigned long long* __restrict__ stamps) {",
+        "  extern __shared__ __attribute__((aligned(16))) char smem[];",
+        "  __shared__ int rowidx[Tile<RX_MT>::BP];",
+        "  __shared__ int flag_lds[2];",
+        "  mlp_persist_body<JitCfg, RX_MT>(dp, od, img, rstats, P, Gr, feats, labels, perm, n_rows, batch, nsteps,",
+        "                                  scratch, metrics, m, v, sched, opt_first, sync, ticks, smem, rowidx,",
+        "                                  flag_lds, stamps);",
+        "}",
     ]
     return "\n".join(out) + "\n"
 
@@ -101,7 +115,7 @@ def _hipcc() -> str:
 
 def _key(src: str) -> str:
     h = hashlib.sha256(src.encode())
-    for f in ("mlp_core.h", "rx_common.h"):
+    for f in ("mlp_core.h", "mlp_opt.h", "mlp_persist.h", "rx_common.h"):
         with open(os.path.join(CSRC_HIP, f), "rb") as fh:
             h.update(fh.read())
     h.update(ARCH.encode())
@@ -138,12 +152,12 @@ def load_specialized(trainer) -> Optional[str]:
     with _lock:
         fns = _loaded.get(path)
         if fns is None:
-            step, ev = ctypes.c_void_p(), ctypes.c_void_p()
-            _hip.check(_hip.lib().rx_jit_load(path.encode(), ctypes.byref(step), ctypes.byref(ev),
+            step, ev, ps = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+            _hip.check(_hip.lib().rx_jit_load(path.encode(), ctypes.byref(step), ctypes.byref(ev), ctypes.byref(ps),
                                               int(trainer.desc.lds_bytes)), "rx_jit_load")
-            fns = (step.value, ev.value)
+            fns = (step.value, ev.value, ps.value)
             _loaded[path] = fns
-    trainer.bufs.jit_step, trainer.bufs.jit_eval = fns
+    trainer.bufs.jit_step, trainer.bufs.jit_eval, trainer.bufs.jit_persist = fns
     return path
 
 

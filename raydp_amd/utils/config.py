@@ -136,6 +136,9 @@ register("spark.ray.mi355x.mlp_wgrad", "str", "opt",
          "fused MLP weight gradients: opt (computed by the optimizer kernel's workgroups from exported "
          "activations) or step (inside the single-workgroup step kernel)", env="RAYDP_MLP_WGRAD",
          choices=["opt", "step"])
+register("spark.ray.mi355x.mlp_persistent", "bool", True,
+         "one GPU: run a whole fused-MLP epoch as one persistent launch with the optimizer beside the "
+         "backward pass (csrc/hip/mlp_persist.h)", env="RAYDP_MLP_PERSISTENT")
 register("spark.ray.mi355x.ddp.bucket_mb", "float", 32.0,
          "DDP gradient bucket size (xGMI rings are per-link bound: few large buckets)", env="RAYDP_DDP_BUCKET_MB")
 register("spark.ray.mi355x.object_store_bytes", "bytes", "0",

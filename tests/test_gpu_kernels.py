@@ -292,3 +292,59 @@ def test_native_rccl_comm_in_step_loop():
     finally:
         reset_cache()
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["nyc_adam", "bnfirst_sgd", "nyc_adamw_tail"])
+def test_persistent_epoch_matches_step_loop(case, monkeypatch):
+    """The one-launch persistent epoch (csrc/hip/mlp_persist.h: optimizer workgroups beside the
+    backward, sc1 hand-offs) reproduces the launch-per-step loop bit for bit: parameters, Adam /
+    momentum state, bf16 weight images, BatchNorm running statistics and loss metrics, over
+    several epochs with a device permutation and a partial last batch."""
+    from raydp_amd.models.mlp_spec import extract_mlp_spec
+    from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+    dev = torch.device("cuda")
+    torch.manual_seed(5)
+    if case == "bnfirst_sgd":
+        model, in_f, out_f, batch, n = BnFirst(), 13, 3, 32, 32 * 20 + 7
+        mk_opt = lambda m: torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+        loss = nn.MSELoss()
+    elif case == "nyc_adamw_tail":
+        model, in_f, out_f, batch, n = NYC(), 20, 1, 64, 64 * 30 + 19
+        mk_opt = lambda m: torch.optim.AdamW(m.parameters(), lr=2e-3, weight_decay=0.01)
+        loss = nn.SmoothL1Loss()
+    else:
+        model, in_f, out_f, batch, n = NYC(), 20, 1, 64, 64 * 40
+        mk_opt = lambda m: torch.optim.Adam(m.parameters(), lr=1e-3)
+        loss = nn.SmoothL1Loss()
+    X = torch.randn(n, in_f) * 2.0
+    Y = torch.randn(n, out_f) * 3.0
+    runs = []
+    for persistent in ("1", "0"):
+        monkeypatch.setenv("RAYDP_MLP_PERSISTENT", persistent)
+        m2 = copy.deepcopy(model)
+        tr = FusedMLPTrainer(extract_mlp_spec(m2), optimizer_config(mk_opt(m2)), loss_code(loss), batch, dev)
+        feats = torch.zeros(n, tr.feat_k, dtype=torch.bfloat16)
+        feats[:, :in_f] = X.to(torch.bfloat16)
+        feats, Yd = feats.to(dev), Y.to(dev)
+        g = torch.Generator(device="cpu").manual_seed(11)
+        mets = []
+        for ep in range(3):
+            perm = torch.randperm(n, generator=g).to(torch.int32).to(dev)
+            mets.append(tr.train_epoch(feats, Yd, n, perm))
+        torch.cuda.synchronize()
+        if persistent == "1":
+            assert tr._ps_ok and tr._ps_grid > 1, "persistent path not taken"
+        runs.append((tr.params.clone(), tr.m.clone(), tr.v.clone(), tr.img.clone(), tr.rstats.clone(), mets))
+    (p1, m1, v1, i1, r1, e1), (p0, m0, v0, i0, r0, e0) = runs
+
+    def where(a, b):
+        return [(kind, off, n, float((a[off:off + n] - b[off:off + n]).abs().max()))
+                for kind, _, off, n in tr.layout if not torch.equal(a[off:off + n], b[off:off + n])]
+    assert torch.equal(p1, p0), ("params", where(p1, p0), "m", where(m1, m0), "v", where(v1, v0),
+                                 "rstats", float((r1 - r0).abs().max()), e1, e0)
+    assert torch.equal(m1, m0) and torch.equal(v1, v0)
+    assert torch.equal(i1, i0)
+    assert torch.equal(r1, r0)
+    for a, b in zip(e1, e0):
+        assert a["batches"] == b["batches"] and a["count"] == b["count"]
+        assert abs(a["loss"] - b["loss"]) <= 1e-6 * max(1.0, abs(b["loss"])), (a, b)
