@@ -34,20 +34,13 @@ constexpr bool kExpNoScratch = false;
 // Saved forward values (BN inputs / ReLU mask sources) stay fp32: a bf16 copy halves their
 // bytes but the BN gamma/beta gradients cancel to near zero for some channels, and Adam turns
 // their rounding error into sign flips of the update (measured: 12 % parameter error).
-#ifdef RX_EXP_SCRATCH16
-constexpr bool kScratchBf16 = true;
-#else
-constexpr bool kScratchBf16 = false;
-#endif
-__device__ __forceinline__ void save_val(float* scratch, int idx, float v) {
-  if (kScratchBf16)
-    reinterpret_cast<u16*>(scratch)[idx] = rx_f2bf(v);
-  else
-    scratch[idx] = v;
-}
-__device__ __forceinline__ float load_val(const float* scratch, int idx) {
-  if (kScratchBf16) return rx_bf2f(rx_g(reinterpret_cast<const u16*>(scratch))[idx]);
-  return rx_g(scratch)[idx];
+// They are stored FRAGMENT-major -- [16-column tile][row tile mt][lane][4 rows] -- i.e. exactly
+// the MFMA accumulator layout, and the backward reads them back with the same lane mapping: one
+// coalesced 16-B store / load per accumulator instead of four scattered 4-B ones (the CU's
+// vector-memory pipe is the bottleneck of the epilogues).
+template <int MT>
+__device__ __forceinline__ int frag_off(int base, int n, int mt, int lane) {
+  return base + ((n * MT + mt) * 64 + lane) * 4;
 }
 
 #ifdef RX_EXP_WTSTORE
@@ -254,7 +247,13 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
                                               const u16* __restrict__ img, const float* __restrict__ P,
                               float* __restrict__ Gr, const float* __restrict__ labels,
                               const int* __restrict__ rowidx, int nvalid, float* __restrict__ scratch,
-                              double* __restrict__ metrics, bf16x8 (&wpre)[RX_PJ][RX_PK], bool ps_wt = true) {
+                              double* __restrict__ metrics, bf16x8 (&wpre)[RX_PJ][RX_PK], bool ps_wt = true,
+                              int l = 0, unsigned long long* __restrict__ stamps = nullptr) {
+  // optional intra-layer timeline (wave 0, s_memtime): [40 + 5 l ..] export, GEMM, epilogue,
+  // first barrier, publish + second barrier
+  auto fst = [&](int k) {
+    if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[40 + 5 * l + k] = __builtin_amdgcn_s_memtime();
+  };
   using T = Tile<MT>;
   const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
   const int lr = lane & 15, lg = lane >> 4;
@@ -266,6 +265,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   if (TRAIN && d.wgrad_mode == 1)  // X^T_l (published by the previous layer / the input load)
     export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
                         ps_wt);
+  fst(0);
 
   f32x4 acc[T::NTW * MT];
 #pragma unroll
@@ -284,6 +284,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
+  fst(1);
   // the next layer's weight head travels while this layer's epilogue runs
   if (!last) fwd_prefetch<PS>(nx, img, wpre);
 
@@ -334,12 +335,11 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
             prw[3 * ly.out_n + c] = (1.f - ly.momentum) * prw[3 * ly.out_n + c] + ly.momentum * mean;
             prw[4 * ly.out_n + c] = (1.f - ly.momentum) * prw[4 * ly.out_n + c] + ly.momentum * unb;
           }
-          // save the BN input for the backward pass (thread-private slots)
+          // save the BN input for the backward pass (fragment-major, see frag_off)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (!kExpNoScratch) save_val(scratch, ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c, acc[j * MT + mt][r]);
+            if (!kExpNoScratch)
+              *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) = acc[j * MT + mt];
         } else {
           mean = colok ? pr[3 * ly.out_n + c] : 0.f;
           invstd = colok ? rsqrtf(pr[4 * ly.out_n + c] + ly.eps) : 0.f;
@@ -357,10 +357,11 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       } else if (TRAIN && !last) {
         // ReLU mask source for the backward pass
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            save_val(scratch, ly.r_off + (mt * 16 + lg * 4 + r) * ly.out_n + c, colok ? acc[j * MT + mt][r] : 0.f);
+        for (int mt = 0; mt < MT; ++mt) {
+          const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+          *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) =
+              colok ? acc[j * MT + mt] : z;
+        }
       }
       // padded rows / columns carry exact zeros through every GEMM
 #pragma unroll
@@ -421,7 +422,9 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       }
     }
   }
+  fst(2);
   __syncthreads();  // every wave finished reading R for this layer
+  fst(3);
   if (last && !TRAIN) return;
 
   // ---- publish y (or G_{L-1}) as bf16: row-major into R, transposed into XT_{l+1} / GT ----
@@ -458,6 +461,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       R[row * RS + cc] = 0;
     }
   }
+  fst(4);
   __syncthreads();
 }
 
@@ -497,9 +501,12 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       if (j * RX_NW < ntiles_d) {
         const int n = min(wave + j * RX_NW, ntiles_d - 1);
         gemm_prefetch<PS>(wpre[j], img, ly.wt_img + (n * 16 + lr) * ly.out_k, ly.out_k, lg);
-        const int sp = pv.r_off + n * 16 + lr;
 #pragma unroll
-        for (int q = 0; q < MT * 4; ++q) svp[j][q] = load_val(scratch, sp + ((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n);
+        for (int mt = 0; mt < MT; ++mt) {
+          const f32x4 t = *reinterpret_cast<const RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(pv.r_off, n, mt, lane));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) svp[j][mt * 4 + r] = t[r];
+        }
       }
     }
   }
@@ -636,14 +643,17 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     // The forward saved this layer's BN input / activation (fp32) for every padded row and
     // column: issue all loads back to back, unconditionally (a load under a per-element
     // branch is waited for on its own -> one dependent L2 round trip per element).
-    const int sp = pv.r_off + c;
     float sv[MT * 4], g[MT * 4];
     if (j < RX_PJ) {
 #pragma unroll
       for (int q = 0; q < MT * 4; ++q) sv[q] = svp[j < RX_PJ ? j : 0][q];
     } else {
 #pragma unroll
-      for (int q = 0; q < MT * 4; ++q) sv[q] = load_val(scratch, sp + ((q >> 2) * 16 + lg * 4 + (q & 3)) * pv.out_n);
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x4 t = *reinterpret_cast<const RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(pv.r_off, n, mt, lane));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sv[mt * 4 + r] = t[r];
+      }
     }
 #pragma unroll
     for (int q = 0; q < MT * 4; ++q) {
@@ -823,7 +833,8 @@ __device__ __forceinline__ void mlp_train_step_body(
   load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, true);
   RX_STAMP();
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
-    layer_forward<MT, true, false>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre);
+    layer_forward<MT, true, false>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre,
+                                   true, l, stamps);
     RX_STAMP();
   });
   store_running_stats<C>(d, smem, rstats);

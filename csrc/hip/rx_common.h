@@ -48,16 +48,22 @@ __device__ __forceinline__ u16 rx_f2bf(float f) {
 
 __device__ __forceinline__ float rx_bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
 
-// sum over the 4 lanes that share (lane & 15): lanes l, l^16, l^32, l^48
+// sum over the 4 lanes that share (lane & 15): lanes l, l^16, l^32, l^48. gfx950's
+// v_permlane16_swap / v_permlane32_swap exchange rows / halves of the wave in the VALU (a
+// __shfl_xor is an LDS-pipeline ds_bpermute round trip); swapping a value with itself leaves
+// x[l] in one result and x[l^16] (x[l^32]) in the other, and a + b == b + a exactly, so every
+// lane gets the bit-identical sum.
 __device__ __forceinline__ float rx_colsum16(float v) {
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 
 __device__ __forceinline__ float rx_wavesum(float v) {
+  v = rx_colsum16(v);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
 

@@ -17,7 +17,7 @@ dev = torch.device("cuda")
 model = NYC()
 tr = FusedMLPTrainer(extract_mlp_spec(model), optimizer_config(torch.optim.Adam(model.parameters())),
                      loss_code(nn.SmoothL1Loss()), 64, dev)
-stamps = torch.zeros(64, dtype=torch.int64, device=dev)
+stamps = torch.zeros(128, dtype=torch.int64, device=dev)
 tr.bufs.stamps = stamps.data_ptr()
 n = 64 * 200
 feats = torch.zeros(n, tr.feat_k, dtype=torch.bfloat16, device=dev)
@@ -44,3 +44,10 @@ for l in range(4, 0, -1):
     start = s[10 - l]
     w, dg, sy, ep = s[20 + 4 * l], s[21 + 4 * l], s[22 + 4 * l], s[23 + 4 * l]
     print(f"bwd{l + 1}: wgrad {w - start:7.0f}  dgrad {dg - w:7.0f}  sync {sy - dg:7.0f}  epi {ep - sy:7.0f}  tail {ends[l] - ep:7.0f}")
+# within-forward breakdown (wave 0): export | GEMM | epilogue | barrier | publish (to the end of the layer)
+s = stamps.cpu().double()
+for l in range(5):
+    b = s[40 + 5 * l: 45 + 5 * l].tolist()
+    start, end = s[1 + l], s[2 + l]
+    print(f"fwd{l + 1}: export {b[0] - start:7.0f}  gemm {b[1] - b[0]:7.0f}  epi {b[2] - b[1]:7.0f}  "
+          f"sync {b[3] - b[2]:7.0f}  publish {b[4] - b[3]:7.0f}  tail {end - b[4]:7.0f}")
