@@ -25,6 +25,12 @@
 #pragma once
 #include "rx_common.h"
 
+// No implicit multiply-add contraction in the training kernels: whether the compiler fuses an
+// a * b + c depends on the inlining context (and on what the SLP vectorizer pairs into v_pk_*
+// ops), so the same expression could round differently in the launch-per-step kernel and in
+// the persistent epoch kernel. Fused multiply-adds are written out (fmaf) where they pay.
+#pragma clang fp contract(off)
+
 // timing experiments only (raydp_amd/ops/mlp_jit.py RAYDP_MLP_EXPERIMENT): drop a store class
 #ifdef RX_EXP_NOSCRATCH
 constexpr bool kExpNoScratch = true;
@@ -322,7 +328,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float dv = acc[j * MT + mt][r] - mean;
-              v += (mt * 16 + lg * 4 + r < nvalid) ? dv * dv : 0.f;
+              v = (mt * 16 + lg * 4 + r < nvalid) ? fmaf(dv, dv, v) : v;
             }
           v = rx_colsum16(v);
           const float var = v / (float)nvalid;
@@ -332,8 +338,8 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
             stats[ly.stat_off + 2 * c + 1] = invstd;
             const float unb = nvalid > 1 ? var * (float)nvalid / (float)(nvalid - 1) : var;
             float* prw = reinterpret_cast<float*>(smem + d.pr_lds_off) + ly.pr_off;
-            prw[3 * ly.out_n + c] = (1.f - ly.momentum) * prw[3 * ly.out_n + c] + ly.momentum * mean;
-            prw[4 * ly.out_n + c] = (1.f - ly.momentum) * prw[4 * ly.out_n + c] + ly.momentum * unb;
+            prw[3 * ly.out_n + c] = fmaf(1.f - ly.momentum, prw[3 * ly.out_n + c], ly.momentum * mean);
+            prw[4 * ly.out_n + c] = fmaf(1.f - ly.momentum, prw[4 * ly.out_n + c], ly.momentum * unb);
           }
           // save the BN input for the backward pass (fragment-major, see frag_off)
 #pragma unroll
@@ -351,7 +357,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float t = (acc[j * MT + mt][r] - mean) * invstd * gam + bet;
+            const float t = fmaf((acc[j * MT + mt][r] - mean) * invstd, gam, bet);
             acc[j * MT + mt][r] = act_after ? act_fwd(ly.act, t) : t;
           }
       } else if (TRAIN && !last) {
@@ -391,7 +397,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
               const float e = acc[j * MT + mt][r] - t;
               const float ae = fabsf(e);
               asum += ae;
-              ssum += e * e;
+              ssum = fmaf(e, e, ssum);
               const float sgn = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
               const bool quad = ae < beta;
               lsum += quad ? 0.5f * e * e / beta : ae - 0.5f * beta;  // smooth-L1 term
@@ -438,18 +444,14 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       const int c = n * 16 + lr;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        u16 h[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          h[r] = rx_f2bf(acc[j * MT + mt][r]);
-          R[(mt * 16 + lg * 4 + r) * RS + c] = h[r];
-        }
-        if (TRAIN || !last) {
-          uint2 pk;
-          pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-          pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
-          *reinterpret_cast<uint2*>(dstT + c * tstride + mt * 16 + lg * 4) = pk;
-        }
+        uint2 pk;
+        pk.x = rx_f2bf2(acc[j * MT + mt][0], acc[j * MT + mt][1]);
+        pk.y = rx_f2bf2(acc[j * MT + mt][2], acc[j * MT + mt][3]);
+        R[(mt * 16 + lg * 4 + 0) * RS + c] = (u16)pk.x;
+        R[(mt * 16 + lg * 4 + 1) * RS + c] = (u16)(pk.x >> 16);
+        R[(mt * 16 + lg * 4 + 2) * RS + c] = (u16)pk.y;
+        R[(mt * 16 + lg * 4 + 3) * RS + c] = (u16)(pk.y >> 16);
+        if (TRAIN || !last) *reinterpret_cast<uint2*>(dstT + c * tstride + mt * 16 + lg * 4) = pk;
       }
     }
   }
@@ -677,13 +679,13 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 #pragma unroll
       for (int q = 0; q < MT * 4; ++q) {
         xh[q] = (sv[q] - mean) * invstd;
-        g[q] = (relu_after && !(xh[q] * gam + bet > 0.f)) ? 0.f : g[q];
+        g[q] = (relu_after && !(fmaf(xh[q], gam, bet) > 0.f)) ? 0.f : g[q];
       }
       float sg = 0.f, sgx = 0.f;
 #pragma unroll
       for (int q = 0; q < MT * 4; ++q) {
         sg += g[q];
-        sgx += g[q] * xh[q];
+        sgx = fmaf(g[q], xh[q], sgx);
       }
       sg = rx_colsum16(sg);
       sgx = rx_colsum16(sgx);
@@ -696,7 +698,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 #pragma unroll
       for (int q = 0; q < MT * 4; ++q) {
         const int row = (q >> 2) * 16 + lg * 4 + (q & 3);
-        float dz = k1 * (g[q] - sg * inv_n - xh[q] * sgx * inv_n);
+        float dz = k1 * (fmaf(-sg, inv_n, g[q]) - xh[q] * (sgx * inv_n));
         dz = (relu_before && !(sv[q] > 0.f)) ? 0.f : dz;
         g[q] = (row < nvalid && colok) ? dz : 0.f;
       }
@@ -710,15 +712,13 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     // publish G_{l-1}
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      u16 h[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        h[r] = rx_f2bf(g[mt * 4 + r]);
-        R[(mt * 16 + lg * 4 + r) * RS + c] = h[r];
-      }
       uint2 pk;
-      pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-      pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+      pk.x = rx_f2bf2(g[mt * 4 + 0], g[mt * 4 + 1]);
+      pk.y = rx_f2bf2(g[mt * 4 + 2], g[mt * 4 + 3]);
+      R[(mt * 16 + lg * 4 + 0) * RS + c] = (u16)pk.x;
+      R[(mt * 16 + lg * 4 + 1) * RS + c] = (u16)(pk.x >> 16);
+      R[(mt * 16 + lg * 4 + 2) * RS + c] = (u16)pk.y;
+      R[(mt * 16 + lg * 4 + 3) * RS + c] = (u16)(pk.y >> 16);
       *reinterpret_cast<uint2*>(GT + c * XS + mt * 16 + lg * 4) = pk;
     }
   }

@@ -8,6 +8,8 @@
 #pragma once
 #include "rx_common.h"
 
+#pragma clang fp contract(off)  // see mlp_core.h
+
 #ifndef RX_MAXL
 #define RX_MAXL 8
 #endif
