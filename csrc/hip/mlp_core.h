@@ -175,7 +175,11 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restric
 // The first PK k-steps of a tile's weight fragments, fetched ahead of time (before the work
 // that precedes the GEMM) so their global round trip overlaps that work.
 constexpr int RX_PJ = 2;  // tiles per wave prefetched
+#ifdef RX_EXP_PK8
+constexpr int RX_PK = 8;  // measured: no gain over 4 (27.95 vs 27.80 us per persistent step)
+#else
 constexpr int RX_PK = 4;  // k-steps per tile prefetched
+#endif
 template <bool PS>
 __device__ __forceinline__ void gemm_prefetch(bf16x8 (&pre)[RX_PK], const u16* __restrict__ img, int boff, int K,
                                               int lg) {
@@ -254,7 +258,8 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
                               float* __restrict__ Gr, const float* __restrict__ labels,
                               const int* __restrict__ rowidx, int nvalid, float* __restrict__ scratch,
                               double* __restrict__ metrics, bf16x8 (&wpre)[RX_PJ][RX_PK], bool ps_wt = true,
-                              int l = 0, unsigned long long* __restrict__ stamps = nullptr) {
+                              int l = 0, unsigned long long* __restrict__ stamps = nullptr,
+                              const float* lab_pre = nullptr) {
   // optional intra-layer timeline (wave 0, s_memtime): [40 + 5 l ..] export, GEMM, epilogue,
   // first barrier, publish + second barrier
   auto fst = [&](int k) {
@@ -384,8 +389,13 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         // labels of all padded rows, loaded back to back (padded rows read row 0)
         const int cl = colok ? c : 0;
         float tl[MT * 4];
+        if (lab_pre != nullptr && ly.out_n == 16) {  // fetched at the start of the step
 #pragma unroll
-        for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
+          for (int q = 0; q < MT * 4; ++q) tl[q] = lab_pre[q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
+        }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -779,6 +789,18 @@ __device__ __forceinline__ void store_running_stats(const D& d, char* smem, floa
   });
 }
 
+// The labels the loss of a single-tile output layer (out <= 16 columns: wave 0, tile 0) reads,
+// fetched right after the batch's row indices are known: their dependent global round trip
+// overlaps the forward instead of sitting in the last layer's epilogue.
+template <int MT, bool PS, class D>
+__device__ __forceinline__ void prefetch_labels(const D& d, const float* __restrict__ labels, const int* rowidx,
+                                                float (&tl)[MT * 4]) {
+  const int lane = rx_tid<PS>() & 63, lr = lane & 15, lg = lane >> 4;
+  const int cl = lr < d.out_dim ? lr : 0;
+#pragma unroll
+  for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
+}
+
 // load the batch's feature rows (gathered through the epoch permutation) into R and XT_0
 template <int MT, bool PS = false, class D, class L0>
 __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem, const u16* __restrict__ feats,
@@ -831,10 +853,12 @@ __device__ __forceinline__ void mlp_train_step_body(
   load_params<C>(d, smem, P, rstats);
   __syncthreads();
   load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, true);
+  float labp[MT * 4];
+  prefetch_labels<MT, false>(d, labels, rowidx, labp);
   RX_STAMP();
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
     layer_forward<MT, true, false>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre,
-                                   true, l, stamps);
+                                   true, l, stamps, labp);
     RX_STAMP();
   });
   store_running_stats<C>(d, smem, rstats);

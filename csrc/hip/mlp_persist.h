@@ -191,6 +191,8 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     __syncthreads();
     // the batch gather does not depend on the weights: it overlaps the last optimizer tiles
     load_inputs<MT, true>(d, C::first(d), smem, feats, rowidx, nvalid, true);
+    float labp[MT * 4];
+    prefetch_labels<MT, true>(d, labels, rowidx, labp);
     stamp(s, 1);
     if (s > 0) {
       if (rx_tid() < 64) {
@@ -230,7 +232,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     fwd_prefetch<true>(C::first(d), img, wpre);
     C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
       layer_forward<MT, true, true>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre,
-                                    ps_wt);
+                                    ps_wt, l, nullptr, labp);
     });
     stamp(s, 3);
     C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {

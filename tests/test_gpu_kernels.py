@@ -124,20 +124,21 @@ def test_fused_mlp_one_step_matches_torch(nvalid, loss):
                 e_fp32 = _relerr(gmap[key], getattr(rmods[name], attr).grad)
                 assert e_emu < 2e-2, (name, attr, e_emu)
                 assert e_fp32 < 0.35, (name, attr, e_fp32)
-    # optimizer step + BN running stats
+    # optimizer step against torch's Adam applied to the kernel's OWN gradient (a first Adam step
+    # moves every element by ~lr * sign(g): comparing against the emulation's gradient would
+    # flip on the near-zero BatchNorm channels, whose sign is noise in any reference)
+    p0 = tr.params.clone()
     tr.opt_step(1e-3, 1 - 0.9, 1 - 0.999, 1.0, True)
-    eopt = torch.optim.Adam(emu.parameters(), lr=1e-3)
-    eopt.step()
+    pt = p0.clone().requires_grad_(True)
+    pt.grad = g.clone()
+    torch.optim.Adam([pt], lr=1e-3).step()
+    err = _relerr(tr.params[:tr.total], pt.detach()[:tr.total])
+    assert err < 1e-4, err
     pmap = tr.unflatten(tr.params)
-    for name, mod in model.named_modules():
-        for attr in ("weight", "bias"):
-            key = (id(mod), attr)
-            if key in pmap:
-                err = _relerr(pmap[key], getattr(emods[name], attr).data)
-                assert err < 5e-3, (name, attr, err)
-                if float(getattr(emods[name], attr).grad.abs().max()) > 1e-6:
-                    moved = _relerr(pmap[key], getattr(rmods[name], attr).data)
-                    assert moved > 0, (name, attr, "parameter not updated")
+    p0map = tr.unflatten(p0)
+    for key in pmap:
+        if float(gmap[key].abs().max()) > 1e-6:
+            assert not torch.equal(pmap[key], p0map[key]), (key, "parameter not updated")
     for bn, rm, rv in tr.run_bufs:
         name = [n for n, mm in model.named_modules() if mm is bn][0]
         assert _relerr(rm, rmods[name].running_mean) < 3e-2
