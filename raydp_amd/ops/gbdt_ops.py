@@ -1,0 +1,71 @@
+"""GBDT gradient histograms (``csrc/hip/gbdt_hist.hip``).
+
+``level_histogram`` builds the (node, feature, bin) -> (sum g, sum h) table of one tree level.
+On a GPU it runs the gfx950 kernel (LDS-privatised fp64 atomics, one launch per level) and
+raises if ``libhipkernels.so`` is missing; on the CPU it is the ``index_add_`` expression that
+``torch_level_histogram`` also exposes as the numerics reference for tests.
+
+Parity: the reference's histogram step lives inside xgboost-ray's ``hist`` tree method
+(``python/raydp/xgboost/estimator.py:54-81``), not in RayDP's own code.
+"""
+import ctypes
+
+import torch
+
+from raydp_amd.ops import _hip
+
+_bound = False
+
+
+def _lib():
+    global _bound
+    L = _hip.lib()
+    if not _bound:
+        vp, i, ll = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+        L.rx_gbdt_hist.argtypes = [vp, vp, vp, vp, vp, ll, i, i, i, vp]
+        L.rx_gbdt_hist.restype = i
+        L.rx_gbdt_hist_group.argtypes = [i, i]
+        L.rx_gbdt_hist_group.restype = i
+        _bound = True
+    return L
+
+
+def torch_level_histogram(bins: torch.Tensor, pos: torch.Tensor, g: torch.Tensor, h: torch.Tensor, K: int,
+                          B: int) -> torch.Tensor:
+    """Reference expression: ``bins`` [n, F] (row-major), ``pos`` [n] (-1 = inactive)."""
+    n, F = bins.shape
+    act = pos >= 0
+    feat_off = (torch.arange(F, device=bins.device) * B)[None, :]
+    idx = pos.clamp_min(0)[:, None] * (F * B) + feat_off + bins.long()
+    gh = torch.stack([g, h], 1).double()
+    hist = torch.zeros(K * F * B, 2, dtype=torch.float64, device=bins.device)
+    hist.index_add_(0, idx[act].reshape(-1), gh[act].repeat_interleave(F, dim=0))
+    return hist
+
+
+def level_histogram(bins_t: torch.Tensor, pos: torch.Tensor, g: torch.Tensor, h: torch.Tensor, K: int,
+                    B: int) -> torch.Tensor:
+    """Histogram [K*F*B, 2] fp64 from column-major ``bins_t`` [F, n] int16 on a GPU."""
+    F, n = bins_t.shape
+    dev = bins_t.device
+    if dev.type != "cuda":
+        return torch_level_histogram(bins_t.t(), pos, g, h, K, B)
+    if bins_t.dtype != torch.int16 or not bins_t.is_contiguous():
+        raise ValueError("bins_t must be a contiguous int16 [F, n] tensor")
+    L = _lib()
+    if L.rx_gbdt_hist_group(int(K), int(B)) <= 0:
+        raise ValueError(f"{B} bins per feature exceed the histogram kernel's LDS slice (max_bin too large)")
+    pos = pos.to(torch.long).contiguous()
+    g = g.to(torch.float32).contiguous()
+    h = h.to(torch.float32).contiguous()
+    if pos.shape[0] != n or g.shape[0] != n or h.shape[0] != n:
+        raise ValueError("pos/g/h must have one entry per row of bins_t")
+    for t in (pos, g, h):
+        if t.device != dev:
+            raise ValueError("all operands must live on the same GPU")
+    hist = torch.zeros(K * F * B, 2, dtype=torch.float64, device=dev)
+    _hip.check(L.rx_gbdt_hist(ctypes.c_void_p(bins_t.data_ptr()), ctypes.c_void_p(pos.data_ptr()),
+                              ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(h.data_ptr()),
+                              ctypes.c_void_p(hist.data_ptr()), n, F, int(B), int(K), _hip.stream_ptr(dev)),
+               "rx_gbdt_hist")
+    return hist

@@ -8,7 +8,8 @@ algorithm natively:
 * features are quantised once into ``max_bin`` quantile bins (bin 0 = missing), cut points
   agreed across workers from an all-gathered sample;
 * trees grow level-wise to ``max_depth``; each level builds one (node, feature, bin) histogram
-  of (gradient, hessian) with a single ``scatter_add`` over the binned matrix, all-reduces it
+  of (gradient, hessian) -- one launch of the gfx950 kernel ``csrc/hip/gbdt_hist.hip`` on a GPU
+  (LDS-privatised fp64 atomics), one ``index_add_`` on the CPU -- all-reduces it
   (``torch.distributed`` – RCCL on MI355X, gloo on CPU) exactly like Rabit's histogram
   all-reduce, and evaluates every split with XGBoost's gain
   ``G_L²/(H_L+λ) + G_R²/(H_R+λ) − G²/(H+λ)`` including the learned default direction for
@@ -185,28 +186,45 @@ class World:
 
 
 # ---------------------------------------------------------------------------- binning ----
-def compute_cuts(x: torch.Tensor, max_bin: int, world: World, sample: int = 200_000, seed: int = 0) -> List[torch.Tensor]:
-    """Per-feature cut points from (all-gathered) quantiles; identical on every worker."""
+def compute_cuts(x: torch.Tensor, max_bin: int, world: World, sample: int = 200_000, seed: int = 0,
+                 device: Optional[torch.device] = None) -> List[torch.Tensor]:
+    """Per-feature cut points from (all-gathered) quantiles; identical on every worker.
+
+    One column-wise sort of the sample (on ``device`` when given, e.g. the GPU) serves every
+    feature: distinct-value counts come from the sorted columns' steps, quantiles from linear
+    interpolation between order statistics (``torch.quantile``'s default), NaNs sort last.
+    """
     g = torch.Generator().manual_seed(seed)
     xs = x if x.shape[0] <= sample else x[torch.randperm(x.shape[0], generator=g)[:sample]]
     xs = world.allgather_rows(xs.float().cpu())
-    qs = torch.linspace(0, 1, max_bin - 1, dtype=torch.float64)[1:-1]
+    if xs.shape[1] == 0:
+        return []
+    srt = torch.sort(xs.to(device or "cpu").double(), dim=0).values          # NaN last
+    m = (~torch.isnan(srt)).sum(0)                                             # non-NaN rows per feature
+    step = (srt[1:] != srt[:-1]) & ~torch.isnan(srt[1:])
+    distinct = torch.where(m > 0, 1 + step.sum(0), torch.zeros_like(m))
+    qs = torch.linspace(0, 1, max_bin - 1, dtype=torch.float64, device=srt.device)[1:-1]
+    posq = qs[:, None] * (m.clamp_min(1) - 1).double()[None, :]               # (Q, F)
+    lo = posq.floor().long()
+    hi = posq.ceil().long()
+    a_lo, a_hi = srt.gather(0, lo), srt.gather(0, hi)
+    quant = a_lo + (a_hi - a_lo) * (posq - lo.double())
+    last = srt.gather(0, (m.clamp_min(1) - 1)[None, :])[0]                     # per-feature max
+    srt, quant, m, distinct, last = (t.cpu() for t in (srt, quant, m, distinct, last))
     cuts = []
     for f in range(xs.shape[1]):
-        col = xs[:, f].double()
-        col = col[~torch.isnan(col)]
-        if col.numel() == 0:
+        if int(m[f]) == 0:
             cuts.append(torch.empty(0))
             continue
-        u = torch.unique(col)
-        if u.numel() <= max_bin - 2:
+        top = last[f:f + 1]
+        pad = top + torch.clamp(top.abs() * 1e-6, min=1e-6)
+        if int(distinct[f]) <= max_bin - 2:
             # all distinct values: cut between neighbours so every value gets its own bin
+            u = torch.unique_consecutive(srt[:int(m[f]), f])
             c = (u[1:] + u[:-1]) / 2 if u.numel() > 1 else u[:0]
-            c = torch.cat([c, u[-1:] + torch.clamp(u[-1:].abs() * 1e-6, min=1e-6)])
         else:
-            c = torch.unique(torch.quantile(col, qs))
-            c = torch.cat([c, u[-1:] + torch.clamp(u[-1:].abs() * 1e-6, min=1e-6)])
-        cuts.append(c.float())
+            c = torch.unique(quant[:, f])
+        cuts.append(torch.cat([c, pad]).float())
     return cuts
 
 
@@ -304,8 +322,14 @@ def _soft(g, alpha):
 
 
 def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: torch.Tensor, p: Dict,
-              world: World, feat_mask: Optional[torch.Tensor] = None) -> Tuple[Tree, torch.Tensor]:
-    """One tree on binned data; returns the tree and each row's leaf value (for margin update)."""
+              world: World, feat_mask: Optional[torch.Tensor] = None,
+              bins_t: Optional[torch.Tensor] = None) -> Tuple[Tree, torch.Tensor]:
+    """One tree on binned data; returns the tree and each row's leaf value (for margin update).
+
+    On a GPU each level's histogram is one launch of the gfx950 kernel
+    (:func:`raydp_amd.ops.gbdt_ops.level_histogram`) over ``bins_t`` (column-major bins,
+    transposed here if the caller did not pass them); on the CPU it is ``index_add_``.
+    """
     dev = bins.device
     n, F = bins.shape
     B = int(max(c.numel() for c in cuts) + 2) if cuts else 2
@@ -318,25 +342,59 @@ def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: 
     leaf_of_row = torch.zeros(n, dtype=torch.long, device=dev)
     feat_off = (torch.arange(F, device=dev) * B)[None, :]
     bins_l = bins.long()
-    gh = torch.stack([g, h], 1).double()
+    on_gpu = dev.type == "cuda"
+    if on_gpu:
+        from raydp_amd.ops.gbdt_ops import level_histogram
+        if bins_t is None:
+            bins_t = bins.t().contiguous()
+        g32, h32 = g.float().contiguous(), h.float().contiguous()
+    else:
+        gh = torch.stack([g, h], 1).double()
     ncuts = torch.tensor([c.numel() for c in cuts], device=dev)
+
+    def build(slot, nslots):
+        """(nslots, F, B, 2) histogram of the rows with slot >= 0, all-reduced over workers."""
+        if on_gpu:
+            hs = level_histogram(bins_t, slot, g32, h32, nslots, B)
+        else:
+            sel = slot >= 0
+            idx = (slot.clamp_min(0)[:, None] * (F * B) + feat_off + bins_l)
+            hs = torch.zeros(nslots * F * B, 2, dtype=torch.float64, device=dev)
+            hs.index_add_(0, idx[sel].reshape(-1), gh[sel].repeat_interleave(F, dim=0))
+        world.allreduce(hs)
+        return hs.view(nslots, F, B, 2)
+
+    pair_parent: List[int] = []                            # level-k pairs (2j, 2j+1) split from parent k'
+    prev_hist = None
     for depth in range(int(p["max_depth"]) + 1):
         K = len(level)
         act = pos >= 0
-        idx = (pos.clamp_min(0)[:, None] * (F * B) + feat_off + bins_l)
-        hist = torch.zeros(K * F * B, 2, dtype=torch.float64, device=dev)
-        sel = idx[act].reshape(-1)
-        hist.index_add_(0, sel, gh[act].repeat_interleave(F, dim=0))
-        world.allreduce(hist)
-        hist = hist.view(K, F, B, 2)
+        if prev_hist is None:
+            hist = build(pos, K)
+        else:
+            # sibling subtraction (XGBoost's hist trick): build only the child with fewer rows
+            # (global counts, so every worker picks the same one), derive the other from the parent
+            cnt = torch.bincount(pos[act], minlength=K).double()
+            world.allreduce(cnt)
+            cnt = cnt.cpu()
+            small = [2 * j + int(cnt[2 * j + 1] < cnt[2 * j]) for j in range(K // 2)]
+            slot_of = torch.full((K + 1,), -1, dtype=torch.long)
+            slot_of[torch.tensor(small, dtype=torch.long)] = torch.arange(K // 2)
+            slot_of = slot_of.to(dev)
+            hs = build(slot_of[torch.where(act, pos, torch.full_like(pos, K))], K // 2)
+            large = torch.tensor([s ^ 1 for s in small], dtype=torch.long, device=dev)
+            hist = torch.empty((K, F, B, 2), dtype=torch.float64, device=dev)
+            hist[torch.tensor(small, dtype=torch.long, device=dev)] = hs
+            hist[large] = prev_hist[torch.tensor(pair_parent, dtype=torch.long, device=dev)] - hs
         tot = hist[:, 0, :, :].sum(1)                         # (K, 2) node totals
         G, H = tot[:, 0], tot[:, 1]
+        tc = tot.cpu()                                         # one device->host copy per level
+        wc = -_soft(tc[:, 0], alpha) / (tc[:, 1] + lam)
+        if mds > 0:
+            wc = torch.clamp(wc, -mds, mds)
         for k, nid in enumerate(level):
-            tree.cover[nid] = float(H[k])
-            w = -_soft(G[k], alpha) / (H[k] + lam)
-            if mds > 0:
-                w = torch.clamp(w, -mds, mds)
-            tree.value[nid] = float(w) * eta
+            tree.cover[nid] = float(tc[k, 1])
+            tree.value[nid] = float(wc[k]) * eta
         if depth == int(p["max_depth"]):
             break
         miss = hist[:, :, 0, :]                                # (K, F, 2)
@@ -361,10 +419,12 @@ def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: 
             best_gain = torch.where(better, gbest, best_gain)
             f_b = torch.stack([arg // cum.shape[2], arg % cum.shape[2], torch.full_like(arg, dl)], 1)
             best = torch.where(better[:, None], f_b, best)
-        new_level, remap = [], torch.full((K,), -1, dtype=torch.long, device=dev)
-        split_feat = torch.full((K,), -1, dtype=torch.long, device=dev)
-        split_bin = torch.zeros((K,), dtype=torch.long, device=dev)
-        split_dl = torch.zeros((K,), dtype=torch.bool, device=dev)
+        # split bookkeeping on the host, shipped to the device in one copy per table
+        prev_hist, pair_parent = hist, []
+        new_level, remap = [], torch.full((K,), -1, dtype=torch.long)
+        split_feat = torch.full((K,), -1, dtype=torch.long)
+        split_bin = torch.zeros((K,), dtype=torch.long)
+        split_dl = torch.zeros((K,), dtype=torch.bool)
         bg, bb = best_gain.cpu(), best.cpu()
         for k, nid in enumerate(level):
             if float(bg[k]) <= max(gamma, 1e-6):
@@ -377,8 +437,10 @@ def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: 
             tree.left[nid] = tree.add()
             tree.right[nid] = tree.add()
             remap[k] = len(new_level)
+            pair_parent.append(k)
             new_level += [tree.left[nid], tree.right[nid]]
             split_feat[k], split_bin[k], split_dl[k] = f, t + 1, dl
+        remap, split_feat, split_bin, split_dl = (t.to(dev) for t in (remap, split_feat, split_bin, split_dl))
         # rows in nodes that became leaves keep their leaf id; others move down
         cur = pos.clamp_min(0)
         node_ids = torch.tensor(level, dtype=torch.long, device=dev)
@@ -500,8 +562,9 @@ def train(params: Dict, dtrain: DMatrix, num_boost_round: int = 10, evals: Seque
     k = int(p["num_class"]) if obj.startswith("multi:") else 1
     x = dtrain.data
     y = dtrain.label.to(dev)
-    cuts = compute_cuts(x, int(p["max_bin"]), world, seed=int(p["seed"]))
+    cuts = compute_cuts(x, int(p["max_bin"]), world, seed=int(p["seed"]), device=dev)
     bins = bin_matrix(x.to(dev), cuts)
+    bins_t = bins.t().contiguous() if dev.type == "cuda" else None   # coalesced per-feature reads
     bst = Booster(p)
     bst.feature_names = dtrain.feature_names
     bst.base_margin = _base_margin(obj, dtrain.label, p["base_score"], world)
@@ -535,7 +598,7 @@ def train(params: Dict, dtrain: DMatrix, num_boost_round: int = 10, evals: Seque
         rtrees = []
         for j in range(k):
             gj, hj = (g[:, j], h[:, j]) if k > 1 else (g, h)
-            tree, leaf_vals = grow_tree(bins, cuts, gj, hj, p, world, fmask)
+            tree, leaf_vals = grow_tree(bins, cuts, gj, hj, p, world, fmask, bins_t)
             rtrees.append(tree)
             if k > 1:
                 margin[:, j] += leaf_vals
