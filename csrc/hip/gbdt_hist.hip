@@ -22,44 +22,72 @@
 #define GH_THREADS 256
 #define GH_LDS_BYTES 65536
 
+#define GH_UNROLL 4
+
 __global__ __launch_bounds__(GH_THREADS) void gbdt_hist_kernel(const int16_t* __restrict__ binsT,
                                                               const long long* __restrict__ pos,
                                                               const float* __restrict__ g,
                                                               const float* __restrict__ h, double* __restrict__ hist,
                                                               long long n, int F, int B, int K, int KG,
                                                               long long rows_per_chunk) {
+  // Two planes (sum g | sum h) rather than interleaved pairs: a double at index 2b maps onto
+  // only 16 distinct bank pairs of the 64-bank LDS, index b onto 32.
   extern __shared__ double sh[];
   const int tid = threadIdx.x;
   const int f = blockIdx.y;
   const int k0 = blockIdx.z * KG;
   const int kg = min(KG, K - k0);
-  const int ent = kg * B * 2;
-  for (int i = tid; i < ent; i += GH_THREADS) sh[i] = 0.0;
+  const int plane = kg * B;
+  double* shg = sh;
+  double* shh = sh + plane;
+  for (int i = tid; i < 2 * plane; i += GH_THREADS) sh[i] = 0.0;
   __syncthreads();
 
   const long long r0 = (long long)blockIdx.x * rows_per_chunk;
   const long long r1 = min(n, r0 + rows_per_chunk);
   const int16_t* col = binsT + (long long)f * n;
-  for (long long r = r0 + tid; r < r1; r += GH_THREADS) {
-    const long long p = pos[r];
-    const unsigned kk = (unsigned)(p - k0);
-    if (p >= 0 && kk < (unsigned)kg) {
-      const unsigned b = (unsigned)(unsigned short)col[r];
-      if (b < (unsigned)B) {
-        double* e = sh + ((kk * B + b) << 1);
-        atomicAdd(e, (double)g[r]);
-        atomicAdd(e + 1, (double)h[r]);
+  // GH_UNROLL rows per thread per trip: all loads of a trip are issued before the first LDS
+  // atomic, so each wave keeps several HBM requests in flight instead of one.
+  for (long long base = r0; base < r1; base += (long long)GH_THREADS * GH_UNROLL) {
+    long long p[GH_UNROLL];
+#pragma unroll
+    for (int u = 0; u < GH_UNROLL; ++u) {
+      const long long r = base + tid + u * GH_THREADS;
+      p[u] = r < r1 ? pos[r] : -1;
+    }
+    unsigned slot[GH_UNROLL];
+    float gv[GH_UNROLL], hv[GH_UNROLL];
+#pragma unroll
+    for (int u = 0; u < GH_UNROLL; ++u) {
+      const long long r = base + tid + u * GH_THREADS;
+      const unsigned kk = (unsigned)(p[u] - k0);
+      slot[u] = 0xffffffffu;
+      gv[u] = 0.f;
+      hv[u] = 0.f;
+      if (p[u] >= 0 && kk < (unsigned)kg) {
+        const unsigned b = (unsigned)(unsigned short)col[r];
+        if (b < (unsigned)B) slot[u] = kk * B + b;
+        gv[u] = g[r];
+        hv[u] = h[r];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GH_UNROLL; ++u) {
+      if (slot[u] != 0xffffffffu) {
+        atomicAdd(shg + slot[u], (double)gv[u]);
+        atomicAdd(shh + slot[u], (double)hv[u]);
       }
     }
   }
   __syncthreads();
 
-  // slice of node kk for this feature: hist[((k0 + kk) * F + f) * B * 2 + j], j < 2B
-  const int sl = B * 2;
+  // node kk of this feature: hist[((k0 + kk) * F + f) * B * 2 + 2 * b + c]
   const bool owner = gridDim.x == 1;  // single row chunk: this workgroup owns the slice outright
-  for (int i = tid; i < ent; i += GH_THREADS) {
-    const int kk = i / sl, j = i - kk * sl;
-    double* dst = hist + ((long long)(k0 + kk) * F + f) * sl + j;
+  for (int i = tid; i < 2 * plane; i += GH_THREADS) {
+    const int c = i >= plane;
+    const int e = i - c * plane;
+    const int kk = e / B, b = e - kk * B;
+    double* dst = hist + ((long long)(k0 + kk) * F + f) * (2 * B) + 2 * b + c;
     const double v = sh[i];
     if (owner)
       *dst = v;
