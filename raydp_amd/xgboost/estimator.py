@@ -43,6 +43,7 @@ def _train_loop(config):
 
     def on_round(rnd, bst, res):
         metrics = {f"{name}-{m}": vals[-1] for name, d in res.items() for m, vals in d.items()}
+        metrics["device"] = dev                     # "cuda": histograms ran on the gfx950 kernel
         ck = None
         if rank == 0:
             bst.save_model(os.path.join(ckdir, MODEL_FILE))

@@ -60,3 +60,31 @@ def test_booster_gpu_matches_cpu():
     pc = cpu.predict(gbdt.DMatrix(x))
     pg = gpu.predict(gbdt.DMatrix(x))
     np.testing.assert_allclose(np.asarray(pg), np.asarray(pc), rtol=1e-5, atol=1e-5)
+
+
+def test_xgboost_estimator_trains_on_gpu():
+    import raydp_amd
+    from raydp_amd import runtime
+    from raydp_amd.spark.functions import rand
+    from raydp_amd.utils import random_split
+    from raydp_amd.xgboost import XGBoostEstimator
+    runtime.shutdown()
+    runtime.init(num_cpus=4, num_gpus=1)
+    try:
+        spark = raydp_amd.init_spark("gpu-xgb", 1, 2, "500M")
+        df = spark.range(0, 20000)
+        df = df.withColumn("x", rand() * 100)
+        df = df.withColumn("y", rand() * 1000)
+        df = df.withColumn("z", df.x * 3 + df.y * 4 + rand() + 5)
+        train_df, test_df = random_split(df.select(df.x, df.y, df.z), [0.7, 0.3])
+        est = XGBoostEstimator({"max_depth": 8, "eta": 0.3, "num_boost_round": 30}, "z",
+                               resources_per_worker={"CPU": 1, "GPU": 1})
+        est.fit_on_spark(train_df, test_df)
+        hist = est.results.metrics_history
+        assert hist[-1]["device"] == "cuda"
+        assert hist[-1]["evaluate-rmse"] < 0.1 * hist[0]["evaluate-rmse"]
+        pred = est.get_model().inplace_predict(np.asarray([[50, 500]]))
+        assert abs(pred[0] - (150 + 2000 + 5.5)) < 0.05 * 2155
+    finally:
+        raydp_amd.stop_spark()
+        runtime.shutdown()
