@@ -96,6 +96,96 @@ __global__ __launch_bounds__(GH_THREADS) void gbdt_hist_kernel(const int16_t* __
   }
 }
 
+// ---------------------------------------------------------------------------- split search ----
+// One wavefront per (node, feature): the B-1 candidate thresholds (bins 1..t go left) are split
+// into contiguous runs per lane; a wave-wide exclusive scan of the run sums gives every lane its
+// starting prefix, then each lane walks its run evaluating XGBoost's gain for both default
+// directions of missing values (dl = 1: bin 0 goes left). Replaces the cumsum + ~40 elementwise
+// kernels + 2 reductions of the tensor formulation with one launch per level.
+// out[(k * F + f) * 4 + {0,1,2,3}] = {gain dl=1, t dl=1, gain dl=0, t dl=0}; ties keep the lowest t.
+__device__ __forceinline__ double gh_soft(double g, double alpha) {
+  if (alpha <= 0.0) return g;
+  const double a = fabs(g) - alpha;
+  return a > 0.0 ? copysign(a, g) : 0.0;
+}
+
+__device__ __forceinline__ void gh_best_reduce(double& gain, int& t) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const double og = __shfl_xor(gain, off, 64);
+    const int ot = __shfl_xor(t, off, 64);
+    if (og > gain || (og == gain && ot < t)) {
+      gain = og;
+      t = ot;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void gbdt_split_kernel(const double* __restrict__ hist, const double* __restrict__ tot,
+                                                       const int* __restrict__ ncuts,
+                                                       const unsigned char* __restrict__ fmask, double* __restrict__ out,
+                                                       int F, int B, double lam, double alpha, double mcw) {
+  const int kf = blockIdx.x;
+  const int k = kf / F, f = kf - k * F;
+  const int lane = threadIdx.x;
+  double* o = out + (long long)kf * 4;
+  if (fmask != nullptr && !fmask[f]) {
+    if (lane == 0) {
+      o[0] = -1.0; o[1] = 0.0; o[2] = -1.0; o[3] = 0.0;
+    }
+    return;
+  }
+  const double* hf = hist + (long long)kf * B * 2;
+  const int nt = B - 1;                 // thresholds t = 0 .. B-2 (bins 1..t+1 go left)
+  const int valid_t = ncuts[f];         // t must index a real cut
+  const int run = (nt + 63) / 64;
+  const int t0 = min(lane * run, nt), t1 = min(t0 + run, nt);
+  double sg = 0.0, sh = 0.0;
+  for (int t = t0; t < t1; ++t) {
+    sg += hf[2 * (t + 1)];
+    sh += hf[2 * (t + 1) + 1];
+  }
+  // inclusive scan over lanes, then exclusive = inclusive - own
+  double ig = sg, ih = sh;
+  for (int off = 1; off < 64; off <<= 1) {
+    const double ug = __shfl_up(ig, off, 64), uh = __shfl_up(ih, off, 64);
+    if (lane >= off) {
+      ig += ug;
+      ih += uh;
+    }
+  }
+  double cg = ig - sg, ch = ih - sh;
+  const double G = tot[2 * k], H = tot[2 * k + 1];
+  const double mg = hf[0], mh = hf[1];
+  const double sG = gh_soft(G, alpha);
+  const double parent = sG * sG / (H + lam);
+  double best1 = -1.0, best0 = -1.0;
+  int bt1 = 0x7fffffff, bt0 = 0x7fffffff;
+  for (int t = t0; t < t1; ++t) {
+    cg += hf[2 * (t + 1)];
+    ch += hf[2 * (t + 1) + 1];
+    if (t >= valid_t) continue;
+#pragma unroll
+    for (int dl = 1; dl >= 0; --dl) {
+      const double Lg = cg + (dl ? mg : 0.0), Lh = ch + (dl ? mh : 0.0);
+      const double Rg = G - Lg, Rh = H - Lh;
+      if (!(Lh >= mcw && Rh >= mcw)) continue;
+      const double sl = gh_soft(Lg, alpha), sr = gh_soft(Rg, alpha);
+      const double gain = sl * sl / (Lh + lam) + sr * sr / (Rh + lam) - parent;
+      if (dl) {
+        if (gain > best1) { best1 = gain; bt1 = t; }
+      } else {
+        if (gain > best0) { best0 = gain; bt0 = t; }
+      }
+    }
+  }
+  gh_best_reduce(best1, bt1);
+  gh_best_reduce(best0, bt0);
+  if (lane == 0) {
+    o[0] = best1; o[1] = bt1 == 0x7fffffff ? 0.0 : (double)bt1;
+    o[2] = best0; o[3] = bt0 == 0x7fffffff ? 0.0 : (double)bt0;
+  }
+}
+
 static inline long long gh_cdiv(long long a, long long b) { return (a + b - 1) / b; }
 
 extern "C" {
@@ -124,6 +214,15 @@ int rx_gbdt_hist(const int16_t* binsT, const long long* pos, const float* g, con
   const size_t lds = (size_t)KG * B * 2 * sizeof(double);
   hipLaunchKernelGGL(gbdt_hist_kernel, dim3((unsigned)chunks, (unsigned)F, (unsigned)groups), dim3(GH_THREADS), lds, s,
                      binsT, pos, g, h, hist, n, F, B, K, KG, rpc);
+  return (int)hipGetLastError();
+}
+
+// Best split per (node, feature) for both default directions (see gbdt_split_kernel).
+int rx_gbdt_split(const double* hist, const double* tot, const int* ncuts, const unsigned char* fmask, double* out,
+                  int K, int F, int B, double lam, double alpha, double mcw, hipStream_t s) {
+  if (K <= 0 || F <= 0 || B < 2) return K <= 0 || F <= 0 ? 0 : -1;
+  hipLaunchKernelGGL(gbdt_split_kernel, dim3((unsigned)(K * F)), dim3(64), 0, s, hist, tot, ncuts, fmask, out, F, B, lam,
+                     alpha, mcw);
   return (int)hipGetLastError();
 }
 

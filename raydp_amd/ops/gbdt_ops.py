@@ -26,6 +26,9 @@ def _lib():
         L.rx_gbdt_hist.restype = i
         L.rx_gbdt_hist_group.argtypes = [i, i]
         L.rx_gbdt_hist_group.restype = i
+        d = ctypes.c_double
+        L.rx_gbdt_split.argtypes = [vp, vp, vp, vp, vp, i, i, i, d, d, d, vp]
+        L.rx_gbdt_split.restype = i
         _bound = True
     return L
 
@@ -69,3 +72,28 @@ def level_histogram(bins_t: torch.Tensor, pos: torch.Tensor, g: torch.Tensor, h:
                               ctypes.c_void_p(hist.data_ptr()), n, F, int(B), int(K), _hip.stream_ptr(dev)),
                "rx_gbdt_hist")
     return hist
+
+
+def split_candidates(hist: torch.Tensor, tot: torch.Tensor, ncuts: torch.Tensor, fmask, lam: float, alpha: float,
+                     mcw: float) -> torch.Tensor:
+    """Best threshold per (node, feature) for both default directions on a GPU.
+
+    ``hist`` [K, F, B, 2] fp64, ``tot`` [K, 2] fp64 node totals, ``ncuts`` [F] int32 real cuts per
+    feature, ``fmask`` [F] uint8 or None. Returns [K, F, 4] fp64: (gain, threshold) for
+    default-left, then for default-right; gain -1 where no valid threshold exists.
+    """
+    K, F, B, two = hist.shape
+    if two != 2 or hist.dtype != torch.float64 or hist.device.type != "cuda":
+        raise ValueError("hist must be a [K, F, B, 2] fp64 GPU tensor")
+    hist = hist.contiguous()
+    tot = tot.to(torch.float64).contiguous()
+    ncuts = ncuts.to(device=hist.device, dtype=torch.int32).contiguous()
+    if tot.shape != (K, 2) or ncuts.shape != (F,) or (fmask is not None and fmask.shape != (F,)):
+        raise ValueError("tot/ncuts/fmask shapes do not match hist")
+    out = torch.empty((K, F, 4), dtype=torch.float64, device=hist.device)
+    _hip.check(_lib().rx_gbdt_split(ctypes.c_void_p(hist.data_ptr()), ctypes.c_void_p(tot.data_ptr()),
+                                    ctypes.c_void_p(ncuts.data_ptr()),
+                                    ctypes.c_void_p(fmask.data_ptr()) if fmask is not None else None,
+                                    ctypes.c_void_p(out.data_ptr()), K, F, B, float(lam), float(alpha), float(mcw),
+                                    _hip.stream_ptr(hist.device)), "rx_gbdt_split")
+    return out

@@ -321,6 +321,22 @@ def _soft(g, alpha):
     return torch.sign(g) * torch.clamp(g.abs() - alpha, min=0.0)
 
 
+def _pick_splits(sc: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(K, F, 4) per-feature candidates -> best gain (K,) and (feature, threshold, default_left)
+    rows, with the tensor path's order: dl = 1 first, dl = 0 only if strictly better, lowest
+    feature on ties."""
+    g1, g0 = sc[:, :, 0], sc[:, :, 2]
+    f1 = torch.argmax(g1, 1) if g1.shape[1] else torch.zeros(sc.shape[0], dtype=torch.long)
+    f0 = torch.argmax(g0, 1) if g0.shape[1] else torch.zeros(sc.shape[0], dtype=torch.long)
+    r = torch.arange(sc.shape[0])
+    b1, b0 = g1[r, f1], g0[r, f0]
+    use0 = b0 > b1
+    gain = torch.where(use0, b0, b1)
+    feat = torch.where(use0, f0, f1)
+    thr = torch.where(use0, sc[r, f0, 3], sc[r, f1, 1]).long()
+    return gain, torch.stack([feat, thr, (~use0).long()], 1)
+
+
 def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: torch.Tensor, p: Dict,
               world: World, feat_mask: Optional[torch.Tensor] = None,
               bins_t: Optional[torch.Tensor] = None) -> Tuple[Tree, torch.Tensor]:
@@ -348,6 +364,9 @@ def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: 
         if bins_t is None:
             bins_t = bins.t().contiguous()
         g32, h32 = g.float().contiguous(), h.float().contiguous()
+        from raydp_amd.ops.gbdt_ops import split_candidates
+        ncuts32 = torch.tensor([c.numel() for c in cuts], dtype=torch.int32, device=dev)
+        fmask_u8 = feat_mask.to(device=dev, dtype=torch.uint8).contiguous() if feat_mask is not None else None
     else:
         gh = torch.stack([g, h], 1).double()
     ncuts = torch.tensor([c.numel() for c in cuts], device=dev)
@@ -397,28 +416,34 @@ def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: 
             tree.value[nid] = float(wc[k]) * eta
         if depth == int(p["max_depth"]):
             break
-        miss = hist[:, :, 0, :]                                # (K, F, 2)
-        cum = hist[:, :, 1:, :].cumsum(2)                      # bins 1..t go left
-        parent = (_soft(G, alpha) ** 2 / (H + lam))[:, None, None]
-        best_gain = torch.full((K,), -1.0, dtype=torch.float64, device=dev)
-        best = torch.zeros((K, 3), dtype=torch.long, device=dev)   # feature, threshold bin, default_left
-        for dl in (1, 0):
-            L = cum + (miss[:, :, None, :] if dl else 0)
-            R = tot[:, None, None, :] - L
-            gain = (_soft(L[..., 0], alpha) ** 2 / (L[..., 1] + lam) + _soft(R[..., 0], alpha) ** 2 / (R[..., 1] + lam)
-                    - parent)
-            valid = (L[..., 1] >= mcw) & (R[..., 1] >= mcw)
-            tpos = torch.arange(cum.shape[2], device=dev)[None, None, :]
-            valid &= tpos < ncuts[None, :, None]                 # threshold must be a real cut
-            if feat_mask is not None:
-                valid &= feat_mask[None, :, None]
-            gain = torch.where(valid, gain, torch.full_like(gain, -1.0))
-            flat = gain.reshape(K, -1)
-            gbest, arg = flat.max(1)
-            better = gbest > best_gain
-            best_gain = torch.where(better, gbest, best_gain)
-            f_b = torch.stack([arg // cum.shape[2], arg % cum.shape[2], torch.full_like(arg, dl)], 1)
-            best = torch.where(better[:, None], f_b, best)
+        if on_gpu:
+            # one wave per (node, feature) scans the bins for both default directions; the
+            # cross-feature choice happens on the host copy (first feature wins ties)
+            sc = split_candidates(hist, tot, ncuts32, fmask_u8, lam, alpha, mcw).cpu()
+            best_gain, best = _pick_splits(sc)
+        else:
+            miss = hist[:, :, 0, :]                                # (K, F, 2)
+            cum = hist[:, :, 1:, :].cumsum(2)                      # bins 1..t go left
+            parent = (_soft(G, alpha) ** 2 / (H + lam))[:, None, None]
+            best_gain = torch.full((K,), -1.0, dtype=torch.float64, device=dev)
+            best = torch.zeros((K, 3), dtype=torch.long, device=dev)   # feature, threshold bin, default_left
+            for dl in (1, 0):
+                L = cum + (miss[:, :, None, :] if dl else 0)
+                R = tot[:, None, None, :] - L
+                gain = (_soft(L[..., 0], alpha) ** 2 / (L[..., 1] + lam) + _soft(R[..., 0], alpha) ** 2 / (R[..., 1] + lam)
+                        - parent)
+                valid = (L[..., 1] >= mcw) & (R[..., 1] >= mcw)
+                tpos = torch.arange(cum.shape[2], device=dev)[None, None, :]
+                valid &= tpos < ncuts[None, :, None]                 # threshold must be a real cut
+                if feat_mask is not None:
+                    valid &= feat_mask[None, :, None]
+                gain = torch.where(valid, gain, torch.full_like(gain, -1.0))
+                flat = gain.reshape(K, -1)
+                gbest, arg = flat.max(1)
+                better = gbest > best_gain
+                best_gain = torch.where(better, gbest, best_gain)
+                f_b = torch.stack([arg // cum.shape[2], arg % cum.shape[2], torch.full_like(arg, dl)], 1)
+                best = torch.where(better[:, None], f_b, best)
         # split bookkeeping on the host, shipped to the device in one copy per table
         prev_hist, pair_parent = hist, []
         new_level, remap = [], torch.full((K,), -1, dtype=torch.long)

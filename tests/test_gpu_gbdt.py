@@ -1,5 +1,6 @@
-"""gfx950 GBDT histogram kernel (csrc/hip/gbdt_hist.hip) against the fp64 ``index_add_``
-reference, and whole-booster parity between the GPU and CPU paths."""
+"""gfx950 GBDT kernels (csrc/hip/gbdt_hist.hip): the histogram build against the fp64
+``index_add_`` reference, and whole-booster parity (histograms + per-(node, feature) split
+search on the GPU vs the tensor formulation on the CPU) over several parameter sets."""
 import numpy as np
 import pytest
 import torch
@@ -48,9 +49,14 @@ def _data(n=20_000, F=10, seed=1):
     return x, y
 
 
-def test_booster_gpu_matches_cpu():
+@pytest.mark.parametrize("extra", [{}, {"alpha": 0.5, "min_child_weight": 20.0, "lambda": 0.3},
+                                   {"colsample_bytree": 0.6, "max_bin": 256, "gamma": 0.1},
+                                   {"objective": "binary:logistic"}])
+def test_booster_gpu_matches_cpu(extra):
     x, y = _data()
-    params = {"objective": "reg:squarederror", "max_depth": 5, "eta": 0.3, "max_bin": 64}
+    params = {"objective": "reg:squarederror", "max_depth": 5, "eta": 0.3, "max_bin": 64, **extra}
+    if params["objective"] == "binary:logistic":
+        y = (y > 0).astype(np.float32)
     cpu = gbdt.train(params, gbdt.DMatrix(x, y), 8, device="cpu")
     gpu = gbdt.train(params, gbdt.DMatrix(x, y), 8, device="cuda")
     for tc, tg in zip(cpu.trees, gpu.trees):
