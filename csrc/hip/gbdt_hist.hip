@@ -186,6 +186,29 @@ __global__ __launch_bounds__(64) void gbdt_split_kernel(const double* __restrict
   }
 }
 
+// ------------------------------------------------------------------------- row partition ----
+// Moves every active row one level down in place: node table tab[k] = {remap, feature, split
+// bin, default_left, tree node id} (remap < 0: node k became a leaf, its rows record the leaf id
+// and leave the active set). Replaces ~10 gather/where kernels per level of the tensor version.
+__global__ __launch_bounds__(256) void gbdt_partition_kernel(const int16_t* __restrict__ binsT,
+                                                            const long long* __restrict__ tab, long long* __restrict__ pos,
+                                                            long long* __restrict__ leaf, long long n, int K) {
+  const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const long long p = pos[r];
+  if (p < 0 || p >= K) return;
+  const long long* t = tab + p * 5;
+  const long long rm = t[0];
+  if (rm < 0) {
+    leaf[r] = t[4];
+    pos[r] = -1;
+    return;
+  }
+  const int b = (int)(unsigned short)binsT[t[1] * n + r];
+  const bool left = b == 0 ? t[3] != 0 : b <= t[2];
+  pos[r] = rm + (left ? 0 : 1);
+}
+
 static inline long long gh_cdiv(long long a, long long b) { return (a + b - 1) / b; }
 
 extern "C" {
@@ -223,6 +246,15 @@ int rx_gbdt_split(const double* hist, const double* tot, const int* ncuts, const
   if (K <= 0 || F <= 0 || B < 2) return K <= 0 || F <= 0 ? 0 : -1;
   hipLaunchKernelGGL(gbdt_split_kernel, dim3((unsigned)(K * F)), dim3(64), 0, s, hist, tot, ncuts, fmask, out, F, B, lam,
                      alpha, mcw);
+  return (int)hipGetLastError();
+}
+
+// One level of row partitioning (see gbdt_partition_kernel); pos/leaf are updated in place.
+int rx_gbdt_partition(const int16_t* binsT, const long long* tab, long long* pos, long long* leaf, long long n, int K,
+                      hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(gbdt_partition_kernel, dim3((unsigned)gh_cdiv(n, 256)), dim3(256), 0, s, binsT, tab, pos, leaf, n,
+                     K);
   return (int)hipGetLastError();
 }
 

@@ -29,6 +29,8 @@ def _lib():
         d = ctypes.c_double
         L.rx_gbdt_split.argtypes = [vp, vp, vp, vp, vp, i, i, i, d, d, d, vp]
         L.rx_gbdt_split.restype = i
+        L.rx_gbdt_partition.argtypes = [vp, vp, vp, vp, ll, i, vp]
+        L.rx_gbdt_partition.restype = i
         _bound = True
     return L
 
@@ -97,3 +99,26 @@ def split_candidates(hist: torch.Tensor, tot: torch.Tensor, ncuts: torch.Tensor,
                                     ctypes.c_void_p(out.data_ptr()), K, F, B, float(lam), float(alpha), float(mcw),
                                     _hip.stream_ptr(hist.device)), "rx_gbdt_split")
     return out
+
+
+def partition_rows_(bins_t: torch.Tensor, table: torch.Tensor, pos: torch.Tensor, leaf: torch.Tensor) -> None:
+    """Move active rows one level down, in place, on a GPU.
+
+    ``table`` [K, 5] int64 rows ``(remap, feature, split_bin, default_left, node_id)``: rows of a
+    node with ``remap < 0`` get ``leaf = node_id`` and ``pos = -1``; others go to child
+    ``remap + (not left)`` where left = ``default_left`` for bin 0 (missing), else
+    ``bin <= split_bin``.
+    """
+    F, n = bins_t.shape
+    if table.dtype != torch.long or table.dim() != 2 or table.shape[1] != 5:
+        raise ValueError("table must be [K, 5] int64")
+    if pos.dtype != torch.long or leaf.dtype != torch.long or pos.shape != (n,) or leaf.shape != (n,):
+        raise ValueError("pos/leaf must be int64 [n]")
+    if not (pos.is_contiguous() and leaf.is_contiguous() and bins_t.is_contiguous()):
+        raise ValueError("operands must be contiguous")
+    if table.shape[0] and int(table[:, 1].max()) >= F:
+        raise ValueError("split feature out of range")
+    table = table.to(bins_t.device).contiguous()
+    _hip.check(_lib().rx_gbdt_partition(ctypes.c_void_p(bins_t.data_ptr()), ctypes.c_void_p(table.data_ptr()),
+                                        ctypes.c_void_p(pos.data_ptr()), ctypes.c_void_p(leaf.data_ptr()), n,
+                                        int(table.shape[0]), _hip.stream_ptr(bins_t.device)), "rx_gbdt_partition")

@@ -364,7 +364,7 @@ def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: 
         if bins_t is None:
             bins_t = bins.t().contiguous()
         g32, h32 = g.float().contiguous(), h.float().contiguous()
-        from raydp_amd.ops.gbdt_ops import split_candidates
+        from raydp_amd.ops.gbdt_ops import partition_rows_, split_candidates
         ncuts32 = torch.tensor([c.numel() for c in cuts], dtype=torch.int32, device=dev)
         fmask_u8 = feat_mask.to(device=dev, dtype=torch.uint8).contiguous() if feat_mask is not None else None
     else:
@@ -465,21 +465,30 @@ def grow_tree(bins: torch.Tensor, cuts: List[torch.Tensor], g: torch.Tensor, h: 
             pair_parent.append(k)
             new_level += [tree.left[nid], tree.right[nid]]
             split_feat[k], split_bin[k], split_dl[k] = f, t + 1, dl
-        remap, split_feat, split_bin, split_dl = (t.to(dev) for t in (remap, split_feat, split_bin, split_dl))
-        # rows in nodes that became leaves keep their leaf id; others move down
-        cur = pos.clamp_min(0)
-        node_ids = torch.tensor(level, dtype=torch.long, device=dev)
-        leaf_rows = act & (remap[cur] < 0)
-        leaf_of_row = torch.where(leaf_rows, node_ids[cur], leaf_of_row)
-        if not new_level:
-            pos = torch.full_like(pos, -1)
-            level = []
-            break
-        f = split_feat[cur]
-        b = bins_l.gather(1, f.clamp_min(0)[:, None])[:, 0]
-        go_left = torch.where(b == 0, split_dl[cur], b <= split_bin[cur])
-        child = remap[cur] + (~go_left).long()
-        pos = torch.where(act & (remap[cur] >= 0), child, torch.full_like(pos, -1))
+        if on_gpu:
+            # one fused launch: leaf bookkeeping + child routing for every row (in place)
+            table = torch.stack([remap, split_feat, split_bin, split_dl.long(),
+                                 torch.tensor(level, dtype=torch.long)], 1)
+            partition_rows_(bins_t, table, pos, leaf_of_row)
+            if not new_level:
+                level = []
+                break
+        else:
+            remap, split_feat, split_bin, split_dl = (t.to(dev) for t in (remap, split_feat, split_bin, split_dl))
+            # rows in nodes that became leaves keep their leaf id; others move down
+            cur = pos.clamp_min(0)
+            node_ids = torch.tensor(level, dtype=torch.long, device=dev)
+            leaf_rows = act & (remap[cur] < 0)
+            leaf_of_row = torch.where(leaf_rows, node_ids[cur], leaf_of_row)
+            if not new_level:
+                pos = torch.full_like(pos, -1)
+                level = []
+                break
+            f = split_feat[cur]
+            b = bins_l.gather(1, f.clamp_min(0)[:, None])[:, 0]
+            go_left = torch.where(b == 0, split_dl[cur], b <= split_bin[cur])
+            child = remap[cur] + (~go_left).long()
+            pos = torch.where(act & (remap[cur] >= 0), child, torch.full_like(pos, -1))
         level = new_level
     if level:
         node_ids = torch.tensor(level, dtype=torch.long, device=dev)
