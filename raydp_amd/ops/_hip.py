@@ -73,9 +73,30 @@ class OptDesc(ctypes.Structure):
 
 class IngestCol(ctypes.Structure):
     _fields_ = [
-        ("type", ctypes.c_int), ("pad_", ctypes.c_int), ("offset", ctypes.c_longlong),
+        ("type", ctypes.c_int), ("pad_", ctypes.c_int), ("vbit", ctypes.c_longlong),
         ("values", ctypes.c_void_p), ("valid", ctypes.c_void_p),
         ("fill", ctypes.c_float), ("pad2_", ctypes.c_int),
+    ]
+
+
+class DmaRegion(ctypes.Structure):
+    """One host byte range DMA'd into a chunk's staging area (csrc/hip/arrow_ingest.hip)."""
+    _fields_ = [("host", ctypes.c_uint64), ("bytes", ctypes.c_longlong), ("off", ctypes.c_longlong)]
+
+
+class DmaCol(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_int), ("has_valid", ctypes.c_int),
+        ("vals_off", ctypes.c_longlong), ("valid_off", ctypes.c_longlong), ("vbit", ctypes.c_longlong),
+        ("fill", ctypes.c_float), ("pad_", ctypes.c_int),
+    ]
+
+
+class DmaChunk(ctypes.Structure):
+    _fields_ = [
+        ("nrows", ctypes.c_longlong), ("out_row0", ctypes.c_longlong), ("bytes", ctypes.c_longlong),
+        ("first_region", ctypes.c_int), ("nregions", ctypes.c_int), ("first_col", ctypes.c_int),
+        ("pad_", ctypes.c_int),
     ]
 
 
@@ -124,6 +145,15 @@ def lib():
     L.rx_mlp_refresh_images.argtypes = [vp, vp, vp, vp]
     L.rx_arrow_ingest.argtypes = [vp, vp, vp]
     L.rx_gather_rows.argtypes = [vp, vp, vp, ll, i, vp]
+    u64 = ctypes.c_uint64
+    L.rx_pin_range.argtypes = [u64, u64, u64, u64, u64]
+    L.rx_pin_stats.argtypes = [vp]
+    L.rx_unpin_arena.argtypes = [u64]
+    L.rx_dma_sizes.argtypes = [vp]
+    # (chunks, nchunks, regions, cols, ncols, out_stride, out_bf16, out, stage, stage_bytes,
+    #  compute, copy, stats)
+    L.rx_ingest_dma.argtypes = [vp, i, vp, vp, i, i, i, vp, vp, ll, vp, vp, vp]
+    L.rx_feistel_perm.argtypes = [vp, ll, u64, vp]
     L.rx_comm_available.restype = i
     L.rx_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.rx_comm_allreduce.argtypes = [vp, i, vp, vp]
@@ -131,11 +161,18 @@ def lib():
     L.rx_comm_destroy.argtypes = [vp]
     for fn in ("rx_mlp_train_steps", "rx_mlp_fwdbwd", "rx_opt_step", "rx_mlp_eval",
                "rx_mlp_refresh_images", "rx_arrow_ingest", "rx_gather_rows", "rx_comm_unique_id",
+               "rx_pin_range", "rx_pin_stats", "rx_unpin_arena", "rx_dma_sizes", "rx_ingest_dma",
+               "rx_feistel_perm",
                "rx_comm_allreduce", "rx_comm_broadcast", "rx_comm_destroy"):
         getattr(L, fn).restype = i
     for name, cls in (("rx_mlp_desc_size", MlpDesc), ("rx_opt_desc_size", OptDesc),
                       ("rx_ingest_args_size", IngestArgs), ("rx_step_bufs_size", StepBufs)):
         got = getattr(L, name)()
+        if got != ctypes.sizeof(cls):
+            raise RuntimeError(f"ABI mismatch for {cls.__name__}: C {got} vs ctypes {ctypes.sizeof(cls)}")
+    sizes = (ctypes.c_int * 3)()
+    L.rx_dma_sizes(sizes)
+    for got, cls in zip(sizes, (DmaRegion, DmaCol, DmaChunk)):
         if got != ctypes.sizeof(cls):
             raise RuntimeError(f"ABI mismatch for {cls.__name__}: C {got} vs ctypes {ctypes.sizeof(cls)}")
     _lib = L

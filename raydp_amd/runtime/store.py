@@ -5,8 +5,10 @@ stream, then serialised through a ``FixedSizeBufferWriter`` over the mapped byte
 back zero-copy: the returned table's buffers point into the shared mapping and keep the object
 pinned until they are garbage collected. Other values are pickled (protocol 5).
 
-On a GPU node the arena is registered with the HIP runtime (``hipHostRegister``) so a block
-can be DMA'd to HBM straight from the store.
+On a GPU node the arena is registered with the HIP runtime (``hipHostRegister``, in 2 MiB
+chunks, lazily, by ``csrc/hip/arrow_ingest.hip:rx_pin_range``) the first time a block inside a
+chunk is ingested, so a block is DMA'd to HBM straight from the store (``raydp_amd/ops/ingest.py``).
+``arena_of(addr)`` finds the mapped arena holding a host address.
 """
 import ctypes
 import os
@@ -27,6 +29,30 @@ _ID_LEN = 32
 
 class StoreFullError(MemoryError):
     pass
+
+
+_mapped_lock = threading.Lock()
+_mapped = weakref.WeakSet()   # every store arena mapped in this process
+
+
+def arena_of(addr: int, nbytes: int = 1) -> Optional[Tuple[int, int]]:
+    """(base, capacity) of the mapped store arena holding [addr, addr + nbytes), or None."""
+    with _mapped_lock:
+        stores = list(_mapped)
+    for st in stores:
+        if st.contains_address(addr, nbytes):
+            return st._base, st.capacity
+    return None
+
+
+def _unpin(base: int):
+    """Drop this process's GPU registrations of an arena before it is unmapped."""
+    import sys
+    if "raydp_amd.ops._hip" not in sys.modules:
+        return
+    from raydp_amd.ops import _hip
+    if _hip._lib is not None:
+        _hip._lib.rx_unpin_arena(ctypes.c_uint64(base))
 
 
 def _lib():
@@ -94,8 +120,9 @@ class SharedObjectStore:
         self._base = self._lib.rt_store_data(self._h)
         self.capacity = int(self._lib.rt_store_capacity(self._h))
         self._pid = os.getpid()
-        self._registered = False
         self._lock = threading.Lock()
+        with _mapped_lock:
+            _mapped.add(self)
 
     # ------------------------------------------------------------------ write ------------
     def _create(self, oid: str, size: int, kind: int) -> Tuple[int, bytes]:
@@ -184,23 +211,14 @@ class SharedObjectStore:
     def base_address(self) -> int:
         return self._base
 
-    def register_with_gpu(self) -> bool:
-        """Pin the arena for DMA (hipHostRegister) once per process."""
-        if self._registered:
-            return True
-        try:
-            import torch
-            if not torch.cuda.is_available():
-                return False
-            rt = torch.cuda.cudart()
-            rc = rt.cudaHostRegister(self._base, self.capacity, 0)
-            self._registered = int(rc) == 0 if not hasattr(rc, "value") else rc.value == 0
-        except Exception:  # noqa: BLE001
-            self._registered = False
-        return self._registered
+    def contains_address(self, addr: int, nbytes: int = 1) -> bool:
+        return self._h is not None and self._base <= addr and addr + nbytes <= self._base + self.capacity
 
     def close(self):
         if self._h is not None:
+            with _mapped_lock:
+                _mapped.discard(self)
+            _unpin(self._base)
             self._lib.rt_store_close(self._h)
             self._h = None
 

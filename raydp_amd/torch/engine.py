@@ -24,6 +24,18 @@ import torch.nn as nn
 from raydp_amd.train import session
 
 
+def _epoch_seed_base(config) -> int:
+    """Per-rank base of the epoch-permutation seeds (``shuffle_seed`` extra config, else 1234)."""
+    base = config.get("shuffle_seed")
+    base = 1234 if base is None else int(base)
+    return (base * 1_000_003 + session.get_world_rank()) * 65_537
+
+
+def random_permutation(n, seed, device):
+    from raydp_amd.ops.ingest import random_permutation as rp
+    return rp(n, seed, device)
+
+
 def _to_tensor_spec(feature_columns, feature_types):
     """Normalise (feature_columns, feature_types) into groups of (cols, dtype)."""
     if feature_columns and isinstance(feature_columns[0], (list, tuple)):
@@ -100,8 +112,8 @@ class FusedMLPEngine:
             self.trainer.refresh_images()
         self.drop_last = bool(config.get("drop_last", False))
         self.shuffle = bool(config.get("shuffle", True))
-        self.gen = torch.Generator(device=device)
-        self.gen.manual_seed(1234 + session.get_world_rank())
+        self.seed = _epoch_seed_base(config)
+        self.epoch = 0
 
     def load(self, train_ds, eval_ds, config):
         fc, ft = config["feature_columns"], config["feature_types"]
@@ -123,7 +135,8 @@ class FusedMLPEngine:
         t = self.train
         perm = None
         if self.shuffle:
-            perm = torch.randperm(t.n, device=self.device, generator=self.gen).to(torch.int32)
+            perm = random_permutation(t.n, self.seed + self.epoch, self.device)
+        self.epoch += 1
         ar, comm, max_steps, xg = None, None, None, None
         if self.world > 1:
             import torch.distributed as dist
@@ -200,8 +213,8 @@ class TorchLoopEngine:
         self.batch = int(config["batch_size"])
         self.drop_last = bool(config.get("drop_last", False))
         self.shuffle = bool(config.get("shuffle", True))
-        self.gen = torch.Generator(device=device)
-        self.gen.manual_seed(1234 + session.get_world_rank())
+        self.seed = _epoch_seed_base(config)
+        self.epoch = 0
         self.graphed = None
         from raydp_amd.torch import graphs
         if graphs.graphs_requested():
@@ -223,7 +236,10 @@ class TorchLoopEngine:
 
     def _batches(self, data: _ShardTensors, shuffle: bool):
         n = data.n
-        idx = torch.randperm(n, device=self.device, generator=self.gen) if shuffle else None
+        idx = None
+        if shuffle:
+            idx = random_permutation(n, self.seed + self.epoch, self.device).long()
+            self.epoch += 1
         stop = n - n % self.batch if self.drop_last else n
         for s in range(0, stop, self.batch):
             if idx is not None:

@@ -193,7 +193,8 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             rows = getattr(getattr(engine, "train", None), "n", None)
             perf = {}
             if rows:
-                perf = {"train_samples_per_s": rows / max(wall, 1e-9), "train_epoch_wall_s": wall}
+                perf = {"train_rows": rows, "train_samples_per_s": rows / max(wall, 1e-9),
+                        "train_epoch_wall_s": wall}
                 if dev_s is not None:
                     perf["train_epoch_device_s"] = dev_s
             session.report(dict(epoch=epoch, train_res=train_res, train_loss=train_loss,
@@ -233,6 +234,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             "evaluate": True,
             "metrics": self._metrics,
             "fused": self._extra_config.get("fused", None),
+            "shuffle_seed": self._extra_config.get("shuffle_seed", None),
         }
         use_gpu = self._extra_config.get("use_gpu")
         if self._resources_per_worker and "GPU" in self._resources_per_worker:

@@ -168,8 +168,12 @@ class GraphedTrainLoop:
         e.model.train()
         d = e.train
         n, b = d.n, e.batch
-        idx = torch.randperm(n, device=e.device, generator=e.gen) if e.shuffle else \
-            torch.arange(n, device=e.device)
+        if e.shuffle:
+            from raydp_amd.torch.engine import random_permutation
+            idx = random_permutation(n, e.seed + e.epoch, e.device).long()
+            e.epoch += 1
+        else:
+            idx = torch.arange(n, device=e.device)
         nfull = n // b
         self.total.zero_()
         s = 0

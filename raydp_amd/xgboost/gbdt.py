@@ -162,27 +162,37 @@ class World:
 
     def allreduce(self, t: torch.Tensor):
         if self.dist is not None and self.size > 1:
-            dev = t.device
-            if self.dist.get_backend() == "nccl" and dev.type != "cuda":
-                c = t.cuda()
+            dev = self._comm_device(t)
+            if dev != t.device:
+                c = t.to(dev)
                 self.dist.all_reduce(c)
-                t.copy_(c.to(dev))
+                t.copy_(c.to(t.device))
             else:
                 self.dist.all_reduce(t)
         return t
 
+    def _comm_device(self, t: torch.Tensor) -> torch.device:
+        """RCCL (backend "nccl") only moves device tensors: stage CPU tensors through the
+        rank's current GPU; gloo keeps them where they are."""
+        if self.dist.get_backend() == "nccl" and t.device.type != "cuda":
+            return torch.device("cuda", torch.cuda.current_device())
+        return t.device
+
     def allgather_rows(self, t: torch.Tensor) -> torch.Tensor:
         if self.dist is None or self.size == 1:
             return t
-        n = torch.tensor([t.shape[0]], dtype=torch.int64)
+        home = t.device
+        dev = self._comm_device(t)
+        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=dev)
         ns = [torch.zeros_like(n) for _ in range(self.size)]
         self.dist.all_gather(ns, n)
-        m = int(max(int(x) for x in ns))
-        pad = torch.full((m, t.shape[1]), float("nan"), dtype=t.dtype)
-        pad[:t.shape[0]] = t
+        counts = [int(x) for x in torch.cat(ns).cpu()]
+        m = max(counts)
+        pad = torch.full((m, t.shape[1]), float("nan"), dtype=t.dtype, device=dev)
+        pad[:t.shape[0]] = t.to(dev)
         outs = [torch.empty_like(pad) for _ in range(self.size)]
         self.dist.all_gather(outs, pad)
-        return torch.cat([o[:int(k)] for o, k in zip(outs, ns)])
+        return torch.cat([o[:k] for o, k in zip(outs, counts)]).to(home)
 
 
 # ---------------------------------------------------------------------------- binning ----
