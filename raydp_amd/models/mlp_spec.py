@@ -40,7 +40,53 @@ class MlpSpec:
 _RELU_FUNCS = {F.relu, torch.relu, torch.nn.functional.relu}
 
 
+_SPEC_CACHE = {}   # structural key -> recipe [(linear name, act, bn, bn name)] or None
+
+
+def _structure_key(model: nn.Module):
+    # by class *name* + forward code object, not the class object: models are often defined
+    # inside a function, which makes a new (identical) class per call
+    f = type(model).forward
+    fwd = getattr(f, "__code__", None)
+    cells = tuple(repr(c.cell_contents) for c in (getattr(f, "__closure__", None) or ()))
+    leaves = tuple((n, type(m).__qualname__, repr(m)) for n, m in model.named_modules()
+                   if not any(True for _ in m.children()))
+    return type(model).__module__, type(model).__qualname__, fwd, cells, leaves
+
+
 def extract_mlp_spec(model: nn.Module) -> Optional[MlpSpec]:
+    """The fusable-MLP spec of ``model`` or None. The fx trace runs once per model structure
+    (class, forward code, leaf modules and their hyper-parameters): a new instance of a seen
+    structure is rebuilt from the cached recipe (the trace costs ~2 ms per fit)."""
+    try:
+        key = _structure_key(model)
+        hash(key)
+    except Exception:  # noqa: BLE001
+        key = None
+    if key is not None and key in _SPEC_CACHE:
+        recipe = _SPEC_CACHE[key]
+        if recipe is None:
+            return None
+        spec = MlpSpec()
+        for lin, act, bn, bn_name in recipe:
+            spec.layers.append(LayerSpec(linear=model.get_submodule(lin), act=act, bn=bn,
+                                         bn_module=model.get_submodule(bn_name) if bn_name else None))
+        return spec
+    spec = _trace_spec(model)
+    if key is not None:
+        if len(_SPEC_CACHE) > 256:
+            _SPEC_CACHE.clear()
+        if spec is None:
+            _SPEC_CACHE[key] = None
+        else:
+            names = {id(m): n for n, m in model.named_modules()}
+            _SPEC_CACHE[key] = [(names[id(ly.linear)], ly.act, ly.bn,
+                                 names[id(ly.bn_module)] if ly.bn_module is not None else None)
+                                for ly in spec.layers]
+    return spec
+
+
+def _trace_spec(model: nn.Module) -> Optional[MlpSpec]:
     try:
         import torch.fx as fx
         gm = fx.symbolic_trace(model)

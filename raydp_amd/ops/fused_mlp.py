@@ -244,17 +244,19 @@ class FusedMLPTrainer:
         act_floats = _ru((act + 1) // 2, 4)
         d.act_off, d.wgrad_mode = act_off, wmode
         self.total = total
-        self.params = torch.cat(flat).to(dev).contiguous()
+        self.params = torch.cat([f.detach().cpu() for f in flat]).to(dev).contiguous()
         self.grads = torch.zeros(act_off + act_floats, dtype=torch.float32, device=dev)
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
         self.scratch = torch.zeros(max(1, scratch_off), dtype=torch.float32, device=dev)
         self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
         self.img = torch.zeros(max(8, img_off), dtype=torch.bfloat16, device=dev)
-        self.rstats = torch.zeros(max(1, rs_total), dtype=torch.float32, device=dev)
+        rs_host = torch.zeros(max(1, rs_total), dtype=torch.float32)
         for bn, ro, n_ in rs_init:
-            self.rstats[ro:ro + n_] = bn.running_mean.detach().to(dev, torch.float32)
-            self.rstats[ro + n_:ro + 2 * n_] = bn.running_var.detach().to(dev, torch.float32)
+            rs_host[ro:ro + n_] = bn.running_mean.detach().cpu().float()
+            rs_host[ro + n_:ro + 2 * n_] = bn.running_var.detach().cpu().float()
+        self.rstats = rs_host.to(dev)
+        for bn, ro, n_ in rs_init:
             self.run_bufs.append((bn, self.rstats[ro:ro + n_], self.rstats[ro + n_:ro + 2 * n_]))
         base = self.img.data_ptr()
         for si, wi, wti in seg_images:
@@ -469,15 +471,20 @@ class FusedMLPTrainer:
     # ----------------------------------------------------------------------- state --------
     @torch.no_grad()
     def write_back(self):
-        """Copy fp32 master params / BN running stats back into the user's modules."""
-        p = self.params.detach().cpu()
+        """Copy fp32 master params / BN running stats back into the user's modules (one D2H
+        copy of each flat buffer, then host-side slicing)."""
+        p = self.params.detach().to("cpu", non_blocking=False)
+        rs = self.rstats.detach().to("cpu", non_blocking=False) if self.run_bufs else None
         for kind, mod, off, n in self.layout:
             t = {"weight": "weight", "bias": "bias", "gamma": "weight", "beta": "bias"}[kind]
             dst = getattr(mod, t)
             dst.data.copy_(p[off:off + n].view_as(dst).to(dst.dtype))
+        base = self.rstats.data_ptr()
         for bn, rm, rv in self.run_bufs:
-            bn.running_mean.copy_(rm.cpu())
-            bn.running_var.copy_(rv.cpu())
+            o = (rm.data_ptr() - base) // 4
+            bn.running_mean.copy_(rs[o:o + rm.numel()])
+            o = (rv.data_ptr() - base) // 4
+            bn.running_var.copy_(rs[o:o + rv.numel()])
             if bn.num_batches_tracked is not None:
                 bn.num_batches_tracked.add_(getattr(self, "_tracked_pending", 0))
         self._tracked_pending = 0

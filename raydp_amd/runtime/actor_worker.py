@@ -78,6 +78,11 @@ def main() -> int:
                 cloudpickle.dump((RuntimeError(repr(e)), traceback.format_exc()), f)
         os.replace(err_path + ".tmp", err_path)
         return 0
+    # the actor's long-lived state (imported modules, warmed engine) moves to the permanent GC
+    # generation: full collections, and heap walks such as gc.get_referrers, then skip it
+    import gc
+    gc.collect()
+    gc.freeze()
     pool = ThreadPoolExecutor(max_workers=int(opts.get("max_concurrency") or 1),
                               thread_name_prefix=f"actor-{aid[:6]}")
     tmp = sock_path + ".tmp"

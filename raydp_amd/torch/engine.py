@@ -104,7 +104,6 @@ class FusedMLPEngine:
         from raydp_amd.ops.fused_mlp import FusedMLPTrainer
         self.model, self.metrics_names, self.device = model, metrics.names, device
         self.world = session.get_world_size()
-        model.to(device)
         self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn)
         if self.world > 1:
             import torch.distributed as dist

@@ -118,7 +118,9 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             raise Exception("Unsupported parameter, we only support torch.nn.Model instance "
                             "or a function(dict -> model)")
         device = session.get_device() or torch.device("cpu")
-        model = model.to(device)
+        # the model stays on the host until the engine is chosen: the fused engine keeps its own
+        # flat device copy of the parameters (one H2D copy) and writes results back to the host
+        # module in one D2H copy; the torch loop moves it to the device below
         # optimizer (instance -> re-instantiate on this worker's parameters)
         if isinstance(config["optimizer"], torch.optim.Optimizer):
             optimizer_cls = config["optimizer"].__class__
@@ -167,6 +169,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                 lr_fn = _make_lr_schedule(optimizer, config["lr_scheduler_creator"], config)
             engine = FusedMLPEngine(model, optimizer, spec, lc, oc, metrics, device, config, lr_fn)
         else:
+            model = model.to(device)       # in place: the optimizer keeps its parameter objects
             sched = config["lr_scheduler_creator"](optimizer, config) if config["lr_scheduler_creator"] else None
             engine = TorchLoopEngine(model, optimizer, loss, metrics, device, config, sched)
         from raydp_amd.utils import tracing
