@@ -232,11 +232,22 @@ class BucketAllreduce:
         except Exception:  # noqa: BLE001
             self.xg = None
 
-    def __call__(self, flat):
-        import torch
+    @property
+    def kind(self) -> str:
+        """What the buckets ride on: the one-shot xGMI kernel for buckets <= 1 MiB (when the peer
+        mapping is up) and torch.distributed (RCCL / gloo) for the rest."""
         import torch.distributed as dist
-        if (self.xg is not None and flat.is_cuda and flat.dtype == torch.float32 and flat.is_contiguous()
-                and flat.numel() * 4 <= XG_BUCKET_MAX_BYTES and not torch.cuda.is_current_stream_capturing()):
+        base = f"torch.distributed:{dist.get_backend(self.group)}" if dist.is_initialized() else "none"
+        return f"xgmi_oneshot(<=1MiB)+{base}" if self.xg is not None else base
+
+    def routes_to_xgmi(self, flat) -> bool:
+        import torch
+        return (self.xg is not None and flat.is_cuda and flat.dtype == torch.float32 and flat.is_contiguous()
+                and flat.numel() * 4 <= XG_BUCKET_MAX_BYTES and not torch.cuda.is_current_stream_capturing())
+
+    def __call__(self, flat):
+        import torch.distributed as dist
+        if self.routes_to_xgmi(flat):
             self.xg.allreduce_(flat)
             return _Done()
         return dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)

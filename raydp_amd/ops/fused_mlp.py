@@ -395,7 +395,11 @@ class FusedMLPTrainer:
         sched = torch.from_numpy(np.concatenate([lr_np, bc1_np, bc2_np])).to(self.device)
         pp = ctypes.c_void_p
         from raydp_amd.utils.config import get as conf_get
-        timeout = max(5.0, float(conf_get("spark.ray.mi355x.allreduce.timeout_s")))
+        timeout = float(conf_get("spark.ray.mi355x.mlp_persistent.timeout_s"))
+        # device-side snapshot of the state the epoch mutates: a wait that times out (the grid was
+        # admitted but a co-tenant still starved a workgroup) rolls back and reruns the epoch on
+        # the launch-per-step loop instead of failing the fit
+        snap = [t.clone() for t in (self.params, self.m, self.v, self.rstats, self.img)]
         rc = self.lib.rx_mlp_train_persistent(
             ctypes.byref(self.desc), ctypes.byref(self.bufs), ctypes.byref(self.opt), self._od, self.mt,
             pp(self.m.data_ptr()), pp(self.v.data_ptr()), pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p,
@@ -406,7 +410,15 @@ class FusedMLPTrainer:
         _hip.check(rc, "rx_mlp_train_persistent")
         self._ps_sched = sched   # kept alive until the launch has consumed it
         if int(self._ps_sync[self._ps_err].item()) != 0:
-            raise RuntimeError("persistent fused-MLP epoch: a workgroup wait timed out (grid not co-resident?)")
+            import warnings
+            warnings.warn("persistent fused-MLP epoch: a workgroup wait timed out; rolled back and "
+                          "rerunning the epoch on the launch-per-step loop")
+            for dst, src in zip((self.params, self.m, self.v, self.rstats, self.img), snap):
+                dst.copy_(src)
+            self.metrics.zero_()
+            self._ps_ok = False          # this trainer stays on the step loop from now on
+            self.persistent_fallbacks = getattr(self, "persistent_fallbacks", 0) + 1
+            return False
         return True
 
     def _check_operands(self, feats, labels, n_rows, perm=None):

@@ -197,9 +197,11 @@ class TorchLoopEngine:
         self.device = device
         self.world = session.get_world_size()
         self.raw_model = model.to(device)
+        self.allreduce_kind = None
         if self.world > 1:
             from raydp_amd.parallel.ddp import DistributedDataParallel
             self.model = DistributedDataParallel(self.raw_model)
+            self.allreduce_kind = self.model._allreduce.kind
         else:
             self.model = self.raw_model
         # optimizer state may reference CPU tensors; move them

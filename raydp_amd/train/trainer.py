@@ -258,7 +258,11 @@ class DataParallelTrainer:
                 if res:
                     opts["resources"] = res
                 workers.append(cls.options(**opts).remote(r, world, storage, use_gpu))
-            runtime.get([w.setup.remote("127.0.0.1", port) for w in workers])
+            # Like Ray Train's shared CUDA_VISIBLE_DEVICES: every worker of a node sees all of
+            # that node's worker GPUs and binds cuda:<local_rank>, so RCCL and the xGMI one-shot
+            # path can map peer memory (a worker that saw only its own GPU could not)
+            layout = _local_layout(workers)
+            runtime.get([w.setup.remote("127.0.0.1", port, *layout[r]) for r, w in enumerate(workers)])
             refs = []
             for r, w in enumerate(workers):
                 shards = _shard(self.datasets, r, world)
@@ -285,19 +289,52 @@ class DataParallelTrainer:
             pgroup.remove_placement_group(pg)
 
 
+def _local_layout(workers):
+    """Per worker: (visible GPU ids of its node, local rank, local world size, node rank)."""
+    nodes, order = {}, []
+    for w in workers:
+        impl = getattr(w, "_impl", None)
+        vn = getattr(impl, "vnode", None)
+        node = vn.node_id if vn is not None else "head"
+        if node not in nodes:
+            nodes[node] = []
+            order.append(node)
+        nodes[node].append(w)
+    out = []
+    for w in workers:
+        impl = getattr(w, "_impl", None)
+        vn = getattr(impl, "vnode", None)
+        node = vn.node_id if vn is not None else "head"
+        peers = nodes[node]
+        gpus = sorted({g for p in peers for g in (getattr(getattr(p, "_impl", None), "gpu_ids", None) or [])})
+        mine = getattr(impl, "gpu_ids", None) or []
+        local = gpus.index(mine[0]) if mine and mine[0] in gpus else peers.index(w)
+        out.append((gpus or None, local, len(peers), order.index(node)))
+    return out
+
+
 class _TrainWorker:
     """One rank of a spawned worker group (a process actor)."""
 
     def __init__(self, rank: int, world: int, storage: str, use_gpu: bool):
         self.rank, self.world, self.storage, self.use_gpu = rank, world, storage, use_gpu
+        self.local_rank, self.local_world, self.node_rank = 0, 1, rank
 
-    def setup(self, addr: str, port: int):
+    def setup(self, addr: str, port: int, visible=None, local_rank: int = 0, local_world: int = 1,
+              node_rank: int = 0):
+        if visible and self.use_gpu:
+            # before the first HIP call of this process: the node's worker GPUs, in order
+            os.environ["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in visible)
+            os.environ.pop("CUDA_VISIBLE_DEVICES", None)
         import torch
+        self.local_rank, self.local_world, self.node_rank = local_rank, local_world, node_rank
         self.device = torch.device("cpu")
         if self.use_gpu and torch.cuda.is_available():
-            torch.cuda.set_device(0)     # the runtime exposes exactly this worker's GPU(s)
-            self.device = torch.device("cuda", 0)
-        os.environ.update({"RANK": str(self.rank), "WORLD_SIZE": str(self.world), "LOCAL_RANK": "0",
+            dev = local_rank % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(dev)
+            self.device = torch.device("cuda", dev)
+        os.environ.update({"RANK": str(self.rank), "WORLD_SIZE": str(self.world),
+                           "LOCAL_RANK": str(local_rank), "LOCAL_WORLD_SIZE": str(local_world),
                            "MASTER_ADDR": addr, "MASTER_PORT": str(port)})
         _init_dist("nccl" if self.device.type == "cuda" else "gloo", self.rank, self.world, addr, port)
         return True
@@ -309,7 +346,8 @@ class _TrainWorker:
 
         def reporter(r, metrics, ckpt):
             reports.append((metrics, ckpt))
-        ctx = S.TrainContext(self.rank, self.world, 0, 1, self.rank, self.device, "raydp", self.storage)
+        ctx = S.TrainContext(self.rank, self.world, self.local_rank, self.local_world, self.node_rank,
+                             self.device, "raydp", self.storage)
         S._set_session(S._Session(ctx, shards, reporter, self.storage, resume))
         try:
             fn(config) if _accepts_arg(fn) else fn()

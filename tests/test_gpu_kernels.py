@@ -349,3 +349,34 @@ def test_persistent_epoch_matches_step_loop(case, monkeypatch):
     for a, b in zip(e1, e0):
         assert a["batches"] == b["batches"] and a["count"] == b["count"]
         assert abs(a["loss"] - b["loss"]) <= 1e-6 * max(1.0, abs(b["loss"])), (a, b)
+
+
+def test_persistent_timeout_rolls_back_to_step_loop(monkeypatch):
+    """A persistent epoch whose workgroup waits time out (forced with a ~0 s bound) is rolled
+    back and rerun on the launch-per-step loop: the result equals a plain step-loop epoch."""
+    import warnings
+    from raydp_amd.models.mlp_spec import extract_mlp_spec
+    from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+    dev = torch.device("cuda")
+    torch.manual_seed(7)
+    model, n = NYC(), 64 * 12
+    X, Y = torch.randn(n, 20), torch.randn(n, 1)
+    runs = []
+    for persistent, tmo in (("1", "1e-7"), ("0", "5")):
+        monkeypatch.setenv("RAYDP_MLP_PERSISTENT", persistent)
+        monkeypatch.setenv("RAYDP_MLP_PERSISTENT_TIMEOUT_S", tmo)
+        m2 = copy.deepcopy(model)
+        tr = FusedMLPTrainer(extract_mlp_spec(m2), optimizer_config(torch.optim.Adam(m2.parameters(), lr=1e-3)),
+                             loss_code(nn.MSELoss()), 64, dev)
+        feats = torch.zeros(n, tr.feat_k, dtype=torch.bfloat16)
+        feats[:, :20] = X.to(torch.bfloat16)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            m = tr.train_epoch(feats.to(dev), Y.to(dev), n, None)
+        if persistent == "1":
+            assert getattr(tr, "persistent_fallbacks", 0) == 1, "timeout path not taken"
+            assert any("rolled back" in str(x.message) for x in w)
+        runs.append((tr.params.clone(), tr.m.clone(), tr.img.clone(), tr.rstats.clone(), m))
+    (p1, m1, i1, r1, e1), (p0, m0, i0, r0, e0) = runs
+    assert torch.equal(p1, p0) and torch.equal(m1, m0) and torch.equal(i1, i0) and torch.equal(r1, r0)
+    assert e1["batches"] == e0["batches"] and abs(e1["loss"] - e0["loss"]) <= 1e-6 * max(1.0, abs(e0["loss"]))

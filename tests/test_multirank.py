@@ -1,0 +1,256 @@
+"""Collectives at world sizes 4 and 8 on gloo (SURVEY.md §4.4 asks for 2-8 ranks): DDP buckets
+and sparse embedding gradients, table-wise sharded embeddings with uneven tables (and ranks that
+own no table), GBDT histogram all-reduce, the all-reduce routing threshold, and the spawned
+TorchEstimator worker group."""
+import math
+import multiprocessing as mp
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from raydp_amd.train.trainer import _free_port
+
+
+def _spawn(target, world, *args, timeout=240):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = sorted((q.get(timeout=timeout) for _ in ps), key=lambda r: r[0])
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    return dist
+
+
+class _EmbMlp(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.emb = nn.Embedding(13, 4, sparse=True)
+        self.l1 = nn.Linear(4 + 3, 32)
+        self.l2 = nn.Linear(32, 16)
+        self.l3 = nn.Linear(16, 1)
+
+    def forward(self, ids, x):
+        h = torch.cat([self.emb(ids), x], 1)
+        return self.l3(torch.relu(self.l2(torch.relu(self.l1(h)))))
+
+
+def _batch(seed, n=12):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, 13, (n,), generator=g), torch.randn(n, 3, generator=g), torch.randn(n, 1, generator=g)
+
+
+def _ddp_rank(rank, world, port, q):
+    dist = _init(rank, world, port)
+    try:
+        from raydp_amd.parallel.ddp import DistributedDataParallel
+        torch.manual_seed(0)
+        m = _EmbMlp()
+        if rank:
+            with torch.no_grad():      # different init: the wrap-time broadcast must fix it
+                for p in m.parameters():
+                    p.add_(0.5)
+        # a bucket cap below one layer's size: several buckets, reduced as backward produces them
+        ddp = DistributedDataParallel(m, bucket_cap_mb=0.0005)
+        ids, x, y = _batch(100 + rank)
+        nn.functional.mse_loss(ddp(ids, x), y).backward()
+        grads = {n: (p.grad.to_dense() if p.grad.is_sparse else p.grad).clone() for n, p in m.named_parameters()}
+        q.put((rank, len(ddp.buckets), {k: v.tolist() for k, v in grads.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_ddp_buckets_and_sparse_grads_match_full_batch(world):
+    res = _spawn(_ddp_rank, world)
+    assert res[0][1] >= 3, "expected several buckets"
+    torch.manual_seed(0)
+    ref = _EmbMlp()
+    # DDP averages per-rank mean-loss gradients: the reference is the mean of per-rank losses
+    loss = sum(nn.functional.mse_loss(ref(*_batch(100 + r)[:2]), _batch(100 + r)[2]) for r in range(world)) / world
+    loss.backward()
+    for name, p in ref.named_parameters():
+        want = p.grad.to_dense() if p.grad.is_sparse else p.grad
+        for r in res:
+            torch.testing.assert_close(torch.tensor(r[2][name]), want, atol=1e-5, rtol=1e-4)
+
+
+SIZES = [5, 9, 17, 40, 3]
+D = 8
+
+
+def _full_table(t):
+    g = torch.Generator().manual_seed(t)
+    s = SIZES[t]
+    return (torch.rand(s, D, generator=g) * 2 - 1) * math.sqrt(1.0 / s)
+
+
+def _sharded_rank(rank, world, port, q, static):
+    dist = _init(rank, world, port)
+    try:
+        from raydp_amd.parallel.embedding_mp import ShardedEmbeddings
+        B = 6 if static else 3 + rank           # uneven batches across ranks when not static
+        g = torch.Generator().manual_seed(100 + rank)
+        idx = torch.stack([torch.randint(0, s, (B,), generator=g) for s in SIZES], 1)
+        mlp = torch.randn(B, D, generator=g)
+        coef = torch.randn(B, len(SIZES) + 1, D, generator=g)
+        emb = ShardedEmbeddings(SIZES, D, static_batch=static)
+        X = emb(mlp, idx)
+        (X * coef).sum().backward()
+        tabs = [_full_table(t).requires_grad_(True) for t in range(len(SIZES))]
+        Xr = torch.cat([mlp.unsqueeze(1)] + [tabs[t][idx[:, t]].unsqueeze(1) for t in range(len(SIZES))], 1)
+        (Xr * coef).sum().backward()
+        fwd_ok = torch.allclose(X, Xr.detach(), atol=1e-6)
+        grads = [t.grad.clone() for t in tabs]
+        for gr in grads:
+            dist.all_reduce(gr)
+        ok = True
+        if emb.local_tables:
+            dense = emb.weight.grad.coalesce().to_dense() if emb.weight.grad is not None else \
+                torch.zeros(emb.weight.shape)
+            for i, t in enumerate(emb.local_tables):
+                o = int(emb.local_offsets[i])
+                ok &= torch.allclose(dense[o:o + SIZES[t]], grads[t], atol=1e-5)
+        q.put((rank, bool(fwd_ok), bool(ok), list(emb.local_tables)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,static", [(4, True), (8, True), (4, False)])
+def test_sharded_embeddings_uneven_tables(world, static):
+    res = _spawn(_sharded_rank, world, static)
+    assert all(r[1] for r in res), res
+    assert all(r[2] for r in res), res
+    owned = sorted(t for r in res for t in r[3])
+    assert owned == list(range(len(SIZES)))
+    if world > len(SIZES):
+        assert any(not r[3] for r in res), "some rank should own no table"
+
+
+def _gbdt_rank(rank, world, port, q, x, y):
+    dist = _init(rank, world, port)
+    try:
+        from raydp_amd.xgboost.gbdt import DMatrix, train
+        n = x.shape[0] // world
+        b = train({"objective": "reg:squarederror", "max_depth": 3, "eta": 0.3, "max_bin": 32},
+                  DMatrix(x[rank * n:(rank + 1) * n].numpy(), y[rank * n:(rank + 1) * n].numpy()), 3)
+        q.put((rank, np.asarray(b.inplace_predict(x[:50].numpy())).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4])
+def test_gbdt_histograms_at_world_4(world):
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((800, 5)).astype(np.float32)
+    y = (x[:, 0] * 2 + x[:, 1] ** 2).astype(np.float32)
+    res = _spawn(_gbdt_rank, world, torch.from_numpy(x), torch.from_numpy(y))
+    preds = [np.array(r[1]) for r in res]
+    for p in preds[1:]:
+        np.testing.assert_allclose(p, preds[0], rtol=0, atol=0)   # every rank holds the same trees
+    assert np.corrcoef(preds[0], y[:50])[0, 1] > 0.7
+
+
+def _allgather_rank(rank, world, port, q):
+    dist = _init(rank, world, port)
+    try:
+        from raydp_amd.xgboost.gbdt import World
+        w = World()
+        rows = torch.full((rank + 1, 2), float(rank))
+        got = w.allgather_rows(rows)
+        t = torch.tensor([float(rank)], dtype=torch.float64)
+        w.allreduce(t)
+        q.put((rank, got.tolist(), float(t)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gbdt_world_allgather_uneven_rows():
+    res = _spawn(_allgather_rank, 4)
+    want = [[float(r)] * 2 for r in range(4) for _ in range(r + 1)]
+    for r in res:
+        assert r[1] == want and r[2] == 6.0
+
+
+def test_gbdt_world_stages_cpu_tensors_through_gpu_for_rccl(monkeypatch):
+    """RCCL (backend "nccl") takes device tensors only: CPU inputs are staged on the current GPU."""
+    from raydp_amd.xgboost.gbdt import World
+
+    class FakeDist:
+        def get_backend(self):
+            return "nccl"
+    w = World.__new__(World)
+    w.dist, w.size = FakeDist(), 2
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 3)
+    assert w._comm_device(torch.zeros(1)) == torch.device("cuda", 3)
+
+    class Gloo(FakeDist):
+        def get_backend(self):
+            return "gloo"
+    w.dist = Gloo()
+    assert w._comm_device(torch.zeros(1)) == torch.device("cpu")
+
+
+def test_bucket_allreduce_never_routes_large_buckets_to_xgmi():
+    """The one-shot xGMI kernel is for latency-bound buckets: > 1 MiB goes to RCCL."""
+    from raydp_amd.ops import comm
+
+    class FakeFlat:
+        def __init__(self, n, dtype=torch.float32):
+            self._n, self.dtype, self.is_cuda = n, dtype, True
+
+        def numel(self):
+            return self._n
+
+        def is_contiguous(self):
+            return True
+    b = comm.BucketAllreduce.__new__(comm.BucketAllreduce)
+    b.group, b.xg = None, object()
+    limit = comm.XG_BUCKET_MAX_BYTES // 4
+    assert comm.XG_BUCKET_MAX_BYTES == 1 << 20
+    assert b.routes_to_xgmi(FakeFlat(limit)) if torch.cuda.is_available() else True
+    assert not b.routes_to_xgmi(FakeFlat(limit + 1))
+    assert not b.routes_to_xgmi(FakeFlat(2_177_185))          # DLRM dense gradient (8.7 MB)
+    assert not b.routes_to_xgmi(FakeFlat(1024, torch.bfloat16))
+    b.xg = None
+    assert not b.routes_to_xgmi(FakeFlat(16))
+
+
+def test_torch_estimator_spawned_world_4(runtime_local, tmp_path):
+    """TorchEstimator(num_workers=4) through the spawned worker group (gloo on CPU): every rank
+    trains its shard, DDP keeps them identical, rank 0 checkpoints, the per-epoch report names
+    the all-reduce path."""
+    import pandas as pd
+    from raydp_amd.data import from_pandas
+    from raydp_amd.torch import TorchEstimator
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((800, 3)).astype(np.float32)
+    df = pd.DataFrame({"a": x[:, 0], "b": x[:, 1], "c": x[:, 2], "y": x @ np.array([1.0, -2.0, 0.5]) + 0.3})
+    ds = from_pandas(df)
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(3, 16), nn.ReLU(), nn.Linear(16, 1))
+    est = TorchEstimator(num_workers=4, model=model, optimizer=torch.optim.Adam(model.parameters(), lr=0.02),
+                         loss=nn.MSELoss(), feature_columns=["a", "b", "c"], label_column="y",
+                         batch_size=50, num_epochs=4, use_gpu=False, storage_path=str(tmp_path))
+    res = est.fit(ds)
+    hist = [m for m in res.metrics_history if "train_loss" in m]
+    assert len(hist) == 4 and hist[-1]["train_loss"] < hist[0]["train_loss"]
+    assert hist[-1]["allreduce"].startswith("torch.distributed:gloo")
+    trained = est.get_model()
+    pred = trained(torch.from_numpy(x[:100])).detach().numpy()[:, 0]
+    assert np.corrcoef(pred, df["y"].to_numpy()[:100])[0, 1] > 0.9
