@@ -287,6 +287,51 @@ class FusedMLPTrainer:
             self.jit = mlp_jit.load_specialized(self)
         self.refresh_images()
 
+    # ------------------------------------------------------------------- optimizer state ----
+    def _param_of(self, kind, mod):
+        return getattr(mod, {"weight": "weight", "bias": "bias", "gamma": "weight", "beta": "bias"}[kind])
+
+    @torch.no_grad()
+    def load_optimizer_state(self, opt: torch.optim.Optimizer) -> bool:
+        """Start from a torch optimizer's state (Adam/AdamW ``exp_avg``/``exp_avg_sq``/``step``,
+        SGD ``momentum_buffer``) -- a resumed fit or an optimizer handed in mid-training."""
+        if not opt.state:
+            return False
+        m_h, v_h = self.m.cpu(), self.v.cpu()
+        step = None
+        for kind, mod, off, n in self.layout:
+            st = opt.state.get(self._param_of(kind, mod))
+            if not st:
+                continue
+            if "exp_avg" in st:
+                m_h[off:off + n] = st["exp_avg"].detach().reshape(-1).float().cpu()
+                v_h[off:off + n] = st["exp_avg_sq"].detach().reshape(-1).float().cpu()
+                step = int(st["step"].item() if torch.is_tensor(st["step"]) else st["step"])
+            elif st.get("momentum_buffer") is not None:
+                m_h[off:off + n] = st["momentum_buffer"].detach().reshape(-1).float().cpu()
+                step = max(step or 0, 1)
+        self.m.copy_(m_h)
+        self.v.copy_(v_h)
+        if step is not None:
+            self.step_count = step
+        return True
+
+    @torch.no_grad()
+    def export_optimizer_state(self, opt: torch.optim.Optimizer) -> dict:
+        """Write the device moments / step into ``opt`` (whose params are the user's module
+        parameters) and return ``opt.state_dict()`` -- the ``optim.pt`` of a checkpoint."""
+        m_h, v_h = self.m.cpu(), self.v.cpu()
+        algo = self.cfg["algo"]
+        for kind, mod, off, n in self.layout:
+            p = self._param_of(kind, mod)
+            if algo in (0, 1):
+                opt.state[p] = {"step": torch.tensor(float(self.step_count)),
+                                "exp_avg": m_h[off:off + n].view_as(p).clone(),
+                                "exp_avg_sq": v_h[off:off + n].view_as(p).clone()}
+            elif self.cfg.get("momentum", 0.0):
+                opt.state[p] = {"momentum_buffer": m_h[off:off + n].view_as(p).clone()}
+        return opt.state_dict()
+
     def refresh_images(self):
         """Rebuild the bf16 W/Wt images from the fp32 master parameters."""
         _hip.check(self.lib.rx_mlp_refresh_images(ctypes.byref(self.opt), self._od,

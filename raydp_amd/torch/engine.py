@@ -105,6 +105,8 @@ class FusedMLPEngine:
         self.model, self.metrics_names, self.device = model, metrics.names, device
         self.world = session.get_world_size()
         self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn)
+        self.optimizer = optimizer
+        self.trainer.load_optimizer_state(optimizer)
         if self.world > 1:
             import torch.distributed as dist
             dist.broadcast(self.trainer.params, 0)
@@ -169,6 +171,9 @@ class FusedMLPEngine:
     def state_dict(self):
         self.trainer.write_back()
         return self.model.state_dict()
+
+    def optimizer_state_dict(self):
+        return self.trainer.export_optimizer_state(self.optimizer)
 
 
 def _xgmi_for(trainer):
@@ -295,3 +300,6 @@ class TorchLoopEngine:
 
     def state_dict(self):
         return self.raw_model.state_dict()
+
+    def optimizer_state_dict(self):
+        return self.optimizer.state_dict()

@@ -39,6 +39,8 @@ def _make_lr_schedule(opt_template: torch.optim.Optimizer, creator, config):
     dummy = torch.nn.Parameter(torch.zeros(1))
     g = dict(opt_template.param_groups[0])
     g.pop("params")
+    if "initial_lr" in g:       # a resumed optimizer carries the decayed lr: restart from the base
+        g["lr"] = g.pop("initial_lr")
     opt = type(opt_template)([dummy], **{k: v for k, v in g.items()
                                          if k in inspect.signature(type(opt_template)).parameters})
     sched = creator(opt, config)
@@ -51,6 +53,46 @@ def _make_lr_schedule(opt_template: torch.optim.Optimizer, creator, config):
             sched.step()
         return cache[t]
     return lr_at
+
+
+OPTIM_KEY, SCHED_KEY, META_KEY = "optim.pt", "sched.pt", "meta.json"
+
+
+def _restore_optimizer(path: str, optimizer):
+    op = os.path.join(path, OPTIM_KEY)
+    if os.path.exists(op):
+        optimizer.load_state_dict(torch.load(op, map_location="cpu", weights_only=True))
+
+
+def _restore_checkpoint(path: str, model) -> int:
+    """Load ``model.pt`` of a checkpoint directory into the worker's model; returns the first
+    epoch still to run (``optim.pt`` is loaded by ``_restore_optimizer`` once the engine's
+    scheduler exists)."""
+    import json
+    model.load_state_dict(torch.load(os.path.join(path, "model.pt"), map_location="cpu", weights_only=True))
+    meta = os.path.join(path, META_KEY)
+    if os.path.exists(meta):
+        with open(meta) as f:
+            return int(json.load(f).get("epoch", -1)) + 1
+    return 0
+
+
+def _report_epoch_checkpoint(engine, epoch: int):
+    """Rank 0 writes ``model.pt`` + ``optim.pt`` (+ ``sched.pt``) + ``meta.json`` after
+    ``epoch``; every rank reports so the group stays in step."""
+    import json
+    ckpt = None
+    with tempfile.TemporaryDirectory() as d:
+        if session.get_world_rank() == 0:
+            torch.save({k: v.detach().cpu() for k, v in engine.state_dict().items()}, os.path.join(d, "model.pt"))
+            torch.save(engine.optimizer_state_dict(), os.path.join(d, OPTIM_KEY))
+            sched = getattr(engine, "scheduler", None)
+            if sched is not None:
+                torch.save(sched.state_dict(), os.path.join(d, SCHED_KEY))
+            with open(os.path.join(d, META_KEY), "w") as f:
+                json.dump({"epoch": epoch}, f)
+            ckpt = Checkpoint.from_directory(d)
+        session.report({"epoch": epoch, "checkpoint_epoch": epoch}, checkpoint=ckpt)
 
 
 class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
@@ -143,6 +185,12 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             raise Exception("Unsupported parameter, we only support torch.nn.modules.loss._Loss "
                             "subclass, subclass instance or a function(dict -> loss)")
         metrics = copy.deepcopy(config["metrics"])
+        # a restarted worker group resumes from the newest checkpoint an earlier attempt wrote
+        start_epoch, resume_dir = 0, None
+        ck = session.get_checkpoint()
+        if ck is not None:
+            resume_dir = ck.path
+            start_epoch = _restore_checkpoint(resume_dir, model)
 
         train_ds = session.get_dataset_shard("train")
         eval_ds = session.get_dataset_shard("evaluate") if config["evaluate"] else None
@@ -164,6 +212,8 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                              "(FusedMLPEngine.applicable)")
         if fused is not None:
             spec, lc, oc = fused
+            if resume_dir:
+                _restore_optimizer(resume_dir, optimizer)
             lr_fn = None
             if config["lr_scheduler_creator"]:
                 lr_fn = _make_lr_schedule(optimizer, config["lr_scheduler_creator"], config)
@@ -171,7 +221,14 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         else:
             model = model.to(device)       # in place: the optimizer keeps its parameter objects
             sched = config["lr_scheduler_creator"](optimizer, config) if config["lr_scheduler_creator"] else None
+            if resume_dir:
+                # after the scheduler: its constructor resets the group's lr, the restored
+                # optimizer state puts the resumed lr back
+                _restore_optimizer(resume_dir, optimizer)
+                if sched is not None and os.path.exists(os.path.join(resume_dir, SCHED_KEY)):
+                    sched.load_state_dict(torch.load(os.path.join(resume_dir, SCHED_KEY), weights_only=True))
             engine = TorchLoopEngine(model, optimizer, loss, metrics, device, config, sched)
+        engine.epoch = start_epoch          # epoch permutations continue where the run left off
         from raydp_amd.utils import tracing
         t_load0 = time.perf_counter()
         with tracing.span("ingest", cat="train", engine=engine.name):
@@ -180,7 +237,8 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         t_train0 = time.perf_counter()
         config.setdefault("_engine_name", engine.name)
         timed = device.type == "cuda"
-        for epoch in range(config["num_epochs"]):
+        ck_every = int(config.get("checkpoint_frequency") or 0)
+        for epoch in range(start_epoch, config["num_epochs"]):
             if timed:   # device-timed epoch (HIP events; no per-step host sync)
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 ev0.record()
@@ -206,6 +264,9 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                 with tracing.span("eval epoch", cat="train", epoch=epoch):
                     eval_res, test_loss = engine.evaluate_epoch()
                 session.report(dict(epoch=epoch, eval_res=eval_res, test_loss=test_loss))
+            if ck_every and (epoch + 1) % ck_every == 0 and epoch + 1 < config["num_epochs"]:
+                with tracing.span("epoch checkpoint", cat="train", epoch=epoch):
+                    _report_epoch_checkpoint(engine, epoch)
         LAST_TIMINGS["train"] = time.perf_counter() - t_train0
         t_ck0 = time.perf_counter()
         with tracing.span("checkpoint", cat="train"):
@@ -238,6 +299,9 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             "metrics": self._metrics,
             "fused": self._extra_config.get("fused", None),
             "shuffle_seed": self._extra_config.get("shuffle_seed", None),
+            # per-epoch checkpoints (model.pt + optim.pt) every N epochs; 0 = only the final
+            # model.pt, as the reference
+            "checkpoint_frequency": int(self._extra_config.get("checkpoint_frequency", 0) or 0),
         }
         use_gpu = self._extra_config.get("use_gpu")
         if self._resources_per_worker and "GPU" in self._resources_per_worker:
@@ -263,7 +327,11 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             train_loop_config["evaluate"] = False
         else:
             datasets["evaluate"] = evaluate_ds
-        torch_config = TorchConfig(backend="ccl") if self._use_ccl else None
+        # use_ccl: the reference swaps in oneCCL (torch/estimator.py:344-347); here TorchConfig
+        # resolves "ccl" to RCCL on GPU workers and gloo on CPU workers
+        torch_config = self._extra_config.get("torch_config")
+        if torch_config is None and self._use_ccl:
+            torch_config = TorchConfig(backend="ccl")
         self._trainer = TorchTrainer(TorchEstimator.train_func,
                                      train_loop_config=train_loop_config,
                                      scaling_config=scaling_config,

@@ -67,11 +67,19 @@ class _Session:
         self.last = now
         persisted = None
         if checkpoint is not None:
-            # persist immediately: the caller's directory may be a TemporaryDirectory
-            dst = os.path.join(self.storage_dir, f"checkpoint_{self.iteration:06d}")
-            if os.path.exists(dst):
-                shutil.rmtree(dst)
-            shutil.copytree(checkpoint.path, dst)
+            # persist immediately (the caller's directory may be a TemporaryDirectory), under a
+            # name that sorts after every checkpoint of this run, restarted attempts included:
+            # the trainer resumes a failed group from the newest one
+            try:
+                n = sum(1 for x in os.listdir(self.storage_dir) if x.startswith("checkpoint_"))
+            except OSError:
+                n = 0
+            dst = os.path.join(self.storage_dir, f"checkpoint_{n:06d}")
+            tmp = dst + f".tmp{os.getpid()}"
+            if os.path.exists(tmp):
+                shutil.rmtree(tmp)
+            shutil.copytree(checkpoint.path, tmp)
+            os.replace(tmp, dst)          # a crash mid-copy never leaves a partial checkpoint
             persisted = dst
         self.reporter(self.ctx.world_rank, m, persisted)
 

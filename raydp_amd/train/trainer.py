@@ -13,7 +13,9 @@ on the same step count, so collectives never deadlock). Three launch modes:
 
 Failures restart the whole group up to ``FailureConfig.max_failures`` times (reference:
 ``RunConfig(failure_config=FailureConfig(max_failures=max_retries))`` at
-``python/raydp/torch/estimator.py:334``).
+``python/raydp/torch/estimator.py:334``), from the newest checkpoint rank 0 reported
+(``session.get_checkpoint()`` in the restarted loop), like Ray Train. The process-group backend
+comes from ``TorchConfig`` (``use_ccl`` in the estimator; RCCL on GPU, gloo on CPU).
 """
 import os
 import pickle
@@ -41,6 +43,7 @@ class Result:
     path: str
     error: Optional[BaseException] = None
     metrics_history: List[Dict[str, Any]] = field(default_factory=list)
+    restored_from: List[str] = field(default_factory=list)   # checkpoints earlier attempts resumed from
 
     @property
     def metrics_dataframe(self):
@@ -77,13 +80,32 @@ def _shard(datasets: Dict[str, Any], rank: int, world: int) -> Dict[str, Any]:
     return out
 
 
-def _init_dist(backend: str, rank: int, world: int, addr: str, port: int):
+def _init_dist(backend: str, rank: int, world: int, addr: str, port: int, timeout_s: Optional[float] = None):
+    import datetime
     import torch.distributed as dist
     if dist.is_initialized():
         return False
+    kw = {"timeout": datetime.timedelta(seconds=float(timeout_s))} if timeout_s else {}
     dist.init_process_group(backend, init_method=f"tcp://{addr}:{port}", rank=rank,
-                            world_size=world)
+                            world_size=world, **kw)
     return True
+
+
+def _backend(torch_config, use_gpu: bool) -> str:
+    """``TorchConfig`` (reference ``python/raydp/torch/config.py:12-45``; ``use_ccl`` asks for
+    oneCCL there) -> the process-group backend: RCCL (``"nccl"``) on GPU workers, gloo on CPU."""
+    if torch_config is not None:
+        return torch_config.resolve(use_gpu)
+    return "nccl" if use_gpu else "gloo"
+
+
+def latest_checkpoint(storage: str) -> Optional[str]:
+    """Newest ``checkpoint_*`` directory under a run's storage path (reported by rank 0)."""
+    try:
+        names = sorted(n for n in os.listdir(storage) if n.startswith("checkpoint_") and ".tmp" not in n)
+    except OSError:
+        return None
+    return os.path.join(storage, names[-1]) if names else None
 
 
 def _worker_entry(rank, world, port, payload, queue):
@@ -163,21 +185,30 @@ class DataParallelTrainer:
         return path
 
     def fit(self) -> Result:
+        """Run the worker group; on a worker failure restart it, up to
+        ``FailureConfig.max_failures`` times, from the newest checkpoint any attempt reported
+        (Ray Train's ``FailureConfig`` semantics, reference ``torch/estimator.py:331-334``)."""
         failures = 0
         max_f = self.run_config.failure_config.max_failures
-        last_err = None
+        storage = self._storage()
+        restored = []
         while True:
             try:
-                return self._fit_once()
+                res = self._fit_once(storage)
+                res.restored_from = restored
+                return res
             except _WorkerFailure as e:
-                last_err = e
                 failures += 1
                 if max_f >= 0 and failures > max_f:
                     raise TrainingFailedError(f"training failed after {failures} attempt(s):\n{e}") from None
+                ck = latest_checkpoint(storage)
+                if ck is not None:
+                    self.resume = Checkpoint(ck)
+                    restored.append(ck)
 
-    def _fit_once(self) -> Result:
+    def _fit_once(self, storage: Optional[str] = None) -> Result:
         world = int(self.scaling.num_workers)
-        storage = self._storage()
+        storage = storage or self._storage()
         use_gpu = self._use_gpu()
         history: List[Dict[str, Any]] = []
         ckpts: List[str] = []
@@ -211,9 +242,13 @@ class DataParallelTrainer:
             device = torch.device("cuda", local % n)
         created = False
         if world > 1:
+            import datetime
             import torch.distributed as dist
             if not dist.is_initialized():
-                dist.init_process_group("nccl" if use_gpu else "gloo")
+                kw = {}
+                if self.torch_config is not None and self.torch_config.timeout_s:
+                    kw["timeout"] = datetime.timedelta(seconds=float(self.torch_config.timeout_s))
+                dist.init_process_group(_backend(self.torch_config, use_gpu), **kw)
                 created = True
         shards = dict(self.datasets) if self.local_shards else _shard(self.datasets, rank, world)
         ctx = S.TrainContext(rank, world, local, world, 0, device, "raydp", storage)
@@ -262,19 +297,28 @@ class DataParallelTrainer:
             # that node's worker GPUs and binds cuda:<local_rank>, so RCCL and the xGMI one-shot
             # path can map peer memory (a worker that saw only its own GPU could not)
             layout = _local_layout(workers)
-            runtime.get([w.setup.remote("127.0.0.1", port, *layout[r]) for r, w in enumerate(workers)])
+            backend = _backend(self.torch_config, use_gpu)
+            tmo = self.torch_config.timeout_s if self.torch_config is not None else None
+            runtime.get([w.setup.remote("127.0.0.1", port, *layout[r], backend=backend, timeout_s=tmo)
+                         for r, w in enumerate(workers)])
             refs = []
             for r, w in enumerate(workers):
                 shards = _shard(self.datasets, r, world)
                 payload = cloudpickle.dumps((self.fn, self.config, shards, self.resume))
                 refs.append(w.run.remote(payload))
+            # wait on all ranks at once: when one dies, its peers are blocked in a collective
+            # that will never complete -- fail the attempt at the first error (the finally
+            # block below kills the survivors) instead of waiting on rank 0 forever
             outs, error = [None] * world, None
-            for r, ref in enumerate(refs):
-                try:
-                    outs[r] = runtime.get(ref)
-                except Exception:  # noqa: BLE001 - a rank failed (user error or lost process)
-                    error = traceback.format_exc()
-                    break
+            pending = list(refs)
+            while pending and error is None:
+                ready, pending = runtime.wait(pending, num_returns=1)
+                for ref in ready:
+                    try:
+                        outs[refs.index(ref)] = runtime.get(ref)
+                    except Exception:  # noqa: BLE001 - a rank failed (user error or lost process)
+                        error = traceback.format_exc()
+                        break
             if error is not None:
                 raise _WorkerFailure(error)
             for r, reports in enumerate(outs):
@@ -321,7 +365,7 @@ class _TrainWorker:
         self.local_rank, self.local_world, self.node_rank = 0, 1, rank
 
     def setup(self, addr: str, port: int, visible=None, local_rank: int = 0, local_world: int = 1,
-              node_rank: int = 0):
+              node_rank: int = 0, backend: Optional[str] = None, timeout_s: Optional[float] = None):
         if visible and self.use_gpu:
             # before the first HIP call of this process: the node's worker GPUs, in order
             os.environ["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in visible)
@@ -336,7 +380,9 @@ class _TrainWorker:
         os.environ.update({"RANK": str(self.rank), "WORLD_SIZE": str(self.world),
                            "LOCAL_RANK": str(local_rank), "LOCAL_WORLD_SIZE": str(local_world),
                            "MASTER_ADDR": addr, "MASTER_PORT": str(port)})
-        _init_dist("nccl" if self.device.type == "cuda" else "gloo", self.rank, self.world, addr, port)
+        if backend is None or (backend == "nccl" and self.device.type != "cuda"):
+            backend = "nccl" if self.device.type == "cuda" else "gloo"
+        _init_dist(backend, self.rank, self.world, addr, port, timeout_s)
         return True
 
     def run(self, payload: bytes):

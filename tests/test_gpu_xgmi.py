@@ -137,8 +137,12 @@ def _run(target, world=2):
     return res
 
 
-def test_xgmi_allreduce_two_ranks_one_gpu():
-    res = _run(_allreduce_main)
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_allreduce_ranks_share_one_gpu(world):
+    """World 4 exercises the N-1 = 3 peer read fan-out and the flag protocol with more than
+    one remote writer per slot."""
+    res = _run(_allreduce_main, world)
+    assert len(res) == world
     for rank, status, worst in res:
         assert status == "ok", (rank, status)
         assert worst < 1e-5, (rank, worst)
