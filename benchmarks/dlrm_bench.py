@@ -31,7 +31,11 @@ def main():
     ap.add_argument("--fused-sgd", action="store_true", help="apply the embedding SGD inside backward")
     ap.add_argument("--amp", action="store_true", help="bf16 autocast for the MLP towers")
     ap.add_argument("--model-parallel", action="store_true", help="sharded tables even on 1 GPU")
+    ap.add_argument("--eager-mlp", action="store_true",
+                    help="run the MLP towers as eager nn.Linear/ReLU instead of the fused MFMA kernels")
     args = ap.parse_args()
+    if args.eager_mlp:
+        os.environ["RAYDP_FUSED_LINEAR"] = "0"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -95,6 +99,7 @@ def main():
                           "per_gpu_batch": args.batch, "steps": args.steps, "warmup": args.warmup,
                           "embeddings": "table-wise sharded + all-to-all" if mp else "replicated fused",
                           "fused_sgd": args.fused_sgd, "amp": args.amp, "loss": float(loss),
+                          "mlp": "eager torch" if args.eager_mlp else "fused MFMA towers (csrc/hip/linear_act.hip)",
                           "tables": 26, "rows_per_table": args.rows_per_table, "scaling": "weak"}), flush=True)
     if mp:
         dist.destroy_process_group()

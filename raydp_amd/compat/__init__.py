@@ -11,8 +11,9 @@ import types
 
 
 def _missing(name: str) -> bool:
+    """True when no real ``name`` package is importable (our own facade does not count)."""
     if name in sys.modules:
-        return getattr(sys.modules[name], "__raydp_facade__", False) is False and False
+        return bool(getattr(sys.modules[name], "__raydp_facade__", False))
     try:
         return importlib.util.find_spec(name) is None
     except (ImportError, ValueError):

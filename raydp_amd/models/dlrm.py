@@ -1,7 +1,8 @@
 """DLRM (Naumov et al.; reference: the ``Dlrm`` model of examples/pytorch_dlrm.ipynb cell 9)
 re-designed for MI355X: the 26 embedding tables are one fused parameter gathered by a HIP
 kernel straight into the interaction input, the dot interaction runs on MFMA
-(``raydp_amd.ops.dlrm_ops``), and the MLP towers are plain Linear+ReLU (hipBLASLt GEMMs).
+(``raydp_amd.ops.dlrm_ops``), and on the GPU both MLP towers run on the fused Linear+bias+ReLU
+MFMA GEMMs (``raydp_amd.ops.linear_ops``; eager ``nn.Linear`` + ``ReLU`` on the CPU).
 
 ``model_parallel=True`` shards the tables over the process group instead (table-wise, all-to-all
 exchange) for multi-GPU training.
@@ -36,8 +37,22 @@ class TorchMlp(nn.Module):
     def weights(self):
         return [m.weight for m in self.layers if isinstance(m, nn.Linear)]
 
+    @property
+    def linears(self):
+        return [m for m in self.layers if isinstance(m, nn.Linear)]
+
     def forward(self, x):
+        if x.is_cuda and _fused_ok(x):
+            if getattr(self, "_fused", None) is None:
+                from raydp_amd.ops.linear_ops import FusedLinearTower
+                self._fused = FusedLinearTower(self.linears, [True] * len(self.linears), out_f32=True)
+            return self._fused(x)
         return self.layers(x)
+
+
+def _fused_ok(x) -> bool:
+    from raydp_amd.ops.linear_ops import tower_enabled
+    return x.dim() == 2 and x.dtype in (torch.float32, torch.bfloat16) and tower_enabled()
 
 
 class Dlrm(nn.Module):
@@ -76,4 +91,13 @@ class Dlrm(nn.Module):
             cats = torch.cat(inputs[self.num_numerical_features:], dim=1)
         mlp_out = self.bottom_mlp(dense.float())
         X = self.embeddings(mlp_out, cats.long())
-        return self.out(self.top_mlp(dot_interaction(X)))
+        Z = dot_interaction(X)
+        if Z.is_cuda and _fused_ok(Z):
+            # the whole top tower including the output layer is one fused op: the last bf16
+            # activation never leaves the chain and the logits come back fp32
+            if getattr(self, "_top_fused", None) is None:
+                from raydp_amd.ops.linear_ops import FusedLinearTower
+                lins = self.top_mlp.linears + [self.out]
+                self._top_fused = FusedLinearTower(lins, [True] * (len(lins) - 1) + [False], out_f32=True)
+            return self._top_fused(Z)
+        return self.out(self.top_mlp(Z))

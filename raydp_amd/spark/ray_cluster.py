@@ -8,6 +8,7 @@ executor processes); the returned session schedules its tasks on those executors
 import logging
 from typing import Any, Dict, Optional
 
+from raydp_amd.services import Cluster
 from raydp_amd.utils import get_node_ip_address, parse_memory_size
 
 logger = logging.getLogger(__name__)
@@ -17,9 +18,13 @@ SPARK_RAY_MASTER_RESOURCE_PREFIX = "spark.ray.raydp_spark_master.actor.resource.
 SPARK_RAY_MASTER_RESOURCE_PREFIX_DEPRECATED = "spark.ray.raydp_spark_master.resource."
 
 
-class SparkCluster:
+class SparkCluster(Cluster):
+    """The ``Cluster`` of a Spark application (reference ``ray_cluster.py:34``): the master is
+    the native app master + driver-side backend, workers are executor actors."""
+
     def __init__(self, app_name: str, num_executors: int, executor_cores: int,
                  executor_memory: Any, enable_hive: bool, configs: Optional[Dict[str, str]] = None):
+        super().__init__(None)
         self._app_name = app_name
         self._num_executors = num_executors
         self._executor_cores = executor_cores
@@ -60,10 +65,18 @@ class SparkCluster:
                     res["CPU" if name.lower() == "cpu" else name] = val
         return res
 
-    def _set_up_master(self):
+    def _set_up_master(self, resources: Optional[Dict[str, float]] = None, kwargs=None):
         from raydp_amd.spark.cluster import ClusterBackend
-        self._backend = ClusterBackend(self._app_name, self._configs, self._master_resources())
+        self._backend = ClusterBackend(self._app_name, self._configs, resources or self._master_resources())
         self._backend.start()
+
+    def _set_up_worker(self, resources: Dict[str, float], kwargs: Dict[str, str]):
+        """One more executor actor, through the app master's dynamic-allocation path (the
+        reference raises "Unsupported operation" here)."""
+        cur = len(self._backend.alive_executors())
+        if not self._backend.request_total_executors(cur + 1):
+            raise RuntimeError("the app master refused another executor (spark.dynamicAllocation.maxExecutors?)")
+        self._num_nodes += 1
 
     def get_cluster_url(self) -> str:
         return self._backend.master_url()

@@ -22,6 +22,15 @@ import pyarrow as pa
 from raydp_amd.spark.types import DataType, parse_type_string
 
 _VERIFY_ROWS = 64
+_REVERIFY_ROWS = 8
+
+
+def _argmin(a):
+    return int(np.nanargmin(a)) if a.dtype.kind == "f" else int(np.argmin(a))
+
+
+def _argmax(a):
+    return int(np.nanargmax(a)) if a.dtype.kind == "f" else int(np.argmax(a))
 
 
 class _Unsupported(Exception):
@@ -263,25 +272,30 @@ class UserDefinedFunction:
         except Exception:  # noqa: BLE001 - any failure means "not vectorizable"
             self._vec_state = "failed"
             return None
-        if self._vec_state == "untried" or n <= _VERIFY_ROWS:
-            # verify against the exact per-row semantics on a sample
-            k = min(n, _VERIFY_ROWS)
-            idx = np.linspace(0, n - 1, k).astype(np.int64)
-            rows = [[a[i].as_py() for a in arrays] for i in idx]
-            try:
-                expect = np.array([self.func(*r) for r in rows]).astype(np_dtype)
-            except Exception:  # noqa: BLE001
-                self._vec_state = "failed"
-                return None
-            got = res[idx]
-            if np.dtype(np_dtype).kind == "f":
-                ok = np.allclose(got, expect, rtol=1e-6, atol=1e-9, equal_nan=True)
-            else:
-                ok = np.array_equal(got, expect)
-            if not ok:
-                self._vec_state = "failed"
-                return None
-            self._vec_state = "ok"
+        # verify against the exact per-row semantics on EVERY batch: the first one on a 64-row
+        # sample, later ones on 8 spread rows, always adding each argument's minimum and maximum
+        # row, so a branch that a new value range takes is checked when that range first shows up
+        first = self._vec_state == "untried" or n <= _VERIFY_ROWS
+        idx = np.linspace(0, n - 1, min(n, _VERIFY_ROWS if first else _REVERIFY_ROWS)).astype(np.int64)
+        ext = [f(a) for a in nps if a.size and a.dtype.kind in "biuf" and not np.isnan(a.astype(np.float64)).all()
+               for f in (_argmin, _argmax)]
+        if ext:
+            idx = np.unique(np.concatenate([idx, np.asarray(ext, dtype=np.int64)]))
+        rows = [[a[i].as_py() for a in arrays] for i in idx]
+        try:
+            expect = np.array([self.func(*r) for r in rows]).astype(np_dtype)
+        except Exception:  # noqa: BLE001
+            self._vec_state = "failed"
+            return None
+        got = res[idx]
+        if np.dtype(np_dtype).kind == "f":
+            ok = np.allclose(got, expect, rtol=1e-6, atol=1e-9, equal_nan=True)
+        else:
+            ok = np.array_equal(got, expect)
+        if not ok:
+            self._vec_state = "failed"
+            return None
+        self._vec_state = "ok"
         return res
 
     def _row_by_row(self, arrays, n, out_type):

@@ -99,21 +99,20 @@ def convert_to_spark(df):
     return _df_helper(df, lambda d: (d, True), lambda d: (d.to_spark(), False))
 
 
+_SIZE_RE = re.compile(r"^\s*([0-9]*\.?[0-9]+)\s*([KMGT]?)(?:I?B)?\s*$", re.IGNORECASE)
+
+
 def parse_memory_size(memory_size) -> int:
-    """Parse a human readable memory size ("10", "10K", "10 kb", "1.5g") into bytes."""
+    """Bytes of a human readable size: "10", "10K", "10 kb", "1.5g", "2 GiB" (powers of 1024,
+    reference ``python/raydp/utils.py:125-146``)."""
     if isinstance(memory_size, (int, np.integer)):
         return int(memory_size)
-    memory_size = str(memory_size).strip().upper()
-    if re.search(r"B", memory_size):
-        memory_size = re.sub(r"B", "", memory_size)
-    try:
-        return int(memory_size)
-    except ValueError:
-        pass
-    if not re.search(r" ", memory_size):
-        memory_size = re.sub(r"([KMGT]+)", r" \1", memory_size)
-    number, unit_index = [item.strip() for item in memory_size.split()]
-    return int(float(number) * MEMORY_SIZE_UNITS[unit_index])
+    m = _SIZE_RE.match(str(memory_size))
+    if m is None:
+        raise ValueError(f"cannot parse memory size {memory_size!r}")
+    number, unit = m.group(1), m.group(2).upper()
+    scale = MEMORY_SIZE_UNITS.get(unit, 1)
+    return int(float(number) * scale) if "." in number else int(number) * scale
 
 
 def divide_blocks(blocks: List[int], world_size: int, shuffle: bool = False,

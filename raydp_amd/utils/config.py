@@ -139,6 +139,9 @@ register("spark.ray.mi355x.mlp_wgrad", "str", "opt",
 register("spark.ray.mi355x.mlp_persistent", "bool", True,
          "one GPU: run a whole fused-MLP epoch as one persistent launch with the optimizer beside the "
          "backward pass (csrc/hip/mlp_persist.h)", env="RAYDP_MLP_PERSISTENT")
+register("spark.ray.mi355x.fused_linear", "bool", True,
+         "run Linear(+ReLU) towers of the DLRM-class models (TorchMlp) on the fused MFMA GEMM kernels "
+         "(csrc/hip/linear_act.hip) instead of eager torch", env="RAYDP_FUSED_LINEAR")
 register("spark.ray.mi355x.mlp_persistent.timeout_s", "float", 5.0,
          "bound on every workgroup hand-off wait of the persistent epoch kernel; on expiry the epoch "
          "is rolled back and rerun on the launch-per-step loop", env="RAYDP_MLP_PERSISTENT_TIMEOUT_S")

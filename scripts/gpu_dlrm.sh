@@ -1,11 +1,16 @@
 #!/bin/bash
-# DLRM throughput: replicated fused embeddings (1 GPU) and the sharded/all-to-all path at world 1 (RCCL).
+# DLRM: fused-tower tests, bench (fused vs eager), rocprof kernel stats of the fused step.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-timeout -k 10 300 python benchmarks/dlrm_bench.py --fused-sgd --amp > gpurun_out/dlrm_1gpu.log 2>&1 || exit $?
-tail -1 gpurun_out/dlrm_1gpu.log
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 benchmarks/dlrm_bench.py --amp --model-parallel > gpurun_out/dlrm_mp1.log 2>&1 || exit $?
-tail -1 gpurun_out/dlrm_mp1.log
-RAYDP_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29542 benchmarks/dlrm_bench.py --amp --steps 50 --warmup 5 > gpurun_out/dlrm_mp2_gloo.log 2>&1
-echo "2-rank gloo rehearsal rc=$?"; grep metric gpurun_out/dlrm_mp2_gloo.log | tail -1; grep -m3 -i error gpurun_out/dlrm_mp2_gloo.log
-exit 0
+R=$(pwd)
+mkdir -p gpurun_out/prof
+timeout -k 10 300 python -u -m pytest tests/test_gpu_linear.py tests/test_gpu_dlrm.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_linear.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|^E  " gpurun_out/gpu_linear.log | tail -12
+if [ $rc -ne 0 ]; then exit $rc; fi
+for mode in "" "--eager-mlp" "--eager-mlp --amp" "--fused-sgd"; do
+  timeout -k 10 200 python benchmarks/dlrm_bench.py $mode >> gpurun_out/dlrm_bench.jsonl 2>gpurun_out/dlrm_err.log
+  rc=$?; if [ $rc -ne 0 ]; then echo "dlrm bench '$mode' rc=$rc"; tail -5 gpurun_out/dlrm_err.log; exit $rc; fi
+done
+cat gpurun_out/dlrm_bench.jsonl | cut -c1-220
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o dlrm -- python3 $R/benchmarks/dlrm_bench.py --steps 50 --warmup 10 > $R/gpurun_out/prof_dlrm.log 2>&1
+rc=$?; echo "prof rc=$rc"; exit $rc
