@@ -59,7 +59,7 @@ class Dlrm(nn.Module):
     def __init__(self, num_numerical_features: int, categorical_feature_sizes: Sequence[int],
                  bottom_mlp_sizes: Sequence[int], top_mlp_sizes: Sequence[int], embedding_dim: int = 32,
                  fused_embedding_sgd_lr: Optional[float] = None, model_parallel: bool = False,
-                 embedding_group=None, static_batch: bool = False):
+                 embedding_group=None, static_batch="auto"):
         super().__init__()
         if embedding_dim != bottom_mlp_sizes[-1]:
             raise ValueError("The last bottom MLP layer must have same size as embedding.")
@@ -89,8 +89,13 @@ class Dlrm(nn.Module):
         else:
             dense = torch.cat(inputs[:self.num_numerical_features], dim=1).float()
             cats = torch.cat(inputs[self.num_numerical_features:], dim=1)
+        pending = None
+        if hasattr(self.embeddings, "start"):
+            # sharded tables: the id all-to-all is in flight while the bottom MLP runs
+            pending = self.embeddings.start(cats)
         mlp_out = self.bottom_mlp(dense.float())
-        X = self.embeddings(mlp_out, cats.long())
+        X = self.embeddings.finish(pending, mlp_out) if pending is not None else \
+            self.embeddings(mlp_out, cats.long())
         Z = dot_interaction(X)
         if Z.is_cuda and _fused_ok(Z):
             # the whole top tower including the output layer is one fused op: the last bf16

@@ -271,6 +271,9 @@ class FusedLinearTower:
         return st
 
     def _refresh_images(self):
+        # inside a HIP-graph capture the refresh is recorded unconditionally: a replayed step
+        # must re-derive the images from the (replayed) optimizer's updates
+        capturing = torch.cuda.is_current_stream_capturing()
         stale = []
         for li, lin in enumerate(self.linears):
             w = lin.weight
@@ -279,7 +282,7 @@ class FusedLinearTower:
                 img = self.images[li] = torch.empty(w.shape, dtype=torch.bfloat16, device=w.device)
                 self._versions[li] = None
             key = (w.data_ptr(), w._version)
-            if self._versions[li] != key:
+            if self._versions[li] != key or capturing:
                 stale.append(li)
                 self._versions[li] = key
         if not stale:

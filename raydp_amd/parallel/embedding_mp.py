@@ -13,7 +13,10 @@ and one training step moves only the looked-up rows:
             sparse gradient of the owner's local table (SGD applies it without densifying).
 
 Collectives are ``torch.distributed.all_to_all_single`` (RCCL over xGMI on MI355X, gloo on
-CPU). Dense parameters (the MLPs) stay data parallel.
+CPU). The id exchange is issued ``async_op`` before the bottom MLP runs (``start`` / ``finish``,
+``Dlrm.forward``) and, with the fused embedding SGD, the reverse gradient exchange overlaps the
+bottom MLP's backward (applied at the end of the backward pass). Batch sizes are exchanged only
+when they change. Dense parameters (the MLPs) stay data parallel.
 """
 from typing import List, Optional, Sequence
 
@@ -39,32 +42,27 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group):
     return out
 
 
+class _Pending:
+    """An id exchange in flight (``ShardedEmbeddings.start``): the all-to-all of the local
+    batch's category ids to the tables' owners, issued ``async_op`` so that the bottom MLP runs
+    while it moves."""
+    __slots__ = ("B", "T", "all_b", "in_splits", "out_splits", "recv", "work")
+
+
 class _ShardedLookup(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, weight, idx, mod):
+    def forward(ctx, weight, pend, mod):
         group, world = mod.group, mod.world
-        B, T = idx.shape
+        B, T = pend.B, pend.T
         D = weight.shape[1]
         dev = weight.device
-        # batch sizes of every rank (ranks may hold different local batch sizes, unless the
-        # module was built with static_batch: then every rank's B equals this one's)
-        if mod.static_batch:
-            all_b = [B] * world
-        else:
-            bs = torch.tensor([B], device=dev)
-            all_b = [torch.zeros_like(bs) for _ in range(world)]
-            dist.all_gather(all_b, bs, group=group)
-            all_b = [int(x) for x in all_b]
-        # 1) ids to owners: for each destination r, my rows' ids of tables r owns ([B, n_r])
-        send = torch.cat([idx[:, mod.tables_of[r]].reshape(-1) for r in range(world)]) if T else idx.reshape(-1)
-        in_splits = [B * len(mod.tables_of[r]) for r in range(world)]
-        out_splits = [all_b[r] * len(mod.local_tables) for r in range(world)]
-        recv = torch.empty(sum(out_splits), dtype=idx.dtype, device=dev)
-        _a2a(recv, send, out_splits, in_splits, group)
+        if pend.work is not None:
+            pend.work.wait()
+        in_splits, out_splits = pend.in_splits, pend.out_splits
         # 2) owner-side gather for every source rank (HIP row gather on the GPU)
         nl = len(mod.local_tables)
         from raydp_amd.ops.dlrm_ops import gather_rows
-        lidx = recv.view(-1, nl) if nl else recv.view(0, 0)
+        lidx = pend.recv.view(-1, nl) if nl else pend.recv.view(0, 0)
         emb = gather_rows(weight, mod.local_offsets, lidx).view(-1, D) if nl else \
             torch.empty(0, D, device=dev, dtype=weight.dtype)
         # 3) embeddings back to the requesting ranks
@@ -87,14 +85,22 @@ class _ShardedLookup(torch.autograd.Function):
         mod, B, T, D, in_splits, out_splits, wshape = ctx.meta
         send = torch.cat([g[:, mod.tables_of[r]].reshape(-1, D) for r in range(mod.world)]) if T else g.reshape(-1, D)
         recv = torch.empty(sum(out_splits), D, dtype=g.dtype, device=g.device)
-        _a2a(recv, send, out_splits, in_splits, mod.group)
         nl = len(mod.local_tables)
-        if not nl:
-            return None, None, None
         if mod.fused_sgd_lr is not None:
-            # apply the rows straight into the owner's tables (no sparse tensor, no optimizer pass)
-            from raydp_amd.ops.dlrm_ops import sgd_rows_
-            sgd_rows_(weight, mod.local_offsets, lidx, recv.view(-1, nl, D), mod.fused_sgd_lr)
+            # the reverse exchange runs while autograd continues with the bottom MLP's backward;
+            # the rows are applied to the owner's tables at the end of the backward pass
+            work = dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=out_splits,
+                                          input_split_sizes=in_splits, group=mod.group, async_op=True)
+
+            def finish():
+                work.wait()
+                if nl:
+                    from raydp_amd.ops.dlrm_ops import sgd_rows_
+                    sgd_rows_(weight, mod.local_offsets, lidx, recv.view(-1, nl, D), mod.fused_sgd_lr)
+            torch.autograd.Variable._execution_engine.queue_callback(finish)
+            return None, None, None
+        _a2a(recv, send, out_splits, in_splits, mod.group)
+        if not nl:
             return None, None, None
         rows = (lidx + mod.local_offsets.view(1, -1)).reshape(-1)
         return torch.sparse_coo_tensor(rows.unsqueeze(0), recv, wshape), None, None
@@ -104,10 +110,15 @@ class ShardedEmbeddings(nn.Module):
     """Drop-in for :class:`raydp_amd.ops.dlrm_ops.FusedEmbeddings` across a process group."""
 
     def __init__(self, table_sizes: Sequence[int], dim: int, group=None, owners: Optional[List[int]] = None,
-                 seed: int = 0, fused_sgd_lr: Optional[float] = None, static_batch: bool = False):
+                 seed: int = 0, fused_sgd_lr: Optional[float] = None, static_batch="auto"):
         super().__init__()
         self.fused_sgd_lr = fused_sgd_lr   # apply SGD to the local tables inside backward
-        self.static_batch = static_batch   # every rank always uses the same local batch size
+        # how ranks learn each other's batch size: True -> always equal to the local one (no
+        # exchange); False -> all_gather every step (host sync); "auto" -> all_gather only when
+        # the local batch size changes (ranks change sizes at the same steps: the trainer's
+        # equal shards guarantee it), so a steady epoch exchanges nothing
+        self.static_batch = static_batch
+        self._last_b, self._all_b = None, None
         import math
         self.group = group
         self.world = dist.get_world_size(group)
@@ -139,6 +150,36 @@ class ShardedEmbeddings(nn.Module):
         o = int(self.local_offsets[i])
         return self.weight[o:o + self.table_sizes[t]]
 
-    def forward(self, mlp_out: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
-        emb = _ShardedLookup.apply(self.weight, idx.long(), self)
+    def _batch_sizes(self, B: int, dev) -> List[int]:
+        if self.static_batch is True or self.world == 1:
+            return [B] * self.world
+        if self.static_batch == "auto" and self._last_b == B and self._all_b is not None:
+            return self._all_b
+        bs = torch.tensor([B], device=dev)
+        all_b = [torch.zeros_like(bs) for _ in range(self.world)]
+        dist.all_gather(all_b, bs, group=self.group)
+        self._all_b = [int(x) for x in torch.cat(all_b).cpu()]
+        self._last_b = B
+        return self._all_b
+
+    def start(self, idx: torch.Tensor) -> _Pending:
+        """Issue the id all-to-all of step 1 asynchronously; ``finish`` completes the lookup."""
+        idx = idx.long()
+        B, T = idx.shape
+        p = _Pending()
+        p.B, p.T = B, T
+        p.all_b = self._batch_sizes(B, idx.device)
+        send = torch.cat([idx[:, self.tables_of[r]].reshape(-1) for r in range(self.world)]) if T else idx.reshape(-1)
+        p.in_splits = [B * len(self.tables_of[r]) for r in range(self.world)]
+        p.out_splits = [p.all_b[r] * len(self.local_tables) for r in range(self.world)]
+        p.recv = torch.empty(sum(p.out_splits), dtype=idx.dtype, device=idx.device)
+        p.work = dist.all_to_all_single(p.recv, send.contiguous(), output_split_sizes=p.out_splits,
+                                        input_split_sizes=p.in_splits, group=self.group, async_op=True)
+        return p
+
+    def finish(self, pend: _Pending, mlp_out: torch.Tensor) -> torch.Tensor:
+        emb = _ShardedLookup.apply(self.weight, pend, self)
         return torch.cat([mlp_out.unsqueeze(1).to(emb.dtype), emb], dim=1)
+
+    def forward(self, mlp_out: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+        return self.finish(self.start(idx), mlp_out)

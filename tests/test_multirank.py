@@ -254,3 +254,36 @@ def test_torch_estimator_spawned_world_4(runtime_local, tmp_path):
     trained = est.get_model()
     pred = trained(torch.from_numpy(x[:100])).detach().numpy()[:, 0]
     assert np.corrcoef(pred, df["y"].to_numpy()[:100])[0, 1] > 0.9
+
+
+def _auto_batch_rank(rank, world, port, q):
+    dist = _init(rank, world, port)
+    try:
+        from raydp_amd.parallel.embedding_mp import ShardedEmbeddings
+        calls = {"n": 0}
+        real = dist.all_gather
+
+        def counting(*a, **k):
+            calls["n"] += 1
+            return real(*a, **k)
+        dist.all_gather = counting
+        emb = ShardedEmbeddings(SIZES, D)            # static_batch="auto"
+        ok = True
+        for B in (6, 6, 6, 4, 4):                    # every rank changes size at the same step
+            g = torch.Generator().manual_seed(7 * B + rank)
+            idx = torch.stack([torch.randint(0, s, (B,), generator=g) for s in SIZES], 1)
+            X = emb(torch.zeros(B, D), idx)
+            ref = torch.cat([torch.zeros(B, 1, D)] + [_full_table(t)[idx[:, t]].unsqueeze(1)
+                                                      for t in range(len(SIZES))], 1)
+            ok &= bool(torch.allclose(X, ref, atol=1e-6))
+        dist.all_gather = real
+        q.put((rank, ok, calls["n"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_embeddings_exchange_batch_sizes_only_on_change():
+    res = _spawn(_auto_batch_rank, 2)
+    for r in res:
+        assert r[1], r
+        assert r[2] == 2, r       # first step and the step where the size changed
