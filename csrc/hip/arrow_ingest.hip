@@ -43,16 +43,21 @@ struct IngestCol {
 struct IngestArgs {
   int ncols;
   int out_stride;  // elements per output row (>= ncols, zero padded)
-  int out_bf16;    // 1: bf16 output, 0: f32 output
+  int out_bf16;    // output element: 0 f32, 1 bf16, 2 int64 (exact integer ids)
   int pad_;
   long long nrows;
   long long out_row0;  // first output row of this chunk
   IngestCol col[RX_INGEST_MAXCOLS];
 };
 
-template <class T>
-__device__ __forceinline__ float rx_cvt(T v) {
-  return (float)v;
+// Column values converted to the tile element type E: float (training features, bf16/f32
+// output) or long long (category ids: exact, no float rounding above 2^24).
+template <class E, class T>
+__device__ __forceinline__ E rx_cvt(T v) {
+  if constexpr (sizeof(E) == 8 && (sizeof(T) == 4 || sizeof(T) == 8) && (T)0.5 != (T)0)
+    return (E)(long long)v;  // float columns to int64: truncation, like a torch cast
+  else
+    return (E)v;
 }
 
 __device__ __forceinline__ bool rx_valid(const IngestCol& c, long long r) {
@@ -64,9 +69,8 @@ __device__ __forceinline__ bool rx_valid(const IngestCol& c, long long r) {
 // One wave loads rows [row0, row0 + nr) of a fixed-width column into tile[0..nr) with 16-B
 // vector loads: vector v covers elements [v*E, v*E + E) of the 16-B aligned base, element e is
 // row e - lead.
-template <class T>
-__device__ __forceinline__ void rx_load_col(const IngestCol& c, long long row0, int nr, float* tile,
-                                            int lane) {
+template <class TE, class T>
+__device__ __forceinline__ void rx_load_col(const IngestCol& c, long long row0, int nr, TE* tile, int lane) {
   constexpr int E = 16 / (int)sizeof(T);
   const uintptr_t p = reinterpret_cast<uintptr_t>(c.values);
   const uintptr_t base = p & ~(uintptr_t)15;
@@ -74,6 +78,7 @@ __device__ __forceinline__ void rx_load_col(const IngestCol& c, long long row0, 
   const long long e0 = lead + row0;
   const long long v0 = e0 / E, v1 = (e0 + nr - 1) / E;
   const u32x4* vp = reinterpret_cast<const u32x4*>(base);
+  const TE fill = (TE)c.fill;
   for (long long v = v0 + lane; v <= v1; v += RX_WAVE) {
     const u32x4 raw = __builtin_nontemporal_load(vp + v);
     T el[E];
@@ -81,18 +86,44 @@ __device__ __forceinline__ void rx_load_col(const IngestCol& c, long long row0, 
 #pragma unroll
     for (int q = 0; q < E; ++q) {
       const long long r = v * E + q - e0;
-      if (r >= 0 && r < nr) tile[r] = rx_valid(c, row0 + r) ? rx_cvt<T>(el[q]) : c.fill;
+      if (r >= 0 && r < nr) tile[r] = rx_valid(c, row0 + r) ? rx_cvt<TE, T>(el[q]) : fill;
     }
   }
 }
 
-__device__ __forceinline__ void rx_load_bool(const IngestCol& c, long long row0, int nr, float* tile,
-                                             int lane) {
+template <class TE>
+__device__ __forceinline__ void rx_load_bool(const IngestCol& c, long long row0, int nr, TE* tile, int lane) {
   const uint8_t* b = reinterpret_cast<const uint8_t*>(c.values);
   for (int r = lane; r < nr; r += RX_WAVE) {
     const long long bit = c.vbit + row0 + r;
-    const float x = (float)((b[bit >> 3] >> (bit & 7)) & 1);
-    tile[r] = c.valid != nullptr && !rx_valid(c, row0 + r) ? c.fill : x;
+    const TE x = (TE)((b[bit >> 3] >> (bit & 7)) & 1);
+    tile[r] = c.valid != nullptr && !rx_valid(c, row0 + r) ? (TE)c.fill : x;
+  }
+}
+
+template <class TE>
+__device__ __forceinline__ void rx_ingest_phase1(const IngestArgs& a, TE* tile, long long row0, int nr) {
+  const int TS = RX_TILE_ROWS + 1;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int nw = blockDim.x >> 6;
+  // column-major; one wave per column, the type switch is wave-uniform
+  for (int c = wave; c < a.ncols; c += nw) {
+    const IngestCol& col = a.col[c];
+    TE* t = tile + c * TS;
+    switch (col.type) {
+      case 0: rx_load_col<TE, double>(col, row0, nr, t, lane); break;
+      case 1: rx_load_col<TE, float>(col, row0, nr, t, lane); break;
+      case 2: rx_load_col<TE, long long>(col, row0, nr, t, lane); break;
+      case 3: rx_load_col<TE, int>(col, row0, nr, t, lane); break;
+      case 4: rx_load_col<TE, short>(col, row0, nr, t, lane); break;
+      case 5: rx_load_col<TE, signed char>(col, row0, nr, t, lane); break;
+      case 6: rx_load_col<TE, unsigned char>(col, row0, nr, t, lane); break;
+      case 7: rx_load_bool<TE>(col, row0, nr, t, lane); break;
+      case 8: rx_load_col<TE, unsigned short>(col, row0, nr, t, lane); break;
+      case 9: rx_load_col<TE, unsigned int>(col, row0, nr, t, lane); break;
+      default:
+        for (int r = lane; r < nr; r += RX_WAVE) t[r] = (TE)0;
+    }
   }
 }
 
@@ -101,27 +132,7 @@ __global__ __launch_bounds__(256) void arrow_ingest_kernel(IngestArgs a, void* _
   const int TS = RX_TILE_ROWS + 1;
   const long long row0 = (long long)blockIdx.x * RX_TILE_ROWS;
   const int nr = (int)min((long long)RX_TILE_ROWS, a.nrows - row0);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int nw = blockDim.x >> 6;
-  // phase 1: column-major; one wave per column, the type switch is wave-uniform
-  for (int c = wave; c < a.ncols; c += nw) {
-    const IngestCol& col = a.col[c];
-    float* t = tile + c * TS;
-    switch (col.type) {
-      case 0: rx_load_col<double>(col, row0, nr, t, lane); break;
-      case 1: rx_load_col<float>(col, row0, nr, t, lane); break;
-      case 2: rx_load_col<long long>(col, row0, nr, t, lane); break;
-      case 3: rx_load_col<int>(col, row0, nr, t, lane); break;
-      case 4: rx_load_col<short>(col, row0, nr, t, lane); break;
-      case 5: rx_load_col<signed char>(col, row0, nr, t, lane); break;
-      case 6: rx_load_col<unsigned char>(col, row0, nr, t, lane); break;
-      case 7: rx_load_bool(col, row0, nr, t, lane); break;
-      case 8: rx_load_col<unsigned short>(col, row0, nr, t, lane); break;
-      case 9: rx_load_col<unsigned int>(col, row0, nr, t, lane); break;
-      default:
-        for (int r = lane; r < nr; r += RX_WAVE) t[r] = 0.f;
-    }
-  }
+  rx_ingest_phase1<float>(a, tile, row0, nr);
   __syncthreads();
   // phase 2: row-major, 16-B stores along the output row (zero padded to out_stride)
   const long long obase = (a.out_row0 + row0) * a.out_stride;
@@ -161,6 +172,23 @@ __global__ __launch_bounds__(256) void arrow_ingest_kernel(IngestArgs a, void* _
       const int r = idx / S, c = idx - r * S;
       o[idx] = c < nc ? tile[c * TS + r] : 0.f;
     }
+  }
+}
+
+// Exact integer columns (category ids, counts) -> int64 row-major [N, stride]: same staging,
+// an int64 LDS tile, 16-B row stores of two ids.
+__global__ __launch_bounds__(256) void arrow_ingest_i64_kernel(IngestArgs a, long long* __restrict__ out) {
+  extern __shared__ long long itile[];  // [ncols][RX_TILE_ROWS + 1]
+  const int TS = RX_TILE_ROWS + 1;
+  const long long row0 = (long long)blockIdx.x * RX_TILE_ROWS;
+  const int nr = (int)min((long long)RX_TILE_ROWS, a.nrows - row0);
+  rx_ingest_phase1<long long>(a, itile, row0, nr);
+  __syncthreads();
+  const int S = a.out_stride, nc = a.ncols;
+  long long* o = out + (a.out_row0 + row0) * S;
+  for (int idx = threadIdx.x; idx < nr * S; idx += blockDim.x) {
+    const int r = idx / S, c = idx - r * S;
+    o[idx] = c < nc ? itile[c * TS + r] : 0LL;
   }
 }
 
@@ -306,13 +334,29 @@ int rx_dma_sizes(int* out) {
   return 0;
 }
 
+static int rx_ingest_launch(const IngestArgs& a, void* out, hipStream_t stream) {
+  const long long blocks = (a.nrows + RX_TILE_ROWS - 1) / RX_TILE_ROWS;
+  if (a.out_bf16 == 2) {
+    static bool attr = false;
+    if (!attr) {  // up to 64 int64 columns x 257 rows = 131.6 KB of LDS
+      RX_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&arrow_ingest_i64_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    const size_t lds = (size_t)a.ncols * (RX_TILE_ROWS + 1) * sizeof(long long);
+    hipLaunchKernelGGL(arrow_ingest_i64_kernel, dim3((unsigned)blocks), dim3(256), lds, stream, a,
+                       reinterpret_cast<long long*>(out));
+  } else {
+    const size_t lds = (size_t)a.ncols * (RX_TILE_ROWS + 1) * sizeof(float);
+    hipLaunchKernelGGL(arrow_ingest_kernel, dim3((unsigned)blocks), dim3(256), lds, stream, a, out);
+  }
+  return (int)hipGetLastError();
+}
+
 int rx_arrow_ingest(const IngestArgs* a, void* out, hipStream_t stream) {
   if (a->ncols > RX_INGEST_MAXCOLS || a->ncols > a->out_stride || a->ncols <= 0) return -1;
   if (a->nrows <= 0) return 0;
-  const long long blocks = (a->nrows + RX_TILE_ROWS - 1) / RX_TILE_ROWS;
-  const size_t lds = (size_t)a->ncols * (RX_TILE_ROWS + 1) * sizeof(float);
-  hipLaunchKernelGGL(arrow_ingest_kernel, dim3((unsigned)blocks), dim3(256), lds, stream, *a, out);
-  return (int)hipGetLastError();
+  return rx_ingest_launch(*a, out, stream);
 }
 
 // Pin [addr, addr + len) of the arena [base, base + cap) (chunk-granular, idempotent).
@@ -460,10 +504,8 @@ int rx_ingest_dma(const RxDmaChunk* chunks, int nchunks, const RxDmaRegion* regi
       ic.pad2_ = 0;
     }
     if (ch.nrows > 0) {
-      const long long blocks = (ch.nrows + RX_TILE_ROWS - 1) / RX_TILE_ROWS;
-      const size_t lds = (size_t)ncols * (RX_TILE_ROWS + 1) * sizeof(float);
-      hipLaunchKernelGGL(arrow_ingest_kernel, dim3((unsigned)blocks), dim3(256), lds, compute, a, out);
-      RX_CHECK(hipGetLastError());
+      const int lrc = rx_ingest_launch(a, out, compute);
+      if (lrc) return lrc;
     }
     RX_CHECK(hipEventRecord(done, compute));
     busy.push_back(Busy{s, e, ev_done});

@@ -148,6 +148,20 @@ def _numpy_matrix(tables, cols, dtype, fill=0.0, stride=None):
     return torch.from_numpy(out).to(dtype)
 
 
+def _numpy_int_matrix(tables, cols, fill, stride):
+    n = sum(t.num_rows for t in tables)
+    out = np.zeros((n, stride), dtype=np.int64)
+    r = 0
+    for t in tables:
+        for j, c in enumerate(cols):
+            a = _prep_array(t.column(c))
+            v = a.fill_null(fill) if a.null_count else a
+            out[r:r + t.num_rows, j] = v.to_numpy(zero_copy_only=False).astype(np.int64)
+        r += t.num_rows
+    _stats["host_copy_bytes"] += int(out.nbytes)
+    return torch.from_numpy(out)
+
+
 def _copy_stream(device) -> "torch.cuda.Stream":
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _copy_streams.get(idx)
@@ -210,14 +224,17 @@ def _reap_inflight():
 
 def ingest_columns(tables: Sequence[pa.Table], cols: List[str], device, out_bf16: bool,
                    stride: Optional[int] = None, fill: float = 0.0,
-                   stage_bytes: Optional[int] = None) -> torch.Tensor:
-    """Build a row-major ``[N, stride]`` (bf16 or f32) device matrix from ``cols``. Returns
-    without a host synchronisation: the matrix is ready in stream order on the current stream."""
+                   stage_bytes: Optional[int] = None, out_i64: bool = False) -> torch.Tensor:
+    """Build a row-major ``[N, stride]`` device matrix from ``cols``: bf16 (``out_bf16``), exact
+    int64 (``out_i64``: category ids) or f32. Returns without a host synchronisation: the matrix
+    is ready in stream order on the current stream."""
     device = torch.device(device)
     stride = stride or len(cols)
     n = int(sum(t.num_rows for t in tables))
-    dtype = torch.bfloat16 if out_bf16 else torch.float32
+    dtype = torch.int64 if out_i64 else (torch.bfloat16 if out_bf16 else torch.float32)
     if device.type != "cuda":
+        if out_i64:
+            return _numpy_int_matrix(tables, cols, int(fill), stride).to(device)
         return _numpy_matrix(tables, cols, dtype, fill, stride).to(device)
     from raydp_amd.ops import _hip
     lib = _hip.lib()
@@ -289,7 +306,7 @@ def ingest_columns(tables: Sequence[pa.Table], cols: List[str], device, out_bf16
         cs = _copy_stream(device)
         compute = torch.cuda.current_stream(device)
         st = (ctypes.c_longlong * 4)()
-        rc = lib.rx_ingest_dma(chunks, len(chunk_l), regs, dcols, len(cols), stride, int(out_bf16),
+        rc = lib.rx_ingest_dma(chunks, len(chunk_l), regs, dcols, len(cols), stride, 2 if out_i64 else int(out_bf16),
                                ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stage.data_ptr()), ring,
                                ctypes.c_void_p(compute.cuda_stream), ctypes.c_void_p(cs.cuda_stream), st)
         _hip.check(rc, "rx_ingest_dma")

@@ -55,7 +55,15 @@ def _to_tensor_spec(feature_columns, feature_types):
     return [list(feature_columns)], [dt or torch.float32], False
 
 
+_INT_DTYPES = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8)
+
+
 class _ShardTensors:
+    """A worker's shard, resident in HBM. Multi-input models (one tensor per column, as DLRM's
+    13 dense + 26 categorical inputs) are ingested as ONE float matrix and ONE exact int64
+    matrix (one DMA-fed ingest launch each), and a batch is one row gather per matrix whose
+    column views are the model inputs."""
+
     def __init__(self, ds, feature_columns, feature_types, label_column, label_type, device,
                  fused_stride: Optional[int] = None):
         tables = ds._get_tables() if ds is not None else []
@@ -63,14 +71,50 @@ class _ShardTensors:
         from raydp_amd.ops.ingest import ingest_columns
         self.groups, self.dtypes, self.multi = _to_tensor_spec(feature_columns, feature_types)
         self.device = device
+        self.feats = None
         if fused_stride is not None:
             self.feats_bf16 = ingest_columns(tables, self.groups[0], device, True, fused_stride)
-            self.feats = None
+        elif self.multi and all(len(g) == 1 for g in self.groups):
+            # one matrix per kind; group i -> (kind, column j)
+            kinds = ["i" if d in _INT_DTYPES else "f" for d in self.dtypes]
+            self.mats, self.where = {}, []
+            for kind in ("f", "i"):
+                cols = [g[0] for g, k in zip(self.groups, kinds) if k == kind]
+                if cols:
+                    self.mats[kind] = ingest_columns(tables, cols, device, False, out_i64=(kind == "i"))
+            pos = {"f": 0, "i": 0}
+            for k, d in zip(kinds, self.dtypes):
+                self.where.append((k, pos[k], d))
+                pos[k] += 1
+            self.feats = self._views(self.mats)
         else:
-            self.feats = [ingest_columns(tables, g, device, False).to(d) for g, d in
-                          zip(self.groups, self.dtypes)]
-        lab = ingest_columns(tables, [label_column], device, False)
-        self.labels = lab.to(label_type or torch.float32)
+            self.feats = [ingest_columns(tables, g, device, False, out_i64=d in _INT_DTYPES).to(d)
+                          for g, d in zip(self.groups, self.dtypes)]
+        lab = ingest_columns(tables, [label_column], device, False,
+                             out_i64=(label_type in _INT_DTYPES)) if label_column is not None else None
+        self.labels = lab.to(label_type or torch.float32) if lab is not None else None
+
+    def _views(self, mats):
+        out = []
+        for k, j, d in self.where:
+            v = mats[k][:, j:j + 1]
+            out.append(v if v.dtype == d else v.to(d))
+        return out
+
+    def batch(self, sel):
+        """Inputs and labels of rows ``sel`` (device index tensor) or of a slice."""
+        if getattr(self, "mats", None) is not None:
+            if isinstance(sel, slice):
+                mats = {k: m[sel] for k, m in self.mats.items()}
+            else:
+                mats = {k: m.index_select(0, sel) for k, m in self.mats.items()}
+            feats = self._views(mats)
+        elif isinstance(sel, slice):
+            feats = [f[sel] for f in self.feats]
+        else:
+            feats = [f.index_select(0, sel) for f in self.feats]
+        lab = self.labels[sel] if isinstance(sel, slice) else self.labels.index_select(0, sel)
+        return feats, lab
 
 
 class FusedMLPEngine:
@@ -248,13 +292,7 @@ class TorchLoopEngine:
             self.epoch += 1
         stop = n - n % self.batch if self.drop_last else n
         for s in range(0, stop, self.batch):
-            if idx is not None:
-                sel = idx[s:s + self.batch]
-                feats = [f.index_select(0, sel) for f in data.feats]
-                lab = data.labels.index_select(0, sel)
-            else:
-                feats = [f[s:s + self.batch] for f in data.feats]
-                lab = data.labels[s:s + self.batch]
+            feats, lab = data.batch(idx[s:s + self.batch] if idx is not None else slice(s, s + self.batch))
             yield (feats if data.multi else feats[0]), lab
 
     def _reset_metrics(self):

@@ -122,7 +122,7 @@ class GraphedTrainLoop:
 
     def _gather(self, sel):
         d = self.e.train
-        return [f.index_select(0, sel) for f in d.feats], d.labels.index_select(0, sel)
+        return d.batch(sel)
 
     def _eager(self, sel):
         self._forward_step(*self._gather(sel))

@@ -113,3 +113,53 @@ def test_feistel_permutation():
     first = np.concatenate([random_permutation(1000, s, "cuda").cpu().numpy()[:64] for s in range(200)])
     counts = np.bincount(first // 100, minlength=10)
     assert counts.min() > 0.7 * counts.mean(), counts
+
+
+def test_int64_ingest_is_exact_above_2_pow_24(store):
+    """Category ids go to HBM as exact int64 (a float tile would round ids above 2^24)."""
+    from raydp_amd.ops import ingest
+    n = 10_000
+    rng = np.random.default_rng(3)
+    big = rng.integers(2 ** 24, 2 ** 40, n)
+    t = pa.table({"a": pa.array(big, pa.int64()),
+                  "b": pa.array([None if i % 5 == 0 else int(v) for i, v in enumerate(rng.integers(0, 2 ** 31 - 1, n))],
+                                pa.int32()),
+                  "c": pa.array(rng.integers(0, 200, n).astype(np.uint8))})
+    oid = uuid.uuid4().hex
+    store.put(oid, t)
+    _, v = store.get(oid)
+    got = ingest.ingest_columns([v.slice(7, 9000), v.slice(0, 7)], ["a", "b", "c"], "cuda", False,
+                                out_i64=True, fill=-1).cpu().numpy()
+    exp = np.zeros((9007, 3), np.int64)
+    for r0, tab in ((0, v.slice(7, 9000)), (9000, v.slice(0, 7))):
+        for j, c in enumerate("abc"):
+            exp[r0:r0 + tab.num_rows, j] = tab.column(c).to_pandas().fillna(-1).to_numpy().astype(np.int64)
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_multi_input_shard_batches():
+    """DLRM-shaped shard: 13 float + 26 int columns become one float and one int64 matrix; a
+    batch is one gather per matrix, the inputs are its column views."""
+    import torch
+    from raydp_amd.data import from_arrow
+    from raydp_amd.torch.engine import _ShardTensors
+    rng = np.random.default_rng(0)
+    n = 3000
+    cols = {f"_c{i}": rng.standard_normal(n) for i in range(1, 14)}
+    cols.update({f"_c{i}": rng.integers(0, 10 ** 9, n) for i in range(14, 40)})
+    cols["_c0"] = rng.integers(0, 2, n).astype(np.float64)
+    ds = from_arrow(pa.table(cols))
+    sh = _ShardTensors(ds, [f"_c{i}" for i in range(1, 40)], [torch.float32] * 13 + [torch.long] * 26, "_c0",
+                       torch.float32, torch.device("cuda"))
+    assert set(sh.mats) == {"f", "i"} and sh.mats["i"].dtype == torch.int64
+    sel = torch.tensor([5, 0, 2999, 17], device="cuda")
+    feats, lab = sh.batch(sel)
+    assert len(feats) == 39 and feats[13].dtype == torch.int64 and feats[0].dtype == torch.float32
+    for j, i in enumerate(range(1, 40)):
+        want = torch.as_tensor(cols[f"_c{i}"][[5, 0, 2999, 17]])
+        got = feats[j].reshape(-1).cpu()
+        if i < 14:
+            torch.testing.assert_close(got, want.float())
+        else:
+            assert torch.equal(got, want.long())
+    torch.testing.assert_close(lab.reshape(-1).cpu(), torch.as_tensor(cols["_c0"][[5, 0, 2999, 17]]).float())

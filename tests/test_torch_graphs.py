@@ -11,7 +11,10 @@ from raydp_amd.torch.metrics import TorchMetric
 from raydp_amd.train import session
 
 
-class _Shard:
+from raydp_amd.torch.engine import _ShardTensors
+
+
+class _Shard(_ShardTensors):
     def __init__(self, feats, labels, multi):
         self.feats, self.labels, self.n, self.multi = feats, labels, labels.shape[0], multi
 
