@@ -49,7 +49,12 @@ class TorchBatchIterable:
             dts = fd if isinstance(fd, (list, tuple)) else [fd] * len(fc)
             return [self._cols(t, list(names), dt) for names, dt in zip(fc, dts)]
         if isinstance(fd, (list, tuple)):
-            return [self._cols(t, [c], dt) for c, dt in zip(fc, fd)]
+            # Ray Data semantics: a flat list of names is ONE [B, F] tensor; per-column dtypes are
+            # applied first and the columns concatenated with type promotion
+            if len({d for d in fd}) <= 1:
+                return self._cols(t, list(fc), fd[0] if fd else None)
+            import torch
+            return torch.cat([self._cols(t, [c], dt) for c, dt in zip(fc, fd)], dim=1)
         return self._cols(t, list(fc), fd)
 
     def __iter__(self):

@@ -24,3 +24,13 @@ def test_example_runs(script, args, expect):
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     assert r.returncode == 0, r.stdout[-3000:]
     assert expect in r.stdout, r.stdout[-3000:]
+
+
+def test_raytrain_tutorial_runs():
+    """tutorials/raytrain_example.ipynb port (B4 workload): legacy Trainer + to_torch shards."""
+    tut = os.path.join(os.path.dirname(EX), "tutorials", "raytrain_example.py")
+    env = dict(os.environ, RAYTRAIN_EPOCHS="2")
+    r = subprocess.run([sys.executable, tut], cwd=os.path.dirname(tut), env=env, timeout=400,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "test_acc" in r.stdout and "'epoch': 1" in r.stdout, r.stdout[-3000:]
