@@ -92,7 +92,68 @@ def test_gbdt_distributed_histograms_match_single_process():
     got = q.get(timeout=120)
     for p in ps:
         p.join(60)
-    np.testing.assert_allclose(got, single, rtol=1e-4, atol=1e-4)
+    # fixed-point histograms: the all-reduced integer sums equal the single-process sums, so the
+    # trees (and predictions) are identical, not merely close
+    np.testing.assert_array_equal(got, single)
+
+
+def test_gbdt_zero_hessian_children_do_not_make_nan():
+    """lambda = 0 and min_child_weight = 0 with subsampling: children with zero hessian are
+    invalid candidates (no 0/0 gains) and zero-hessian nodes get weight 0."""
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((3000, 4)).astype(np.float32)
+    y = (x[:, 0] > 0).astype(np.float32)
+    bst = train({"objective": "binary:logistic", "lambda": 0.0, "min_child_weight": 0.0, "subsample": 0.3,
+                 "max_depth": 6}, DMatrix(x, y), 5)
+    for (t,) in bst.trees:
+        assert np.isfinite(t.value).all() and np.isfinite(t.gain).all()
+    assert np.isfinite(bst.predict(DMatrix(x))).all()
+
+
+def test_gbdt_max_bin_validated():
+    with pytest.raises(ValueError):
+        train({"max_bin": 40000}, DMatrix(np.zeros((10, 1)), np.zeros(10)), 1)
+
+
+def test_split_candidates_tensor_formulation_matches_bruteforce():
+    """torch_split_candidates (CPU path, and the GPU kernel's reference) against a per-threshold
+    Python loop: same gains, lowest threshold on ties, -1 where nothing is valid."""
+    import torch
+    from raydp_amd.ops.gbdt_ops import torch_split_candidates
+    g = torch.Generator().manual_seed(0)
+    K, F, B = 2, 3, 12
+    hist = torch.zeros(K, F, B, 2, dtype=torch.int64)
+    hist[..., 0] = torch.randint(-50, 50, (K, F, B), generator=g)
+    hist[..., 1] = torch.randint(0, 20, (K, F, B), generator=g)
+    hist[0, 1, 3:7] = 0                                   # empty bins -> tied gains
+    tot = hist[:, 0].sum(1)
+    for f in range(1, F):
+        hist[:, f, B - 1] += tot - hist[:, f].sum(1)
+    ncuts = torch.tensor([B - 2, 5, 0])
+    lam, alpha, mcw, ig, ih = 1.0, 0.0, 2.0, 0.5, 0.25
+    out = torch_split_candidates(hist, tot, ncuts, None, ig, ih, lam, alpha, mcw)
+    for k in range(K):
+        G, H = float(tot[k, 0]) * ig, float(tot[k, 1]) * ih
+        parent = G * G / (H + lam)
+        for f in range(F):
+            for c, dl in ((0, 1), (2, 0)):
+                best, bt = -1.0, 0
+                cg = ch = 0
+                for t in range(B - 1):
+                    cg += int(hist[k, f, t + 1, 0])
+                    ch += int(hist[k, f, t + 1, 1])
+                    if t >= int(ncuts[f]):
+                        continue
+                    lg = cg + (int(hist[k, f, 0, 0]) if dl else 0)
+                    lh = ch + (int(hist[k, f, 0, 1]) if dl else 0)
+                    Lg, Lh = lg * ig, lh * ih
+                    Rg, Rh = (int(tot[k, 0]) - lg) * ig, (int(tot[k, 1]) - lh) * ih
+                    if not (Lh >= mcw and Rh >= mcw and Lh + lam > 0 and Rh + lam > 0):
+                        continue
+                    gain = Lg * Lg / (Lh + lam) + Rg * Rg / (Rh + lam) - parent
+                    if gain > best:
+                        best, bt = gain, t
+                assert float(out[k, f, c]) == best and int(out[k, f, c + 1]) == bt, (k, f, dl)
 
 
 def test_tf_estimator_reports_missing_tensorflow():
