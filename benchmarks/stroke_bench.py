@@ -40,14 +40,17 @@ def main():
     n_train = tr.count()
     n_test = te.count()
     out = {"metric": "stroke tutorial fit_on_spark (30 train + 30 eval epochs)", "fit_wall_s": round(wall, 3),
-           "train_epoch_s_median": round(statistics.median(train_t), 4),
-           "eval_epoch_s_median": round(statistics.median(eval_t), 4),
+           "train_epoch_s_median": round(statistics.median(train_t), 6),
+           "eval_epoch_s_median": round(statistics.median(eval_t), 6),
            "train_rows": n_train, "test_rows": n_test,
            "train_samples_per_s": round(n_train / statistics.median(train_t), 1),
            "fit_samples_per_s": round(n_train * epochs / wall, 1),
            "engine": hist[0].get("engine"), "reference": REF,
            "speedup_fit": round(REF["fit_wall_s"] / wall, 2),
-           "final": {k: v for k, v in hist[-1].items() if not k.startswith("_")}}
+           "final_train": {k: v for k, v in [h for h in hist if "train_loss" in h][-1].items()
+                           if not k.startswith("_")},
+           "final_eval": {k: v for k, v in ([h for h in hist if "test_loss" in h] or [{}])[-1].items()
+                          if not k.startswith("_")}}
     print(json.dumps(out))
     raydp.stop_spark()
     ray.shutdown()

@@ -84,6 +84,16 @@ struct MlpLayer {
   int gg_off;        //               bf16 offset of G^T_l [out_n][BP]
 };
 
+// Embedding front (MlpDesc::front_n > 0): column k of the first Linear's input is either a copy
+// of raw input column `src` (poff < 0) or element j of the embedding row selected by raw column
+// `src` (poff = flat offset of the table's element [0][j], stride = embedding_dim, rows =
+// num_embeddings). This is the stroke tutorial's NET_Model shape (per-column nn.Embedding
+// lookups concatenated with dense columns in front of an MLP).
+struct FrontCol {
+  int src, poff, stride, rows;
+};
+#define RX_MAXF 64
+
 struct MlpDesc {
   int L;
   int r_lds_off, gt_lds_off, stats_lds_off, lds_bytes;
@@ -98,6 +108,12 @@ struct MlpDesc {
   int act_off;       // float offset (in the gradient buffer) of the exported activation area
   int wgrad_mode;    // 0: weight gradients computed and stored here; 1: X^T / G^T exported and
                      //    the optimizer kernel computes dW = X^T G on its own workgroups
+  int front_n;       // embedding front: columns it produces (0 = none; feats is layer 0's input)
+  int front_q;       // (column, table row) pairs of the front's embedding columns
+  int acc_mode;      // 1: binary accuracy, (pred > acc_thr) == (long)label counted in metrics[5]
+  float acc_thr;
+  FrontCol front[RX_MAXF];
+  int front_qbase[RX_MAXF];  // prefix of `rows` over the front's embedding columns
 };
 
 // run-time descriptor: loops over layers are ordinary loops
@@ -382,7 +398,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
           if (!colok || mt * 16 + lg * 4 + r >= nvalid) acc[j * MT + mt][r] = 0.f;
       if (last) {
         // loss, metrics and dL/dy (mean reduction over nvalid * out_dim elements)
-        float lsum = 0.f, asum = 0.f, ssum = 0.f, gsum = 0.f;
+        float lsum = 0.f, asum = 0.f, ssum = 0.f, gsum = 0.f, csum = 0.f;
         const float inv_n = 1.f / (float)(nvalid * ly.out);
         const int lcode = d.loss;
         const float beta = d.beta;
@@ -408,6 +424,8 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
               const float ae = fabsf(e);
               asum += ae;
               ssum = fmaf(e, e, ssum);
+              if (d.acc_mode == 1)  // torch: (pred > thr).long() == target.long()
+                csum += ((acc[j * MT + mt][r] > d.acc_thr ? 1 : 0) == (int)t) ? 1.f : 0.f;
               const float sgn = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
               const bool quad = ae < beta;
               lsum += quad ? 0.5f * e * e / beta : ae - 0.5f * beta;  // smooth-L1 term
@@ -420,12 +438,14 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         lsum = rx_wavesum(lsum);
         asum = rx_wavesum(asum);
         ssum = rx_wavesum(ssum);
+        if (d.acc_mode == 1) csum = rx_wavesum(csum);
         if (lcode == 0) lsum = ssum;
         else if (lcode == 2) lsum = asum;
         if (lane == 0) {
           atomicAdd(&metrics[0], (double)(lsum * inv_n));
           atomicAdd(&metrics[1], (double)asum);
           atomicAdd(&metrics[2], (double)ssum);
+          if (d.acc_mode == 1) atomicAdd(&metrics[5], (double)csum);
           if (n == 0) {
             atomicAdd(&metrics[3], (double)(nvalid * ly.out));
             atomicAdd(&metrics[4], 1.0);
@@ -801,10 +821,108 @@ __device__ __forceinline__ void prefetch_labels(const D& d, const float* __restr
   for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
 }
 
+// Embedding front: build layer 0's input [BP][in_k] from the raw feature rows -- dense columns
+// copied, embedding columns gathered from the fp32 master tables in P (rounded to bf16 like
+// every other activation). Ids come from bf16 features (exact for ids < 256, the host's limit);
+// an id outside [0, rows) is clamped and counted in metrics[6] (the host raises on it).
+template <int MT, bool PS, class D, class L0>
+__device__ __forceinline__ void load_front(const D& d, const MlpDesc* __restrict__ dp, const L0& l0, char* smem,
+                                           const u16* __restrict__ feats, const float* __restrict__ P,
+                                           const int* __restrict__ rowidx, int nvalid, bool need_t,
+                                           double* __restrict__ metrics) {
+  using T = Tile<MT>;
+  const int RS = d.max_k + 8;
+  u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
+  u16* XT = reinterpret_cast<u16*>(smem + l0.xt_off);
+  const int in_k = l0.in_k, fn = d.front_n;
+  int bad = 0;
+  for (int idx = rx_tid<PS>(); idx < T::BP * in_k; idx += RX_THREADS) {
+    const int row = idx / in_k, k = idx - row * in_k;
+    u16 v = 0;
+    if (row < nvalid && k < fn) {
+      const FrontCol fc = dp->front[k];
+      const u16 raw = rx_g(feats)[(size_t)rowidx[row] * d.feat_k + fc.src];
+      if (fc.poff < 0) {
+        v = raw;
+      } else {
+        int id = (int)rx_bf2f(raw);
+        if (id < 0 || id >= fc.rows) {
+          bad = 1;
+          id = id < 0 ? 0 : fc.rows - 1;
+        }
+        v = rx_f2bf(rx_g(P)[fc.poff + id * fc.stride]);
+      }
+    }
+    R[row * RS + k] = v;
+    if (need_t && k < l0.in_n) XT[k * T::XS + row] = v;
+  }
+  if (bad && metrics != nullptr) atomicAdd(&metrics[6], 1.0);
+  __syncthreads();
+}
+
+// Embedding front, backward: dX_0 = G_0 W_0 for the front's columns (one 16-column dgrad tile
+// per wave), then every (column, table row) pair sums its rows' dX in row order and STORES the
+// table element's gradient -- deterministic, and every element of every table is written each
+// step (no zeroing, no atomics). G_0 is still in R (layer 0's backward only exported it); the
+// G^T area is free and holds dX [BP][in_n] fp32 and the ids [BP][front_n] int16.
+template <int MT, class D, class L0>
+__device__ __forceinline__ void front_backward(const D& d, const MlpDesc* __restrict__ dp, const L0& l0, char* smem,
+                                               const u16* __restrict__ img, float* __restrict__ Gr,
+                                               const u16* __restrict__ feats, const int* __restrict__ rowidx,
+                                               int nvalid) {
+  using T = Tile<MT>;
+  const int lane = rx_tid<false>() & 63, wave = rx_wave<false>();
+  const int lr = lane & 15, lg = lane >> 4;
+  const int RS = d.max_k + 8;
+  const u16* R = reinterpret_cast<const u16*>(smem + d.r_lds_off);
+  float* dx = reinterpret_cast<float*>(smem + d.gt_lds_off);
+  short* ids = reinterpret_cast<short*>(dx + T::BP * l0.in_n);
+  const int fn = d.front_n;
+  __syncthreads();  // layer 0's G^T export has read the G^T area
+  for (int n = wave; n < (l0.in_n >> 4); n += RX_NW) {
+    f32x4 part[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_tile<MT, false>(part, R + lr * RS, RS, img, l0.wt_img + (n * 16 + lr) * l0.out_k, l0.out_k, lg);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dx[(mt * 16 + lg * 4 + r) * l0.in_n + n * 16 + lr] = part[mt][r];
+  }
+  for (int idx = rx_tid<false>(); idx < T::BP * fn; idx += RX_THREADS) {
+    const int row = idx / fn, k = idx - row * fn;
+    const FrontCol fc = dp->front[k];
+    int id = -1;
+    if (row < nvalid && fc.poff >= 0) {
+      id = (int)rx_bf2f(rx_g(feats)[(size_t)rowidx[row] * d.feat_k + fc.src]);
+      id = id < 0 ? 0 : (id >= fc.rows ? fc.rows - 1 : id);
+    }
+    ids[row * fn + k] = (short)id;
+  }
+  __syncthreads();
+  for (int q = rx_tid<false>(); q < d.front_q; q += RX_THREADS) {
+    int k = 0;
+    while (k + 1 < fn && dp->front_qbase[k + 1] <= q) ++k;
+    while (k + 1 < fn && dp->front[k].poff < 0) ++k;  // a dense column shares the next one's qbase
+    const FrontCol fc = dp->front[k];
+    const int v = q - dp->front_qbase[k];
+    float s = 0.f;
+    for (int row = 0; row < nvalid; ++row) s += ids[row * fn + k] == v ? dx[row * l0.in_n + k] : 0.f;
+    Gr[fc.poff + v * fc.stride] = s;
+  }
+}
+
 // load the batch's feature rows (gathered through the epoch permutation) into R and XT_0
 template <int MT, bool PS = false, class D, class L0>
 __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem, const u16* __restrict__ feats,
-                                            const int* __restrict__ rowidx, int nvalid, bool need_t) {
+                                            const int* __restrict__ rowidx, int nvalid, bool need_t,
+                                            const MlpDesc* __restrict__ dp = nullptr,
+                                            const float* __restrict__ P = nullptr,
+                                            double* __restrict__ metrics = nullptr) {
+  if (d.front_n > 0) {
+    load_front<MT, PS>(d, dp, l0, smem, feats, P, rowidx, nvalid, need_t, metrics);
+    return;
+  }
   using T = Tile<MT>;
   const int RS = d.max_k + 8;
   u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
@@ -852,7 +970,7 @@ __device__ __forceinline__ void mlp_train_step_body(
     rowidx[i] = i < nvalid ? (perm ? rx_g(perm)[row0 + i] : row0 + i) : (perm ? rx_g(perm)[row0] : row0);
   load_params<C>(d, smem, P, rstats);
   __syncthreads();
-  load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, true);
+  load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, true, dp, P, metrics);
   float labp[MT * 4];
   prefetch_labels<MT, false>(d, labels, rowidx, labp);
   RX_STAMP();
@@ -866,6 +984,7 @@ __device__ __forceinline__ void mlp_train_step_body(
     layer_backward<MT, false>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, stamps);
     RX_STAMP();
   });
+  if (d.front_n > 0) front_backward<MT>(d, dp, C::first(d), smem, img, Gr, feats, rowidx, nvalid);
 #undef RX_STAMP
 }
 
@@ -882,7 +1001,7 @@ __device__ __forceinline__ void mlp_eval_body(const MlpDesc* __restrict__ dp, co
   for (int i = rx_tid<false>(); i < Tile<MT>::BP; i += RX_THREADS) rowidx[i] = i < nvalid ? row0 + i : row0;
   load_params<C>(d, smem, P, rstats);
   __syncthreads();
-  load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, false);
+  load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, false, dp, P, metrics);
   bf16x8 wpre[RX_PJ][RX_PK];
   fwd_prefetch<false>(C::first(d), img, wpre);
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {

@@ -190,7 +190,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       rowidx[i] = i < nvalid ? (perm ? rx_g(perm)[row0 + i] : row0 + i) : (perm ? rx_g(perm)[row0] : row0);
     __syncthreads();
     // the batch gather does not depend on the weights: it overlaps the last optimizer tiles
-    load_inputs<MT, true>(d, C::first(d), smem, feats, rowidx, nvalid, true);
+    load_inputs<MT, true>(d, C::first(d), smem, feats, rowidx, nvalid, true, dp, P, metrics);
     float labp[MT * 4];
     prefetch_labels<MT, true>(d, labels, rowidx, labp);
     stamp(s, 1);

@@ -29,6 +29,14 @@ class MlpLayer(ctypes.Structure):
     ]
 
 
+class FrontCol(ctypes.Structure):
+    """One column of an embedding front (csrc/hip/mlp_core.h FrontCol)."""
+    _fields_ = [("src", ctypes.c_int), ("poff", ctypes.c_int), ("stride", ctypes.c_int), ("rows", ctypes.c_int)]
+
+
+MAXF = 64
+
+
 class MlpDesc(ctypes.Structure):
     _fields_ = [
         ("L", ctypes.c_int),
@@ -40,6 +48,8 @@ class MlpDesc(ctypes.Structure):
         ("layer", MlpLayer * MAXL),
         ("pr_lds_off", ctypes.c_int), ("pr_total", ctypes.c_int),
         ("act_off", ctypes.c_int), ("wgrad_mode", ctypes.c_int),
+        ("front_n", ctypes.c_int), ("front_q", ctypes.c_int), ("acc_mode", ctypes.c_int),
+        ("acc_thr", ctypes.c_float), ("front", FrontCol * MAXF), ("front_qbase", ctypes.c_int * MAXF),
     ]
 
 

@@ -81,6 +81,9 @@ def persistent_enabled() -> bool:
     return bool(conf_get("spark.ray.mi355x.mlp_persistent"))
 
 
+_ATTR = {"weight": "weight", "bias": "bias", "gamma": "weight", "beta": "bias", "emb": "weight"}
+
+
 def pick_mt(batch: int) -> Optional[int]:
     for mt in (2, 4, 8):
         if batch <= mt * 16:
@@ -91,7 +94,7 @@ def pick_mt(batch: int) -> Optional[int]:
 class FusedMLPTrainer:
     def __init__(self, spec: MlpSpec, opt_cfg: dict, loss: tuple, batch_size: int,
                  device: torch.device, lr_schedule: Optional[Callable[[int], float]] = None,
-                 layout_only: bool = False):
+                 layout_only: bool = False, acc_thr: Optional[float] = None):
         # layout_only: build the descriptors on the host (no GPU needed) -- used to warm the
         # specialised-kernel cache at build time
         self.layout_only = layout_only
@@ -103,6 +106,7 @@ class FusedMLPTrainer:
         self.bp = self.mt * 16
         self.loss_code, self.beta = loss
         self.lr_schedule = lr_schedule
+        self.acc_thr = acc_thr           # binary accuracy threshold (None: not counted)
         self.step_count = 0
         self.lib = _hip.lib()
         self._build()
@@ -226,13 +230,46 @@ class FusedMLPTrainer:
             scratch_off += bp * out_n
             x.pr_off = pr_total
             pr_total += 5 * out_n
+        # embedding front: every table is one contiguous run of the flat vector (element-wise
+        # optimizer segment); front column k reads element [id][j] at poff + id * stride
+        front = spec.front or []
+        if len(front) > _hip.MAXF:
+            raise ValueError("embedding front wider than the kernel's column table")
+        d.front_n = len(front)
+        if front:
+            tab_off = {}
+            pad4()
+            emb_start = off
+            for e in spec.embeddings():
+                tab_off[id(e)] = off
+                flat.append(e.weight.detach().reshape(-1).float())
+                self.layout.append(("emb", e, off, e.weight.numel()))
+                off += e.weight.numel()
+            vseg(emb_start, off - emb_start)
+            q = 0
+            for k, c in enumerate(front):
+                fc = d.front[k]
+                fc.src = c.src
+                d.front_qbase[k] = q
+                if c.emb is None:
+                    fc.poff, fc.stride, fc.rows = -1, 0, 0
+                else:
+                    fc.poff = tab_off[id(c.emb)] + c.j
+                    fc.stride, fc.rows = c.emb.embedding_dim, c.emb.num_embeddings
+                    q += fc.rows
+            d.front_q = q
+            l0 = d.layer[0]
+            if bp * l0.in_n * 4 + bp * len(front) * 2 > max_n * xs * 2:
+                raise ValueError("embedding front's backward scratch exceeds the G^T area")
+        d.acc_mode = 1 if self.acc_thr is not None else 0
+        d.acc_thr = float(self.acc_thr) if self.acc_thr is not None else 0.5
         d.pr_lds_off = alloc(pr_total * 4)
         d.pr_total = pr_total
         d.lds_bytes = lds
         d.max_k, d.max_n = max_k, max_n
         d.loss, d.beta = self.loss_code, self.beta
         d.out_dim = spec.out_features
-        d.feat_k = dims[0][2]
+        d.feat_k = _ru(spec.raw_features, 8) if front else dims[0][2]
         if lds > 160 * 1024:
             raise ValueError(f"fused MLP needs {lds} B of LDS (> 160 KiB)")
         self.desc = d
@@ -289,7 +326,7 @@ class FusedMLPTrainer:
 
     # ------------------------------------------------------------------- optimizer state ----
     def _param_of(self, kind, mod):
-        return getattr(mod, {"weight": "weight", "bias": "bias", "gamma": "weight", "beta": "bias"}[kind])
+        return getattr(mod, _ATTR[kind])
 
     @torch.no_grad()
     def load_optimizer_state(self, opt: torch.optim.Optimizer) -> bool:
@@ -427,7 +464,9 @@ class FusedMLPTrainer:
     def _run_persistent(self, feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream) -> bool:
         """The whole epoch as one persistent launch (csrc/hip/mlp_persist.h); False when this
         model / configuration cannot use it (the caller then runs the launch-per-step loop)."""
-        if self.desc.wgrad_mode != 1 or not persistent_enabled():
+        if self.desc.wgrad_mode != 1 or not persistent_enabled() or self.desc.front_n:
+            # (an embedding front's tables are updated between steps by the optimizer kernel,
+            # which the persistent epoch does not run)
             return False
         if getattr(self, "_ps_grid", None) is None:
             self._ps_grid = int(self.lib.rx_ps_grid_blocks(ctypes.byref(self.opt)))
@@ -504,7 +543,7 @@ class FusedMLPTrainer:
         """Map a flat vector (params/grads) onto ``{module_param_name: tensor}`` by identity."""
         out = {}
         for kind, mod, off, n in self.layout:
-            attr = {"weight": "weight", "bias": "bias", "gamma": "weight", "beta": "bias"}[kind]
+            attr = _ATTR[kind]
             out[(id(mod), attr)] = flat[off:off + n].view_as(getattr(mod, attr))
         return out
 
@@ -520,10 +559,13 @@ class FusedMLPTrainer:
 
     def _read_metrics(self) -> Dict[str, float]:
         m = self.metrics.cpu().numpy()
+        if m[6] > 0:
+            raise IndexError("embedding id out of range in the fused trainer's input "
+                             f"({int(m[6])} batch(es) clamped)")
         nb = max(m[4], 1.0)
         cnt = max(m[3], 1.0)
         return {"loss": float(m[0] / nb), "mae": float(m[1] / cnt), "mse": float(m[2] / cnt),
-                "count": float(m[3]), "batches": float(m[4])}
+                "acc": float(m[5] / cnt), "count": float(m[3]), "batches": float(m[4])}
 
     # ----------------------------------------------------------------------- state --------
     @torch.no_grad()
@@ -533,7 +575,7 @@ class FusedMLPTrainer:
         p = self.params.detach().to("cpu", non_blocking=False)
         rs = self.rstats.detach().to("cpu", non_blocking=False) if self.run_bufs else None
         for kind, mod, off, n in self.layout:
-            t = {"weight": "weight", "bias": "bias", "gamma": "weight", "beta": "bias"}[kind]
+            t = _ATTR[kind]
             dst = getattr(mod, t)
             dst.data.copy_(p[off:off + n].view_as(dst).to(dst.dtype))
         base = self.rstats.data_ptr()

@@ -33,7 +33,7 @@ _loaded = {}
 _LAYER_INT = ("in_", "out", "in_k", "out_k", "in_n", "out_n", "w_img", "wt_img", "w_off", "b_off", "act", "bn",
               "g_off", "be_off", "rs_off", "xt_off", "stat_off", "r_off", "pr_off", "xg_off", "gg_off")
 _DESC_INT = ("L", "r_lds_off", "gt_lds_off", "stats_lds_off", "lds_bytes", "max_k", "max_n", "loss", "out_dim",
-             "feat_k", "pr_lds_off", "pr_total", "act_off", "wgrad_mode")
+             "feat_k", "pr_lds_off", "pr_total", "act_off", "wgrad_mode", "front_n", "front_q", "acc_mode")
 
 
 def _f(x: float) -> str:
@@ -49,6 +49,7 @@ def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
     for k in _DESC_INT:
         out.append(f"  static constexpr int {k} = {int(getattr(desc, k))};")
     out.append(f"  static constexpr float beta = {_f(desc.beta)};")
+    out.append(f"  static constexpr float acc_thr = {_f(desc.acc_thr)};")
     out.append("};")
     for li in range(L):
         ly = desc.layer[li]
@@ -161,10 +162,10 @@ def load_specialized(trainer) -> Optional[str]:
     return path
 
 
-def precompile(model, optimizer, loss, batch_size: int) -> str:
+def precompile(model, optimizer, loss, batch_size: int, acc_thr=None) -> str:
     """Warm the code-object cache for one model/optimizer/loss/batch on a host without a GPU."""
     from raydp_amd.models.mlp_spec import extract_mlp_spec
     from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
     tr = FusedMLPTrainer(extract_mlp_spec(model), optimizer_config(optimizer), loss_code(loss), batch_size,
-                         None, layout_only=True)
+                         None, layout_only=True, acc_thr=acc_thr)
     return compile_for(tr)

@@ -328,8 +328,11 @@ class ClusterBackend:
         if missing:
             placed = self._sched.persist(rec["plan"].compute, rdd_id, missing)
             with self._lock:
-                for (i, _oid, _node, _path, _rows, ex_id) in placed:
-                    rec["locations"][i] = ex_id
+                for entry in placed:
+                    rec["locations"][entry[0]] = entry[5]
+                if rec.get("placed") is not None:
+                    fresh = {e[0]: e for e in placed}
+                    rec["placed"] = [fresh.get(e[0], e) for e in rec["placed"]]
         return len(missing)
 
     def _initial_executors(self) -> int:
@@ -479,15 +482,23 @@ class ClusterBackend:
             return rdd_id, [objects.put(t.replace_schema_metadata(),
                                         _lineage=functools.partial(self._recompute, plan, i))
                             for i, t in enumerate(df._cached.tables)]
-        placed = sched.persist(plan.compute, rdd_id, range(n))
-        placed.sort(key=lambda x: x[0])
+        with self._lock:
+            rec = self._recoverable.get(rdd_id)
+        if rec is not None and rec.get("placed") is not None and rec.get("plan") is plan:
+            # the same DataFrame converted again (e.g. fit_on_spark(df, df)): its blocks are
+            # already persisted under (rdd_id, i) -- hand out references to them, as Spark's
+            # persist() of an already-persisted RDD is a no-op
+            placed = rec["placed"]
+        else:
+            placed = sched.persist(plan.compute, rdd_id, range(n))
+            placed.sort(key=lambda x: x[0])
         refs, loc = [], {}
         for (i, oid, node_id, path, rows, ex_id) in placed:
             refs.append(ObjectRef(oid, owner=f"raydp-executor-{ex_id}", node_id=node_id,
                                   lineage=functools.partial(self._recompute, plan, i)))
             loc[i] = ex_id
         with self._lock:
-            self._recoverable[rdd_id] = {"df": df, "plan": plan, "locations": loc}
+            self._recoverable[rdd_id] = {"df": df, "plan": plan, "locations": loc, "placed": placed}
         return rdd_id, refs
 
     def _recompute(self, plan, i):

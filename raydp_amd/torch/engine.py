@@ -4,8 +4,11 @@
   once (one pinned DMA + the ``arrow_ingest`` HIP kernel); every epoch is one native call that
   enqueues, per batch, the single-workgroup fused fwd/bwd kernel, the (optional) RCCL
   all-reduce and the fused optimizer kernel; the epoch shuffle is a device permutation read by
-  the kernel's row gather. Used when the model is a fusable MLP (``models/mlp_spec.py``), the
-  loss is MSE/SmoothL1/L1, the optimizer Adam/AdamW/SGD and the metrics are MAE/MSE.
+  the kernel's row gather. Used when the model is a fusable MLP (``models/mlp_spec.py``) --
+  optionally behind an embedding front (per-column ``nn.Embedding`` lookups concatenated with
+  dense columns, the stroke tutorial's NET_Model: the kernel gathers the table rows and stores
+  their gradients itself) -- the loss is MSE/SmoothL1/L1, the optimizer Adam/AdamW/SGD and the
+  metrics are MAE/MSE/binary Accuracy.
 * ``TorchLoopEngine`` — any other model. Still device-resident (data ingested once, batches are
   device slices of a permuted index), loss and metrics accumulated on the device and read once
   per epoch; DDP via ``raydp_amd.parallel.ddp`` when ``world_size > 1``. On one GPU the whole
@@ -133,22 +136,26 @@ class FusedMLPEngine:
             return None
         if isinstance(feature_types, (list, tuple)) and len({t for t in feature_types}) > 1:
             return None
-        if any(n not in ("MeanAbsoluteError", "MeanSquaredError") for n in metrics.names):
+        acc_thr = _binary_accuracy_threshold(metrics)
+        if acc_thr is False:
             return None
         spec = extract_mlp_spec(model)
         lc = loss_code(loss)
         oc = optimizer_config(optimizer)
         if spec is None or lc is None or oc is None:
             return None
-        if spec.in_features != len(feature_columns):
+        if (spec.raw_features or spec.in_features) != len(feature_columns):
             return None
-        return spec, lc, oc
+        if acc_thr is not None and spec.out_features != 1:
+            return None
+        return spec, lc, oc, acc_thr
 
-    def __init__(self, model, optimizer, spec, lc, oc, metrics, device, config, lr_scheduler_fn):
+    def __init__(self, model, optimizer, spec, lc, oc, acc_thr, metrics, device, config, lr_scheduler_fn):
         from raydp_amd.ops.fused_mlp import FusedMLPTrainer
         self.model, self.metrics_names, self.device = model, metrics.names, device
         self.world = session.get_world_size()
-        self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn)
+        self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn,
+                                       acc_thr=acc_thr)
         self.optimizer = optimizer
         self.trainer.load_optimizer_state(optimizer)
         if self.world > 1:
@@ -174,6 +181,9 @@ class FusedMLPEngine:
             out["MeanAbsoluteError"] = m["mae"]
         if "MeanSquaredError" in self.metrics_names:
             out["MeanSquaredError"] = m["mse"]
+        for n in ("Accuracy", "BinaryAccuracy"):
+            if n in self.metrics_names:
+                out[n] = m["acc"]
         return out
 
     def train_epoch(self):
@@ -218,6 +228,27 @@ class FusedMLPEngine:
 
     def optimizer_state_dict(self):
         return self.trainer.export_optimizer_state(self.optimizer)
+
+
+def _binary_accuracy_threshold(metrics):
+    """The fused kernel computes MAE, MSE and single-output threshold accuracy (the built-in
+    ``Accuracy``: ``(pred > threshold).long() == target.long()``). Returns the accuracy
+    threshold (None when no accuracy metric is asked for) or False when some metric is
+    something else."""
+    from raydp_amd.torch import metrics as M
+    thr = None
+    for n in metrics.names:
+        if n in ("MeanAbsoluteError", "MeanSquaredError"):
+            continue
+        m = metrics._metrics.get(n)
+        if n in ("Accuracy", "BinaryAccuracy") and type(m) in (M.Accuracy, M.BinaryAccuracy):
+            kw = getattr(m, "kwargs", {})
+            if kw.get("task", "binary") != "binary" or kw.get("num_classes") not in (None, 2):
+                return False
+            thr = float(kw.get("threshold", 0.5))
+            continue
+        return False
+    return thr
 
 
 def _xgmi_for(trainer):

@@ -211,13 +211,13 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             raise ValueError("spark.ray.mi355x.fused=on but the model / optimizer / loss is not fusable "
                              "(FusedMLPEngine.applicable)")
         if fused is not None:
-            spec, lc, oc = fused
+            spec, lc, oc, acc_thr = fused
             if resume_dir:
                 _restore_optimizer(resume_dir, optimizer)
             lr_fn = None
             if config["lr_scheduler_creator"]:
                 lr_fn = _make_lr_schedule(optimizer, config["lr_scheduler_creator"], config)
-            engine = FusedMLPEngine(model, optimizer, spec, lc, oc, metrics, device, config, lr_fn)
+            engine = FusedMLPEngine(model, optimizer, spec, lc, oc, acc_thr, metrics, device, config, lr_fn)
         else:
             model = model.to(device)       # in place: the optimizer keeps its parameter objects
             sched = config["lr_scheduler_creator"](optimizer, config) if config["lr_scheduler_creator"] else None
