@@ -41,7 +41,8 @@ _EXE_SOURCES = {"supervisor.cc"}
 
 
 LIBS = {
-    "exec_kernels": dict(kind="cpu", sources=lambda: [os.path.join(CSRC, "exec", "exec_kernels.cc")]),
+    "exec_kernels": dict(kind="cpu", sources=lambda: [os.path.join(CSRC, "exec", "exec_kernels.cc"),
+                                                       os.path.join(CSRC, "exec", "expr", "expr_vm.cc")]),
     "raydp_runtime": dict(kind="cpu", sources=_runtime_sources, libs=["-lpthread", "-lrt", "-ldl"]),
     "hipkernels": dict(kind="hip", sources=_hip_sources),
     # executables: the per-node actor supervisor, the application master (native control

@@ -288,6 +288,8 @@ class UnaryOp(Expr):
 class Func(Expr):
     """A built-in SQL function: ``impl(list_of_evaluated_args, batch) -> array/scalar``."""
 
+    native = None  # opcode tag when the fused expression VM implements this function
+
     def __init__(self, fname: str, args: List[Expr], impl: Callable, display: Optional[str] = None):
         self.fname, self.args, self.impl, self.display = fname, args, impl, display
 

@@ -250,7 +250,12 @@ class DataFrame:
             if e.is_aggregate():
                 return self.agg(*cols)
             exprs.append((e, e.name()))
-        return self._map(lambda t, i: _eval_projection(t, exprs), "project")
+        node = P.MapPlan(self._src(), lambda t, i: _eval_projection(t, exprs), "project")
+        if not any(isinstance(x, Func) and x.fname in ("__explode__", "__posexplode__") or
+                   isinstance(x, Alias) and isinstance(x.child, Func)
+                   and x.child.fname in ("__explode__", "__posexplode__") for x, _ in exprs):
+            node.rel = ("project", list(exprs))
+        return self._with(node)
 
     def selectExpr(self, *exprs):
         from raydp_amd.spark.functions import expr
@@ -282,7 +287,9 @@ class DataFrame:
             if colName in t.column_names:
                 return t.set_column(t.column_names.index(colName), colName, v)
             return t.append_column(colName, v)
-        return self._map(fn, f"withColumn({colName})")
+        node = P.MapPlan(self._src(), fn, f"withColumn({colName})")
+        node.rel = ("with", colName, e)
+        return self._with(node)
 
     def withColumns(self, colsMap: Dict[str, Column]):
         df = self
@@ -304,7 +311,9 @@ class DataFrame:
         names = set()
         for c in cols:
             names.add(c if isinstance(c, str) else c._expr.name())
-        return self._map(lambda t, i: t.drop([c for c in t.column_names if c in names]), "drop")
+        node = P.MapPlan(self._src(), lambda t, i: t.drop([c for c in t.column_names if c in names]), "drop")
+        node.rel = ("drop", frozenset(names))
+        return self._with(node)
 
     def filter(self, condition):
         if isinstance(condition, str):
@@ -331,6 +340,7 @@ class DataFrame:
             return t.filter(mask, null_selection_behavior="drop")
         node = P.MapPlan(src, fn, "filter")
         node.filter_preds = preds
+        node.rel = ("filter", list(preds))
         return self._with(node)
 
     where = filter

@@ -1,0 +1,1274 @@
+"""Fused narrow-operator execution: a chain of ``filter`` / ``withColumn`` / ``select`` /
+``drop`` operators is compiled into ONE register program and run by the native expression VM
+(``csrc/exec/expr/expr_vm.cc``) in a single call per partition.
+
+Spark runs the same chain as whole-stage generated Java code inside its executors (reference:
+the executors hosted by ``RayDPExecutor.scala``; the measured chain is
+``examples/data_process.py``: 14 filters, 9 time features, 2+8 Python UDF calls, 7 drops).
+The single-operator path (``dataframe.py`` + ``column.py``) makes one or more pyarrow calls per
+expression node and materialises a new table per operator; here every intermediate column
+lives in VM registers, filters compact the live registers in place, and only the final
+columns are written.
+
+Compilation (once per chain *structure* per process; cached):
+
+* Spark expressions are typed the way the Arrow path types them - the result type of every
+  arithmetic node is obtained from pyarrow itself on empty arrays, explicit casts are inserted,
+  and the final schema is checked against the plan's own (Arrow-path) schema; any mismatch
+  disables fusion for that chain.
+* Python row UDFs whose body the compiler understands (the ``_Vectorizer`` subset in
+  ``udf.py``: arithmetic, comparisons incl. chained ones, ``and``/``or``/``not``, if/else
+  returns, ``int()``/``float()``/``abs()``/``np.abs``/``math.fabs``/``sqrt``/``min``/``max``)
+  are inlined with numpy's typing rules. Each call site exports its arguments and result so
+  every partition is checked against the Python function on a sample of rows (plus each
+  argument's extreme rows); a mismatch retires that UDF to the per-row path, and a null
+  argument sends the partition through the per-row path (Spark's ``None`` semantics).
+* Anything else becomes a *host leaf* evaluated by the Arrow path on the segment input
+  (allowed while no filter precedes it, or for the timestamp parse, which never raises), or
+  splits the chain into VM segments around a host operator.
+"""
+import ast
+import builtins
+import ctypes
+import math
+import os
+import threading
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+
+from raydp_amd.spark import column as C
+
+T_BOOL, T_I32, T_I64, T_F32, T_F64 = 0, 1, 2, 3, 4
+OP_LOAD, OP_CONST, OP_CAST, OP_BIN, OP_CMP, OP_UN, OP_AND, OP_OR, OP_IFELSE, OP_DT, OP_FILTER, \
+    OP_ISNULL, OP_FILLNULL = range(1, 14)
+B_ADD, B_SUB, B_MUL, B_DIV, B_MOD_SPARK, B_MOD_PY, B_FLOORDIV_PY, B_POW, B_MIN, B_MAX = range(10)
+C_LT, C_LE, C_GT, C_GE, C_EQ, C_NE = range(6)
+U_NEG, U_ABS, U_NOT, U_SQRT, U_FLOOR, U_CEIL, U_TRUNC, U_ISNAN = range(8)
+D_FIELDS = {"year": 0, "month": 1, "dayofmonth": 2, "hour": 3, "minute": 4, "second": 5,
+            "dayofweek": 6, "weekofyear": 7, "quarter": 8, "dayofyear": 9}
+_ELEM = {T_BOOL: 1, T_I32: 4, T_I64: 8, T_F32: 4, T_F64: 8}
+_NP = {T_BOOL: np.bool_, T_I32: np.int32, T_I64: np.int64, T_F32: np.float32, T_F64: np.float64}
+_NP_TO_CT = {np.dtype(v): k for k, v in _NP.items()}
+_ARROW_OF = {T_BOOL: pa.bool_(), T_I32: pa.int32(), T_I64: pa.int64(), T_F32: pa.float32(),
+             T_F64: pa.float64()}
+
+_VERIFY_FIRST, _VERIFY_LATER = 64, 4
+STATS = {"fused_partitions": 0, "fallback_partitions": 0, "compiles": 0, "udf_retired": 0}
+
+
+class _Unsupported(Exception):
+    pass
+
+
+def _ct(t: pa.DataType) -> Optional[int]:
+    if t == pa.bool_():
+        return T_BOOL
+    if t == pa.int32():
+        return T_I32
+    if t == pa.int64() or pa.types.is_timestamp(t):
+        return T_I64
+    if t == pa.float32():
+        return T_F32
+    if t == pa.float64():
+        return T_F64
+    return None
+
+
+def _is_num(t):
+    return pa.types.is_integer(t) or pa.types.is_floating(t)
+
+
+_probe_cache: Dict[tuple, object] = {}
+
+
+def _probe(fname, ta, tb):
+    """Result type pyarrow gives ``fname`` on operands of these types (types only)."""
+    key = (fname, ta, tb)
+    r = _probe_cache.get(key)
+    if r is None:
+        try:
+            r = getattr(pc, fname)(pa.array([], ta), pa.array([], tb)).type
+        except Exception as e:  # noqa: BLE001 - the Arrow path would raise too
+            r = e
+        _probe_cache[key] = r
+    if isinstance(r, Exception):
+        raise _Unsupported(f"{fname}({ta}, {tb})")
+    return r
+
+
+# ------------------------------------------------------------------------------------------
+# program builder
+# ------------------------------------------------------------------------------------------
+class Val:
+    __slots__ = ("id", "atype", "ct", "const")
+
+    def __init__(self, vid, atype, ct, const=None):
+        self.id, self.atype, self.ct, self.const = vid, atype, ct, const
+
+
+class Weak:
+    """A Python scalar inside a UDF body (numpy NEP 50 'weak' operand)."""
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+
+class _Builder:
+    def __init__(self, schema: pa.Schema):
+        self.schema = schema
+        self.code: List[list] = []
+        self.fconst: List[float] = []
+        self.iconst: List[int] = []
+        self.nvals = 0
+        self.inputs: List[tuple] = []      # ("col", index) | ("ts", index) | ("host", expr, type)
+        self.input_ix: Dict[tuple, int] = {}
+        self.loaded: Dict[int, Val] = {}
+        self.filtered = False
+        self.taps: List[tuple] = []        # (udf, site values) for verification
+
+    def mark(self):
+        return (len(self.code), len(self.fconst), len(self.iconst), self.nvals, len(self.inputs),
+                dict(self.input_ix), dict(self.loaded), self.filtered, len(self.taps))
+
+    def rollback(self, m):
+        (nc, nf, ni, self.nvals, nin, self.input_ix, self.loaded, self.filtered, nt) = m
+        del self.code[nc:], self.fconst[nf:], self.iconst[ni:], self.inputs[nin:], self.taps[nt:]
+
+    def new(self, atype, ct, const=None) -> Val:
+        v = Val(self.nvals, atype, ct, const)
+        self.nvals += 1
+        return v
+
+    def emit(self, op, dst, a=-1, b=-1, c=-1, type=0, aux=0, imm=0):
+        self.code.append([op, dst, a, b, c, type, aux, imm])
+
+    # -- values ---------------------------------------------------------------------------
+    def const(self, value, atype: pa.DataType) -> Val:
+        ct = _ct(atype)
+        if ct is None:
+            raise _Unsupported(f"constant of type {atype}")
+        v = self.new(atype, ct, const=value)
+        if value is None:
+            pool = self.fconst if ct in (T_F32, T_F64) else self.iconst
+            pool.append(0)
+            self.emit(OP_CONST, v.id, type=ct, aux=1, imm=len(pool) - 1)
+        elif ct in (T_F32, T_F64):
+            self.fconst.append(float(value))
+            self.emit(OP_CONST, v.id, type=ct, imm=len(self.fconst) - 1)
+        else:
+            self.iconst.append(int(value))
+            self.emit(OP_CONST, v.id, type=ct, imm=len(self.iconst) - 1)
+        return v
+
+    def load(self, key: tuple, atype: pa.DataType) -> Val:
+        ix = self.input_ix.get(key)
+        if ix is None:
+            ix = len(self.inputs)
+            self.inputs.append(key)
+            self.input_ix[key] = ix
+        v = self.loaded.get(ix)
+        if v is None:
+            ct = _ct(atype)
+            if ct is None:
+                raise _Unsupported(f"input of type {atype}")
+            v = self.new(atype, ct)
+            self.emit(OP_LOAD, v.id, type=ct, imm=ix)
+            self.loaded[ix] = v
+        return v
+
+    def cast(self, v: Val, ct: int, atype: Optional[pa.DataType] = None) -> Val:
+        atype = atype or _ARROW_OF[ct]
+        if v.ct == ct:
+            return v if v.atype == atype else Val(v.id, atype, ct, v.const)
+        out = self.new(atype, ct)
+        self.emit(OP_CAST, out.id, v.id, type=ct, aux=v.ct)
+        return out
+
+    def bin(self, kind, a: Val, b: Val, ct, atype=None) -> Val:
+        out = self.new(atype or _ARROW_OF[ct], ct)
+        self.emit(OP_BIN, out.id, a.id, b.id, type=ct, aux=kind)
+        return out
+
+    def cmp(self, kind, a: Val, b: Val, ct) -> Val:
+        out = self.new(pa.bool_(), T_BOOL)
+        self.emit(OP_CMP, out.id, a.id, b.id, type=ct, aux=kind)
+        return out
+
+    def un(self, kind, a: Val, ct=None, atype=None) -> Val:
+        ct = a.ct if ct is None else ct
+        out = self.new(atype or (a.atype if ct == a.ct else _ARROW_OF[ct]), ct)
+        self.emit(OP_UN, out.id, a.id, type=a.ct if kind == U_ISNAN else ct, aux=kind)
+        return out
+
+    def logic(self, op, a: Val, b: Val) -> Val:
+        out = self.new(pa.bool_(), T_BOOL)
+        self.emit(op, out.id, a.id, b.id, type=T_BOOL)
+        return out
+
+    def ifelse(self, c: Val, a: Val, b: Val, null_is_false: bool) -> Val:
+        out = self.new(a.atype, a.ct)
+        self.emit(OP_IFELSE, out.id, a.id, b.id, c.id, type=a.ct, aux=1 if null_is_false else 0)
+        return out
+
+    def isnull(self, a: Val, negate=False) -> Val:
+        out = self.new(pa.bool_(), T_BOOL)
+        self.emit(OP_ISNULL, out.id, a.id, type=a.ct, aux=1 if negate else 0)
+        return out
+
+    def fillnull(self, a: Val, b: Val) -> Val:
+        out = self.new(a.atype, a.ct)
+        self.emit(OP_FILLNULL, out.id, a.id, b.id, type=a.ct)
+        return out
+
+    def filter(self, c: Val):
+        self.emit(OP_FILTER, -1, c.id, type=T_BOOL)
+        self.filtered = True
+
+
+# ------------------------------------------------------------------------------------------
+# Spark expression compiler (Arrow-path semantics)
+# ------------------------------------------------------------------------------------------
+_ARITH = {"+": ("add", B_ADD), "-": ("subtract", B_SUB), "*": ("multiply", B_MUL)}
+_CMPK = {"<": C_LT, "<=": C_LE, ">": C_GT, ">=": C_GE, "==": C_EQ, "!=": C_NE}
+
+
+class _ChainCompiler:
+    """Compiles one segment of narrow operators against its input schema."""
+
+    def __init__(self, schema: pa.Schema):
+        self.b = _Builder(schema)
+        # current columns: list of [name, ("in", index) | ("val", Val)]
+        self.cols: List[list] = [[f.name, ("in", i)] for i, f in enumerate(schema)]
+
+    # -- columns ------------------------------------------------------------------------
+    def _resolve(self, name):
+        for c in self.cols:
+            if c[0] == name:
+                return c
+        low = name.lower()
+        for c in self.cols:
+            if c[0].lower() == low:
+                return c
+        raise _Unsupported(f"unresolved column {name}")
+
+    def _col_val(self, ref) -> Val:
+        kind, x = ref
+        if kind == "val":
+            return x
+        f = self.b.schema.field(x)
+        return self.b.load(("col", x), f.type)
+
+    # -- host leaves --------------------------------------------------------------------
+    def _host(self, e: C.Expr) -> Val:
+        """Evaluate ``e`` with the Arrow path on the segment input; only sound while every row
+        of the input reaches it (no filter emitted yet) and it reads only untouched inputs."""
+        if self.b.filtered:
+            raise _Unsupported("host expression after a filter")
+        names = self.b.schema.names
+        for r in e.references():
+            c = self._resolve(r)
+            # the leaf is evaluated on the segment's input table, so every column it reads must
+            # still be that input column under its input name (and the name unambiguous)
+            if c[1][0] != "in" or names[c[1][1]] != r or names.count(r) != 1:
+                raise _Unsupported("host expression over a derived column")
+        typ = C.as_array(e.eval(self.b.schema.empty_table()), 0).type
+        if _ct(typ) is None:
+            raise _Unsupported(f"host expression of type {typ}")
+        return self.b.load(("host", e, typ), typ)
+
+    def _ts(self, e: C.Expr) -> Val:
+        """Timestamp operand of a datetime function (Arrow ``to_timestamp`` semantics)."""
+        inner = e
+        while isinstance(inner, C.Alias):
+            inner = inner.child
+        if isinstance(inner, C.ColRef):
+            c = self._resolve(inner.col_name)
+            if c[1][0] == "in":
+                t = self.b.schema.field(c[1][1]).type
+                if C._is_str(t):
+                    # string -> timestamp[s] parse: never raises, so it may run before filters
+                    return self.b.load(("ts", c[1][1]), pa.timestamp("s"))
+        v = self.expr(e)
+        if not pa.types.is_timestamp(v.atype):
+            raise _Unsupported("datetime of non-timestamp")
+        return v
+
+    # -- expressions --------------------------------------------------------------------
+    def expr(self, e: C.Expr) -> Val:
+        try:
+            return self._expr(e)
+        except _Unsupported:
+            if isinstance(e, (C.ColRef, C.Lit, C.Alias)):
+                raise
+            return self._host(e)
+
+    def _expr(self, e: C.Expr) -> Val:
+        b = self.b
+        if isinstance(e, C.Alias):
+            return self.expr(e.child)
+        if isinstance(e, C.ColRef):
+            return self._col_val(self._resolve(e.col_name)[1])
+        if isinstance(e, C.Lit):
+            v = e.value
+            s = v if isinstance(v, pa.Scalar) else pa.scalar(v)
+            if not s.is_valid:
+                raise _Unsupported("null literal")
+            return b.const(s.as_py(), s.type)
+        if isinstance(e, C.BinOp):
+            return self._binop(e)
+        if isinstance(e, C.UnaryOp):
+            v = self.expr(e.child)
+            if e.op == "-":
+                if not _is_num(v.atype):
+                    raise _Unsupported("negate")
+                return b.un(U_NEG, v)
+            if e.op == "~":
+                if v.ct != T_BOOL:
+                    raise _Unsupported("invert")
+                return b.un(U_NOT, v)
+            if e.op in ("isnull", "isnotnull"):
+                return b.isnull(v, negate=e.op == "isnotnull")
+            if e.op == "isnan":
+                return b.un(U_ISNAN, self._double(v), T_BOOL, pa.bool_())
+            raise _Unsupported(e.op)
+        if isinstance(e, C.Func):
+            tag = getattr(e, "native", None)
+            if tag is None:
+                raise _Unsupported(e.fname)
+            if tag[0] == "dt":
+                ts = self._ts(e.args[0])
+                out = b.new(pa.int32(), T_I32)
+                unit = ts.atype.unit
+                ups = {"s": 1, "ms": 1000, "us": 1000000, "ns": 1000000000}[unit]
+                b.emit(OP_DT, out.id, ts.id, type=T_I64, aux=D_FIELDS[tag[1]], imm=ups)
+                return out
+            v = self.expr(e.args[0])
+            if tag[0] == "abs":
+                if not _is_num(v.atype) or v.ct is None:
+                    raise _Unsupported("abs")
+                return b.un(U_ABS, v)
+            if tag[0] == "sqrt":
+                return b.un(U_SQRT, self._double(v))
+            if tag[0] == "isnan":
+                return b.un(U_ISNAN, self._double(v), T_BOOL, pa.bool_())
+            raise _Unsupported(str(tag))
+        if isinstance(e, C.Cast):
+            return self._cast(e)
+        if isinstance(e, C.CaseWhen):
+            return self._casewhen(e)
+        if isinstance(e, C.UDFExpr):
+            return self._udf(e)
+        raise _Unsupported(type(e).__name__)
+
+    def _double(self, v: Val) -> Val:
+        t = v.atype
+        if pa.types.is_floating(t) or pa.types.is_integer(t) or pa.types.is_boolean(t):
+            return self.b.cast(v, T_F64)
+        raise _Unsupported(f"to double {t}")
+
+    def _binop(self, e: C.BinOp) -> Val:
+        b = self.b
+        x, y = self.expr(e.left), self.expr(e.right)
+        op = e.op
+        if op in _ARITH:
+            if not (_is_num(x.atype) and _is_num(y.atype)):
+                raise _Unsupported("arith types")
+            rt = _probe(_ARITH[op][0], x.atype, y.atype)
+            ct = _ct(rt)
+            if ct is None:
+                raise _Unsupported(f"arith result {rt}")
+            return b.bin(_ARITH[op][1], b.cast(x, ct), b.cast(y, ct), ct, rt)
+        if op == "/":
+            return b.bin(B_DIV, self._double(x), self._double(y), T_F64)
+        if op == "%":
+            if pa.types.is_integer(x.atype) and pa.types.is_integer(y.atype):
+                raise _Unsupported("integer remainder (raises on zero)")
+            return b.bin(B_MOD_SPARK, self._double(x), self._double(y), T_F64)
+        if op == "**":
+            return b.bin(B_POW, self._double(x), self._double(y), T_F64)
+        if op in _CMPK:
+            return b.cmp(_CMPK[op], *self._cmp_operands(x, y))
+        if op in ("&", "|"):
+            if x.ct != T_BOOL or y.ct != T_BOOL:
+                raise _Unsupported("logic on non-bool")
+            return b.logic(OP_AND if op == "&" else OP_OR, x, y)
+        if op == "<=>":
+            xa, ya, ct = self._cmp_operands(x, y)
+            eq = b.fillnull(b.cmp(C_EQ, xa, ya, ct), b.const(False, pa.bool_()))
+            both = b.logic(OP_AND, b.isnull(x), b.isnull(y))
+            return b.logic(OP_OR, eq, both)
+        raise _Unsupported(op)
+
+    def _cmp_operands(self, x: Val, y: Val):
+        if x.ct == T_BOOL and y.ct == T_BOOL:
+            return x, y, T_BOOL
+        if pa.types.is_timestamp(x.atype) or pa.types.is_timestamp(y.atype):
+            if x.atype != y.atype:
+                raise _Unsupported("timestamp compare")
+            return x, y, T_I64
+        if not (_is_num(x.atype) and _is_num(y.atype)):
+            raise _Unsupported("compare types")
+        ct = _ct(_probe("add", x.atype, y.atype))
+        if ct is None:
+            raise _Unsupported("compare type")
+        return self.b.cast(x, ct), self.b.cast(y, ct), ct
+
+    def _cast(self, e: C.Cast) -> Val:
+        t = e.to.to_arrow()
+        if pa.types.is_timestamp(t):
+            return self._ts(e.child)
+        v = self.expr(e.child)
+        ct = _ct(t)
+        if ct is None or not (_is_num(v.atype) or v.ct == T_BOOL):
+            raise _Unsupported(f"cast {v.atype} -> {t}")
+        if pa.types.is_integer(t) and pa.types.is_floating(v.atype):
+            v = self.b.un(U_TRUNC, v)
+        return self.b.cast(v, ct, t)
+
+    def _casewhen(self, e: C.CaseWhen) -> Val:
+        b = self.b
+        vals = [self.expr(v) for _, v in e.branches]
+        other = self.expr(e.otherwise) if e.otherwise is not None else None
+        target = None
+        for v in vals + ([other] if other is not None else []):
+            target = v.atype if target is None else C._wider(target, v.atype)
+        ct = _ct(target) if target is not None else None
+        if ct is None or pa.types.is_timestamp(target):
+            raise _Unsupported("case type")
+        for v in vals + ([other] if other is not None else []):
+            if not (_is_num(v.atype) or v.ct == T_BOOL) or (v.atype != target and not _widening(v.atype, target)):
+                raise _Unsupported("case branch cast")
+        out = b.cast(other, ct, target) if other is not None else b.const(None, target)
+        for (c, _), v in reversed(list(zip(e.branches, vals))):
+            cond = self.expr(c)
+            if cond.ct != T_BOOL:
+                raise _Unsupported("case condition")
+            out = b.ifelse(cond, b.cast(v, ct, target), out, null_is_false=True)
+        return out
+
+    def _udf(self, e: C.UDFExpr) -> Val:
+        u = e.udf
+        if getattr(u, "_vec_state", None) == "failed" or _udf_key(u) in _RETIRED:
+            raise _Unsupported("udf retired")
+        args = [self.expr(a) for a in e.args]
+        for a in args:
+            if not (_is_num(a.atype) or a.ct == T_BOOL):
+                raise _Unsupported("udf arg type")
+        res = _UdfCompiler(self.b, u).compile(args)
+        self.b.taps.append((u, res, args))
+        return res
+
+    # -- operators ----------------------------------------------------------------------
+    def op(self, rel):
+        kind = rel[0]
+        m = self.b.mark()
+        saved_cols = [list(c) for c in self.cols]
+        try:
+            if kind == "with":
+                _, name, e = rel
+                v = self.expr(e)
+                for c in self.cols:
+                    if c[0] == name:
+                        c[1] = ("val", v)
+                        break
+                else:
+                    self.cols.append([name, ("val", v)])
+            elif kind == "filter":
+                for p in rel[1]:
+                    v = self.expr(p)
+                    if v.ct != T_BOOL:
+                        raise _Unsupported("non-bool predicate")
+                    self.b.filter(v)
+            elif kind == "drop":
+                names = rel[1]
+                self.cols = [c for c in self.cols if c[0] not in names]
+            elif kind == "project":
+                new = []
+                for e, name in rel[1]:
+                    inner = e
+                    while isinstance(inner, C.Alias):
+                        inner = inner.child
+                    if isinstance(inner, C.ColRef):
+                        new.append([name, self._resolve(inner.col_name)[1]])
+                    else:
+                        new.append([name, ("val", self.expr(e))])
+                self.cols = new
+            else:
+                raise _Unsupported(kind)
+        except _Unsupported:
+            self.b.rollback(m)
+            self.cols = saved_cols
+            raise
+
+    def finish(self) -> "Program":
+        return Program(self.b, self.cols)
+
+
+def _widening(a: pa.DataType, b: pa.DataType) -> bool:
+    order = [pa.bool_(), pa.int32(), pa.int64(), pa.float32(), pa.float64()]
+    return a in order and b in order and order.index(a) <= order.index(b) and \
+        not (a == pa.int64() and b == pa.float32())
+
+
+# ------------------------------------------------------------------------------------------
+# Python UDF compiler (numpy semantics, like udf._Vectorizer)
+# ------------------------------------------------------------------------------------------
+_RETIRED = set()
+
+
+def _udf_key(u):
+    f = getattr(u, "func", None)
+    code = getattr(f, "__code__", None)
+    if code is None:
+        return None
+    try:
+        consts = []
+        if f.__closure__:
+            for cell in f.__closure__:
+                v = cell.cell_contents
+                hash(v)
+                consts.append(v if isinstance(v, (int, float, bool, str, tuple, type(None))) else id(v))
+        glob = tuple((n, f.__globals__[n]) for n in code.co_names
+                     if n in f.__globals__ and isinstance(f.__globals__[n], (int, float, bool, tuple)))
+        return (code.co_code, code.co_consts, code.co_names, tuple(consts), glob,
+                str(u.returnType), getattr(f, "__qualname__", ""))
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def _np_promote(x, y) -> int:
+    """numpy NEP 50 result type code of a binary arithmetic op on Val/Weak operands."""
+    if isinstance(x, Weak) and isinstance(y, Weak):
+        raise _Unsupported("fold")
+    if isinstance(x, Weak):
+        x, y = y, x
+    if isinstance(y, Weak):
+        v = y.v
+        if isinstance(v, bool):
+            return x.ct
+        if isinstance(v, int):
+            if x.ct == T_BOOL:
+                return T_I64
+            info = np.iinfo(_NP[x.ct]) if x.ct in (T_I32, T_I64) else None
+            if info is not None and not (info.min <= v <= info.max):
+                raise _Unsupported("python int out of range")
+            return x.ct
+        if isinstance(v, float):
+            return x.ct if x.ct in (T_F32, T_F64) else T_F64
+        raise _Unsupported("weak type")
+    return _NP_TO_CT[np.result_type(_NP[x.ct], _NP[y.ct])]
+
+
+class _UdfCompiler:
+    def __init__(self, b: _Builder, u):
+        import inspect
+        import textwrap
+        self.b, self.u = b, u
+        fn = u.func
+        try:
+            src = textwrap.dedent(inspect.getsource(fn))
+        except (OSError, TypeError) as e:
+            raise _Unsupported("no source") from e
+        tree = ast.parse(src)
+        fdef = tree.body[0]
+        if not isinstance(fdef, ast.FunctionDef) or fdef.args.vararg or fdef.args.kwarg or \
+                fdef.args.kwonlyargs or fdef.args.defaults:
+            raise _Unsupported("signature")
+        self.fdef = fdef
+        self.arg_names = [a.arg for a in fdef.args.args]
+        self.globals = dict(fn.__globals__)
+        if fn.__closure__:
+            for name, cell in zip(fn.__code__.co_freevars, fn.__closure__):
+                self.globals[name] = cell.cell_contents
+
+    def compile(self, args: List[Val]) -> Val:
+        if len(args) != len(self.arg_names):
+            raise _Unsupported("arity")
+        env = dict(zip(self.arg_names, args))
+        out = self._block(self.fdef.body, env)
+        if out is None:
+            raise _Unsupported("no return")
+        rt = self.u.returnType.to_arrow()
+        ct = _ct(rt)
+        if ct is None or pa.types.is_timestamp(rt):
+            raise _Unsupported("udf return type")
+        out = self._strong(out, None)
+        return self.b.cast(out, ct, rt)
+
+    # weak scalars become constants of the type numpy would give them
+    def _strong(self, v, like: Optional[Val]):
+        if isinstance(v, Val):
+            return v
+        if isinstance(v, Weak):
+            x = v.v
+            if like is not None:
+                ct = _np_promote(like, v)
+            elif isinstance(x, bool):
+                ct = T_BOOL
+            elif isinstance(x, int):
+                ct = T_I64
+            elif isinstance(x, float):
+                ct = T_F64
+            else:
+                raise _Unsupported("scalar")
+            return self.b.const(x, _ARROW_OF[ct])
+        raise _Unsupported("value")
+
+    def _block(self, stmts, env):
+        for i, st in enumerate(stmts):
+            if isinstance(st, ast.Return):
+                return self._expr(st.value, env) if st.value is not None else None
+            if isinstance(st, ast.Expr) and isinstance(st.value, ast.Constant):
+                continue
+            if isinstance(st, ast.Assign) and len(st.targets) == 1 and isinstance(st.targets[0], ast.Name):
+                env[st.targets[0].id] = self._expr(st.value, env)
+                continue
+            if isinstance(st, ast.If):
+                cond = self._cond(st.test, env)
+                then_v = self._block(st.body, dict(env))
+                rest = st.orelse if st.orelse else stmts[i + 1:]
+                else_v = self._block(rest, dict(env))
+                if then_v is None or else_v is None:
+                    raise _Unsupported("branch without return")
+                return self._where(cond, then_v, else_v)
+            raise _Unsupported(type(st).__name__)
+        return None
+
+    def _where(self, cond: Val, a, b):
+        if isinstance(a, Weak) and isinstance(b, Weak):
+            ct = _NP_TO_CT.get(np.result_type(np.asarray(a.v), np.asarray(b.v)))
+            if ct is None:
+                raise _Unsupported("where types")
+            av, bv = self.b.const(a.v, _ARROW_OF[ct]), self.b.const(b.v, _ARROW_OF[ct])
+        else:
+            ct = _np_promote(a if isinstance(a, Val) else b, b if isinstance(a, Val) else a) \
+                if isinstance(a, Weak) or isinstance(b, Weak) else _np_promote(a, b)
+            av = self.b.cast(self._strong(a, b if isinstance(b, Val) else None), ct)
+            bv = self.b.cast(self._strong(b, a if isinstance(a, Val) else None), ct)
+        return self.b.ifelse(cond, av, bv, null_is_false=False)
+
+    def _cond(self, node, env) -> Val:
+        if isinstance(node, ast.BoolOp):
+            parts = [self._cond(v, env) for v in node.values]
+            out = parts[0]
+            for p in parts[1:]:
+                out = self.b.logic(OP_AND if isinstance(node.op, ast.And) else OP_OR, out, p)
+            return out
+        if isinstance(node, ast.UnaryOp) and isinstance(node.op, ast.Not):
+            return self.b.un(U_NOT, self._cond(node.operand, env))
+        v = self._expr(node, env)
+        if isinstance(v, Weak):
+            return self.b.const(bool(v.v), pa.bool_())
+        return self.b.cast(v, T_BOOL)
+
+    def _name(self, n, env):
+        if n in env:
+            return env[n]
+        if n in self.globals:
+            v = self.globals[n]
+            if isinstance(v, (bool, int, float)) or isinstance(v, tuple):
+                return Weak(v) if not isinstance(v, tuple) else tuple(Weak(x) for x in v)
+            if isinstance(v, np.floating):
+                return Weak(float(v))
+        raise _Unsupported(f"name {n}")
+
+    def _expr(self, node, env):
+        b = self.b
+        if isinstance(node, ast.Constant):
+            if isinstance(node.value, (bool, int, float)):
+                return Weak(node.value)
+            raise _Unsupported("constant")
+        if isinstance(node, ast.Name):
+            return self._name(node.id, env)
+        if isinstance(node, ast.Tuple):
+            return tuple(self._expr(e, env) for e in node.elts)
+        if isinstance(node, ast.Subscript):
+            base = self._expr(node.value, env)
+            idx = self._expr(node.slice, env)
+            if isinstance(base, tuple) and isinstance(idx, Weak) and isinstance(idx.v, int):
+                return base[idx.v]
+            raise _Unsupported("subscript")
+        if isinstance(node, ast.BinOp):
+            x, y = self._expr(node.left, env), self._expr(node.right, env)
+            kinds = {ast.Add: B_ADD, ast.Sub: B_SUB, ast.Mult: B_MUL, ast.Div: B_DIV,
+                     ast.FloorDiv: B_FLOORDIV_PY, ast.Mod: B_MOD_PY, ast.Pow: B_POW}
+            k = kinds.get(type(node.op))
+            if k is None or isinstance(x, tuple) or isinstance(y, tuple):
+                raise _Unsupported("binop")
+            ct = _np_promote(x, y)
+            if ct == T_BOOL:
+                raise _Unsupported("bool arithmetic")
+            if k == B_DIV and ct in (T_I32, T_I64):
+                ct = T_F64
+            if k == B_POW and ct not in (T_F32, T_F64):
+                raise _Unsupported("integer power")
+            xv = b.cast(self._strong(x, y if isinstance(y, Val) else None), ct)
+            yv = b.cast(self._strong(y, x if isinstance(x, Val) else None), ct)
+            return b.bin(k, xv, yv, ct)
+        if isinstance(node, ast.UnaryOp):
+            v = self._expr(node.operand, env)
+            if isinstance(node.op, ast.UAdd):
+                return v
+            if isinstance(node.op, ast.USub):
+                if isinstance(v, Weak):
+                    return Weak(-v.v)
+                if v.ct == T_BOOL:
+                    raise _Unsupported("negate bool")
+                return b.un(U_NEG, v)
+            if isinstance(node.op, ast.Not):
+                return b.un(U_NOT, self._cond(node.operand, env))
+            raise _Unsupported("unary")
+        if isinstance(node, ast.Compare):
+            left = self._expr(node.left, env)
+            out = None
+            cmpk = {ast.Lt: C_LT, ast.LtE: C_LE, ast.Gt: C_GT, ast.GtE: C_GE, ast.Eq: C_EQ,
+                    ast.NotEq: C_NE}
+            for op, rnode in zip(node.ops, node.comparators):
+                k = cmpk.get(type(op))
+                if k is None:
+                    raise _Unsupported("compare op")
+                right = self._expr(rnode, env)
+                if isinstance(left, Weak) and isinstance(right, Weak):
+                    raise _Unsupported("constant compare")
+                ct = _np_promote(left, right)
+                lv = b.cast(self._strong(left, right if isinstance(right, Val) else None), ct)
+                rv = b.cast(self._strong(right, left if isinstance(left, Val) else None), ct)
+                r = b.cmp(k, lv, rv, ct)
+                out = r if out is None else b.logic(OP_AND, out, r)
+                left = right
+            return out
+        if isinstance(node, ast.BoolOp):
+            return self._cond(node, env)
+        if isinstance(node, ast.IfExp):
+            return self._where(self._cond(node.test, env), self._expr(node.body, env),
+                               self._expr(node.orelse, env))
+        if isinstance(node, ast.Call):
+            if node.keywords:
+                raise _Unsupported("kwargs")
+            name = self._callable(node.func)
+            args = [self._expr(a, env) for a in node.args]
+            return self._call(name, args)
+        raise _Unsupported(type(node).__name__)
+
+    def _callable(self, fnode) -> str:
+        if isinstance(fnode, ast.Name):
+            obj = self.globals.get(fnode.id, getattr(builtins, fnode.id, None))
+            for nm in ("int", "float", "abs", "bool", "min", "max"):
+                if obj is getattr(builtins, nm):
+                    return nm
+            if obj is math.fabs or obj is np.abs or obj is np.absolute:
+                return "abs"
+            if obj is math.sqrt or obj is np.sqrt:
+                return "sqrt"
+            raise _Unsupported(f"call {fnode.id}")
+        if isinstance(fnode, ast.Attribute) and isinstance(fnode.value, ast.Name):
+            mod = self.globals.get(fnode.value.id)
+            if mod is np and fnode.attr in ("abs", "absolute", "fabs"):
+                return "abs"
+            if mod is np and fnode.attr in ("sqrt", "minimum", "maximum"):
+                return {"minimum": "min", "maximum": "max"}.get(fnode.attr, fnode.attr)
+            if mod is math and fnode.attr in ("fabs", "sqrt"):
+                return "abs" if fnode.attr == "fabs" else "sqrt"
+        raise _Unsupported("callable")
+
+    def _call(self, name, args):
+        b = self.b
+        if any(isinstance(a, tuple) for a in args):
+            raise _Unsupported("tuple argument")
+        if args and all(isinstance(a, Weak) for a in args):
+            # calls on Python constants: numpy makes int()/float()/bool() results strong
+            # 0-d arrays of the default dtype, abs/min/max stay Python scalars
+            vs = [a.v for a in args]
+            if name == "int":
+                return b.const(int(vs[0]), pa.int64())
+            if name == "float":
+                return b.const(float(vs[0]), pa.float64())
+            if name == "bool":
+                return b.const(bool(vs[0]), pa.bool_())
+            if name == "abs":
+                return Weak(abs(vs[0]))
+            if name in ("min", "max") and len(vs) >= 2:
+                return Weak(min(vs) if name == "min" else max(vs))
+            raise _Unsupported("constant call")
+        args = [self._strong(a, next((x for x in args if isinstance(x, Val)), None)) for a in args]
+        if name == "int":
+            (v,) = args
+            if v.ct in (T_F32, T_F64):
+                v = b.un(U_TRUNC, v)
+            return b.cast(v, T_I64)
+        if name == "float":
+            (v,) = args
+            return b.cast(v, T_F64)
+        if name == "bool":
+            (v,) = args
+            return b.cast(v, T_BOOL)
+        if name == "abs":
+            (v,) = args
+            if v.ct == T_BOOL:
+                raise _Unsupported("abs bool")
+            return b.un(U_ABS, v)
+        if name == "sqrt":
+            (v,) = args
+            ct = v.ct if v.ct in (T_F32, T_F64) else T_F64
+            if v.ct == T_BOOL:
+                raise _Unsupported("sqrt bool")
+            return b.un(U_SQRT, b.cast(v, ct))
+        if name in ("min", "max"):
+            if len(args) < 2:
+                raise _Unsupported("min/max arity")
+            out = args[0]
+            for y in args[1:]:
+                ct = _np_promote(out, y)
+                xv = b.cast(self._strong(out, y if isinstance(y, Val) else None), ct)
+                yv = b.cast(self._strong(y, out if isinstance(out, Val) else None), ct)
+                out = b.bin(B_MIN if name == "min" else B_MAX, xv, yv, ct)
+            return out
+        raise _Unsupported(name)
+
+
+# ------------------------------------------------------------------------------------------
+# finished program: register allocation + native call
+# ------------------------------------------------------------------------------------------
+class Program:
+    def __init__(self, b: _Builder, cols):
+        self.inputs = b.inputs
+        self.schema = b.schema
+        self.has_filter = any(c[0] == OP_FILTER for c in b.code)
+        # outputs: final VM columns, then UDF taps (result, args) for verification; a value is
+        # exported once however many columns/taps use it, constant arguments are not exported
+        outs: List[Val] = []
+        index: Dict[tuple, int] = {}
+
+        def export(v: Val) -> int:
+            k = (v.id, v.atype)
+            if k not in index:
+                index[k] = len(outs)
+                outs.append(v)
+            return index[k]
+        self.columns = []  # (name, ("vm", out_index) | ("in", input column index))
+        for name, ref in cols:
+            if ref[0] == "val":
+                self.columns.append((name, ("vm", export(ref[1]))))
+            else:
+                self.columns.append((name, ref))
+        self.taps = []
+        for u, res, args in b.taps:
+            self.taps.append((u, export(res), [("k", a.const) if a.const is not None else ("o", export(a))
+                                               for a in args]))
+        self.out_types = [v.atype for v in outs]
+        self.out_ct = [v.ct for v in outs]
+        self._allocate(b, outs)
+        self.fconst = np.asarray(b.fconst + [0.0], dtype=np.float64)
+        self.iconst = np.asarray(b.iconst + [0], dtype=np.int64)
+        self.verified = [False] * len(self.taps)
+        self._lock = threading.Lock()
+
+    def _allocate(self, b: _Builder, outs: List[Val]):
+        """Linear-scan register allocation over the SSA program; FILTERs get their live sets."""
+        code = [list(c) for c in b.code]
+        n = len(code)
+        last = {}
+        first = {}
+        for k, ins in enumerate(code):
+            for s in (ins[2], ins[3], ins[4]):
+                if s >= 0:
+                    last[s] = k
+            if ins[1] >= 0 and ins[1] not in first:
+                first[ins[1]] = k
+        for v in outs:
+            last[v.id] = n
+        vtype = {}
+        for ins in code:
+            if ins[1] >= 0:
+                op = ins[0]
+                vtype[ins[1]] = T_BOOL if op in (OP_CMP, OP_AND, OP_OR, OP_ISNULL) or \
+                    (op == OP_UN and ins[6] == U_ISNAN) else (T_I32 if op == OP_DT else ins[5])
+        phys = {}
+        free: List[int] = []
+        nslots = 0
+        live_lists: List[int] = []
+        for k, ins in enumerate(code):
+            if ins[0] == OP_FILTER:
+                live = sorted({s for s in phys if first.get(s, -1) < k and last.get(s, -1) > k})
+                ins[7] = len(live_lists)
+                live_lists.append(len(live))
+                for s in live:
+                    live_lists += [phys[s], vtype[s]]
+            srcs = [s for s in (ins[2], ins[3], ins[4]) if s >= 0]
+            mapped = [phys[s] for s in srcs]
+            # the destination never shares a register with this instruction's own operands
+            # (widening casts / selects would overwrite rows not yet read): sources are
+            # released only after the destination has been placed
+            dying = [s for s in set(srcs) if last.get(s) == k]
+            d = ins[1]
+            if d >= 0:
+                if d in phys:
+                    pd = phys[d]
+                elif free:
+                    pd = free.pop()
+                    phys[d] = pd
+                else:
+                    pd = nslots
+                    nslots += 1
+                    phys[d] = pd
+                if last.get(d) is None:
+                    # dead value (never read): release right away
+                    free.append(phys.pop(d))
+                ins[1] = pd
+            for s in dying:
+                free.append(phys.pop(s))
+            it = iter(mapped)
+            for j in (2, 3, 4):
+                if ins[j] >= 0:
+                    ins[j] = next(it)
+        self.code = np.asarray(code, dtype=np.int32).reshape(-1, 8) if code else np.zeros((0, 8), np.int32)
+        self.live = np.asarray(live_lists + [0], dtype=np.int32)
+        self.out_slots = np.asarray([phys[v.id] for v in outs], dtype=np.int32)
+        self.nslots = max(1, nslots)
+
+    # -- execution ------------------------------------------------------------------------
+    def run(self, t: pa.Table):
+        """Returns the output table, or None when this partition must take the Arrow path."""
+        n = t.num_rows
+        arrays = []
+        for key in self.inputs:
+            if key[0] == "col":
+                a = t.column(key[1])
+                exp_t = self.schema.field(key[1]).type
+            elif key[0] == "ts":
+                a = C.to_timestamp(t.column(key[1]))
+                exp_t = pa.timestamp("s")
+            else:
+                a = C.as_array(key[1].eval(t), n)
+                exp_t = key[2]
+            a = C.as_array(a, n)
+            if a.type != exp_t:
+                return None
+            arrays.append(a)
+        nin = max(1, len(arrays))
+        in_vals = (ctypes.c_void_p * nin)()
+        in_valid = (ctypes.c_void_p * nin)()
+        in_off = (ctypes.c_int64 * nin)()
+        for j, a in enumerate(arrays):
+            bufs = a.buffers()
+            in_valid[j] = bufs[0].address if (bufs[0] is not None and a.null_count) else None
+            in_vals[j] = bufs[1].address if bufs[1] is not None else None
+            in_off[j] = a.offset
+        nout = len(self.out_ct)
+        nbits = (n + 7) // 8
+        out_bufs, valid_bufs = [], []
+        o_vals = (ctypes.c_void_p * max(1, nout))()
+        o_valid = (ctypes.c_void_p * max(1, nout))()
+        for j, ct in enumerate(self.out_ct):
+            vb = np.empty(nbits if ct == T_BOOL else n * _ELEM[ct] + 8, dtype=np.uint8)
+            mb = np.empty(nbits + 1, dtype=np.uint8)
+            out_bufs.append(vb)
+            valid_bufs.append(mb)
+            o_vals[j] = vb.ctypes.data
+            o_valid[j] = mb.ctypes.data
+        nulls = np.zeros(max(1, nout), dtype=np.int64)
+        sel = np.empty(max(1, n), dtype=np.int32) if self.has_filter else None
+        lib = _lib()
+        m = lib.rx_expr_run(self.code.ctypes.data, len(self.code), self.fconst.ctypes.data,
+                            self.iconst.ctypes.data, self.live.ctypes.data, self.nslots, n,
+                            in_vals, in_valid, in_off, self.out_slots.ctypes.data,
+                            np.asarray(self.out_ct, dtype=np.int32).ctypes.data, o_vals, o_valid,
+                            nulls.ctypes.data, nout, None if sel is None else sel.ctypes.data)
+        if m < 0:
+            raise RuntimeError("expression VM rejected the program")
+        outs = []
+        for j, ct in enumerate(self.out_ct):
+            typ = self.out_types[j]
+            validity = pa.py_buffer(valid_bufs[j]) if nulls[j] else None
+            outs.append(pa.Array.from_buffers(typ, m, [validity, pa.py_buffer(out_bufs[j])],
+                                              null_count=int(nulls[j])))
+        # UDF call sites: null arguments -> Spark's per-row None semantics (Arrow path);
+        # otherwise check the Python function on a sample of rows
+        views = {}
+
+        def view(j):
+            v = views.get(j)
+            if v is None:
+                ct = self.out_ct[j]
+                v = outs[j].to_numpy(zero_copy_only=False) if ct == T_BOOL else \
+                    out_bufs[j][:m * _ELEM[ct]].view(_NP[ct])
+                views[j] = v
+            return v
+        for k, (u, r, argix) in enumerate(self.taps):
+            if any(a[0] == "o" and outs[a[1]].null_count for a in argix):
+                return None
+            args = [view(a[1]) if a[0] == "o" else a[1] for a in argix]
+            if not self._verify(k, u, view(r), args, m):
+                _retire(u)
+                raise _Retry()
+        cols, names = [], []
+        pass_idx = [ref[1] for _, ref in self.columns if ref[0] == "in"]
+        passed = {}
+        if pass_idx:
+            if self.has_filter:
+                sub = t.select(pass_idx).take(pa.array(sel[:m]))
+                for j, ix in enumerate(pass_idx):
+                    passed[ix] = sub.column(j)
+            else:
+                for ix in pass_idx:
+                    passed[ix] = t.column(ix)
+        for name, ref in self.columns:
+            cols.append(outs[ref[1]] if ref[0] == "vm" else passed[ref[1]])
+            names.append(name)
+        return pa.Table.from_arrays(cols, names=names)
+
+    def _verify(self, k, u, res: np.ndarray, args: list, m: int) -> bool:
+        """Python function vs VM result on spread rows plus every argument's extreme rows."""
+        if m == 0:
+            return True
+        cnt = min(m, _VERIFY_FIRST if not self.verified[k] else _VERIFY_LATER)
+        idx = {(j * (m - 1)) // max(1, cnt - 1) for j in range(cnt)}
+        arrs = [a for a in args if isinstance(a, np.ndarray)]
+        for a in arrs:
+            if a.dtype.kind in "biuf":
+                idx.add(_argmin(a))
+                idx.add(_argmax(a))
+        f = u.func
+        floating = res.dtype.kind == "f"
+        cast = res.dtype.type
+        try:
+            for i in sorted(idx):
+                want = cast(f(*[a[i].item() if isinstance(a, np.ndarray) else a for a in args]))
+                got = res[i]
+                if floating:
+                    if not (got == want or (got != got and want != want) or
+                            abs(float(got) - float(want)) <= 1e-9 + 1e-6 * abs(float(want))):
+                        return False
+                elif got != want:
+                    return False
+        except Exception:  # noqa: BLE001 - the function fails on these rows: Arrow path decides
+            return False
+        self.verified[k] = True
+        return True
+
+
+def _argmin(a):
+    i = int(a.argmin())
+    if a.dtype.kind == "f" and a[i] != a[i]:  # argmin stops at the first NaN
+        return int(np.nanargmin(a)) if not np.isnan(a).all() else i
+    return i
+
+
+def _argmax(a):
+    i = int(a.argmax())
+    if a.dtype.kind == "f" and a[i] != a[i]:
+        return int(np.nanargmax(a)) if not np.isnan(a).all() else i
+    return i
+
+
+class _Retry(Exception):
+    pass
+
+
+def _retire(u):
+    STATS["udf_retired"] += 1
+    k = _udf_key(u)
+    if k is not None:
+        _RETIRED.add(k)
+    try:
+        u._vec_state = "failed"
+    except AttributeError:
+        pass
+    with _cache_lock:
+        _cache.clear()
+
+
+_lib_handle = None
+
+
+def _lib():
+    global _lib_handle
+    if _lib_handle is None:
+        from raydp_amd.native import loader
+        lib = loader.load("exec_kernels")
+        lib.rx_expr_run.restype = ctypes.c_int64
+        lib.rx_expr_run.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+        _lib_handle = lib
+    return _lib_handle
+
+
+# ------------------------------------------------------------------------------------------
+# chains, caching and the MapPlan hook
+# ------------------------------------------------------------------------------------------
+def enabled() -> bool:
+    return os.environ.get("RAYDP_FUSED_ETL", "1") != "0"
+
+
+def _skey(e) -> Optional[tuple]:
+    """Structural key of an expression, or None when it holds state a key cannot capture."""
+    if isinstance(e, C.ColRef):
+        return ("c", e.col_name)
+    if isinstance(e, C.Lit):
+        v = e.value
+        s = v if isinstance(v, pa.Scalar) else pa.scalar(v)
+        return ("l", str(s.type), repr(s.as_py()))
+    if isinstance(e, C.Alias):
+        k = _skey(e.child)
+        return None if k is None else ("a", e.alias, k)
+    if isinstance(e, C.BinOp):
+        a, b = _skey(e.left), _skey(e.right)
+        return None if a is None or b is None else ("b", e.op, a, b)
+    if isinstance(e, C.UnaryOp):
+        a = _skey(e.child)
+        return None if a is None else ("u", e.op, a)
+    if isinstance(e, C.Cast):
+        a = _skey(e.child)
+        return None if a is None else ("x", str(e.to.to_arrow()), a)
+    if isinstance(e, C.Func) and getattr(e, "native", None) is not None:
+        args = [_skey(a) for a in e.args]
+        return None if any(a is None for a in args) else ("f", e.native, tuple(args))
+    if isinstance(e, C.CaseWhen):
+        parts = [(_skey(c), _skey(v)) for c, v in e.branches]
+        o = _skey(e.otherwise) if e.otherwise is not None else ("none",)
+        if o is None or any(a is None or b is None for a, b in parts):
+            return None
+        return ("w", tuple(parts), o)
+    if isinstance(e, C.UDFExpr):
+        uk = _udf_key(e.udf)
+        args = [_skey(a) for a in e.args]
+        return None if uk is None or any(a is None for a in args) else ("udf", uk, tuple(args))
+    return None
+
+
+def _rel_key(rel):
+    kind = rel[0]
+    if kind == "with":
+        k = _skey(rel[2])
+        return None if k is None else ("with", rel[1], k)
+    if kind == "filter":
+        ks = [_skey(p) for p in rel[1]]
+        return None if any(k is None for k in ks) else ("filter", tuple(ks))
+    if kind == "drop":
+        return ("drop", tuple(sorted(rel[1])))
+    if kind == "project":
+        ks = [(_skey(e), n) for e, n in rel[1]]
+        return None if any(k[0] is None for k in ks) else ("project", tuple(ks))
+    return None
+
+
+_cache: Dict[tuple, list] = {}
+_cache_lock = threading.Lock()
+
+
+def _compile_chain(nodes, base_schema: pa.Schema):
+    """Segments: ("vm", Program, first, last) or ("host", node_index). None = no fusion."""
+    STATS["compiles"] += 1
+    segs = []
+    k = 0
+    schema = base_schema
+    while k < len(nodes):
+        cc = _ChainCompiler(schema)
+        j = k
+        while j < len(nodes):
+            try:
+                cc.op(nodes[j].rel)
+            except _Unsupported:
+                break
+            j += 1
+        if j > k:
+            prog = cc.finish()
+            out_schema = pa.schema([pa.field(nm, prog.out_types[ref[1]] if ref[0] == "vm"
+                                             else schema.field(ref[1]).type)
+                                    for nm, ref in prog.columns])
+            want = nodes[j - 1].schema
+            if out_schema.names != want.names or out_schema.types != want.types:
+                return None
+            segs.append(("vm", prog))
+            schema = want
+            k = j
+        else:
+            segs.append(("host", k))
+            schema = nodes[k].schema
+            k += 1
+    if not any(s[0] == "vm" for s in segs):
+        return None
+    return segs
+
+
+def chain_of(top):
+    from raydp_amd.spark.plan import MapPlan
+    nodes = []
+    p = top
+    while isinstance(p, MapPlan) and getattr(p, "rel", None) is not None:
+        nodes.append(p)
+        p = p.child
+    nodes.reverse()
+    return nodes, p
+
+
+def _node_key(n):
+    k = n.__dict__.get("_rkey", False)
+    if k is False:
+        k = _rel_key(n.rel)
+        n.__dict__["_rkey"] = k
+    return k
+
+
+def segments_for(top, nodes, base):
+    keys = [_node_key(n) for n in nodes]
+    base_schema = base.schema
+    if all(k is not None for k in keys):
+        key = (tuple(keys), base_schema)
+        with _cache_lock:
+            hit = _cache.get(key, False)
+        if hit is not False:
+            return hit
+        segs = _compile_chain(nodes, base_schema)
+        with _cache_lock:
+            _cache[key] = segs
+        return segs
+    segs = top.__dict__.get("_fused_segs", False)
+    if segs is False:
+        segs = _compile_chain(nodes, base_schema)
+        top.__dict__["_fused_segs"] = segs
+    return segs
+
+
+def compute_fused(top, i):
+    """MapPlan.compute for the top of a chain of narrow operators."""
+    from raydp_amd.spark.plan import _PartitionScope
+    nodes, base = chain_of(top)
+    for _ in range(8):
+        segs = segments_for(top, nodes, base)
+        if segs is None:
+            return _per_operator(nodes, base, i)
+        t = base.compute(i)
+        try:
+            with _PartitionScope(i):
+                for s in segs:
+                    if s[0] == "host":
+                        t = nodes[s[1]].fn(t, i)
+                        continue
+                    out = s[1].run(t)
+                    if out is None:
+                        STATS["fallback_partitions"] += 1
+                        return _per_operator(nodes, base, i)
+                    t = out
+        except _Retry:
+            top.__dict__.pop("_fused_segs", None)
+            continue
+        STATS["fused_partitions"] += 1
+        return t
+    return _per_operator(nodes, base, i)
+
+
+def _per_operator(nodes, base, i):
+    from raydp_amd.spark.plan import _PartitionScope
+    t = base.compute(i)
+    with _PartitionScope(i):
+        for n in nodes:
+            t = n.fn(t, i)
+    return t

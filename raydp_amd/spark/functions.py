@@ -40,20 +40,22 @@ def expr(s: str) -> Column:
     return parse(s)
 
 
-def _fn(name, cols, impl, display=None):
-    return Column(Func(name, [_to_expr(c, name_is_col=True) for c in cols], impl, display))
+def _fn(name, cols, impl, display=None, native=None):
+    e = Func(name, [_to_expr(c, name_is_col=True) for c in cols], impl, display)
+    e.native = native  # opcode tag for the fused expression VM (spark/exprc.py), None = host only
+    return Column(e)
 
 
-def _unary(name, f):
+def _unary(name, f, native=None):
     def builder(c):
-        return _fn(name, [c], lambda a, b: f(a[0]))
+        return _fn(name, [c], lambda a, b: f(a[0]), native=native)
     builder.__name__ = name
     return builder
 
 
 # ---------------------------------------------------------------------------- math ---------
-abs = _unary("abs", pc.abs)  # noqa: A001 - Spark name
-sqrt = _unary("SQRT", lambda v: pc.sqrt(_to_double(v)))
+abs = _unary("abs", pc.abs, native=("abs",))  # noqa: A001 - Spark name
+sqrt = _unary("SQRT", lambda v: pc.sqrt(_to_double(v)), native=("sqrt",))
 exp = _unary("EXP", lambda v: pc.exp(_to_double(v)))
 floor = _unary("FLOOR", lambda v: pc.cast(pc.floor(_to_double(v)), pa.int64()))
 ceil = _unary("CEIL", lambda v: pc.cast(pc.ceil(_to_double(v)), pa.int64()))
@@ -64,7 +66,7 @@ signum = _unary("SIGNUM", lambda v: pc.cast(pc.sign(_to_double(v)), pa.float64()
 log10 = _unary("LOG10", lambda v: _nan_to_null(pc.log10(_to_double(v))))
 log2 = _unary("LOG2", lambda v: _nan_to_null(pc.log2(_to_double(v))))
 log1p = _unary("LOG1P", lambda v: _nan_to_null(pc.log1p(_to_double(v))))
-isnan = _unary("isnan", lambda v: pc.is_nan(_to_double(v)))
+isnan = _unary("isnan", lambda v: pc.is_nan(_to_double(v)), native=("isnan",))
 isnull = _unary("isnull", pc.is_null)
 
 
@@ -154,7 +156,7 @@ def _dt(name, f):
     def builder(c):
         return _fn(name, [c], lambda a, b: pc.cast(f(_to_ts(
             a[0] if not isinstance(a[0], pa.Scalar) else as_array(a[0], b.num_rows))),
-                                                   pa.int32()))
+                                                   pa.int32()), native=("dt", name))
     builder.__name__ = name
     return builder
 

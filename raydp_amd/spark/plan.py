@@ -165,10 +165,22 @@ class MapPlan(Plan):
     def num_partitions(self):
         return self.child.num_partitions()
 
+    rel = None  # relational description (spark/exprc.py) when the operator is fusible
+
     def compute(self, i):
+        if self.rel is not None:
+            from raydp_amd.spark import exprc
+            if exprc.enabled():
+                # the whole chain of fusible operators below runs as one native program
+                return exprc.compute_fused(self, i)
         t = self.child.compute(i)
         with _PartitionScope(i):
             return self.fn(t, i)
+
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st.pop("_fused_segs", None)  # compiled programs are per process
+        return st
 
     def empty(self):
         with _PartitionScope(0):
