@@ -33,6 +33,7 @@ sys.path.insert(0, os.path.join(HERE, "examples"))
 BASELINE_SAMPLES_PER_S = None
 BATCH = 64
 REFERENCE_CSV = os.path.join(HERE, "examples", "data", "fake_nyctaxi.csv")
+DRIVER_TIMINGS = {}   # driver-side phases of the last run_pipeline (inside the timed region)
 
 
 def make_csv(path: str, n: int, seed: int):
@@ -93,13 +94,17 @@ def run_pipeline(spark, csv_path, steps, world, storage, fused=True):
     import torch.nn as nn
     from data_process import nyc_taxi_preprocess
     from raydp_amd.torch import TorchEstimator
+    t0 = time.perf_counter()
     data = spark.read.format("csv").option("header", "true").option("inferSchema", "true") \
         .load("file://" + csv_path)
+    t1 = time.perf_counter()
     data = nyc_taxi_preprocess(data)
     features = [f.name for f in data.schema if f.name != "fare_amount"]
+    t2 = time.perf_counter()
     torch.manual_seed(0)
     model = nyc_model(len(features))
     opt = torch.optim.Adam(model.parameters(), lr=0.001)
+    DRIVER_TIMINGS.update(csv_schema=t1 - t0, plan_build=t2 - t1, model_init=time.perf_counter() - t2)
     est = TorchEstimator(num_workers=world, model=model, optimizer=opt, loss=nn.SmoothL1Loss(),
                          feature_columns=features, feature_types=torch.float,
                          label_column="fare_amount", label_type=torch.float, batch_size=BATCH,
@@ -197,9 +202,11 @@ def main():
     gc.collect()
     gc.freeze()
     barrier()
+    from raydp_amd.utils import tracing
     t0 = time.perf_counter()
-    res = run_pipeline(spark, main_csv, args.steps, world, storage, fused=not args.no_fused)
-    barrier()
+    with tracing.span("timed run", cat="bench"):
+        res = run_pipeline(spark, main_csv, args.steps, world, storage, fused=not args.no_fused)
+        barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -232,7 +239,9 @@ def main():
                        "final_train_loss": res.metrics_history[0].get("train_loss")
                        if res.metrics_history else None,
                        "rank0_breakdown_s": dict({k: round(v, 4) for k, v in LAST_TIMINGS.items()},
-                                                 other=round(dt - sum(LAST_TIMINGS.values()), 4))},
+                                                 **{k: round(v, 4) for k, v in DRIVER_TIMINGS.items()},
+                                                 other=round(dt - sum(LAST_TIMINGS.values())
+                                                             - sum(DRIVER_TIMINGS.values()), 4))},
         }
         if world == 1 and not args.no_reference_config:
             # the reference example's own config (untimed by the driver; reported alongside)

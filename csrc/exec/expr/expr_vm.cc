@@ -182,38 +182,129 @@ inline int64_t days_from_civil(int64_t y, int m, int d) {
   return era * 146097 + doe - 719468;
 }
 
-inline int32_t dt_field(int64_t secs, int field) {
-  const int64_t days = floor_div(secs, 86400);
-  const int64_t sod = secs - days * 86400;
-  switch (field) {
-    case D_HOUR: return int32_t(sod / 3600);
-    case D_MINUTE: return int32_t((sod / 60) % 60);
-    case D_SECOND: return int32_t(sod % 60);
-    case D_DOW_SPARK: {  // 1 = Sunday .. 7 = Saturday; 1970-01-01 was a Thursday
-      int64_t w = (days + 4) % 7;
-      if (w < 0) w += 7;
-      return int32_t(w + 1);
-    }
-    case D_ISOWEEK: {
-      int64_t wd = (days + 3) % 7;  // Monday = 0
-      if (wd < 0) wd += 7;
-      const int64_t thu = days - wd + 3;
-      int64_t y; int m, d;
-      civil(thu, &y, &m, &d);
-      return int32_t((thu - days_from_civil(y, 1, 1)) / 7 + 1);
-    }
-    default: break;
-  }
+// Neri & Schneider, "Euclidean affine functions and their application to calendar
+// algorithms" (2022): civil date from a day count with 32-bit multiply/shift only. Valid for
+// |days| < 2^29 (about +-1.4 million years); wider values take the 64-bit routine above.
+struct Civil { int32_t y; int32_t m; int32_t d; int32_t doy; };
+inline Civil civil32(int32_t days) {
+  constexpr uint32_t s = 82, K = 719468 + 146097 * s, L = 400 * s;
+  const uint32_t N = uint32_t(days) + K;
+  const uint32_t N1 = 4 * N + 3;
+  const uint32_t C = N1 / 146097;
+  const uint32_t NC = N1 % 146097 / 4;
+  const uint32_t N2 = 4 * NC + 3;
+  const uint64_t P2 = uint64_t(2939745) * N2;
+  const uint32_t Z = uint32_t(P2 >> 32);
+  const uint32_t NY = uint32_t(P2) / 2939745 / 4;  // day of the March-based year
+  const uint32_t Y = 100 * C + Z;
+  const uint32_t N3 = 2141 * NY + 197913;
+  const uint32_t M = N3 >> 16;
+  const uint32_t D = (N3 & 65535) / 2141;
+  const uint32_t J = NY >= 306;                     // January or February
+  Civil c;
+  c.y = int32_t(Y - L + J);
+  c.m = int32_t(J ? M - 12 : M);
+  c.d = int32_t(D + 1);
+  const int32_t leap = (c.y % 4 == 0) & ((c.y % 100 != 0) | (c.y % 400 == 0));
+  c.doy = J ? int32_t(NY) - 305 : int32_t(NY) + 60 + leap;
+  return c;
+}
+
+inline Civil civil_any(int64_t days) {
+  if (days > -(int64_t(1) << 29) && days < (int64_t(1) << 29)) return civil32(int32_t(days));
   int64_t y; int m, d;
   civil(days, &y, &m, &d);
-  switch (field) {
-    case D_YEAR: return int32_t(y);
-    case D_MONTH: return m;
-    case D_DAY: return d;
-    case D_QUARTER: return (m - 1) / 3 + 1;
-    case D_DOY: return int32_t(days - days_from_civil(y, 1, 1) + 1);
-    default: return 0;
+  return Civil{int32_t(y), m, d, int32_t(days - days_from_civil(y, 1, 1) + 1)};
+}
+
+template <int F> inline int32_t dt_field(int64_t secs) {
+  const int64_t days = floor_div(secs, 86400);
+  const int64_t sod = secs - days * 86400;
+  if constexpr (F == D_HOUR) return int32_t(sod / 3600);
+  if constexpr (F == D_MINUTE) return int32_t((sod / 60) % 60);
+  if constexpr (F == D_SECOND) return int32_t(sod % 60);
+  if constexpr (F == D_DOW_SPARK) {  // 1 = Sunday .. 7 = Saturday; 1970-01-01 was a Thursday
+    int64_t w = (days + 4) % 7;
+    if (w < 0) w += 7;
+    return int32_t(w + 1);
   }
+  if constexpr (F == D_ISOWEEK) {    // ISO-8601: the week belongs to the year of its Thursday
+    int64_t wd = (days + 3) % 7;     // Monday = 0
+    if (wd < 0) wd += 7;
+    return (civil_any(days - wd + 3).doy - 1) / 7 + 1;
+  }
+  const Civil c = civil_any(days);
+  if constexpr (F == D_YEAR) return c.y;
+  if constexpr (F == D_MONTH) return c.m;
+  if constexpr (F == D_DAY) return c.d;
+  if constexpr (F == D_QUARTER) return (c.m - 1) / 3 + 1;
+  if constexpr (F == D_DOY) return c.doy;
+  return 0;
+}
+
+template <int F> void run_dt_field(const int64_t* a, int32_t* o, int n, int64_t ups) {
+  if (ups == 1) {
+    for (int i = 0; i < n; ++i) o[i] = dt_field<F>(a[i]);
+  } else {
+    for (int i = 0; i < n; ++i) o[i] = dt_field<F>(floor_div(a[i], ups));
+  }
+}
+
+void run_dt(const int64_t* a, int32_t* o, int n, int64_t ups, int field) {
+  switch (field) {
+    case D_YEAR: run_dt_field<D_YEAR>(a, o, n, ups); break;
+    case D_MONTH: run_dt_field<D_MONTH>(a, o, n, ups); break;
+    case D_DAY: run_dt_field<D_DAY>(a, o, n, ups); break;
+    case D_HOUR: run_dt_field<D_HOUR>(a, o, n, ups); break;
+    case D_MINUTE: run_dt_field<D_MINUTE>(a, o, n, ups); break;
+    case D_SECOND: run_dt_field<D_SECOND>(a, o, n, ups); break;
+    case D_DOW_SPARK: run_dt_field<D_DOW_SPARK>(a, o, n, ups); break;
+    case D_ISOWEEK: run_dt_field<D_ISOWEEK>(a, o, n, ups); break;
+    case D_QUARTER: run_dt_field<D_QUARTER>(a, o, n, ups); break;
+    case D_DOY: run_dt_field<D_DOY>(a, o, n, ups); break;
+    default: for (int i = 0; i < n; ++i) o[i] = 0; break;
+  }
+}
+
+// Sets bits [pos, pos + n) of a bitmap (whole bytes at a time where aligned).
+inline void set_bits(uint8_t* bm, int64_t pos, int64_t n) {
+  while (n > 0 && (pos & 7)) {
+    bm[pos >> 3] |= uint8_t(1u << (pos & 7));
+    ++pos;
+    --n;
+  }
+  if (n >= 8) {
+    std::memset(bm + (pos >> 3), 0xff, size_t(n >> 3));
+    pos += n & ~int64_t(7);
+    n &= 7;
+  }
+  while (n > 0) {
+    bm[pos >> 3] |= uint8_t(1u << (pos & 7));
+    ++pos;
+    --n;
+  }
+}
+
+// Packs n byte flags (0/1) into a bitmap at bit position pos; returns the number of zeros.
+inline int64_t pack_bits(uint8_t* bm, int64_t pos, const uint8_t* flags, int n) {
+  int64_t zeros = 0;
+  int i = 0;
+  while (i < n && ((pos + i) & 7)) {
+    if (flags[i]) bm[(pos + i) >> 3] |= uint8_t(1u << ((pos + i) & 7));
+    else ++zeros;
+    ++i;
+  }
+  for (; i + 8 <= n; i += 8) {
+    uint8_t b = 0;
+    for (int k = 0; k < 8; ++k) b |= uint8_t((flags[i + k] & 1) << k);
+    bm[(pos + i) >> 3] = b;
+    zeros += 8 - __builtin_popcount(b);
+  }
+  for (; i < n; ++i) {
+    if (flags[i]) bm[(pos + i) >> 3] |= uint8_t(1u << ((pos + i) & 7));
+    else ++zeros;
+  }
+  return zeros;
 }
 
 // --------------------------------------------------------------- typed dispatch -----------
@@ -518,14 +609,10 @@ int64_t rx_expr_run(const int32_t* code, int32_t ncode, const double* fconst, co
           }
           break;
         }
-        case OP_DT: {
-          const int64_t* a = R.p<int64_t>(I.a);
-          int32_t* o = R.p<int32_t>(I.dst);
-          const int64_t ups = I.imm > 0 ? I.imm : 1;
-          for (int i = 0; i < n; ++i) o[i] = dt_field(ups == 1 ? a[i] : floor_div(a[i], ups), I.aux);
+        case OP_DT:
+          run_dt(R.p<int64_t>(I.a), R.p<int32_t>(I.dst), n, I.imm > 0 ? I.imm : 1, I.aux);
           and_valid(R, I.dst, I.a, -1, n);
           break;
-        }
         case OP_ISNULL: {
           uint8_t* o = R.p<uint8_t>(I.dst);
           const bool va = R.allvalid[I.a];
@@ -598,27 +685,15 @@ int64_t rx_expr_run(const int32_t* code, int32_t ncode, const double* fconst, co
     for (int o = 0; o < nout; ++o) {
       const int s = out_slot[o], ty = out_type[o];
       if (ty == T_BOOL) {
-        uint8_t* bits = static_cast<uint8_t*>(out_vals[o]);
-        const uint8_t* d = R.p<uint8_t>(s);
-        for (int i = 0; i < n; ++i)
-          if (d[i]) bits[(pos + i) >> 3] |= uint8_t(1u << ((pos + i) & 7));
+        pack_bits(static_cast<uint8_t*>(out_vals[o]), pos, R.p<uint8_t>(s), n);
       } else {
         std::memcpy(static_cast<uint8_t*>(out_vals[o]) + size_t(pos) * elem_size(ty),
                     R.p<uint8_t>(s), size_t(n) * elem_size(ty));
       }
       uint8_t* vb = out_valid[o];
       if (vb == nullptr) continue;
-      if (R.allvalid[s]) {
-        for (int i = 0; i < n; ++i) vb[(pos + i) >> 3] |= uint8_t(1u << ((pos + i) & 7));
-      } else {
-        const uint8_t* v = R.v(s);
-        int64_t nulls = 0;
-        for (int i = 0; i < n; ++i) {
-          if (v[i]) vb[(pos + i) >> 3] |= uint8_t(1u << ((pos + i) & 7));
-          else ++nulls;
-        }
-        out_nulls[o] += nulls;
-      }
+      if (R.allvalid[s]) set_bits(vb, pos, n);
+      else out_nulls[o] += pack_bits(vb, pos, R.v(s), n);
     }
     if (sel_out != nullptr) std::memcpy(sel_out + pos, rowid.data(), sizeof(int32_t) * size_t(n));
     pos += n;

@@ -126,7 +126,8 @@ class ExecutorTaskScheduler(P.TaskScheduler):
     def persist(self, fn, rdd_id: str, indices) -> List[tuple]:
         indices = list(indices)
         from raydp_amd.utils import tracing
-        payload, key = self._stage_payload(fn)
+        with tracing.span("stage payload", cat="etl"):
+            payload, key = self._stage_payload(fn)
         out = []
         try:
             with tracing.span("persist stage", cat="etl", tasks=len(indices)):

@@ -111,10 +111,11 @@ class RayDPExecutor:
         """Compute ``indices`` and seal them in this node's store; returns
         ``[(index, object_id, node_id, store_path, num_rows)]``."""
         import pyarrow as pa
-        fn = self._fn(payload)
+        from raydp_amd.utils import tracing
+        with tracing.span("stage unpickle", cat="executor"):
+            fn = self._fn(payload)
         st = self._node.store
         out = []
-        from raydp_amd.utils import tracing
         for i in indices:
             with tracing.span("task", cat="executor", partition=i, persist=rdd_id):
                 t = fn(i)
@@ -126,7 +127,8 @@ class RayDPExecutor:
                 old = self._cache.pop((rdd_id, i), None)
             if old is not None or st.contains(oid):
                 st.delete(oid)
-            st.put(oid, t)
+            with tracing.span("store put", cat="executor", rows=t.num_rows):
+                st.put(oid, t)
             with self._lock:
                 self._cache[(rdd_id, i)] = oid
             out.append((i, oid, st.node_id, st.path, t.num_rows))

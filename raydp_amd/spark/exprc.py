@@ -964,12 +964,14 @@ class Program:
         o_vals = (ctypes.c_void_p * max(1, nout))()
         o_valid = (ctypes.c_void_p * max(1, nout))()
         for j, ct in enumerate(self.out_ct):
-            vb = np.empty(nbits if ct == T_BOOL else n * _ELEM[ct] + 8, dtype=np.uint8)
-            mb = np.empty(nbits + 1, dtype=np.uint8)
+            # Arrow's memory pool recycles pages across partitions (fresh numpy buffers of this
+            # size would be new mmaps, page-faulted row by row inside the VM)
+            vb = pa.allocate_buffer(nbits + 1 if ct == T_BOOL else n * _ELEM[ct] + 8)
+            mb = pa.allocate_buffer(nbits + 1)
             out_bufs.append(vb)
             valid_bufs.append(mb)
-            o_vals[j] = vb.ctypes.data
-            o_valid[j] = mb.ctypes.data
+            o_vals[j] = vb.address
+            o_valid[j] = mb.address
         nulls = np.zeros(max(1, nout), dtype=np.int64)
         sel = np.empty(max(1, n), dtype=np.int32) if self.has_filter else None
         lib = _lib()
@@ -983,8 +985,8 @@ class Program:
         outs = []
         for j, ct in enumerate(self.out_ct):
             typ = self.out_types[j]
-            validity = pa.py_buffer(valid_bufs[j]) if nulls[j] else None
-            outs.append(pa.Array.from_buffers(typ, m, [validity, pa.py_buffer(out_bufs[j])],
+            validity = valid_bufs[j] if nulls[j] else None
+            outs.append(pa.Array.from_buffers(typ, m, [validity, out_bufs[j]],
                                               null_count=int(nulls[j])))
         # UDF call sites: null arguments -> Spark's per-row None semantics (Arrow path);
         # otherwise check the Python function on a sample of rows
@@ -995,7 +997,7 @@ class Program:
             if v is None:
                 ct = self.out_ct[j]
                 v = outs[j].to_numpy(zero_copy_only=False) if ct == T_BOOL else \
-                    out_bufs[j][:m * _ELEM[ct]].view(_NP[ct])
+                    np.frombuffer(out_bufs[j], dtype=_NP[ct], count=m)
                 views[j] = v
             return v
         for k, (u, r, argix) in enumerate(self.taps):
@@ -1240,14 +1242,17 @@ def segments_for(top, nodes, base):
 def compute_fused(top, i):
     """MapPlan.compute for the top of a chain of narrow operators."""
     from raydp_amd.spark.plan import _PartitionScope
+    from raydp_amd.utils import tracing
     nodes, base = chain_of(top)
     for _ in range(8):
         segs = segments_for(top, nodes, base)
         if segs is None:
             return _per_operator(nodes, base, i)
-        t = base.compute(i)
+        with tracing.span("chain input", cat="executor"):
+            t = base.compute(i)
         try:
-            with _PartitionScope(i):
+            with _PartitionScope(i), tracing.span("fused chain", cat="executor", ops=len(nodes),
+                                                  rows=t.num_rows):
                 for s in segs:
                     if s[0] == "host":
                         t = nodes[s[1]].fn(t, i)
@@ -1272,3 +1277,111 @@ def _per_operator(nodes, base, i):
         for n in nodes:
             t = n.fn(t, i)
     return t
+
+
+# ------------------------------------------------------------------------------------------
+# static schema inference for plan building
+# ------------------------------------------------------------------------------------------
+def _stype(e, schema: pa.Schema) -> pa.DataType:
+    """Output type of ``e`` over ``schema`` without executing it; raises _Unsupported for any
+    construct whose type is not certain (the caller then executes the operator on an empty
+    table as before)."""
+    if isinstance(e, C.Alias):
+        return _stype(e.child, schema)
+    if isinstance(e, C.ColRef):
+        names = schema.names
+        if e.col_name in names:
+            if names.count(e.col_name) != 1:
+                raise _Unsupported("ambiguous")
+            return schema.field(e.col_name).type
+        low = e.col_name.lower()
+        for f in schema:
+            if f.name.lower() == low:
+                return f.type
+        raise _Unsupported("unresolved")
+    if isinstance(e, C.Lit):
+        v = e.value
+        s = v if isinstance(v, pa.Scalar) else pa.scalar(v)
+        if not s.is_valid:
+            raise _Unsupported("null literal")
+        return s.type
+    if isinstance(e, C.BinOp):
+        a, b = _stype(e.left, schema), _stype(e.right, schema)
+        if e.op in _ARITH:
+            if not (_is_num(a) and _is_num(b)):
+                raise _Unsupported("arith")
+            return _probe(_ARITH[e.op][0], a, b)
+        if e.op == "/":
+            if not all(_is_num(t) or pa.types.is_boolean(t) for t in (a, b)):
+                raise _Unsupported("div")
+            return pa.float64()
+        if e.op in _CMPK or e.op == "<=>":
+            if (_is_num(a) and _is_num(b)) or a == b:
+                return pa.bool_()
+            raise _Unsupported("compare")
+        if e.op in ("&", "|") and a == pa.bool_() and b == pa.bool_():
+            return pa.bool_()
+        raise _Unsupported(e.op)
+    if isinstance(e, C.UnaryOp):
+        t = _stype(e.child, schema)
+        if e.op == "-" and _is_num(t):
+            return t
+        if e.op == "~" and t == pa.bool_():
+            return t
+        if e.op in ("isnull", "isnotnull"):
+            return pa.bool_()
+        if e.op == "isnan" and (_is_num(t) or pa.types.is_boolean(t)):
+            return pa.bool_()
+        raise _Unsupported(e.op)
+    if isinstance(e, C.Func):
+        tag = getattr(e, "native", None)
+        if tag is None or len(e.args) != 1:
+            raise _Unsupported("func")
+        t = _stype(e.args[0], schema)
+        if tag[0] == "dt" and (C._is_str(t) or pa.types.is_timestamp(t) or pa.types.is_date(t)):
+            return pa.int32()
+        if tag[0] == "abs" and _is_num(t):
+            return t
+        if tag[0] == "sqrt" and (_is_num(t) or pa.types.is_boolean(t)):
+            return pa.float64()
+        if tag[0] == "isnan" and (_is_num(t) or pa.types.is_boolean(t)):
+            return pa.bool_()
+        raise _Unsupported(str(tag))
+    if isinstance(e, C.UDFExpr):
+        for a in e.args:
+            _stype(a, schema)
+        return e.udf.returnType.to_arrow()
+    raise _Unsupported(type(e).__name__)
+
+
+def static_schema(node) -> Optional[pa.Schema]:
+    """Output schema of a fusible operator from its child's schema, or None (execute it)."""
+    rel = getattr(node, "rel", None)
+    if rel is None:
+        return None
+    try:
+        cs = node.child.schema
+        kind = rel[0]
+        if kind == "filter":
+            for p in rel[1]:
+                if _stype(p, cs) != pa.bool_():
+                    return None
+            return cs
+        if kind == "drop":
+            return pa.schema([f for f in cs if f.name not in rel[1]])
+        if kind == "with":
+            _, name, e = rel
+            t = _stype(e, cs)
+            fields = list(cs)
+            for j, f in enumerate(fields):
+                if f.name == name:
+                    fields[j] = pa.field(name, t)
+                    break
+            else:
+                fields.append(pa.field(name, t))
+            return pa.schema(fields)
+        if kind == "project":
+            return pa.schema([pa.field(name, _stype(e, cs)) for e, name in rel[1]])
+    except _Unsupported:
+        return None
+    return None

@@ -182,6 +182,16 @@ class MapPlan(Plan):
         st.pop("_fused_segs", None)  # compiled programs are per process
         return st
 
+    @property
+    def schema(self) -> pa.Schema:
+        if self._schema is None and self.rel is not None:
+            # type the operator statically when every expression's type is certain
+            from raydp_amd.spark import exprc
+            self._schema = exprc.static_schema(self)
+        if self._schema is None:
+            self._schema = self.empty().schema
+        return self._schema
+
     def empty(self):
         with _PartitionScope(0):
             return self.fn(self.child.schema.empty_table(), 0)

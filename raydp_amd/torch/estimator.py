@@ -272,12 +272,14 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         with tracing.span("checkpoint", cat="train"):
             states = engine.state_dict()
             states = {k: v.detach().cpu() for k, v in states.items()}
-            with tempfile.TemporaryDirectory() as temp_checkpoint_dir:
-                checkpoint = None
-                if session.get_world_rank() == 0:
-                    torch.save(states, os.path.join(temp_checkpoint_dir, "model.pt"))
-                    checkpoint = Checkpoint.from_directory(temp_checkpoint_dir)
-                session.report({}, checkpoint=checkpoint)
+            checkpoint = None
+            if session.get_world_rank() == 0:
+                # model.pt is written straight into a staging dir of the run's storage and
+                # renamed into place by report()
+                stage = session.staging_dir()
+                torch.save(states, os.path.join(stage, "model.pt"))
+                checkpoint = Checkpoint(stage, movable=True)
+            session.report({}, checkpoint=checkpoint)
         LAST_TIMINGS["checkpoint"] = time.perf_counter() - t_ck0
 
     # ------------------------------------------------------------------------- driver -----

@@ -16,8 +16,11 @@ MODEL_KEY = "model.pt"
 
 
 class Checkpoint:
-    def __init__(self, path: str):
+    def __init__(self, path: str, movable: bool = False):
         self.path = os.path.abspath(path)
+        # a staging directory the framework owns (session.staging_dir): report() renames it
+        # into place instead of copying it
+        self._movable = movable
 
     @classmethod
     def from_directory(cls, path: str) -> "Checkpoint":

@@ -6,6 +6,7 @@ Reference use inside ``TorchEstimator.train_func``: ``session.get_dataset_shard(
 """
 import os
 import shutil
+import tempfile
 import threading
 import time
 from typing import Any, Callable, Dict, Optional
@@ -75,13 +76,25 @@ class _Session:
             except OSError:
                 n = 0
             dst = os.path.join(self.storage_dir, f"checkpoint_{n:06d}")
-            tmp = dst + f".tmp{os.getpid()}"
-            if os.path.exists(tmp):
-                shutil.rmtree(tmp)
-            shutil.copytree(checkpoint.path, tmp)
-            os.replace(tmp, dst)          # a crash mid-copy never leaves a partial checkpoint
+            if getattr(checkpoint, "_movable", False) and \
+                    os.path.dirname(checkpoint.path) == os.path.abspath(self.storage_dir):
+                os.replace(checkpoint.path, dst)   # complete staging dir: one rename
+            else:
+                tmp = dst + f".tmp{os.getpid()}"
+                if os.path.exists(tmp):
+                    shutil.rmtree(tmp)
+                shutil.copytree(checkpoint.path, tmp)
+                os.replace(tmp, dst)          # a crash mid-copy never leaves a partial checkpoint
             persisted = dst
         self.reporter(self.ctx.world_rank, m, persisted)
+
+
+def staging_dir() -> str:
+    """A fresh directory inside the run's storage (same filesystem): a checkpoint written there
+    and reported as ``Checkpoint(path, movable=True)`` is renamed into place, not copied."""
+    s = _get_session()
+    os.makedirs(s.storage_dir, exist_ok=True)
+    return tempfile.mkdtemp(prefix=".stage_", dir=s.storage_dir)
 
 
 def _set_session(s: Optional[_Session]):

@@ -21,7 +21,17 @@ def _collect(df, fused, monkeypatch):
     return pa.concat_tables(parts) if parts else None
 
 
+def _check_static_schemas(df):
+    """Statically inferred operator schemas equal the ones the Arrow path produces."""
+    nodes, _ = exprc.chain_of(df._plan)
+    for n in nodes:
+        st = exprc.static_schema(n)
+        if st is not None:
+            assert st == n.empty().schema, (n.desc, st, n.empty().schema)
+
+
 def _same(df, monkeypatch):
+    _check_static_schemas(df)
     before = dict(exprc.STATS)
     ref = _collect(df, False, monkeypatch)
     got = _collect(df, True, monkeypatch)
