@@ -7,6 +7,7 @@ window functions, randomSplit, repartition, cache/persist, collect/take/count/to
 parquet/csv writers. Every operator builds a ``Plan`` node (``plan.py``/``wide.py``); nothing
 executes until an action.
 """
+import functools
 import json
 import os
 import uuid
@@ -49,6 +50,55 @@ def _names_of(cols):
         else:
             out.append(c)
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# relational narrow operators: module-level appliers bound with functools.partial, so a plan
+# pickles as data (expression trees) instead of one closure code object per operator, and the
+# same ``rel`` tuple drives both this per-operator path and the fused VM (spark/exprc.py)
+# ------------------------------------------------------------------------------------------
+def _apply_with(col_name, e, t: pa.Table, i) -> pa.Table:
+    v = as_array(e.eval(t), t.num_rows)
+    if col_name in t.column_names:
+        return t.set_column(t.column_names.index(col_name), col_name, v)
+    return t.append_column(col_name, v)
+
+
+def _apply_filter(preds, t: pa.Table, i) -> pa.Table:
+    mask = None
+    for e in preds:
+        m = e.eval(t)
+        if isinstance(m, pa.Scalar):
+            if not m.as_py():
+                return t.slice(0, 0)
+            continue
+        mask = m if mask is None else pc.and_kleene(mask, m)
+    if mask is None:
+        return t
+    return t.filter(mask, null_selection_behavior="drop")
+
+
+def _apply_drop(names, t: pa.Table, i) -> pa.Table:
+    return t.drop([c for c in t.column_names if c in names])
+
+
+def _apply_project(exprs, t: pa.Table, i) -> pa.Table:
+    return _eval_projection(t, exprs)
+
+
+def _rel_node(src: "P.Plan", rel: tuple, desc: str) -> "P.MapPlan":
+    kind = rel[0]
+    if kind == "with":
+        fn = functools.partial(_apply_with, rel[1], rel[2])
+    elif kind == "filter":
+        fn = functools.partial(_apply_filter, rel[1])
+    elif kind == "drop":
+        fn = functools.partial(_apply_drop, rel[1])
+    else:
+        fn = functools.partial(_apply_project, rel[1])
+    node = P.MapPlan(src, fn, desc)
+    node.rel = rel
+    return node
 
 
 def _eval_projection(t: pa.Table, exprs) -> pa.Table:
@@ -250,12 +300,11 @@ class DataFrame:
             if e.is_aggregate():
                 return self.agg(*cols)
             exprs.append((e, e.name()))
-        node = P.MapPlan(self._src(), lambda t, i: _eval_projection(t, exprs), "project")
         if not any(isinstance(x, Func) and x.fname in ("__explode__", "__posexplode__") or
                    isinstance(x, Alias) and isinstance(x.child, Func)
                    and x.child.fname in ("__explode__", "__posexplode__") for x, _ in exprs):
-            node.rel = ("project", list(exprs))
-        return self._with(node)
+            return self._with(_rel_node(self._src(), ("project", list(exprs)), "project"))
+        return self._map(functools.partial(_apply_project, exprs), "project")
 
     def selectExpr(self, *exprs):
         from raydp_amd.spark.functions import expr
@@ -280,16 +329,8 @@ class DataFrame:
             for tmp, we in hoisted:
                 df = df._with(W.WindowPlan(df._src(), tmp, we.fn, we.args, we.window))
             return df.withColumn(colName, Column(e)).drop(*[t for t, _ in hoisted])
-        names = self.columns
-
-        def fn(t, i):
-            v = as_array(e.eval(t), t.num_rows)
-            if colName in t.column_names:
-                return t.set_column(t.column_names.index(colName), colName, v)
-            return t.append_column(colName, v)
-        node = P.MapPlan(self._src(), fn, f"withColumn({colName})")
-        node.rel = ("with", colName, e)
-        return self._with(node)
+        self.columns   # resolves the input schema (analysis errors surface here, as in Spark)
+        return self._with(_rel_node(self._src(), ("with", colName, e), f"withColumn({colName})"))
 
     def withColumns(self, colsMap: Dict[str, Column]):
         df = self
@@ -311,9 +352,7 @@ class DataFrame:
         names = set()
         for c in cols:
             names.add(c if isinstance(c, str) else c._expr.name())
-        node = P.MapPlan(self._src(), lambda t, i: t.drop([c for c in t.column_names if c in names]), "drop")
-        node.rel = ("drop", frozenset(names))
-        return self._with(node)
+        return self._with(_rel_node(self._src(), ("drop", frozenset(names)), "drop"))
 
     def filter(self, condition):
         if isinstance(condition, str):
@@ -326,21 +365,8 @@ class DataFrame:
             preds = src.filter_preds + preds
             src = src.child
 
-        def fn(t, i, preds=preds):
-            mask = None
-            for e in preds:
-                m = e.eval(t)
-                if isinstance(m, pa.Scalar):
-                    if not m.as_py():
-                        return t.slice(0, 0)
-                    continue
-                mask = m if mask is None else pc.and_kleene(mask, m)
-            if mask is None:
-                return t
-            return t.filter(mask, null_selection_behavior="drop")
-        node = P.MapPlan(src, fn, "filter")
+        node = _rel_node(src, ("filter", list(preds)), "filter")
         node.filter_preds = preds
-        node.rel = ("filter", list(preds))
         return self._with(node)
 
     where = filter

@@ -6,6 +6,7 @@ Covers what the reference examples and notebooks use (``examples/data_process.py
 ``monotonically_increasing_id``, ``array``/``posexplode``, ``count``) plus the common
 aggregates and math/string helpers.
 """
+import functools
 import math
 
 import numpy as np
@@ -46,9 +47,14 @@ def _fn(name, cols, impl, display=None, native=None):
     return Column(e)
 
 
+def _unary_impl(f, a, b):
+    return f(a[0])
+
+
 def _unary(name, f, native=None):
+    # module-level impl bound with partial: pickles by reference when ``f`` does (pc.abs, ...)
     def builder(c):
-        return _fn(name, [c], lambda a, b: f(a[0]), native=native)
+        return _fn(name, [c], functools.partial(_unary_impl, f), native=native)
     builder.__name__ = name
     return builder
 
@@ -152,11 +158,19 @@ def spark_partition_id():
 
 
 # ---------------------------------------------------------------------- datetime ---------
+def _dt_impl(f, a, b):
+    return pc.cast(f(_to_ts(a[0] if not isinstance(a[0], pa.Scalar) else as_array(a[0], b.num_rows))),
+                   pa.int32())
+
+
+def _spark_dayofweek(t):
+    # Spark: 1 = Sunday ... 7 = Saturday
+    return pc.add(pc.day_of_week(t, count_from_zero=False, week_start=7), 0)
+
+
 def _dt(name, f):
     def builder(c):
-        return _fn(name, [c], lambda a, b: pc.cast(f(_to_ts(
-            a[0] if not isinstance(a[0], pa.Scalar) else as_array(a[0], b.num_rows))),
-                                                   pa.int32()), native=("dt", name))
+        return _fn(name, [c], functools.partial(_dt_impl, f), native=("dt", name))
     builder.__name__ = name
     return builder
 
@@ -171,8 +185,7 @@ quarter = _dt("quarter", pc.quarter)
 weekofyear = _dt("weekofyear", pc.iso_week)
 dayofyear = _dt("dayofyear", pc.day_of_year)
 # Spark: 1 = Sunday ... 7 = Saturday; Arrow (count_from_zero, week_start=Monday): Monday=0
-dayofweek = _dt("dayofweek", lambda t: pc.add(pc.day_of_week(t, count_from_zero=False,
-                                                               week_start=7), 0))
+dayofweek = _dt("dayofweek", _spark_dayofweek)
 
 
 def to_date(c, format=None):  # noqa: A002

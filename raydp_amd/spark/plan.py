@@ -180,6 +180,8 @@ class MapPlan(Plan):
     def __getstate__(self):
         st = dict(self.__dict__)
         st.pop("_fused_segs", None)  # compiled programs are per process
+        if st.pop("_schema_static", False):
+            st.pop("_schema", None)  # re-derived statically where needed: not worth shipping
         return st
 
     @property
@@ -188,6 +190,7 @@ class MapPlan(Plan):
             # type the operator statically when every expression's type is certain
             from raydp_amd.spark import exprc
             self._schema = exprc.static_schema(self)
+            self._schema_static = self._schema is not None
         if self._schema is None:
             self._schema = self.empty().schema
         return self._schema
