@@ -185,6 +185,13 @@ class XgmiComm:
             return False
 
 
+def forget_xgmi(comm) -> None:
+    """Retire a communicator whose peers missed a deadline: later users get a fresh decision."""
+    for k, v in list(_cache.items()):
+        if v is comm:
+            _cache.pop(k, None)
+
+
 def _agree(ok: bool, group=None) -> bool:
     """True on every rank iff ``ok`` on every rank."""
     import torch

@@ -461,6 +461,18 @@ class FusedMLPTrainer:
             xg.check()
         return out
 
+    def snapshot(self):
+        """Device copy of everything an epoch mutates (see :meth:`restore`)."""
+        return ([t.clone() for t in (self.params, self.m, self.v, self.rstats, self.img)],
+                self.step_count)
+
+    def restore(self, snap):
+        tensors, step = snap
+        for dst, src in zip((self.params, self.m, self.v, self.rstats, self.img), tensors):
+            dst.copy_(src)
+        self.step_count = step
+        self.metrics.zero_()
+
     def _run_persistent(self, feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream) -> bool:
         """The whole epoch as one persistent launch (csrc/hip/mlp_persist.h); False when this
         model / configuration cannot use it (the caller then runs the launch-per-step loop)."""

@@ -166,6 +166,12 @@ class _Pickler(cloudpickle.CloudPickler):
             # small tables travel inline as Arrow IPC: unlike Arrow's own pickling, IPC writes
             # only the sliced range of each buffer (a slice must not drag its parent along)
             return _from_ipc, (_to_ipc(obj), isinstance(obj, pa.RecordBatch))
+        if type(obj).__name__ == "MapPlan" and getattr(obj, "rel", None) is not None:
+            # a chain of fusible operators ships as a cached structure + its source
+            from raydp_amd.spark import exprc
+            red = exprc.chain_reduce(obj)
+            if red is not None:
+                return red
         if self.store is not None and isinstance(obj, (pa.Table, pa.RecordBatch)) and obj.nbytes >= THRESHOLD:
             existing = _view_oid(obj)
             if existing is not None:

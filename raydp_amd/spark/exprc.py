@@ -1115,6 +1115,8 @@ def _skey(e) -> Optional[tuple]:
         return ("c", e.col_name)
     if isinstance(e, C.Lit):
         v = e.value
+        if v is None or isinstance(v, (bool, int, float, str)):
+            return ("l", type(v).__name__, repr(v))
         s = v if isinstance(v, pa.Scalar) else pa.scalar(v)
         return ("l", str(s.type), repr(s.as_py()))
     if isinstance(e, C.Alias):
@@ -1139,7 +1141,10 @@ def _skey(e) -> Optional[tuple]:
             return None
         return ("w", tuple(parts), o)
     if isinstance(e, C.UDFExpr):
-        uk = _udf_key(e.udf)
+        uk = e.udf.__dict__.get("_rx_key", False)
+        if uk is False:
+            uk = _udf_key(e.udf)
+            e.udf.__dict__["_rx_key"] = uk
         args = [_skey(a) for a in e.args]
         return None if uk is None or any(a is None for a in args) else ("udf", uk, tuple(args))
     return None
@@ -1385,3 +1390,68 @@ def static_schema(node) -> Optional[pa.Schema]:
     except _Unsupported:
         return None
     return None
+
+
+# ------------------------------------------------------------------------------------------
+# structure-cached shipping of operator chains
+# ------------------------------------------------------------------------------------------
+# A stage payload is the plan pickled by value. Two DataFrames built by the same code (the
+# warm-up and the measured run of a pipeline, every epoch of an ETL loop) differ only in their
+# source; their chains of narrow operators are the same expressions, UDF code and constants.
+# The driver pickles each chain *structure* once and afterwards ships those bytes under an id;
+# each executor unpickles a structure once and re-links fresh operator nodes to the new source.
+_ship_lock = threading.Lock()
+_shipped: Dict[tuple, tuple] = {}    # driver: (chain key, base schema) -> (id, template bytes)
+_templates: Dict[str, list] = {}     # executor: id -> template nodes (child unset)
+
+
+def chain_reduce(top):
+    """Pickle reduction for the top node of a fusible chain, or None (pickle normally)."""
+    if not enabled():
+        return None
+    nodes, base = chain_of(top)
+    if len(nodes) < 2:
+        return None
+    keys = [_node_key(n) for n in nodes]
+    if any(k is None for k in keys):
+        return None
+    try:
+        bschema = base.schema
+    except Exception:  # noqa: BLE001
+        return None
+    key = (tuple(keys), bschema)
+    with _ship_lock:
+        hit = _shipped.get(key)
+    if hit is None:
+        import uuid
+        from raydp_amd.runtime import serialization as S
+        tmpl = []
+        for n in nodes:
+            c = object.__new__(type(n))
+            st = n.__getstate__()
+            st["child"] = None
+            c.__dict__.update(st)
+            tmpl.append(c)
+        hit = (uuid.uuid4().hex, S.dumps(tmpl, transfer=False))
+        with _ship_lock:
+            _shipped[key] = hit
+    return _relink_chain, (hit[0], hit[1], base)
+
+
+def _relink_chain(tid: str, data: bytes, base):
+    with _ship_lock:
+        tmpl = _templates.get(tid)
+    if tmpl is None:
+        from raydp_amd.runtime import serialization as S
+        tmpl = S.loads(data)
+        with _ship_lock:
+            _templates[tid] = tmpl
+            while len(_templates) > 64:
+                _templates.pop(next(iter(_templates)))
+    child = base
+    for t in tmpl:
+        n = object.__new__(type(t))
+        n.__dict__.update({k: v for k, v in t.__dict__.items() if k != "_fused_segs"})
+        n.child = child
+        child = n
+    return child

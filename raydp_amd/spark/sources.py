@@ -8,7 +8,7 @@ multi-threaded C++ CSV reader with the schema inferred once from the head of the
 import glob
 import io
 import os
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import numpy as np
 import pyarrow as pa
@@ -136,14 +136,20 @@ class CsvSource(Source):
             for j in range(nsplit):
                 self.splits.append((f, int(b[j]), int(b[j + 1])))
         self._header_line = None
+        # small-file fast path: when schema inference parsed a whole single-split file, that
+        # parse IS the partition (same parser, same types, same null tokens), so the task
+        # ships it instead of parsing the file a second time
+        self._parsed: Dict[int, pa.Table] = {}
         if schema is not None:
             self._schema = schema
         else:
             self._schema = self._infer(infer_schema)
 
-    def _read_opts(self, column_names=None):
+    def _read_opts(self, column_names=None, nbytes=None):
+        # Arrow's threaded reader only pays off past a few blocks
         ro = pacsv.ReadOptions(column_names=column_names, autogenerate_column_names=not self.header
-                               and column_names is None, use_threads=True)
+                               and column_names is None,
+                               use_threads=nbytes is None or nbytes > (4 << 20))
         return ro
 
     def _infer(self, infer):
@@ -159,7 +165,7 @@ class CsvSource(Source):
         nulls = [self.null_value] if self.null_value else [""]
         conv = pacsv.ConvertOptions(strings_can_be_null=True, null_values=nulls) if infer else \
             pacsv.ConvertOptions(column_types=None, null_values=nulls)
-        t = pacsv.read_csv(io.BytesIO(head), read_options=self._read_opts(),
+        t = pacsv.read_csv(pa.BufferReader(pa.py_buffer(head)), read_options=self._read_opts(nbytes=len(head)),
                            parse_options=pacsv.ParseOptions(delimiter=self.sep),
                            convert_options=conv)
         if not infer:
@@ -171,7 +177,13 @@ class CsvSource(Source):
             if pa.types.is_null(ty):
                 ty = pa.string()
             fields.append(pa.field(fld.name, ty))
-        return pa.schema(fields)
+        schema = pa.schema(fields)
+        whole = len(head) == os.path.getsize(f)
+        if whole and len(self.splits) == 1 and self.splits[0] == (f, 0, len(head)) and \
+                self.null_value is None and t.num_rows and \
+                all(a == b for a, b in zip(t.schema.types, schema.types)):
+            self._parsed[0] = t.replace_schema_metadata()
+        return schema
 
     def num_partitions(self):
         return len(self.splits)
@@ -180,6 +192,9 @@ class CsvSource(Source):
         return self._schema
 
     def load(self, i):
+        hit = self._parsed.get(i)
+        if hit is not None:
+            return hit
         f, lo, hi = self.splits[i]
         with open(f, "rb") as fh:
             header = b""
@@ -203,8 +218,9 @@ class CsvSource(Source):
                                     null_values=[self.null_value] if self.null_value else [""])
         if not data.strip():
             return self._schema.empty_table()
-        t = pacsv.read_csv(io.BytesIO(data),
-                           read_options=pacsv.ReadOptions(column_names=names, use_threads=True,
+        t = pacsv.read_csv(pa.BufferReader(pa.py_buffer(data)),
+                           read_options=pacsv.ReadOptions(column_names=names,
+                                                          use_threads=len(data) > (4 << 20),
                                                           block_size=max(1 << 20, len(data) + 1)),
                            parse_options=pacsv.ParseOptions(delimiter=self.sep),
                            convert_options=conv)

@@ -243,6 +243,14 @@ class UserDefinedFunction:
         self._vec = None
         self._vec_state = "untried"  # untried | ok | failed
 
+    def __getstate__(self):
+        # per-process caches stay behind: the vectoriser holds the function's module globals,
+        # the structural key (spark/exprc.py) may hold process-local ids
+        st = dict(self.__dict__)
+        st.pop("_rx_key", None)
+        st["_vec"] = None
+        return st
+
     def __call__(self, *cols):
         from raydp_amd.spark.column import Column, UDFExpr, _to_expr
         return Column(UDFExpr(self, [_to_expr(c, name_is_col=True) for c in cols]))

@@ -202,7 +202,7 @@ class FusedMLPEngine:
             s = torch.tensor([mine], device=self.device, dtype=torch.int64)
             dist.all_reduce(s, op=dist.ReduceOp.MIN)
             max_steps = int(s.item())
-            xg = _xgmi_for(self.trainer)
+            xg = None if getattr(self, "_xgmi_broken", False) else _xgmi_for(self.trainer)
             comm = None
             if xg is None:
                 comm = NativeComm.from_process_group() if dist.get_backend() == "nccl" else None
@@ -211,11 +211,47 @@ class FusedMLPEngine:
             if comm is None and xg is None:
                 def ar(g):
                     dist.all_reduce(g)
-        m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, allreduce=ar,
-                                     world_size=self.world, drop_last=self.drop_last, comm=comm,
-                                     max_steps=max_steps, xg=xg if self.world > 1 else None)
+        if xg is None:
+            m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, allreduce=ar,
+                                         world_size=self.world, drop_last=self.drop_last, comm=comm,
+                                         max_steps=max_steps)
+        else:
+            m = self._xgmi_epoch(xg, t, perm, max_steps)
         self.trainer.note_steps(self.trainer.steps_in_epoch)
         return self._res(m), m["loss"]
+
+    def _xgmi_epoch(self, xg, t, perm, max_steps):
+        """One epoch with the one-shot xGMI all-reduce fused into the optimizer kernel. Every
+        peer wait in that kernel is bounded; if any rank saw a timeout, all ranks roll back to
+        the epoch-start snapshot, drop the xGMI path for good and rerun the epoch over RCCL
+        (matched on every rank by one agreement collective per epoch)."""
+        import torch.distributed as dist
+        from raydp_amd.exceptions import CollectiveError
+        from raydp_amd.ops.comm import NativeComm, _agree, forget_xgmi
+        snap = self.trainer.snapshot()
+        ok = True
+        try:
+            m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, world_size=self.world,
+                                         drop_last=self.drop_last, max_steps=max_steps, xg=xg)
+        except CollectiveError:
+            ok = False
+        if _agree(ok):
+            return m
+        import warnings
+        warnings.warn("xGMI one-shot all-reduce timed out on some rank: rolled back, rerunning "
+                      "the epoch over RCCL and staying on it")
+        forget_xgmi(xg)
+        self._xgmi_broken = True
+        self.trainer.restore(snap)
+        comm = NativeComm.from_process_group() if dist.get_backend() == "nccl" else None
+        ar = None
+        if comm is None:
+            def ar(g):
+                dist.all_reduce(g)
+        self.allreduce_kind = "rccl_native" if comm is not None else f"torch.distributed:{dist.get_backend()}"
+        return self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, allreduce=ar,
+                                        world_size=self.world, drop_last=self.drop_last, comm=comm,
+                                        max_steps=max_steps)
 
     def evaluate_epoch(self):
         e = self.eval

@@ -151,6 +151,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
     # ------------------------------------------------------------------------- worker -----
     @staticmethod
     def train_func(config):
+        t_setup0 = time.time_ns()
         # model
         if isinstance(config["model"], torch.nn.Module):
             model = copy.deepcopy(config["model"])
@@ -230,6 +231,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             engine = TorchLoopEngine(model, optimizer, loss, metrics, device, config, sched)
         engine.epoch = start_epoch          # epoch permutations continue where the run left off
         from raydp_amd.utils import tracing
+        tracing.complete("worker setup", t_setup0, cat="train", engine=engine.name)
         t_load0 = time.perf_counter()
         with tracing.span("ingest", cat="train", engine=engine.name):
             engine.load(train_ds, eval_ds, config)
@@ -334,6 +336,8 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         torch_config = self._extra_config.get("torch_config")
         if torch_config is None and self._use_ccl:
             torch_config = TorchConfig(backend="ccl")
+        from raydp_amd.utils import tracing
+        tracing.instant("trainer start", cat="train")
         self._trainer = TorchTrainer(TorchEstimator.train_func,
                                      train_loop_config=train_loop_config,
                                      scaling_config=scaling_config,

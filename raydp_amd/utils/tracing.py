@@ -112,6 +112,14 @@ def span(name: str, cat: str = "raydp", **args) -> Iterator[None]:
                    "pid": os.getpid(), "tid": threading.get_ident() % 100000, "args": args})
 
 
+def complete(name: str, t0_ns: int, cat: str = "raydp", **args):
+    """Record a span that started at ``t0_ns`` (``time.time_ns()``) and ends now."""
+    if _path():
+        t1 = time.time_ns()
+        _emit({"name": name, "cat": cat, "ph": "X", "ts": t0_ns / 1000.0, "dur": (t1 - t0_ns) / 1000.0,
+               "pid": os.getpid(), "tid": threading.get_ident() % 100000, "args": args})
+
+
 def instant(name: str, cat: str = "raydp", **args):
     if _roctx_enabled():
         rl = _roctx_lib()

@@ -246,3 +246,21 @@ def test_program_register_reuse_is_safe():
     np.testing.assert_array_equal(out.column("w").to_numpy(), np.arange(3000, dtype=np.float64))
     want = np.where(np.arange(3000) % 3 == 0, np.arange(3000) + 1, np.arange(3000))
     np.testing.assert_array_equal(out.column("s").to_numpy(), want)
+
+
+def test_small_csv_inference_parse_is_the_partition(tmp_path):
+    """A single-split file parsed whole by schema inference ships that parse as its partition;
+    it must equal what the task-side parse with the inferred schema produces."""
+    import os
+    import bench
+    from raydp_amd.spark.sources import CsvSource
+    for p in (str(tmp_path / "nyc.csv"), os.path.join(os.path.dirname(bench.__file__), "examples",
+                                                       "data", "fake_nyctaxi.csv")):
+        if not os.path.exists(p):
+            bench.make_csv(p, 2000, 11)
+        src = CsvSource(p, header=True, infer_schema=True)
+        assert 0 in src._parsed
+        fast = src.load(0)
+        src._parsed.clear()
+        slow = src.load(0)
+        assert fast.schema == slow.schema and fast.equals(slow)

@@ -201,3 +201,67 @@ def test_ddp_small_buckets_take_the_xgmi_path():
         assert used_xg and not used_fallback, (rank, used_xg, used_fallback)
         assert same, "DDP replicas diverged"
         assert diff < 1e-5, (rank, diff)
+
+
+def _fallback_main(rank, world, port, q):
+    import types
+
+    import torch
+    import torch.distributed as dist
+    import torch.nn as nn
+    _init(rank, world, port)
+    try:
+        from raydp_amd.exceptions import CollectiveError
+        from raydp_amd.models.mlp_spec import extract_mlp_spec
+        from raydp_amd.ops.comm import XgmiComm
+        from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+        from raydp_amd.torch.engine import FusedMLPEngine
+        dev = torch.device("cuda", 0)
+
+        def trainer():
+            torch.manual_seed(0)
+            model = _nyc()
+            opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+            return FusedMLPTrainer(extract_mlp_spec(model), optimizer_config(opt), loss_code(nn.MSELoss()), 64, dev)
+        tr = trainer()
+        g = torch.Generator().manual_seed(7 + rank)
+        n = 64 * 16
+        feats = torch.zeros(n, tr.feat_k, dtype=torch.bfloat16)
+        feats[:, :20] = torch.randn(n, 20, generator=g).to(torch.bfloat16)
+        labels = torch.randn(n, 1, generator=g)
+        feats, labels = feats.to(dev), labels.to(dev)
+        xg = XgmiComm.create(tr.grads.numel(), timeout_s=20.0)
+        if xg is None:
+            q.put((rank, "create failed", None, None))
+            return
+        real = tr.train_epoch
+
+        def flaky(*a, **k):
+            out = real(*a, **k)      # the epoch really ran (and mutated the state) ...
+            if k.get("xg") is not None and rank == 1:
+                raise CollectiveError("injected peer timeout")   # ... then one rank reports a miss
+            return out
+        tr.train_epoch = flaky
+        eng = types.SimpleNamespace(trainer=tr, world=world, drop_last=False, allreduce_kind="xgmi_oneshot")
+        FusedMLPEngine._xgmi_epoch(eng, xg, types.SimpleNamespace(feats_bf16=feats, labels=labels, n=n),
+                                   None, None)
+        torch.cuda.synchronize()
+        # reference: the same epoch from the same start over gloo
+        ref = trainer()
+
+        def ar(gr):
+            dist.all_reduce(gr)
+        ref.train_epoch(feats, labels, n, None, allreduce=ar, world_size=world)
+        torch.cuda.synchronize()
+        q.put((rank, eng.allreduce_kind, bool(eng._xgmi_broken),
+               bool(torch.equal(tr.params, ref.params)) and tr.step_count == ref.step_count))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_xgmi_epoch_timeout_rolls_back_and_reruns_over_the_process_group():
+    res = _run(_fallback_main)
+    for rank, kind, broken, same in res:
+        assert kind == "torch.distributed:gloo", (rank, kind)
+        assert broken and same, (rank, broken, same)
