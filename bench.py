@@ -154,6 +154,8 @@ def main():
     ap.add_argument("--no-fused", action="store_true")
     ap.add_argument("--no-reference-config", action="store_true",
                     help="skip the extra (untimed-by-the-driver) reference-config measurement")
+    ap.add_argument("--profile-timed", default=None,
+                    help="cProfile the timed region (driver process) into this text file")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -203,11 +205,26 @@ def main():
     gc.freeze()
     barrier()
     from raydp_amd.utils import tracing
+    prof = None
+    if args.profile_timed:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     with tracing.span("timed run", cat="bench"):
         res = run_pipeline(spark, main_csv, args.steps, world, storage, fused=not args.no_fused)
         barrier()
     dt = time.perf_counter() - t0
+    if prof is not None:
+        prof.disable()
+        import io
+        import pstats
+        buf = io.StringIO()
+        st = pstats.Stats(prof, stream=buf)
+        st.sort_stats("cumulative").print_stats(70)
+        st.sort_stats("tottime").print_stats(40)
+        with open(args.profile_timed, "w") as f:
+            f.write(buf.getvalue())
     t = torch.tensor([dt], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -598,7 +598,37 @@ class FusedMLPTrainer:
             bn.running_var.copy_(rs[o:o + rv.numel()])
             if bn.num_batches_tracked is not None:
                 bn.num_batches_tracked.add_(getattr(self, "_tracked_pending", 0))
+        self._tracked_total = getattr(self, "_tracked_total", 0) + getattr(self, "_tracked_pending", 0)
         self._tracked_pending = 0
+
+    @torch.no_grad()
+    def state_dict_from_buffers(self, model: torch.nn.Module):
+        """``model.state_dict()`` as :meth:`write_back` would leave it, built from the device
+        buffers without touching ``model`` (whose modules the layout references): trained
+        entries are views of one host copy of each flat buffer, the rest are the module's own."""
+        import collections
+        names = {id(m): n for n, m in model.named_modules()}
+        out = collections.OrderedDict(model.state_dict())
+        p = self.params.detach().to("cpu")
+        rs = self.rstats.detach().to("cpu") if self.run_bufs else None
+
+        def key(mod, attr):
+            n = names[id(mod)]
+            return f"{n}.{attr}" if n else attr
+        for kind, mod, off, n in self.layout:
+            attr = _ATTR[kind]
+            ref = getattr(mod, attr)
+            out[key(mod, attr)] = p[off:off + n].view_as(ref).to(ref.dtype)
+        base = self.rstats.data_ptr()
+        tracked = getattr(self, "_tracked_total", 0) + getattr(self, "_tracked_pending", 0)
+        for bn, rm, rv in self.run_bufs:
+            o = (rm.data_ptr() - base) // 4
+            out[key(bn, "running_mean")] = rs[o:o + rm.numel()].clone()
+            o = (rv.data_ptr() - base) // 4
+            out[key(bn, "running_var")] = rs[o:o + rv.numel()].clone()
+            if bn.num_batches_tracked is not None:
+                out[key(bn, "num_batches_tracked")] = bn.num_batches_tracked + tracked
+        return out
 
     def note_steps(self, n):
         self._tracked_pending = getattr(self, "_tracked_pending", 0) + n

@@ -150,9 +150,14 @@ class FusedMLPEngine:
             return None
         return spec, lc, oc, acc_thr
 
-    def __init__(self, model, optimizer, spec, lc, oc, acc_thr, metrics, device, config, lr_scheduler_fn):
+    def __init__(self, model, optimizer, spec, lc, oc, acc_thr, metrics, device, config, lr_scheduler_fn,
+                 detached: bool = False):
+        """``detached``: ``model`` / ``optimizer`` are the caller's own objects, only read here
+        (parameters, running statistics, hyper-parameters and moments are copied to the device
+        once); results are exported from the device buffers and the objects are never written."""
         from raydp_amd.ops.fused_mlp import FusedMLPTrainer
         self.model, self.metrics_names, self.device = model, metrics.names, device
+        self.detached = detached
         self.world = session.get_world_size()
         self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn,
                                        acc_thr=acc_thr)
@@ -259,11 +264,19 @@ class FusedMLPEngine:
         return self._res(m), m["loss"]
 
     def state_dict(self):
+        if self.detached:
+            return self.trainer.state_dict_from_buffers(self.model)
         self.trainer.write_back()
         return self.model.state_dict()
 
     def optimizer_state_dict(self):
-        return self.trainer.export_optimizer_state(self.optimizer)
+        opt = self.optimizer
+        if self.detached:
+            # export into a private optimizer over the same parameters, never the caller's
+            priv = type(opt)(self.model.parameters(), lr=0.1)
+            priv.load_state_dict(opt.state_dict())
+            opt = priv
+        return self.trainer.export_optimizer_state(opt)
 
 
 def _binary_accuracy_threshold(metrics):

@@ -152,6 +152,12 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
     @staticmethod
     def train_func(config):
         t_setup0 = time.time_ns()
+        from raydp_amd.utils import tracing
+        device = session.get_device() or torch.device("cpu")
+        engine = TorchEstimator._detached_fused_engine(config, device)
+        if engine is not None:
+            tracing.complete("worker setup", t_setup0, cat="train", engine=engine.name, detached=True)
+            return TorchEstimator._train_loop(config, engine, 0, device)
         # model
         if isinstance(config["model"], torch.nn.Module):
             model = copy.deepcopy(config["model"])
@@ -160,7 +166,6 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         else:
             raise Exception("Unsupported parameter, we only support torch.nn.Model instance "
                             "or a function(dict -> model)")
-        device = session.get_device() or torch.device("cpu")
         # the model stays on the host until the engine is chosen: the fused engine keeps its own
         # flat device copy of the parameters (one H2D copy) and writes results back to the host
         # module in one D2H copy; the torch loop moves it to the device below
@@ -192,9 +197,6 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         if ck is not None:
             resume_dir = ck.path
             start_epoch = _restore_checkpoint(resume_dir, model)
-
-        train_ds = session.get_dataset_shard("train")
-        eval_ds = session.get_dataset_shard("evaluate") if config["evaluate"] else None
 
         from raydp_amd.torch.engine import FusedMLPEngine, TorchLoopEngine
         engine = None
@@ -229,9 +231,43 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                 if sched is not None and os.path.exists(os.path.join(resume_dir, SCHED_KEY)):
                     sched.load_state_dict(torch.load(os.path.join(resume_dir, SCHED_KEY), weights_only=True))
             engine = TorchLoopEngine(model, optimizer, loss, metrics, device, config, sched)
-        engine.epoch = start_epoch          # epoch permutations continue where the run left off
-        from raydp_amd.utils import tracing
         tracing.complete("worker setup", t_setup0, cat="train", engine=engine.name)
+        return TorchEstimator._train_loop(config, engine, start_epoch, device)
+
+    @staticmethod
+    def _detached_fused_engine(config, device):
+        """The fused engine over the caller's own model and optimizer objects (read, never
+        written: results come from the device buffers), which saves copying the model for the
+        worker. Only for a fresh run of a fusable model with an optimizer instance, a loss
+        instance and no LR scheduler; anything else takes the copying path."""
+        model, opt, loss = config["model"], config["optimizer"], config["loss"]
+        if not (isinstance(model, torch.nn.Module) and isinstance(opt, torch.optim.Optimizer)
+                and isinstance(loss, TLoss)) or config["lr_scheduler_creator"] is not None \
+                or session.get_checkpoint() is not None or device.type != "cuda":
+            return None
+        fused_mode = config.get("fused", None)
+        if fused_mode is None:
+            from raydp_amd.utils.config import get as conf_get
+            fused_mode = conf_get("spark.ray.mi355x.fused")
+        fused_mode = {True: "auto", False: "off"}.get(fused_mode, fused_mode)
+        if fused_mode == "off":
+            return None
+        from raydp_amd.torch.engine import FusedMLPEngine
+        metrics = copy.deepcopy(config["metrics"])
+        fused = FusedMLPEngine.applicable(model, opt, loss, metrics, device, config["batch_size"],
+                                          config["feature_columns"], config["feature_types"])
+        if fused is None:
+            return None
+        spec, lc, oc, acc_thr = fused
+        return FusedMLPEngine(model, opt, spec, lc, oc, acc_thr, metrics, device, config, None,
+                              detached=True)
+
+    @staticmethod
+    def _train_loop(config, engine, start_epoch, device):
+        from raydp_amd.utils import tracing
+        train_ds = session.get_dataset_shard("train")
+        eval_ds = session.get_dataset_shard("evaluate") if config["evaluate"] else None
+        engine.epoch = start_epoch          # epoch permutations continue where the run left off
         t_load0 = time.perf_counter()
         with tracing.span("ingest", cat="train", engine=engine.name):
             engine.load(train_ds, eval_ds, config)

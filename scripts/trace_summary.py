@@ -22,6 +22,8 @@ def main(prefix):
                     continue
                 if e.get("ph") == "X":
                     events.append(e)
+                elif e.get("ph") == "i":
+                    events.append(dict(e, dur=0.0))
     runs = [e for e in events if e["name"] == "timed run"]
     if not runs:
         raise SystemExit("no 'timed run' span")

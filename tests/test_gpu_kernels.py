@@ -380,3 +380,50 @@ def test_persistent_timeout_rolls_back_to_step_loop(monkeypatch):
     (p1, m1, i1, r1, e1), (p0, m0, i0, r0, e0) = runs
     assert torch.equal(p1, p0) and torch.equal(m1, m0) and torch.equal(i1, i0) and torch.equal(r1, r0)
     assert e1["batches"] == e0["batches"] and abs(e1["loss"] - e0["loss"]) <= 1e-6 * max(1.0, abs(e0["loss"]))
+
+
+def test_detached_fused_engine_leaves_caller_objects_and_matches_copying_path():
+    """A fresh fusable fit trains on the caller's own model/optimizer objects without copying
+    them; they must stay untouched, and the checkpoint must equal the copying path's (the
+    same engine with a deep-copied model written back)."""
+    import os
+    import raydp_amd
+    from raydp_amd import runtime
+    from raydp_amd.torch import TorchEstimator
+    from data_process import nyc_taxi_preprocess
+    runtime.shutdown()
+    runtime.init(num_cpus=4)
+    try:
+        spark = raydp_amd.init_spark("gpu-detached", 1, 2, "500M")
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        df = spark.read.format("csv").option("header", "true").option("inferSchema", "true") \
+            .load(os.path.join(root, "examples", "data", "fake_nyctaxi.csv"))
+        df = nyc_taxi_preprocess(df)
+        feats = [c for c in df.columns if c != "fare_amount"]
+        ckpts = {}
+        for detached in (True, False):
+            torch.manual_seed(0)
+            model = NYC(len(feats))
+            opt = torch.optim.Adam(model.parameters(), lr=3e-3)
+            before = {k: v.clone() for k, v in model.state_dict().items()}
+            est = TorchEstimator(num_workers=1, model=model, optimizer=opt, loss=nn.SmoothL1Loss(),
+                                 feature_columns=feats, feature_types=torch.float,
+                                 label_column="fare_amount", label_type=torch.float, batch_size=64,
+                                 num_epochs=3, metrics_name=["MeanAbsoluteError"], shuffle_seed=5)
+            if not detached:
+                # an LR scheduler creator that keeps the LR constant forces the copying path
+                est._lr_scheduler_creator = lambda o, c: torch.optim.lr_scheduler.LambdaLR(o, lambda s: 1.0)
+            est.fit_on_spark(df)
+            assert est.results.metrics_history[0]["engine"] == "fused_mlp_hip"
+            after = model.state_dict()
+            assert all(torch.equal(before[k], after[k]) for k in before), "caller's model was written"
+            assert not opt.state, "caller's optimizer was stepped"
+            ck = est.results.checkpoint.path
+            ckpts[detached] = torch.load(os.path.join(ck, "model.pt"), weights_only=True)
+        a, b = ckpts[True], ckpts[False]
+        assert list(a) == list(b)
+        for k in a:
+            assert a[k].dtype == b[k].dtype and torch.equal(a[k], b[k]), k
+    finally:
+        raydp_amd.stop_spark()
+        runtime.shutdown()
