@@ -31,6 +31,8 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.trace", "RAYDP_TRACE", ""},
     {"spark.ray.mi355x.roctx", "RAYDP_ROCTX", "0"},
     {"spark.ray.mi355x.opt_xcd_affine", "RAYDP_OPT_XCD_AFFINE", "1"},
+    {"spark.ray.mi355x.fused_etl", "RAYDP_FUSED_ETL", "1"},
+    {"spark.ray.mi355x.local_exec_bytes", "RAYDP_LOCAL_EXEC_BYTES", "4m"},
     {"spark.ray.mi355x.xg_opt_stride", "RAYDP_XG_OPT_STRIDE", "1"},
 };
 

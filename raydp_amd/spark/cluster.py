@@ -28,6 +28,7 @@ import collections
 import concurrent.futures as cf
 import functools
 import logging
+import os
 import threading
 import time
 from typing import Dict, List, Optional
@@ -68,6 +69,36 @@ class ExecutorInfo:
         return f"Executor({self.executor_id}, {self.state})"
 
 
+def _driver_resident_bytes(plan, limit) -> Optional[int]:
+    """Bytes of the driver-resident tables a plan reads, or None when any leaf lives elsewhere
+    (files, the object store of an executor) or a wide operator is still unmaterialised."""
+    from raydp_amd.spark.sources import TableSource
+    total = 0
+    stack = [plan]
+    while stack:
+        p = stack.pop()
+        if isinstance(p, P.MaterializedPlan):
+            total += sum(t.nbytes for t in p.tables)
+        elif isinstance(p, P.SourcePlan):
+            if not isinstance(p.source, TableSource):
+                return None
+            total += sum(t.nbytes for t in p.source.tables)
+        elif isinstance(p, P.MapPlan):
+            stack.append(p.child)
+        elif isinstance(p, P.UnionPlan):
+            stack.extend(p.plans)
+        elif getattr(p, "_broadcast", None) is not None:
+            total += p._broadcast.nbytes
+            stack.append(p.left)
+        elif isinstance(p, P.WidePlan) and getattr(p, "_out", None) is not None:
+            total += sum(t.nbytes for t in p._out)
+        else:
+            return None
+        if total > limit:
+            return None
+    return total
+
+
 class ExecutorTaskScheduler(P.TaskScheduler):
     """Runs stage tasks on the executor actor processes of one application."""
 
@@ -86,6 +117,15 @@ class ExecutorTaskScheduler(P.TaskScheduler):
         if not indices:
             return []
         from raydp_amd.utils import tracing
+        if self._runs_locally(fn):
+            # Spark's LocalTableScan: a stage over small driver-resident tables (cached results,
+            # local data) runs in the driver; shipping it costs more than computing it
+            with tracing.span("local stage", cat="etl", tasks=len(indices)):
+                out = []
+                for i in indices:
+                    with P._PartitionScope(i):
+                        out.append(fn(i))
+                return out
         t0 = time.perf_counter()
         payload, key = self._stage_payload(fn)
         t1 = time.perf_counter()
@@ -101,6 +141,21 @@ class ExecutorTaskScheduler(P.TaskScheduler):
                 logger.warning("stage: %d tasks, payload %d B (%d store objs), pickle %.3fs, run %.3fs",
                                len(indices), len(payload.data), len(payload.oids), t1 - t0,
                                time.perf_counter() - t1)
+
+    def _runs_locally(self, fn) -> bool:
+        plan = getattr(fn, "__self__", None)
+        if not isinstance(plan, P.Plan):
+            return False
+        limit = self.__dict__.get("_local_bytes")
+        if limit is None:
+            from raydp_amd.utils import parse_memory_size
+            limit = parse_memory_size(str(self.backend.conf.get(
+                "spark.ray.mi355x.local_exec_bytes", os.environ.get("RAYDP_LOCAL_EXEC_BYTES", "4m"))))
+            self._local_bytes = limit
+        if limit <= 0:
+            return False
+        total = _driver_resident_bytes(plan, limit)
+        return total is not None and total <= limit
 
     @staticmethod
     def _stage_payload(fn):

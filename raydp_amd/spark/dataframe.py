@@ -57,6 +57,10 @@ def _names_of(cols):
 # pickles as data (expression trees) instead of one closure code object per operator, and the
 # same ``rel`` tuple drives both this per-operator path and the fused VM (spark/exprc.py)
 # ------------------------------------------------------------------------------------------
+def _count_rows(t: pa.Table, i) -> pa.Table:
+    return pa.table({"n": [t.num_rows]})
+
+
 def _apply_with(col_name, e, t: pa.Table, i) -> pa.Table:
     v = as_array(e.eval(t), t.num_rows)
     if col_name in t.column_names:
@@ -478,11 +482,20 @@ class DataFrame:
         return self._with(P.UnionPlan([self._src(), other._src()], by_name=True))
 
     def repartition(self, numPartitions, *cols):
+        adaptive = None
         if isinstance(numPartitions, (str, Column)):
             cols = (numPartitions,) + cols
             numPartitions = self._session.conf.get("spark.sql.shuffle.partitions", "200")
+            conf = self._session.conf
+            if str(conf.get("spark.sql.adaptive.enabled", "true")).lower() == "true" and \
+                    str(conf.get("spark.sql.adaptive.coalescePartitions.enabled", "true")).lower() == "true":
+                from raydp_amd.utils import parse_memory_size
+                advisory = parse_memory_size(str(conf.get("spark.sql.adaptive.advisoryPartitionSizeInBytes", "64m")))
+                min_parts = int(conf.get("spark.sql.adaptive.coalescePartitions.minPartitionNum",
+                                         str(self._session._default_parallelism())))
+                adaptive = (advisory, min_parts)
         keys = [c if isinstance(c, str) else c._expr.name() for c in _names_of(cols)] or None
-        return self._with(P.RepartitionPlan(self._src(), int(numPartitions), keys))
+        return self._with(P.RepartitionPlan(self._src(), int(numPartitions), keys, adaptive=adaptive))
 
     def coalesce(self, numPartitions):
         return self._with(P.CoalescePlan(self._src(), numPartitions))
@@ -630,9 +643,8 @@ class DataFrame:
 
     def count(self) -> int:
         src = self._src()
-        return int(sum(self._session._run(P.MapPlan(src, lambda t, i: pa.table(
-            {"n": [t.num_rows]}), "count"))[j].column(0)[0].as_py()
-            for j in range(src.num_partitions())))
+        parts = self._session._run(P.MapPlan(src, _count_rows, "count"))
+        return int(sum(t.column(0)[0].as_py() for t in parts))
 
     def collect(self) -> List[Row]:
         t = self.toArrow()

@@ -57,23 +57,110 @@ class JoinPlan(WidePlan):
                       use_threads=True, coalesce_keys=same)
         if overlap:
             out = out.rename_columns([c[:-2] if c.endswith("#r") else c for c in out.column_names])
-        order = [c for c in lt.column_names] + [c for c in out.column_names if c not in lt.column_names]
-        seen, cols, names = set(), [], []
-        for i, c in enumerate(out.column_names):
-            names.append(c)
         return out
 
     def _empty(self):
+        st = self.static_schema()
+        if st is not None:
+            return st.empty_table()
         return self._join(self.left.schema.empty_table(), self.right.schema.empty_table())
+
+    def static_schema(self) -> Optional[pa.Schema]:
+        """Output schema without running a join (inner / left outer / semi / anti: left fields,
+        then the right side's, minus the keys when both sides name them alike, which Arrow
+        coalesces); None for the join types whose column order Arrow arranges differently."""
+        ls, rs = self.left.schema, self.right.schema
+        if self.how in ("left semi", "left anti"):
+            return ls
+        if self.how not in ("inner", "left outer"):
+            return None
+        same = self.lk == self.rk
+        return pa.schema(list(ls) + [f for f in rs if not (same and f.name in self.rk)])
+
+    # Broadcast hash join is a NARROW operator (Spark's BroadcastHashJoinExec inside whole-stage
+    # codegen): only the small side is materialised; each left partition is joined against it
+    # inside whatever task computes that partition, so a chain of dimension joins (the DLRM
+    # notebook's 26 categorical-model joins) runs in one pass per partition instead of one
+    # materialised stage per join.
+    def materialize(self, scheduler):
+        with self._lock:
+            if self._out is not None or self._broadcast is not None:
+                return
+            rparts = scheduler.map(self.right.compute, range(self.right.num_partitions()))
+            rsize = sum(t.nbytes for t in rparts)
+            if rsize <= _BROADCAST_BYTES and self.how in ("inner", "left outer", "left semi", "left anti"):
+                self._broadcast = concat(rparts, self.right.schema)
+                self.n = self.left.num_partitions()
+                return
+            self._out = self._shuffle_join(scheduler, rparts)
+
+    def compute(self, i):
+        if self._out is None and self._broadcast is None:
+            from raydp_amd.spark.plan import get_scheduler
+            self.materialize(get_scheduler())
+        if self._broadcast is not None:
+            return self._broadcast_join(self.left.compute(i))
+        return self._out[i]
+
+    def _broadcast_join(self, lt: pa.Table) -> pa.Table:
+        """Join one left partition against the broadcast table. A single-key inner / left
+        join whose build keys are unique (a dimension table, e.g. the DLRM value->id models) is
+        a hash LOOKUP: one ``index_in`` over the build keys and a ``take`` of its columns,
+        preserving the left rows' order; anything else runs Arrow's hash join."""
+        rt = self._broadcast
+        ok = self.__dict__.get("_lookup_ok")
+        if ok is None:
+            ok = self._can_lookup(rt)
+            self.__dict__["_lookup_ok"] = ok
+        if not ok:
+            return self._join(lt, rt)
+        key_l = lt.column(self.lk[0])
+        if key_l.type != rt.schema.field(self.rk[0]).type:
+            return self._join(lt, rt)
+        vs = self.__dict__.get("_lookup_vs")
+        if vs is None:
+            vs = rt.column(self.rk[0]).combine_chunks()
+            self.__dict__["_lookup_vs"] = vs
+        idx = pc.index_in(key_l, options=pc.SetLookupOptions(value_set=vs, skip_nulls=True))
+        if self.how == "inner":
+            keep = pc.is_valid(idx)
+            lt, idx = lt.filter(keep), idx.filter(keep)
+        same = self.lk == self.rk
+        rnames = [c for c in rt.column_names if not (same and c in self.rk)]
+        taken = rt.select(rnames).take(idx)
+        out = lt
+        for c in rnames:
+            out = out.append_column(c, taken.column(c))
+        return out
+
+    def _can_lookup(self, rt: pa.Table) -> bool:
+        if len(self.lk) != 1 or self.how not in ("inner", "left outer"):
+            return False
+        overlap = (set(rt.column_names) & set(self.left.schema.names)) - \
+            (set(self.lk) if self.lk == self.rk else set())
+        if overlap:
+            return False
+        k = rt.column(self.rk[0])
+        valid = len(k) - k.null_count
+        return valid == len(k) and pc.count_distinct(k, mode="only_valid").as_py() == valid
+
+    def __getstate__(self):
+        if self._broadcast is not None:
+            # ships the left lineage (computed per task) and the broadcast table, not the right
+            st = dict(self.__dict__)
+            st.pop("_lock", None)
+            st["_schema"] = self.schema
+            st["right"] = None
+            st["_cut"] = True
+            st.pop("_lookup_vs", None)
+            return st
+        return super().__getstate__()
 
     def execute(self, scheduler):
         rparts = scheduler.map(self.right.compute, range(self.right.num_partitions()))
-        rsize = sum(t.nbytes for t in rparts)
-        if rsize <= _BROADCAST_BYTES and self.how in ("inner", "left outer", "left semi", "left anti"):
-            rt = concat(rparts, self.right.schema)
-            n_left = self.left.num_partitions()
-            self.n = n_left
-            return scheduler.map(lambda i: self._join(self.left.compute(i), rt), range(n_left))
+        return self._shuffle_join(scheduler, rparts)
+
+    def _shuffle_join(self, scheduler, rparts):
         n = self.n
         ls, rs = self.left.schema, self.right.schema
         lsh = exchange(scheduler, self.left.compute, self.left.num_partitions(), self.lk, n, ls)

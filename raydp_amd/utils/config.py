@@ -155,6 +155,12 @@ register("spark.ray.mi355x.roctx", "bool", False, "emit roctx ranges for every s
          env="RAYDP_ROCTX")
 register("spark.ray.mi355x.opt_xcd_affine", "bool", True,
          "run the fused optimizer only on XCD 0's workgroups (the step kernel's L2)", env="RAYDP_OPT_XCD_AFFINE")
+register("spark.ray.mi355x.fused_etl", "bool", True,
+         "run chains of filter/withColumn/select/drop as one native expression-VM program per partition "
+         "(csrc/exec/expr/expr_vm.cc)", env="RAYDP_FUSED_ETL")
+register("spark.ray.mi355x.local_exec_bytes", "bytes", "4m",
+         "stages whose inputs are driver-resident tables (cached / local data) below this size run in "
+         "the driver process instead of on executors (0: never)", env="RAYDP_LOCAL_EXEC_BYTES")
 register("spark.ray.mi355x.xg_opt_stride", "int", 1,
          "workgroup stride of the fused reduce+optimizer kernel (1: every XCD pulls peer lines)",
          env="RAYDP_XG_OPT_STRIDE")

@@ -264,3 +264,73 @@ def test_small_csv_inference_parse_is_the_partition(tmp_path):
         src._parsed.clear()
         slow = src.load(0)
         assert fast.schema == slow.schema and fast.equals(slow)
+
+
+@pytest.mark.parametrize("how", ["left", "inner"])
+def test_broadcast_lookup_join_matches_hash_join(spark, monkeypatch, how):
+    """Dimension-table joins run as a narrow hash lookup (left order kept); rows, values and
+    nulls must equal Arrow's hash join (compared order-insensitively)."""
+    rng = np.random.default_rng(3)
+    n = 3000
+    keys = np.array([f"v{i}" for i in range(60)], dtype=object)
+    left = pa.table({"k": pa.array(keys[rng.integers(0, 60, n)], mask=rng.random(n) < 0.05),
+                     "x": pa.array(rng.normal(size=n))})
+    dim = pa.table({"k": pa.array(keys[:40]), "id": pa.array(np.arange(40, dtype=np.int64))})
+    out = spark.createDataFrame(left).join(spark.createDataFrame(dim), "k", how=how)
+    plan = out._plan
+    from raydp_amd.spark.plan import get_scheduler, prepare
+    prepare(plan, get_scheduler())
+    assert plan._broadcast is not None
+    got = pa.concat_tables([plan.compute(i) for i in range(plan.num_partitions())])
+    ref = pa.concat_tables([plan._join(plan.left.compute(i), plan._broadcast)
+                            for i in range(plan.num_partitions())])
+    assert got.schema == ref.schema
+    key = [("x", "ascending")]
+    assert got.sort_by(key).equals(ref.sort_by(key))
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "right", "outer", "left_semi", "left_anti"])
+@pytest.mark.parametrize("same_keys", [True, False])
+def test_static_join_schema_matches_arrow_join(spark, how, same_keys):
+    left = pa.table({"k": pa.array([1, 2, 3], pa.int64()), "x": pa.array([1.0, 2.0, 3.0]),
+                     "s": pa.array(["a", "b", "c"])})
+    right = pa.table({("k" if same_keys else "rk"): pa.array([2, 3, 4], pa.int64()),
+                      "y": pa.array([5, 6, 7], pa.int32()), "s2": pa.array(["u", "v", "w"])})
+    a, b = spark.createDataFrame(left), spark.createDataFrame(right)
+    on = "k" if same_keys else (a["k"] == b["rk"])
+    plan = a.join(b, on, how=how)._plan
+    ran = plan._join(plan.left.schema.empty_table(), plan.right.schema.empty_table()).schema
+    st = plan.static_schema()
+    assert st is None or st == ran
+    assert plan.schema == ran
+
+
+def test_adaptive_repartition_coalesces_buckets_and_keeps_keys_together(spark):
+    rng = np.random.default_rng(9)
+    t = pa.table({"k": pa.array(rng.integers(0, 500, 20000)), "v": pa.array(rng.normal(size=20000))})
+    df = spark.createDataFrame(t).repartition("k")             # 200 requested, tiny data
+    parts = df._session._run(df._src())
+    assert 1 <= len(parts) < 200 and len(parts) == df._src().num_partitions()
+    assert sum(p.num_rows for p in parts) == 20000
+    seen = {}
+    for j, p in enumerate(parts):
+        for k in set(p.column("k").to_pylist()):
+            assert seen.setdefault(k, j) == j                  # every key in exactly one partition
+    # an explicit count is honoured, and so is a count someone sized itself on beforehand
+    assert spark.createDataFrame(t).repartition(7, "k")._src().num_partitions() == 7
+    df2 = spark.createDataFrame(t).repartition("k")
+    n_seen = df2._src().num_partitions()          # sized on before the shuffle ran
+    assert len(df2._session._run(df2._src())) == n_seen == 200
+    df3 = spark.createDataFrame(t).repartition("k")
+    assert df3.rdd.getNumPartitions() == len(df3._session._run(df3._src())) < 200
+
+
+def test_map_output_travels_as_one_table():
+    import pickle
+    from raydp_amd.spark.plan import MapOutput, hash_partition
+    t = pa.table({"k": pa.array(np.arange(1000) % 37), "v": pa.array(np.arange(1000.0))})
+    mo = hash_partition(t, ["k"], 16)
+    assert isinstance(mo, MapOutput) and len(mo) == 16
+    assert sum(b.num_rows for b in mo) == 1000
+    back = pickle.loads(pickle.dumps(mo))
+    assert all(a.equals(b) for a, b in zip(mo, back))
