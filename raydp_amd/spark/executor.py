@@ -25,6 +25,11 @@ class RayDPExecutor:
         self.app_id = app_id
         self.cores = cores
         self.conf = dict(conf)
+        # the session's spark.ray.mi355x.* settings (e.g. fused_etl) reach executor-side code
+        # through the environment, as they reach trainer workers
+        import os
+        from raydp_amd.utils.config import env_for_workers
+        os.environ.update(env_for_workers(self.conf))
         self._fns: Dict[str, object] = {}
         self._fn_order: List[str] = []
         self._lock = threading.Lock()

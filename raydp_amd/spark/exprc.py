@@ -1106,7 +1106,19 @@ def _lib():
 # chains, caching and the MapPlan hook
 # ------------------------------------------------------------------------------------------
 def enabled() -> bool:
-    return os.environ.get("RAYDP_FUSED_ETL", "1") != "0"
+    # spark.ray.mi355x.fused_etl: executors receive it in their environment (executor.py);
+    # the driver reads its active session first
+    v = None
+    try:
+        from raydp_amd.spark.session import SparkSession
+        s = SparkSession.getActiveSession()
+        if s is not None:
+            v = s.conf.get("spark.ray.mi355x.fused_etl", None)
+    except Exception:  # noqa: BLE001
+        v = None
+    if v is None:
+        v = os.environ.get("RAYDP_FUSED_ETL", "1")
+    return str(v).lower() not in ("0", "false", "off", "no")
 
 
 def _skey(e) -> Optional[tuple]:
