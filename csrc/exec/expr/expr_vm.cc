@@ -106,6 +106,13 @@ template <typename To, typename From> inline To cvt(From x) {
   if constexpr (std::is_floating_point<From>::value && std::is_integral<To>::value &&
                 !std::is_same<To, uint8_t>::value) {
     return f2i<To>(x);
+  } else if constexpr (std::is_same<From, double>::value && std::is_same<To, float>::value) {
+    // IEEE round-to-nearest overflows to +-inf at FLT_MAX + half an ulp (2^103); the C++
+    // conversion of a value beyond float's range is undefined, so that case is spelled out
+    constexpr double kOver = 3.4028235677973366e38;   // FLT_MAX + 2^103
+    if (x >= kOver) return std::numeric_limits<float>::infinity();
+    if (x <= -kOver) return -std::numeric_limits<float>::infinity();
+    return static_cast<float>(x);
   } else if constexpr (std::is_same<To, uint8_t>::value) {
     return static_cast<uint8_t>(x != From(0));
   } else {
@@ -183,8 +190,11 @@ inline int64_t days_from_civil(int64_t y, int m, int d) {
 }
 
 // Neri & Schneider, "Euclidean affine functions and their application to calendar
-// algorithms" (2022): civil date from a day count with 32-bit multiply/shift only. Valid for
-// |days| < 2^29 (about +-1.4 million years); wider values take the 64-bit routine above.
+// algorithms" (2022): civil date from a day count with 32-bit multiply/shift only. With the
+// shift s = 82 it is exact for days in [-K, (2^32 - 3) / 4 - K] (K = 12,699,422: about 32,800
+// BC to 2.9 million AD); other values take the 64-bit routine above.
+constexpr int64_t kCivil32Lo = -12699422;
+constexpr int64_t kCivil32Hi = 1073741823LL - 12699422;
 struct Civil { int32_t y; int32_t m; int32_t d; int32_t doy; };
 inline Civil civil32(int32_t days) {
   constexpr uint32_t s = 82, K = 719468 + 146097 * s, L = 400 * s;
@@ -211,7 +221,7 @@ inline Civil civil32(int32_t days) {
 }
 
 inline Civil civil_any(int64_t days) {
-  if (days > -(int64_t(1) << 29) && days < (int64_t(1) << 29)) return civil32(int32_t(days));
+  if (days >= kCivil32Lo && days < kCivil32Hi) return civil32(int32_t(days));
   int64_t y; int m, d;
   civil(days, &y, &m, &d);
   return Civil{int32_t(y), m, d, int32_t(days - days_from_civil(y, 1, 1) + 1)};
@@ -219,7 +229,8 @@ inline Civil civil_any(int64_t days) {
 
 template <int F> inline int32_t dt_field(int64_t secs) {
   const int64_t days = floor_div(secs, 86400);
-  const int64_t sod = secs - days * 86400;
+  int64_t sod = secs % 86400;             // not secs - days * 86400: that overflows near INT64_MIN
+  if (sod < 0) sod += 86400;
   if constexpr (F == D_HOUR) return int32_t(sod / 3600);
   if constexpr (F == D_MINUTE) return int32_t((sod / 60) % 60);
   if constexpr (F == D_SECOND) return int32_t(sod % 60);
@@ -475,6 +486,22 @@ int elem_size(int type) { return type == T_BOOL ? 1 : (type == T_I32 || type == 
 }  // namespace
 
 extern "C" {
+
+// Calendar self-check (tests/test_sanitizers.py): the 32-bit civil path against the 64-bit one
+// over `n` day counts spread across [lo, hi]; returns the number of mismatching fields.
+int64_t rx_expr_calendar_check(int64_t lo, int64_t hi, int64_t n) {
+  int64_t bad = 0;
+  const double step = n > 1 ? double(hi - lo) / double(n - 1) : 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t days = lo + int64_t(step * double(k));
+    int64_t y; int m, d;
+    civil(days, &y, &m, &d);
+    const Civil c = civil_any(days);
+    const int64_t doy = days - days_from_civil(y, 1, 1) + 1;
+    bad += (c.y != int32_t(y)) + (c.m != m) + (c.d != d) + (c.doy != doy);
+  }
+  return bad;
+}
 
 // Runs `ncode` instructions over `nrows` input rows. Returns the number of output rows, or -1
 // on a malformed program. `sel_out` (nullable) receives the input row id of every output row.

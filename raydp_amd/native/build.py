@@ -106,7 +106,8 @@ def build_one(name: str, force: bool = False) -> str:
     return out
 
 
-SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+SANITIZERS = {"asan": ["-fsanitize=address,undefined,float-cast-overflow", "-fno-omit-frame-pointer",
+                        "-fno-sanitize-recover=undefined,float-cast-overflow"],
               "tsan": ["-fsanitize=thread"]}
 
 
@@ -129,6 +130,12 @@ def build_sanitized(kind: str, out_dir: str, names=("raydp_supervisor", "raydp_a
              [os.path.join(CSRC, "tests", "runtime_stress.cc"), os.path.join(CSRC, "runtime", "objstore.cc"),
               "-o", p, "-lpthread", "-lrt"])
         out["runtime_stress"] = p
+        # random well-typed programs through the fused expression VM (adversarial values)
+        p = os.path.join(out_dir, "expr_vm_fuzz")
+        _run([cxx, "-O1", "-g", "-std=c++17"] + flags + inc +
+             [os.path.join(CSRC, "tests", "expr_vm_fuzz.cc"), os.path.join(CSRC, "exec", "expr", "expr_vm.cc"),
+              "-o", p])
+        out["expr_vm_fuzz"] = p
     return out
 
 

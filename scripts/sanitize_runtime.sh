@@ -11,4 +11,5 @@ python -m raydp_amd.native.build --sanitize asan "$OUT/asan"
 python -m raydp_amd.native.build --sanitize tsan "$OUT/tsan"
 "$OUT/asan/runtime_stress" 4 3 3000
 "$OUT/tsan/runtime_stress" 4 1 2000
+"$OUT/asan/expr_vm_fuzz" 1000 1
 python -m pytest tests/test_sanitizers.py -q -p no:cacheprovider

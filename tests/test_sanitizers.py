@@ -2,6 +2,8 @@
 
 * the object-store / frame stress test (csrc/tests/runtime_stress.cc) built with
   AddressSanitizer+UBSan and with ThreadSanitizer, run with several threads and processes;
+* the fused expression VM driven by random well-typed programs (csrc/tests/expr_vm_fuzz.cc)
+  under AddressSanitizer+UBSan (incl. float-cast-overflow);
 * the supervisor, app master and shuffle service built with ASan+UBSan and driven through a
   protocol session (spawn / kill / restart, registration / restart remap / kill, map-output
   register / fd-passing fetch); their logs must hold no sanitizer report.
@@ -37,6 +39,18 @@ def test_runtime_stress_under_sanitizer(kind, args):
                        env=env)
     assert r.returncode == 0, r.stdout[-4000:]
     assert "store errors 0" in r.stdout and "Sanitizer" not in r.stdout
+
+
+def test_expression_vm_random_programs_under_asan_ubsan():
+    """csrc/tests/expr_vm_fuzz.cc: well-typed random programs of every opcode over adversarial
+    values (nulls, NaN/inf, INT_MIN, huge timestamps, zero divisors) and random filters; the
+    32-bit calendar path is checked against the 64-bit one over its whole range."""
+    exe = os.path.join(_built("asan"), "expr_vm_fuzz")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe, "250", "7"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert "calendar mismatches 0" in r.stdout and "runtime error" not in r.stdout
 
 
 def _no_reports(path):
