@@ -257,7 +257,8 @@ def main():
                        if res.metrics_history else None,
                        "rank0_breakdown_s": dict({k: round(v, 4) for k, v in LAST_TIMINGS.items()},
                                                  **{k: round(v, 4) for k, v in DRIVER_TIMINGS.items()},
-                                                 other=round(dt - sum(LAST_TIMINGS.values())
+                                                 other=round(dt - sum(v for k, v in LAST_TIMINGS.items()
+                                                                      if not k.endswith("_concurrent"))
                                                              - sum(DRIVER_TIMINGS.values()), 4))},
         }
         if world == 1 and not args.no_reference_config:

@@ -41,11 +41,68 @@ def _resolve(b) -> pa.Table:
     return b
 
 
+class DeferredDatasetError(RuntimeError):
+    """The computation behind a deferred Dataset failed; ``original`` is its exception. Trainers
+    pass it through untouched (no worker-group restart: rerunning the workers cannot fix the
+    input) and ``fit_on_spark`` re-raises ``original``."""
+
+    def __init__(self, original: BaseException):
+        super().__init__(f"dataset computation failed: {original!r}")
+        self.original = original
+
+
 class Dataset:
     def __init__(self, blocks: List[Union[ObjectRef, pa.Table]], schema: Optional[pa.Schema] = None):
-        self._blocks = list(blocks)
-        self._schema = schema
+        self._pending = None
+        self._blocks_ = list(blocks)
+        self._schema_ = schema
         self._tables: Optional[List[pa.Table]] = None
+
+    @classmethod
+    def deferred(cls, future) -> "Dataset":
+        """A Dataset whose blocks are still being produced: ``future`` (``concurrent.futures``)
+        yields a ``Dataset``. Ray Data datasets are lazy the same way; the estimators use it to
+        build the training engine while the Spark stage that fills the blocks runs on the
+        executors. Anything touching blocks or schema waits for the future."""
+        ds = cls([], None)
+        ds._pending = future
+        return ds
+
+    def _wait(self):
+        fut, self._pending = self._pending, None
+        try:
+            done = fut.result()
+        except BaseException as e:  # noqa: BLE001
+            self._pending = fut           # every later access reports the same failure
+            raise DeferredDatasetError(e) from e
+        self._blocks_, self._schema_ = done._blocks, done._schema
+
+    @property
+    def _blocks(self):
+        if self._pending is not None:
+            self._wait()
+        return self._blocks_
+
+    @_blocks.setter
+    def _blocks(self, v):
+        self._blocks_ = v
+
+    @property
+    def _schema(self):
+        if self._pending is not None:
+            self._wait()
+        return self._schema_
+
+    @_schema.setter
+    def _schema(self, v):
+        self._schema_ = v
+
+    def __getstate__(self):
+        # shipping a dataset to another process ships its resolved blocks
+        _ = self._blocks
+        d = dict(self.__dict__)
+        d["_pending"] = None
+        return d
 
     # ---------------------------------------------------------------- internals ----------
     def _get_tables(self) -> List[pa.Table]:

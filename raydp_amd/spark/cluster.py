@@ -42,6 +42,14 @@ EXECUTOR_RESOURCE_PREFIX = "spark.ray.raydp_spark_executor.actor.resource."
 LEGACY_ACTOR_CPU = "spark.ray.actor.resource.cpu"
 MASTER_SUFFIX = "_SPARK_MASTER"
 _TRACE = bool(__import__("os").environ.get("RAYDP_TRACE_STAGES"))
+# per-thread ``on_wait()`` callback: called each time a stage has its tasks in flight and the
+# dispatching thread is about to block on them (fit_on_spark's overlapped conversion uses it to
+# start building the training engine only once the driver-side stage work is done)
+_dispatch_hooks = threading.local()
+
+
+def set_dispatch_hook(fn) -> None:
+    _dispatch_hooks.on_wait = fn
 
 
 def _seconds(v) -> float:
@@ -259,6 +267,9 @@ class ExecutorTaskScheduler(P.TaskScheduler):
             if not inflight:
                 time.sleep(0.01)
                 continue
+            hook = getattr(_dispatch_hooks, "on_wait", None)
+            if hook is not None:
+                hook()
             done, _ = cf.wait(list(inflight), return_when=cf.FIRST_COMPLETED,
                               timeout=self.locality_wait if todo and prefs else None)
             for f in done:

@@ -13,6 +13,7 @@ instead of being silently dropped (:163).
 """
 import copy
 import inspect
+from concurrent.futures import wait as cf_wait
 import os
 import time
 import tempfile
@@ -30,8 +31,28 @@ from raydp_amd.train.checkpoint import Checkpoint, TorchCheckpoint
 from raydp_amd.train.config import FailureConfig, RunConfig, ScalingConfig
 from raydp_amd.train.trainer import TorchTrainer
 
-# wall-clock phase marks of the last fit in this process (bench / profiling)
+# wall-clock phase marks of the last fit in this process (bench / profiling); keys ending in
+# "_concurrent" ran beside the other phases and are not part of their sequential sum
 LAST_TIMINGS = {}
+_CONV_POOL = None
+
+
+def _conversion_pool():
+    global _CONV_POOL
+    if _CONV_POOL is None:
+        import concurrent.futures as cf
+        _CONV_POOL = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="raydp-conversion")
+    return _CONV_POOL
+
+
+class _Pick:
+    """Future-like view of one element of another future's tuple result."""
+
+    def __init__(self, fut, i):
+        self.fut, self.i = fut, i
+
+    def result(self):
+        return self.fut.result()[self.i]
 
 
 def _make_lr_schedule(opt_template: torch.optim.Optimizer, creator, config):
@@ -157,6 +178,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         engine = TorchEstimator._detached_fused_engine(config, device)
         if engine is not None:
             tracing.complete("worker setup", t_setup0, cat="train", engine=engine.name, detached=True)
+            LAST_TIMINGS["worker_setup"] = (time.time_ns() - t_setup0) / 1e9
             return TorchEstimator._train_loop(config, engine, 0, device)
         # model
         if isinstance(config["model"], torch.nn.Module):
@@ -232,6 +254,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                     sched.load_state_dict(torch.load(os.path.join(resume_dir, SCHED_KEY), weights_only=True))
             engine = TorchLoopEngine(model, optimizer, loss, metrics, device, config, sched)
         tracing.complete("worker setup", t_setup0, cat="train", engine=engine.name)
+        LAST_TIMINGS["worker_setup"] = (time.time_ns() - t_setup0) / 1e9
         return TorchEstimator._train_loop(config, engine, start_epoch, device)
 
     @staticmethod
@@ -268,6 +291,13 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         train_ds = session.get_dataset_shard("train")
         eval_ds = session.get_dataset_shard("evaluate") if config["evaluate"] else None
         engine.epoch = start_epoch          # epoch permutations continue where the run left off
+        t_wait0 = time.perf_counter()
+        deferred = [ds for ds in (train_ds, eval_ds) if getattr(ds, "_pending", None) is not None]
+        if deferred:   # fit_on_spark built this engine while the conversion stage ran
+            with tracing.span("conversion wait", cat="train"):
+                for ds in deferred:
+                    ds.num_blocks()
+            LAST_TIMINGS["conversion_wait"] = time.perf_counter() - t_wait0
         t_load0 = time.perf_counter()
         with tracing.span("ingest", cat="train", engine=engine.name):
             engine.load(train_ds, eval_ds, config)
@@ -388,36 +418,90 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                      fs_directory: Optional[str] = None, compression: Optional[str] = None,
                      stop_spark_after_conversion=False):
         from raydp_amd.utils import tracing
+        from raydp_amd.utils.config import get as conf_get
         t_conv0 = time.perf_counter()
+        for k in ("conversion_wait", "etl_and_conversion_concurrent"):
+            LAST_TIMINGS.pop(k, None)
+        if fs_directory is None and not stop_spark_after_conversion \
+                and conf_get("spark.ray.mi355x.overlap_conversion"):
+            # The Spark stage that materialises the blocks runs on the executors while this
+            # thread builds the training engine (device buffers, kernel load, parameter upload);
+            # the engine awaits the blocks at ingest (Dataset.deferred). The engine build starts
+            # once the driver-side stage work (plan, payload, dispatch) is done and the
+            # conversion thread is blocked on the executors, and the GIL switch interval is
+            # short meanwhile, so the two threads do not queue behind each other's Python.
+            import sys
+            import threading
+            from raydp_amd.data.dataset import Dataset, DeferredDatasetError
+            from raydp_amd.spark import cluster as spark_cluster
+            in_flight = threading.Event()
+
+            def convert():
+                t0 = time.perf_counter()
+                spark_cluster.set_dispatch_hook(in_flight.set)
+                try:
+                    with tracing.span("etl + conversion", cat="etl"):
+                        out = self._convert_via_store(train_df, evaluate_df, None)
+                finally:
+                    spark_cluster.set_dispatch_hook(None)
+                    in_flight.set()
+                LAST_TIMINGS["etl_and_conversion_concurrent"] = time.perf_counter() - t0
+                return out
+            switch = sys.getswitchinterval()
+            sys.setswitchinterval(min(switch, 2e-4))
+            try:
+                fut = _conversion_pool().submit(convert)
+                train_ds = Dataset.deferred(_Pick(fut, 0))
+                evaluate_ds = Dataset.deferred(_Pick(fut, 1)) if evaluate_df is not None else None
+                in_flight.wait()
+                LAST_TIMINGS["etl_and_conversion"] = time.perf_counter() - t_conv0
+                try:
+                    return self.fit(train_ds, evaluate_ds, max_retries)
+                except DeferredDatasetError as e:
+                    raise e.original from None
+                finally:
+                    cf_wait([fut])     # never leave a stage running behind a failed fit
+            finally:
+                sys.setswitchinterval(switch)
         with tracing.span("etl + conversion", cat="etl"):
-            super().fit_on_spark(train_df, evaluate_df)
-            train_df = self._check_and_convert(train_df)
-            evaluate_ds = None
-            if fs_directory is not None:
-                from raydp_amd.spark.dataset import read_spark_parquet
-                app_id = train_df.sparkSession.sparkContext.applicationId
-                path = fs_directory.rstrip("/") + f"/{app_id}"
-                train_df.write.parquet(path + "/train", compression=compression)
-                train_ds = read_spark_parquet(path + "/train")
-                if evaluate_df is not None:
-                    evaluate_df = self._check_and_convert(evaluate_df)
-                    evaluate_df.write.parquet(path + "/test", compression=compression)
-                    evaluate_ds = read_spark_parquet(path + "/test")
+            if fs_directory is None:
+                from raydp_amd.spark.dataset import get_raydp_master_owner
+                owner = get_raydp_master_owner(train_df.sparkSession) if stop_spark_after_conversion else None
+                train_ds, evaluate_ds = self._convert_via_store(train_df, evaluate_df, owner)
             else:
-                from raydp_amd.spark.dataset import (get_raydp_master_owner,
-                                                     spark_dataframe_to_ray_dataset)
-                owner = None
-                if stop_spark_after_conversion:
-                    owner = get_raydp_master_owner(train_df.sparkSession)
-                train_ds = spark_dataframe_to_ray_dataset(train_df, owner=owner)
-                if evaluate_df is not None:
-                    evaluate_df = self._check_and_convert(evaluate_df)
-                    evaluate_ds = spark_dataframe_to_ray_dataset(evaluate_df, owner=owner)
+                train_ds, evaluate_ds = self._convert_via_parquet(train_df, evaluate_df, fs_directory,
+                                                                  compression)
         LAST_TIMINGS["etl_and_conversion"] = time.perf_counter() - t_conv0
         if stop_spark_after_conversion:
             from raydp_amd.context import stop_spark
             stop_spark(cleanup_data=False)
         return self.fit(train_ds, evaluate_ds, max_retries)
+
+    def _convert_via_store(self, train_df, evaluate_df, owner):
+        from raydp_amd.spark.dataset import spark_dataframe_to_ray_dataset
+        super().fit_on_spark(train_df, evaluate_df)
+        train_df = self._check_and_convert(train_df)
+        train_ds = spark_dataframe_to_ray_dataset(train_df, owner=owner)
+        evaluate_ds = None
+        if evaluate_df is not None:
+            evaluate_df = self._check_and_convert(evaluate_df)
+            evaluate_ds = spark_dataframe_to_ray_dataset(evaluate_df, owner=owner)
+        return train_ds, evaluate_ds
+
+    def _convert_via_parquet(self, train_df, evaluate_df, fs_directory, compression):
+        from raydp_amd.spark.dataset import read_spark_parquet
+        super().fit_on_spark(train_df, evaluate_df)
+        train_df = self._check_and_convert(train_df)
+        evaluate_ds = None
+        app_id = train_df.sparkSession.sparkContext.applicationId
+        path = fs_directory.rstrip("/") + f"/{app_id}"
+        train_df.write.parquet(path + "/train", compression=compression)
+        train_ds = read_spark_parquet(path + "/train")
+        if evaluate_df is not None:
+            evaluate_df = self._check_and_convert(evaluate_df)
+            evaluate_df.write.parquet(path + "/test", compression=compression)
+            evaluate_ds = read_spark_parquet(path + "/test")
+        return train_ds, evaluate_ds
 
     def get_model(self):
         assert self._trainer is not None, "Must call fit first"

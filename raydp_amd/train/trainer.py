@@ -254,8 +254,11 @@ class DataParallelTrainer:
         ctx = S.TrainContext(rank, world, local, world, 0, device, "raydp", storage)
         sess = S._Session(ctx, shards, reporter, storage, self.resume)
         S._set_session(sess)
+        from raydp_amd.data.dataset import DeferredDatasetError
         try:
             self.fn(self.config) if _accepts_arg(self.fn) else self.fn()
+        except DeferredDatasetError:
+            raise     # the input failed to materialise: restarting the workers cannot fix it
         except Exception as e:  # noqa: BLE001
             raise _WorkerFailure(traceback.format_exc()) from e
         finally:

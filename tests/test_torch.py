@@ -87,3 +87,78 @@ def test_fused_trainer_rejects_mismatched_operands_on_host():
         tr._check_operands(feats.float(), labels, 32)  # wrong dtype
     with pytest.raises(ValueError):
         tr._check_operands(feats, labels, 32, perm=torch.arange(16, dtype=torch.int32))
+
+
+def _tiny_df(spark, n=512):
+    import numpy as np
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(n, 2))
+    rows = [(float(a), float(b), float(3 * a - 2 * b + 1)) for a, b in x]
+    return spark.createDataFrame(rows, ["x", "y", "z"])
+
+
+def _fit_linear(df, **kw):
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(2, 8), torch.nn.ReLU(), torch.nn.Linear(8, 1))
+    est = TorchEstimator(num_workers=1, model=model, optimizer=torch.optim.Adam(model.parameters(), lr=1e-2),
+                         loss=torch.nn.MSELoss(), feature_columns=["x", "y"], feature_types=torch.float,
+                         label_column="z", label_type=torch.float, batch_size=64, num_epochs=2,
+                         use_gpu=False, shuffle_seed=7, **kw)
+    est.fit_on_spark(df)
+    return est
+
+
+def test_overlapped_conversion_matches_sequential(spark_on_ray_small, monkeypatch):
+    """fit_on_spark builds the engine while the conversion stage runs (Dataset.deferred); the
+    trained model is the same as with the conversion finished first."""
+    from raydp_amd.torch.estimator import LAST_TIMINGS
+    df = _tiny_df(spark_on_ray_small)
+    monkeypatch.setenv("RAYDP_OVERLAP_CONVERSION", "0")
+    a = _fit_linear(df)
+    assert "conversion_wait" not in LAST_TIMINGS
+    monkeypatch.setenv("RAYDP_OVERLAP_CONVERSION", "1")
+    b = _fit_linear(df)
+    assert "conversion_wait" in LAST_TIMINGS and "etl_and_conversion_concurrent" in LAST_TIMINGS
+    sa, sb = a.get_model().state_dict(), b.get_model().state_dict()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    ha = [h["train_loss"] for h in a.results.metrics_history if "train_loss" in h]
+    hb = [h["train_loss"] for h in b.results.metrics_history if "train_loss" in h]
+    assert ha == hb
+
+
+def test_deferred_conversion_failure_is_raised_once(spark_on_ray_small, monkeypatch):
+    """A conversion that fails surfaces as its own error from fit_on_spark, without the
+    trainer's worker-group restarts (max_retries) rerunning the workers."""
+    from pyspark.sql.functions import col, udf
+    from raydp_amd.data.dataset import Dataset, DeferredDatasetError
+    from raydp_amd.train.trainer import TrainingFailedError
+    monkeypatch.setenv("RAYDP_OVERLAP_CONVERSION", "1")
+
+    @udf("double")
+    def boom(v):
+        raise ValueError("bad row")
+    df = _tiny_df(spark_on_ray_small, 64).withColumn("x", boom(col("x")))
+    calls = []
+
+    def model_creator(config):
+        calls.append(1)
+        return torch.nn.Linear(2, 1)
+    est = TorchEstimator(num_workers=1, model=model_creator,
+                         optimizer=lambda m, c: torch.optim.SGD(m.parameters(), lr=0.1),
+                         loss=torch.nn.MSELoss(), feature_columns=["x", "y"], feature_types=torch.float,
+                         label_column="z", label_type=torch.float, batch_size=16, num_epochs=1,
+                         use_gpu=False)
+    with pytest.raises(Exception) as ei:
+        est.fit_on_spark(df, max_retries=3)
+    assert not isinstance(ei.value, (TrainingFailedError, DeferredDatasetError))
+    assert len(calls) == 1
+    # a deferred dataset reports the same failure on every access
+    import concurrent.futures as cf
+    f = cf.Future()
+    f.set_exception(KeyError("k"))
+    ds = Dataset.deferred(f)
+    for _ in range(2):
+        with pytest.raises(DeferredDatasetError) as e2:
+            ds.count()
+        assert isinstance(e2.value.original, KeyError)
