@@ -605,7 +605,8 @@ class FusedMLPTrainer:
     def state_dict_from_buffers(self, model: torch.nn.Module):
         """``model.state_dict()`` as :meth:`write_back` would leave it, built from the device
         buffers without touching ``model`` (whose modules the layout references): trained
-        entries are views of one host copy of each flat buffer, the rest are the module's own."""
+        entries and running statistics are views of one host copy of each flat buffer (two
+        storages in ``model.pt``), the rest are the module's own."""
         import collections
         names = {id(m): n for n, m in model.named_modules()}
         out = collections.OrderedDict(model.state_dict())
@@ -623,9 +624,9 @@ class FusedMLPTrainer:
         tracked = getattr(self, "_tracked_total", 0) + getattr(self, "_tracked_pending", 0)
         for bn, rm, rv in self.run_bufs:
             o = (rm.data_ptr() - base) // 4
-            out[key(bn, "running_mean")] = rs[o:o + rm.numel()].clone()
+            out[key(bn, "running_mean")] = rs[o:o + rm.numel()]
             o = (rv.data_ptr() - base) // 4
-            out[key(bn, "running_var")] = rs[o:o + rv.numel()].clone()
+            out[key(bn, "running_var")] = rs[o:o + rv.numel()]
             if bn.num_batches_tracked is not None:
                 out[key(bn, "num_batches_tracked")] = bn.num_batches_tracked + tracked
         return out

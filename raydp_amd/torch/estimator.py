@@ -29,6 +29,7 @@ from raydp_amd.torch.metrics import TorchMetric
 from raydp_amd.train import session
 from raydp_amd.train.checkpoint import Checkpoint, TorchCheckpoint
 from raydp_amd.train.config import FailureConfig, RunConfig, ScalingConfig
+from raydp_amd.train.fast_save import save_state_dict
 from raydp_amd.train.trainer import TorchTrainer
 
 # wall-clock phase marks of the last fit in this process (bench / profiling); keys ending in
@@ -105,7 +106,8 @@ def _report_epoch_checkpoint(engine, epoch: int):
     ckpt = None
     with tempfile.TemporaryDirectory() as d:
         if session.get_world_rank() == 0:
-            torch.save({k: v.detach().cpu() for k, v in engine.state_dict().items()}, os.path.join(d, "model.pt"))
+            save_state_dict({k: v.detach().cpu() for k, v in engine.state_dict().items()},
+                            os.path.join(d, "model.pt"))
             torch.save(engine.optimizer_state_dict(), os.path.join(d, OPTIM_KEY))
             sched = getattr(engine, "scheduler", None)
             if sched is not None:
@@ -345,7 +347,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                 # model.pt is written straight into a staging dir of the run's storage and
                 # renamed into place by report()
                 stage = session.staging_dir()
-                torch.save(states, os.path.join(stage, "model.pt"))
+                save_state_dict(states, os.path.join(stage, "model.pt"))
                 checkpoint = Checkpoint(stage, movable=True)
             session.report({}, checkpoint=checkpoint)
         LAST_TIMINGS["checkpoint"] = time.perf_counter() - t_ck0
