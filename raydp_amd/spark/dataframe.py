@@ -203,7 +203,15 @@ class DataFrame:
         self._session = session
         self._cached: Optional[P.MaterializedPlan] = None
         self._storage_level = None
-        self._id = uuid.uuid4().hex
+        self._id_ = None
+
+    @property
+    def _id(self) -> str:
+        # drawn on first use (persist / conversion): a chain of transformations builds dozens
+        # of intermediate DataFrames that never need one
+        if self._id_ is None:
+            self._id_ = uuid.uuid4().hex
+        return self._id_
 
     # ------------------------------------------------------------------ metadata ---------
     @property
@@ -776,7 +784,17 @@ def _hoist_windows(e):
                 return type(x)(out) if isinstance(x, tuple) else out
             return x
         return x
-    if isinstance(e, WindowExpr):
+    if isinstance(e, WindowExpr) or not _has_window(e):
         return e, []
     ne = walk(e)
     return (ne, found) if found else (e, [])
+
+
+def _has_window(x) -> bool:
+    if isinstance(x, WindowExpr):
+        return True
+    if isinstance(x, Expr):
+        return any(_has_window(v) for v in vars(x).values() if isinstance(v, (Expr, list, tuple)))
+    if isinstance(x, (list, tuple)):
+        return any(_has_window(v) for v in x if isinstance(v, (Expr, list, tuple)))
+    return False

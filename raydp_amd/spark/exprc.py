@@ -1371,13 +1371,37 @@ def _stype(e, schema: pa.Schema) -> pa.DataType:
     raise _Unsupported(type(e).__name__)
 
 
+_static_memo: Dict[tuple, object] = {}
+
+
 def static_schema(node) -> Optional[pa.Schema]:
-    """Output schema of a fusible operator from its child's schema, or None (execute it)."""
+    """Output schema of a fusible operator from its child's schema, or None (execute it).
+    Memoised on (structural key of the operator, child schema): a pipeline rebuilt by the same
+    code (every epoch / run of an ETL job) types each operator once."""
     rel = getattr(node, "rel", None)
     if rel is None:
         return None
+    cs = node.child.schema
+    k = _node_key(node)
+    if k is None:
+        return _static_schema(rel, cs)
+    # operators typed from the memo hand the SAME schema object to their parents, so the
+    # lookup goes by schema identity first (pa.Schema hashes all its fields on every call)
+    ent = _static_memo.get((k, id(cs)))
+    if ent is not None and ent[0] is cs:
+        return ent[1]
+    hit = _static_memo.get((k, cs), False)
+    if hit is False:
+        hit = _static_schema(rel, cs)
+        if len(_static_memo) > 8192:
+            _static_memo.clear()
+        _static_memo[(k, cs)] = hit
+    _static_memo[(k, id(cs))] = (cs, hit)
+    return hit
+
+
+def _static_schema(rel, cs) -> Optional[pa.Schema]:
     try:
-        cs = node.child.schema
         kind = rel[0]
         if kind == "filter":
             for p in rel[1]:
