@@ -1000,11 +1000,26 @@ class Program:
                     np.frombuffer(out_bufs[j], dtype=_NP[ct], count=m)
                 views[j] = v
             return v
+        stats = {}
+
+        def extremes(j):
+            # (argmin, argmax, min, max) of a numeric output slot, once per partition
+            st = stats.get(j)
+            if st is None:
+                v = view(j)
+                if v.dtype.kind in "biuf" and m:
+                    i0, i1 = _argmin(v), _argmax(v)
+                    st = (i0, i1, v[i0], v[i1])
+                else:
+                    st = ()
+                stats[j] = st
+            return st
         for k, (u, r, argix) in enumerate(self.taps):
             if any(a[0] == "o" and outs[a[1]].null_count for a in argix):
                 return None
             args = [view(a[1]) if a[0] == "o" else a[1] for a in argix]
-            if not self._verify(k, u, view(r), args, m):
+            ext = [extremes(a[1]) if a[0] == "o" else () for a in argix]
+            if not self._verify(k, u, view(r), args, m, ext):
                 _retire(u)
                 raise _Retry()
         cols, names = [], []
@@ -1023,17 +1038,27 @@ class Program:
             names.append(name)
         return pa.Table.from_arrays(cols, names=names)
 
-    def _verify(self, k, u, res: np.ndarray, args: list, m: int) -> bool:
-        """Python function vs VM result on spread rows plus every argument's extreme rows."""
+    def _verify(self, k, u, res: np.ndarray, args: list, m: int, ext: list) -> bool:
+        """Python function vs VM result. First partition of a call site: 64 spread rows plus
+        every argument's extreme rows. Later partitions: a few spread rows, plus the extreme
+        rows of every argument whose values leave the range already checked at this site."""
         if m == 0:
             return True
-        cnt = min(m, _VERIFY_FIRST if not self.verified[k] else _VERIFY_LATER)
+        first = not self.verified[k]
+        cnt = min(m, _VERIFY_FIRST if first else _VERIFY_LATER)
         idx = {(j * (m - 1)) // max(1, cnt - 1) for j in range(cnt)}
-        arrs = [a for a in args if isinstance(a, np.ndarray)]
-        for a in arrs:
-            if a.dtype.kind in "biuf":
-                idx.add(_argmin(a))
-                idx.add(_argmax(a))
+        seen = self.__dict__.setdefault("_ranges", {}).get(k)
+        grow = []
+        for j, e in enumerate(ext):
+            if not e:
+                continue
+            i0, i1, lo, hi = e
+            r = seen[j] if seen is not None else None
+            # NaN bounds compare False: such a partition always has its extremes checked
+            if first or r is None or not (r[0] <= lo and hi <= r[1]):
+                idx.add(i0)
+                idx.add(i1)
+                grow.append((j, lo, hi))
         f = u.func
         floating = res.dtype.kind == "f"
         cast = res.dtype.type
@@ -1050,6 +1075,12 @@ class Program:
         except Exception:  # noqa: BLE001 - the function fails on these rows: Arrow path decides
             return False
         self.verified[k] = True
+        if grow:
+            cur = list(seen) if seen is not None else [None] * len(ext)
+            for j, lo, hi in grow:
+                r = cur[j]
+                cur[j] = (lo, hi) if r is None else (min(r[0], lo), max(r[1], hi))
+            self._ranges[k] = cur
         return True
 
 

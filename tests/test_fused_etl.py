@@ -224,6 +224,32 @@ def test_udf_verification_retires_mismatching_udf(spark, monkeypatch):
     assert exprc.STATS["udf_retired"] > before
 
 
+def test_udf_verification_follows_new_value_ranges(spark, monkeypatch):
+    """Partitions inside the value range already checked at a call site only get spread rows
+    checked; a later partition that leaves that range has its extreme rows checked: the
+    mismatch (negative base) is caught there and the UDF retired."""
+    def _root2(x):          # its own function: retirement is remembered per function
+        return x ** 0.5
+    u = udf(_root2, "double")
+    good = np.linspace(1, 9, 200)
+    parts = [pa.table({"x": pa.array(good)}), pa.table({"x": pa.array(good[::-1].copy())}),
+             pa.table({"x": pa.array(np.concatenate([good[:150], [-4.0], good[150:]]))})]
+    monkeypatch.setenv("RAYDP_FUSED_ETL", "1")
+    before = exprc.STATS["udf_retired"]
+
+    def run(t):   # same chain structure: the same compiled program (and checked ranges) serves all
+        df = spark.createDataFrame(t).withColumn("r", u("x"))
+        return pa.concat_tables([df._plan.compute(i) for i in range(df._plan.num_partitions())])
+    for t in parts[:2]:
+        np.testing.assert_allclose(np.asarray(run(t).column("r")), np.sqrt(np.asarray(t.column("x"))))
+    assert exprc.STATS["udf_retired"] == before
+    fused = exprc.STATS["fused_partitions"]
+    assert fused > 0
+    with pytest.raises((TypeError, pa.ArrowInvalid)):
+        run(parts[2])
+    assert exprc.STATS["udf_retired"] > before
+
+
 def test_all_rows_filtered_and_empty_input(spark, monkeypatch):
     df = spark.createDataFrame(_table(seed=6)).filter(col("i32") > 1000).withColumn("z", col("f64") + 1)
     _same(df, monkeypatch)
