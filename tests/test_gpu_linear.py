@@ -167,3 +167,36 @@ def test_split_k_is_deterministic_and_exact(splits):
     ref = G.float().T @ X.float()
     assert _rel(outs[0][0], ref) < 1e-5
     assert _rel(outs[0][1], G.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_all_epilogues_ragged(splits):
+    """Every epilogue on ragged edges in every dimension (M, N, K not multiples of the 64-wide
+    tiles), bf16 and fp32 operands in both memory orientations, split and unsplit, against fp32
+    references of the bf16-rounded operands."""
+    from raydp_amd.ops import linear_ops as L
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K = 777, 333, 1000
+    X = torch.randn(M, K, device="cuda", generator=g)                        # fp32, ROW
+    W = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)     # bf16, ROW
+    b = torch.randn(N, device="cuda", generator=g)
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    y32 = torch.empty(M, N, device="cuda")
+    L.gemm(L.FWD, M, N, K, X, L.ROW, W, L.ROW, y, bias=b, relu=True, out2=y32, splits=splits)
+    ref = torch.relu(_bf(X) @ W.float().T + b)
+    assert _rel(y32, ref) < 1e-5 and _rel(y.float(), ref) < 1e-2
+    # dgrad: dX = (G W) * mask with W read transposed ([K][N] memory = RED)
+    G = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+    Wt = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)   # memory [N][K] = [red][rows]
+    mask = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    dx = torch.empty(M, K, device="cuda")
+    L.gemm(L.DGRAD, M, K, N, G, L.ROW, Wt, L.RED, dx, mask=mask, splits=splits)
+    ref = (G.float() @ Wt.float()) * (mask.float() > 0).float()
+    assert _rel(dx, ref) < 1e-5
+    # wgrad: dW = G^T X over the batch (both stored [batch][rows] = RED), bias-gradient row sums
+    Xb = torch.randn(M, K, device="cuda", generator=g)                       # fp32 RED operand
+    dW = torch.empty(K, N, device="cuda")
+    db = torch.empty(K, device="cuda")
+    L.gemm(L.WGRAD, K, N, M, Xb, L.RED, G, L.RED, dW, dbias=db, splits=splits)
+    assert _rel(dW, _bf(Xb).T @ G.float()) < 1e-5
+    assert _rel(db, _bf(Xb).sum(0)) < 1e-5
