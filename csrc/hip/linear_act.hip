@@ -355,13 +355,16 @@ extern "C" {
 int rx_lin_args_size() { return (int)sizeof(LinArgs); }
 int rx_lin_refresh_size() { return (int)sizeof(LinRefresh); }
 
-// Split-K factor for a problem: enough workgroups to keep several resident per CU (the K loop is
-// latency bound at these sizes), each split at least two 64-deep stages.
+// Split-K factor for a problem: about two workgroups per CU, each split at least four 64-deep
+// stages. Measured per DLRM tower GEMM (profiles/r2_linear_gemm_kernel_times.txt): the
+// split-K fix-up costs more than it hides once a problem has ~one tile per CU (the wide
+// forward / dgrad GEMMs run fastest unsplit), while the weight-gradient GEMMs (few output tiles,
+// K = batch) gain 2-3x from 2-8 splits.
 int rx_lin_splits(int M, int N, int K, int cus) {
   const long long tiles = (long long)((M + LIN_T - 1) / LIN_T) * ((N + LIN_T - 1) / LIN_T);
   const int nk = (K + LIN_T - 1) / LIN_T;
-  long long want = (4LL * cus + tiles - 1) / tiles;
-  long long mx = nk / 2;
+  long long want = (2LL * cus + tiles - 1) / tiles;
+  long long mx = nk / 4;
   if (want > mx) want = mx;
   if (want > 64) want = 64;
   return want < 1 ? 1 : (int)want;
