@@ -105,6 +105,9 @@ def save_state_dict(sd, path: str) -> bool:
         except Exception:  # noqa: BLE001
             pkl = None
         with _lock:
+            if len(_layouts) >= 256:        # bounded: layouts of long-gone models drop out
+                _layouts.clear()
+                _verified.clear()
             _layouts[key] = pkl
         if pkl is None:
             torch.save(sd, path)
