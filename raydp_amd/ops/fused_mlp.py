@@ -144,7 +144,7 @@ class FusedMLPTrainer:
             lds = _ru(lds + nbytes, 16)
             return start
 
-        d.r_lds_off = alloc(bp * (max_k + 8) * 2)
+        d.r_lds_off = alloc(bp * (max_k + 16) * 2)   # row stride max_k + RX_RPAD (csrc/hip/mlp_core.h)
         d.gt_lds_off = alloc(max_n * xs * 2)
         stat_total = sum(2 * dm[5] for dm in dims)
         d.stats_lds_off = alloc(stat_total * 4)
