@@ -157,9 +157,26 @@ def load_specialized(trainer) -> Optional[str]:
             _hip.check(_hip.lib().rx_jit_load(path.encode(), ctypes.byref(step), ctypes.byref(ev), ctypes.byref(ps),
                                               int(trainer.desc.lds_bytes)), "rx_jit_load")
             fns = (step.value, ev.value, ps.value)
+            if not _loaded:
+                import atexit
+                atexit.register(_unload_all)
             _loaded[path] = fns
     trainer.bufs.jit_step, trainer.bufs.jit_eval, trainer.bufs.jit_persist = fns
     return path
+
+
+def _unload_all():
+    """Interpreter exit: wait for the device, then unload the specialised modules (before the HIP
+    runtime's own teardown, which a profiling tool may already have finalised)."""
+    try:
+        import torch
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+        with _lock:
+            _hip.lib().rx_jit_unload_all()
+            _loaded.clear()
+    except Exception:  # noqa: BLE001 - best effort at exit
+        pass
 
 
 def precompile(model, optimizer, loss, batch_size: int, acc_thr=None) -> str:

@@ -13,7 +13,7 @@ REGEX="rx_jit_persist|mlp_persist|lin_gemm|arrow_ingest|ingest"
 i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $P --kernel-include-regex "$REGEX" --output-format csv -d $R/gpurun_out/pmc -o bench_p$i -- python3 $R/bench.py --steps 200 --warmup 5 --no-reference-config > $R/gpurun_out/pmc/bench_p$i.log 2>&1 || { echo "bench pass $i failed"; tail -5 $R/gpurun_out/pmc/bench_p$i.log; exit 1; }
+  RAYDP_MLP_COOPERATIVE=0 timeout -s KILL 150 rocprofv3 --pmc $P --kernel-include-regex "$REGEX" --output-format csv -d $R/gpurun_out/pmc -o bench_p$i -- python3 $R/bench.py --steps 200 --warmup 5 --no-reference-config > $R/gpurun_out/pmc/bench_p$i.log 2>&1 || { echo "bench pass $i failed"; tail -5 $R/gpurun_out/pmc/bench_p$i.log; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc $P --kernel-include-regex "$REGEX" --output-format csv -d $R/gpurun_out/pmc -o lin_p$i -- python3 $R/benchmarks/linear_gemm_bench.py --reps 3 > $R/gpurun_out/pmc/lin_p$i.log 2>&1 || { echo "lin pass $i failed"; tail -5 $R/gpurun_out/pmc/lin_p$i.log; exit 1; }
   echo "pass $i ok"
 done

@@ -15,6 +15,6 @@ if [ "$2" = bench ]; then
 else
   CMD="python3 $R/benchmarks/linear_gemm_bench.py --reps 3"
 fi
-timeout -s KILL 150 rocprofv3 --pmc $P --kernel-include-regex "$REGEX" --output-format csv -d $R/gpurun_out/pmc -o $2_p$1 -- $CMD > $R/gpurun_out/pmc/$2_p$1.log 2>&1
+RAYDP_MLP_COOPERATIVE=0 timeout -s KILL 150 rocprofv3 --pmc $P --kernel-include-regex "$REGEX" --output-format csv -d $R/gpurun_out/pmc -o $2_p$1 -- $CMD > $R/gpurun_out/pmc/$2_p$1.log 2>&1
 rc=$?
 echo "rc=$rc rows=$(wc -l < $R/gpurun_out/pmc/$2_p$1_counter_collection.csv)"
