@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--fused-sgd", action="store_true", help="apply the embedding SGD inside backward")
     ap.add_argument("--amp", action="store_true", help="bf16 autocast for the MLP towers")
     ap.add_argument("--model-parallel", action="store_true", help="sharded tables even on 1 GPU")
+    ap.add_argument("--graph", action="store_true",
+                    help="one GPU: replay the 8 steps of a data cycle from one captured HIP graph")
     ap.add_argument("--eager-mlp", action="store_true",
                     help="run the MLP towers as eager nn.Linear/ReLU instead of the fused MFMA kernels")
     args = ap.parse_args()
@@ -82,10 +84,20 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    graph, graph_err = None, None
+    if args.graph and not mp:
+        graph, graph_err = _capture_cycle(_graph_step(net, lossf, opt, dense, cats, y, args), opt, dev)
     barrier()
     t = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(i)
+    if graph is not None:
+        g, static_loss = graph
+        assert args.steps % 8 == 0, "--graph replays whole 8-step data cycles"
+        for _ in range(args.steps // 8):
+            g.replay()
+        loss = static_loss
+    else:
+        for i in range(args.steps):
+            loss = step(i)
     barrier()
     dt = time.perf_counter() - t
     if mp:
@@ -100,9 +112,49 @@ def main():
                           "embeddings": "table-wise sharded + all-to-all" if mp else "replicated fused",
                           "fused_sgd": args.fused_sgd, "amp": args.amp, "loss": float(loss),
                           "mlp": "eager torch" if args.eager_mlp else "fused MFMA towers (csrc/hip/linear_act.hip)",
-                          "tables": 26, "rows_per_table": args.rows_per_table, "scaling": "weak"}), flush=True)
+                          "tables": 26, "rows_per_table": args.rows_per_table, "scaling": "weak",
+                          "hip_graph": graph is not None, "graph_error": graph_err}), flush=True)
     if mp:
         dist.destroy_process_group()
+
+
+def _graph_step(net, lossf, opt, dense, cats, y, args):
+    """The training step of data slice k for capture: gradients are zeroed in place (a captured
+    memset) except on the cycle's first step, whose backward assigns them."""
+    def run(k, first):
+        s = k * args.batch
+        out = net(dense[s:s + args.batch], cats[s:s + args.batch])
+        loss = lossf(out.float(), y[s:s + args.batch])
+        if not first:
+            opt.zero_grad(set_to_none=False)
+        loss.backward()
+        opt.step()
+        return loss
+    return run
+
+
+def _capture_cycle(run, opt, dev):
+    """Capture the 8 steps of one data cycle into one graph; (graph, last loss) or the error."""
+    try:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):       # eager steps on a side stream first, as capture requires
+            for k in range(2):
+                run(k, False)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)    # the cycle's first captured backward assigns the grads
+        with torch.cuda.graph(g):
+            loss = None
+            for k in range(8):
+                loss = run(k, k == 0)
+        g.replay()
+        torch.cuda.synchronize(dev)
+        return (g, loss), None
+    except Exception as e:  # noqa: BLE001 - report and run eagerly
+        torch.cuda.synchronize(dev)
+        return None, repr(e)[:300]
 
 
 if __name__ == "__main__":

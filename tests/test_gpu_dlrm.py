@@ -106,3 +106,45 @@ def test_packed_row_gather_and_sgd_match_torch():
     sgd_rows_(W2, offs, idx, G, 0.1)
     torch.cuda.synchronize()
     assert torch.allclose(W2, ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("fused_sgd", [False, True])
+def test_dlrm_graph_cycle_matches_eager(fused_sgd):
+    """benchmarks/dlrm_bench.py --graph: one captured 8-step cycle replayed twice trains like 16
+    eager steps (fused towers, fused embeddings, SGD)."""
+    import importlib.util
+    import os
+    import types
+    from raydp_amd.models.dlrm import Dlrm
+    spec = importlib.util.spec_from_file_location(
+        "dlrm_bench", os.path.join(os.path.dirname(__file__), "..", "benchmarks", "dlrm_bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    dev = torch.device("cuda", 0)
+    args = types.SimpleNamespace(batch=256)
+    g = torch.Generator(device=dev).manual_seed(3)
+    dense = torch.randn(8 * 256, 13, device=dev, generator=g)
+    cats = torch.randint(0, 500, (8 * 256, 26), device=dev, generator=g)
+    y = torch.randint(0, 2, (8 * 256, 1), device=dev, generator=g).float()
+    lossf = torch.nn.BCEWithLogitsLoss()
+
+    def make():
+        torch.manual_seed(0)
+        m = Dlrm(13, [500] * 26, [64, 32], [128, 64, 1], 32,
+                 fused_embedding_sgd_lr=0.05 if fused_sgd else None, static_batch=True).to(dev)
+        return m, torch.optim.SGD([p for p in m.parameters() if p.requires_grad], lr=0.05)
+    # eager: 2 side-stream warm-up steps (as the capture does) + 16 steps
+    m_e, o_e = make()
+    run_e = bench._graph_step(m_e, lossf, o_e, dense, cats, y, args)
+    for k in range(2):
+        run_e(k, False)
+    for i in range(16):
+        o_e.zero_grad(set_to_none=True)
+        run_e(i % 8, True)
+    m_g, o_g = make()
+    graph, err = bench._capture_cycle(bench._graph_step(m_g, lossf, o_g, dense, cats, y, args), o_g, dev)
+    assert err is None, err
+    graph[0].replay()      # _capture_cycle replayed once already: 1 + 1 = 2 cycles = 16 steps
+    torch.cuda.synchronize()
+    for (n, a), (_, b) in zip(m_e.state_dict().items(), m_g.state_dict().items()):
+        assert torch.allclose(a.float(), b.float(), rtol=1e-3, atol=1e-4), n
