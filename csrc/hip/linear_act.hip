@@ -99,14 +99,14 @@ __device__ __forceinline__ uint4 lin_load8(const LinOperand& o, long long i, lon
 
 // The two 16-B chunks a thread stages for one operand tile: tile rows r0.., reduction k0..
 // (memory orientation: ROW -> (i, j) = (row, k); RED -> (i, j) = (k, row)).
-template <int F32>
+template <int F32, int LAY>
 __device__ __forceinline__ void lin_fetch(const LinOperand& o, long long r0, long long k0, long long R, long long Kd,
                                           int tid, uint4 (&v)[2]) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int c = tid + 256 * t;
     const int i = c >> 3, jc = (c & 7) * 8;
-    if (o.lay == LIN_ROW)
+    if (LAY == LIN_ROW)
       v[t] = lin_load8<F32>(o, r0 + i, k0 + jc, R, Kd);
     else
       v[t] = lin_load8<F32>(o, k0 + i, r0 + jc, Kd, R);
@@ -150,7 +150,10 @@ __device__ __forceinline__ float lin_bsum(const bf16x8& f) {
   return s;
 }
 
-template <int AF32, int BF32>
+// LA / LB: the operands' memory orientations as template constants (FWD: ROW x ROW, DGRAD:
+// ROW x RED, WGRAD: RED x RED), so the fragment reads compile to straight-line ds_reads the
+// scheduler can batch ahead of the MFMAs instead of layout branches between them.
+template <int AF32, int BF32, int LA, int LB>
 __global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
   __shared__ __attribute__((aligned(16))) u16 lds[2][2][LIN_T * LIN_S];  // [buffer][A|B]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -172,29 +175,28 @@ __global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
     for (int y = 0; y < 2; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float asum[2] = {0.f, 0.f};
 
-  uint4 va[2], vb[2];
-  if (nk > 0) {
-    lin_fetch<AF32>(a.a, m0, (long long)k_begin * LIN_T, a.M, a.K, tid, va);
-    lin_fetch<BF32>(a.b, n0, (long long)k_begin * LIN_T, a.N, a.K, tid, vb);
-    lin_stash(lds[0][0], tid, va);
-    lin_stash(lds[0][1], tid, vb);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
+  // Global -> register -> LDS pipeline two stages deep: while stage kt is multiplied out of LDS,
+  // stage kt+1 sits in one register set (loaded an iteration ago, stashed after the MFMAs) and
+  // stage kt+2's loads are in flight into the other set -- each load has two stages of MFMAs to
+  // arrive in. The loop is unrolled by two so the sets swap roles without register copies
+  // (a copy would wait for the loads it copies).
+  uint4 ra[2], rb[2], qa[2], qb[2];
+  auto fetch = [&](int kt, uint4 (&fa_)[2], uint4 (&fb_)[2]) {
+    lin_fetch<AF32, LA>(a.a, m0, (long long)(k_begin + kt) * LIN_T, a.M, a.K, tid, fa_);
+    lin_fetch<BF32, LB>(a.b, n0, (long long)(k_begin + kt) * LIN_T, a.N, a.K, tid, fb_);
+  };
+  auto stage = [&](int kt, uint4 (&sa)[2], uint4 (&sb)[2], uint4 (&la)[2], uint4 (&lb)[2]) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) {  // next stage's global loads overlap this stage's MFMAs
-      lin_fetch<AF32>(a.a, m0, (long long)(k_begin + kt + 1) * LIN_T, a.M, a.K, tid, va);
-      lin_fetch<BF32>(a.b, n0, (long long)(k_begin + kt + 1) * LIN_T, a.N, a.K, tid, vb);
-    }
+    if (kt + 2 < nk) fetch(kt + 2, la, lb);
     const u16* ia = lds[cur][0];
     const u16* ib = lds[cur][1];
 #pragma unroll
     for (int ks = 0; ks < LIN_T; ks += 32) {
       bf16x8 fa[2], fb[2];
 #pragma unroll
-      for (int x = 0; x < 2; ++x) fa[x] = lin_frag(ia, a.a.lay, wm * 32 + 16 * x, ks, lane);
+      for (int x = 0; x < 2; ++x) fa[x] = lin_frag(ia, LA, wm * 32 + 16 * x, ks, lane);
 #pragma unroll
-      for (int y = 0; y < 2; ++y) fb[y] = lin_frag(ib, a.b.lay, wn * 32 + 16 * y, ks, lane);
+      for (int y = 0; y < 2; ++y) fb[y] = lin_frag(ib, LB, wn * 32 + 16 * y, ks, lane);
 #pragma unroll
       for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -205,10 +207,21 @@ __global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
       }
     }
     if (kt + 1 < nk) {
-      lin_stash(lds[cur ^ 1][0], tid, va);
-      lin_stash(lds[cur ^ 1][1], tid, vb);
+      lin_stash(lds[cur ^ 1][0], tid, sa);
+      lin_stash(lds[cur ^ 1][1], tid, sb);
     }
     __syncthreads();
+  };
+  if (nk > 0) {
+    fetch(0, ra, rb);
+    lin_stash(lds[0][0], tid, ra);
+    lin_stash(lds[0][1], tid, rb);
+    if (nk > 1) fetch(1, ra, rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    stage(kt, ra, rb, qa, qb);                  // stash stage kt+1 from r*, load kt+2 into q*
+    if (kt + 1 < nk) stage(kt + 1, qa, qb, ra, rb);
   }
 
   if (a.splits > 1) {
@@ -238,13 +251,15 @@ __global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
-    __shared__ unsigned last_flag;
+    // the flag lives in the (now idle) operand images: a separate __shared__ word would push the
+    // block past 40 KiB of LDS and cost a fourth resident workgroup per CU
+    unsigned* last_flag = reinterpret_cast<unsigned*>(&lds[0][0][0]);
     if (tid == 0) {
       const unsigned done = __hip_atomic_fetch_add(a.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last_flag = done + 1 == (unsigned)a.splits;
+      *last_flag = done + 1 == (unsigned)a.splits;
     }
     __syncthreads();
-    if (!last_flag) return;
+    if (!*last_flag) return;
     const float* base = a.ws + (long long)tile * a.splits * TW;
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -382,14 +397,25 @@ int rx_lin_gemm(const LinArgs* a, hipStream_t stream) {
   if (a->splits > 1 && (a->ws == nullptr || a->counters == nullptr)) return -1;
   const dim3 grid((unsigned)((a->M + LIN_T - 1) / LIN_T), (unsigned)((a->N + LIN_T - 1) / LIN_T),
                   (unsigned)a->splits);
-  if (a->a.f32 && a->b.f32)
-    hipLaunchKernelGGL((lin_gemm_kernel<1, 1>), grid, dim3(256), 0, stream, *a);
-  else if (a->a.f32)
-    hipLaunchKernelGGL((lin_gemm_kernel<1, 0>), grid, dim3(256), 0, stream, *a);
-  else if (a->b.f32)
-    hipLaunchKernelGGL((lin_gemm_kernel<0, 1>), grid, dim3(256), 0, stream, *a);
-  else
-    hipLaunchKernelGGL((lin_gemm_kernel<0, 0>), grid, dim3(256), 0, stream, *a);
+#define RX_LIN_LAY(AF, BF)                                                                          \
+  if (a->a.lay == LIN_ROW && a->b.lay == LIN_ROW)                                                  \
+    hipLaunchKernelGGL((lin_gemm_kernel<AF, BF, LIN_ROW, LIN_ROW>), grid, dim3(256), 0, stream, *a); \
+  else if (a->a.lay == LIN_ROW)                                                                    \
+    hipLaunchKernelGGL((lin_gemm_kernel<AF, BF, LIN_ROW, LIN_RED>), grid, dim3(256), 0, stream, *a); \
+  else if (a->b.lay == LIN_ROW)                                                                    \
+    hipLaunchKernelGGL((lin_gemm_kernel<AF, BF, LIN_RED, LIN_ROW>), grid, dim3(256), 0, stream, *a); \
+  else                                                                                             \
+    hipLaunchKernelGGL((lin_gemm_kernel<AF, BF, LIN_RED, LIN_RED>), grid, dim3(256), 0, stream, *a);
+  if (a->a.f32 && a->b.f32) {
+    RX_LIN_LAY(1, 1)
+  } else if (a->a.f32) {
+    RX_LIN_LAY(1, 0)
+  } else if (a->b.f32) {
+    RX_LIN_LAY(0, 1)
+  } else {
+    RX_LIN_LAY(0, 0)
+  }
+#undef RX_LIN_LAY
   return (int)hipGetLastError();
 }
 
