@@ -139,9 +139,10 @@ register("spark.ray.mi355x.mlp_wgrad", "str", "opt",
 register("spark.ray.mi355x.mlp_persistent", "bool", True,
          "one GPU: run a whole fused-MLP epoch as one persistent launch with the optimizer beside the "
          "backward pass (csrc/hip/mlp_persist.h)", env="RAYDP_MLP_PERSISTENT")
-register("spark.ray.mi355x.mlp_persistent.cooperative", "bool", True,
+register("spark.ray.mi355x.mlp_persistent.cooperative", "bool", False,
          "launch the persistent epoch kernel cooperatively (the runtime admits it only when the whole "
-         "grid is resident); 0: plain launch after an occupancy check", env="RAYDP_MLP_COOPERATIVE")
+         "grid is resident); default: plain launch after this process checked the occupancy (same "
+         "speed; the cooperative queue's teardown faults at exit under rocprofv3)", env="RAYDP_MLP_COOPERATIVE")
 register("spark.ray.mi355x.fused_linear", "bool", True,
          "run Linear(+ReLU) towers of the DLRM-class models (TorchMlp) on the fused MFMA GEMM kernels "
          "(csrc/hip/linear_act.hip) instead of eager torch", env="RAYDP_FUSED_LINEAR")
