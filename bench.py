@@ -14,8 +14,20 @@ Each sample passes through ETL once (1 epoch). Data: synthetic NYCTaxi rows with
 reference generator's distributions (examples/random_nyctaxi.py), written to a per-rank CSV
 before timing. Weights: random init. Weak scaling: 64 rows/step/GPU.
 
-Launch: ``python bench.py --gpus 1 --steps K --warmup W`` or, for N GPUs,
-``torchrun --nproc-per-node N ... bench.py --gpus N``. Rank 0 prints ONE JSON line.
+Launch: ``python bench.py --gpus N --steps K --warmup W``. For N > 1 outside a torchrun job
+the script starts the N rank processes itself (fresh child processes, before any GPU call;
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set for each) and waits
+for them; under ``torchrun --nproc-per-node N ... bench.py --gpus N`` every rank runs directly.
+Rank 0 prints ONE JSON line.
+
+Topologies (``--topology``):
+* ``spmd`` (default): one process per GPU, each running the whole pipeline on its own rows
+  (own Spark session, own executors, own CSV) and training over RCCL/xGMI with its peers --
+  the way the driver's torchrun launch scales it;
+* ``estimator``: the reference's own topology (``python/raydp/torch/estimator.py:331-355``):
+  ONE driver process, ONE Spark session, ``TorchEstimator(num_workers=N)`` whose N worker
+  processes (one per GPU, spawned by the worker-group trainer and kept warm between fits, as
+  Ray's prestarted workers are) each ingest one equal shard of the converted dataset.
 """
 import argparse
 import json
@@ -88,8 +100,9 @@ def nyc_model(cols):
     return NYC_Model(cols)
 
 
-def run_pipeline(spark, csv_path, steps, world, storage, fused=True):
-    """One full fit_on_spark over a file holding exactly steps*BATCH rows."""
+def run_pipeline(spark, csv_path, steps, world, storage, fused=True, topology="spmd", gpu_share=1.0):
+    """One full fit_on_spark over a file holding exactly steps*BATCH rows (x world for the
+    estimator topology, whose one driver feeds every worker)."""
     import torch
     import torch.nn as nn
     from data_process import nyc_taxi_preprocess
@@ -105,12 +118,13 @@ def run_pipeline(spark, csv_path, steps, world, storage, fused=True):
     model = nyc_model(len(features))
     opt = torch.optim.Adam(model.parameters(), lr=0.001)
     DRIVER_TIMINGS.update(csv_schema=t1 - t0, plan_build=t2 - t1, model_init=time.perf_counter() - t2)
+    extra = {"spmd_local_shards": True} if topology == "spmd" else \
+        {"resources_per_worker": {"CPU": 1, "GPU": gpu_share}}
     est = TorchEstimator(num_workers=world, model=model, optimizer=opt, loss=nn.SmoothL1Loss(),
                          feature_columns=features, feature_types=torch.float,
                          label_column="fare_amount", label_type=torch.float, batch_size=BATCH,
                          num_epochs=1, metrics_name=["MeanAbsoluteError", "MeanSquaredError"],
-                         drop_last=True, spmd_local_shards=True, storage_path=storage,
-                         fused=fused, shuffle_seed=1234)
+                         drop_last=True, storage_path=storage, fused=fused, shuffle_seed=1234, **extra)
     res = est.fit_on_spark(data)
     return res
 
@@ -146,11 +160,59 @@ def run_reference_config(spark, storage, epochs=30):
     return wall, rows, res
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n: int) -> int:
+    """Start ranks 0..n-1 of this script as child processes (this process never touches the
+    GPU: no exec from a HIP-initialised process), wait for all of them, return the exit code
+    (the first failure's; the others are then stopped)."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in live:          # a dead rank leaves its peers in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3000)
     ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--topology", choices=["spmd", "estimator"], default="spmd",
+                    help="spmd: one pipeline per GPU rank; estimator: one driver + "
+                         "TorchEstimator(num_workers=N) (the reference topology)")
+    ap.add_argument("--gpu-share", type=float, default=1.0,
+                    help="estimator topology: GPUs per worker (< 1 rehearses N workers on fewer GPUs)")
     ap.add_argument("--no-fused", action="store_true")
     ap.add_argument("--no-reference-config", action="store_true",
                     help="skip the extra (untimed-by-the-driver) reference-config measurement")
@@ -158,11 +220,20 @@ def main():
                     help="cProfile the timed region (driver process) into this text file")
     args = ap.parse_args()
 
+    if args.topology == "estimator" and args.gpu_share < 1.0:
+        # workers sharing a card cannot form an RCCL ring: gloo bootstraps them (the gradient
+        # still rides the xGMI one-shot path between the processes)
+        os.environ.setdefault("RAYDP_TRAIN_BACKEND", "gloo")
+    if args.topology == "spmd" and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(self_launch(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
+    if args.topology == "estimator":
+        if world != 1:
+            raise SystemExit("--topology estimator runs as ONE driver process (it spawns the workers)")
+    elif world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     import torch
     import torch.distributed as dist
     # modulo: lets a rehearsal put several ranks on a 1-GPU box (RAYDP_BENCH_BACKEND=gloo)
@@ -174,6 +245,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
+    n_train = args.gpus if args.topology == "estimator" else world   # ranks that train
 
     import raydp  # noqa: F401 - API facade
     from raydp_amd import context, runtime
@@ -181,10 +253,13 @@ def main():
     tmp = tempfile.mkdtemp(prefix=f"raydp_bench_r{rank}_")
     warm_csv = os.path.join(tmp, "warm.csv")
     main_csv = os.path.join(tmp, "main.csv")
-    make_csv(warm_csv, max(1, args.warmup) * BATCH, 1000 + rank)
-    make_csv(main_csv, args.steps * BATCH, 2000 + rank)
+    rows_per = 1 if args.topology == "spmd" else n_train
+    make_csv(warm_csv, max(1, args.warmup) * BATCH * rows_per, 1000 + rank)
+    make_csv(main_csv, args.steps * BATCH * rows_per, 2000 + rank)
 
-    runtime.init(num_cpus=int(os.environ.get("RAYDP_BENCH_CPUS", "4")))
+    cpus = int(os.environ.get("RAYDP_BENCH_CPUS", "4"))
+    # estimator topology: one CPU per training worker on top of the executors'
+    runtime.init(num_cpus=cpus + (n_train if args.topology == "estimator" else 0))
     # one single-core executor process per CPU: Arrow ETL scales without sharing a GIL
     spark = context.init_spark(f"nyc-bench-r{rank}", int(os.environ.get("RAYDP_BENCH_CPUS", "4")), 1, "1G")
     spark.conf.set("spark.sql.session.timeZone", "UTC")
@@ -197,7 +272,8 @@ def main():
             torch.cuda.synchronize()
 
     # warmup: one full pipeline on W steps (compiles kernels, vectorises UDFs, warms caches)
-    run_pipeline(spark, warm_csv, args.warmup, world, storage, fused=not args.no_fused)
+    kw = dict(fused=not args.no_fused, topology=args.topology, gpu_share=args.gpu_share)
+    run_pipeline(spark, warm_csv, args.warmup, n_train, storage, **kw)
     # long-lived framework state (modules, plans, kernels) goes to the permanent GC generation:
     # a full collection over it costs ~100 ms and would land at random inside the timed region
     import gc
@@ -212,7 +288,7 @@ def main():
         prof.enable()
     t0 = time.perf_counter()
     with tracing.span("timed run", cat="bench"):
-        res = run_pipeline(spark, main_csv, args.steps, world, storage, fused=not args.no_fused)
+        res = run_pipeline(spark, main_csv, args.steps, n_train, storage, **kw)
         barrier()
     dt = time.perf_counter() - t0
     if prof is not None:
@@ -229,7 +305,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    samples = args.steps * BATCH * world
+    samples = args.steps * BATCH * n_train
     value = samples / dt
     engine = res.metrics_history[0].get("engine") if res.metrics_history else None
     from raydp_amd.torch.estimator import LAST_TIMINGS
@@ -238,7 +314,7 @@ def main():
             "metric": "end-to-end samples/sec (Spark ETL+train) NYCTaxi TorchEstimator",
             "value": round(value, 1),
             "unit": "samples/s",
-            "n_gpus": world,
+            "n_gpus": n_train,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt * 1000.0 / args.steps, 4),
@@ -248,8 +324,9 @@ def main():
             "dtype": "bf16",
             "data": "synthetic NYCTaxi CSV (examples/random_nyctaxi.py distributions), random-init weights",
             "config": {"model": "NYC_Model (examples/pytorch_nyctaxi.py, 48,513 params)",
-                       "global_batch": BATCH * world, "seq_len": None,
-                       "parallelism": f"dp{world}", "per_gpu_batch": BATCH, "epochs": 1,
+                       "global_batch": BATCH * n_train, "seq_len": None,
+                       "parallelism": f"dp{n_train}", "per_gpu_batch": BATCH, "epochs": 1,
+                       "topology": args.topology,
                        "engine": engine,
                        "allreduce": res.metrics_history[0].get("allreduce") if res.metrics_history else None,
                        "timed_region": "csv read+ETL+from_spark+shuffle+HBM ingest+train+checkpoint",
@@ -261,7 +338,7 @@ def main():
                                                                       if not k.endswith("_concurrent"))
                                                              - sum(DRIVER_TIMINGS.values()), 4))},
         }
-        if world == 1 and not args.no_reference_config:
+        if n_train == 1 and not args.no_reference_config:
             # the reference example's own config (untimed by the driver; reported alongside)
             run_reference_config(spark, storage, epochs=2)          # warm its shapes
             wall, rows, ref = run_reference_config(spark, storage)

@@ -33,6 +33,10 @@ def main():
     ap.add_argument("--model-parallel", action="store_true", help="sharded tables even on 1 GPU")
     ap.add_argument("--graph", action="store_true",
                     help="one GPU: replay the 8 steps of a data cycle from one captured HIP graph")
+    ap.add_argument("--eager-tail", action="store_true",
+                    help="torch SGD + nn.BCEWithLogitsLoss + sparse embedding gradients instead of the fused "
+                         "step tail (multi-tensor SGD writing the tower images, fused BCE, embedding SGD in "
+                         "backward: raydp_amd/ops/fused_optim.py)")
     ap.add_argument("--eager-mlp", action="store_true",
                     help="run the MLP towers as eager nn.Linear/ReLU instead of the fused MFMA kernels")
     args = ap.parse_args()
@@ -51,15 +55,18 @@ def main():
     torch.manual_seed(0)
     sizes = [args.rows_per_table] * 26
     lr = 0.01
+    fused_tail = not args.eager_tail
     model = Dlrm(13, sizes, [512, 128, 32], [1024, 1024, 512, 256, 1], 32,
-                 fused_embedding_sgd_lr=lr if args.fused_sgd else None, model_parallel=mp,
+                 fused_embedding_sgd_lr=lr if (args.fused_sgd or fused_tail) else None, model_parallel=mp,
                  static_batch=True).to(dev)
     net = model
     if mp:
         from raydp_amd.parallel.ddp import DistributedDataParallel
         net = DistributedDataParallel(model)
-    opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=lr)
-    lossf = torch.nn.BCEWithLogitsLoss()
+    from raydp_amd.ops.fused_optim import FusedBCEWithLogits, FusedSGD
+    opt_cls = FusedSGD if fused_tail else torch.optim.SGD
+    opt = opt_cls([p for p in model.parameters() if p.requires_grad], lr=lr)
+    lossf = FusedBCEWithLogits() if fused_tail else torch.nn.BCEWithLogitsLoss()
     n = args.batch * 8
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     dense = torch.randn(n, 13, device=dev, generator=g)
@@ -110,7 +117,8 @@ def main():
                           "n_gpus": world, "ms_per_step": round(dt * 1e3 / args.steps, 3),
                           "per_gpu_batch": args.batch, "steps": args.steps, "warmup": args.warmup,
                           "embeddings": "table-wise sharded + all-to-all" if mp else "replicated fused",
-                          "fused_sgd": args.fused_sgd, "amp": args.amp, "loss": float(loss),
+                          "fused_sgd": args.fused_sgd or fused_tail, "fused_tail": fused_tail,
+                          "amp": args.amp, "loss": float(loss),
                           "mlp": "eager torch" if args.eager_mlp else "fused MFMA towers (csrc/hip/linear_act.hip)",
                           "tables": 26, "rows_per_table": args.rows_per_table, "scaling": "weak",
                           "hip_graph": graph is not None, "graph_error": graph_err}), flush=True)

@@ -7,29 +7,41 @@
 // NYC model's whole gradient is 194 KB, so a ring is pure latency: 2*(N-1) link hops, each a
 // kernel-to-kernel hand-off. MI355X GPUs of a node are fully connected by xGMI (7 links per
 // GPU), so every rank can read every peer's gradient directly: one flag exchange, then each
-// rank sums the N buffers itself while it applies the optimizer (N-1 reads in parallel, one per
-// link). No extra launch, no staging copy.
+// rank sums the N buffers itself (N-1 reads in parallel, one per link). No staging copy.
 //
 // Memory: each rank owns one exchange region allocated uncached (hipDeviceMallocUncached, so
 // no L2 on either side holds a stale line) and exports it with hipIpcGetMemHandle:
-//   [slot 0: nf floats][slot 1: nf floats][flags: RX_XG_MAXR u32]
-// Step s writes its gradient into slot (s & 1) of its own region, then (in the consumer kernel)
-// publishes seq = s + base by storing it into flags[rank] of EVERY peer's region, waits until
-// its own flags[p] >= seq for every peer p, and reads slot (s & 1) of every region.
+//   [slot 0: nf floats][slot 1: nf floats][flags: RX_XG_MAXR u32][votes: 2 x RX_XG_MAXR u32]
+// Step s writes its gradient into slot (s & 1) of its own region, then publishes seq = s + base
+// by storing it into flags[rank] of EVERY peer's region, waits until its own flags[p] >= seq for
+// every peer p, and reads slot (s & 1) of every region.
 // Double buffering makes one flag round per step enough: rank r overwrites slot (s & 1) at step
-// s + 2 only after its consumer kernel of step s + 1 saw every peer's seq s + 1 flag, which
-// each peer publishes only after its step-s consumer kernel (the reads of slot (s & 1)) ended.
+// s + 2 only after its kernel of step s + 1 saw every peer's seq s + 1 flag, which each peer
+// publishes only after its step-s kernel (the reads of slot (s & 1)) ended.
 //
-// Every wait is bounded (spin_ticks of the 100 MHz wall clock): a missing peer sets *err and
-// the kernel returns instead of hanging the GPU; the host checks *err after the epoch.
+// One rendezvous per LAUNCH, not per workgroup: every workgroup counts itself in on a local
+// arrival word; the last one to arrive does the cross-rank flag exchange and then opens a local
+// "go" word the others spin on (rx_xg_grid_rendezvous). A 1 MiB bucket is one flag round.
+//
+// Sequence numbers: the fused step loop takes them on the host (rx_xg_take_seq); the stand-alone
+// all-reduce keeps them on the device (ctl[1], bumped by the launch's last workgroup), so its
+// launch arguments never change and a HIP graph can replay it. A communicator is used in one
+// of the two modes only (raydp_amd/ops/comm.py keys them apart).
+//
+// Every wait is bounded (spin_ticks of the 100 MHz wall clock): a missing peer sets ctl[0] and
+// the kernel returns instead of hanging the GPU; the host reads it with the epoch's metrics.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #define RX_XG_MAXR 16
 
+// ctl words (this rank's local device memory, zeroed at create)
+enum : int { kXgErr = 0, kXgDevSeq = 1, kXgArrive = 2, kXgGo = 3, kXgDone = 4, kXgCtlWords = 16 };
+
 struct XgDev {
   float* region[RX_XG_MAXR];  // region base of rank p, mapped into this process
-  unsigned* err;              // this rank's error word (device memory)
+  unsigned* err;              // == ctl + kXgErr
+  unsigned* ctl;              // local control words (kXg*)
   unsigned long long spin_ticks;
   int world, rank, nf;        // nf: floats per slot (multiple of 64)
   int pad_;
@@ -39,11 +51,21 @@ __device__ __forceinline__ unsigned* rx_xg_flags(const XgDev& x, int p) {
   return reinterpret_cast<unsigned*>(x.region[p] + 2 * (size_t)x.nf);
 }
 
-// Publish `seq` to every peer and wait for theirs. Call from ONE lane; the caller then
-// barriers its workgroup. Returns false on timeout (after setting *err).
+// vote words of rank p's region for a meeting of sequence seq (double-buffered by parity)
+__device__ __forceinline__ unsigned* rx_xg_votes(const XgDev& x, int p, unsigned seq) {
+  return rx_xg_flags(x, p) + RX_XG_MAXR * (1 + (int)(seq & 1u));
+}
+
+__device__ __forceinline__ void rx_xg_fail(const XgDev& x) {
+  __hip_atomic_store(x.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Publish `seq` to every peer and wait for theirs. Call from ONE lane. Returns false on timeout
+// (after setting *err).
 __device__ __forceinline__ bool rx_xg_rendezvous(const XgDev& x, unsigned seq) {
-  // my slot was written by the previous kernel (or by this rank's copy): make it visible to
-  // readers on other devices before they can see the flag
+  // my slot was written before this call (previous kernel, or this launch's workgroups before
+  // they counted themselves in): make it visible to readers on other devices before they can
+  // see the flag
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   for (int p = 0; p < x.world; ++p)
     if (p != x.rank)
@@ -54,7 +76,7 @@ __device__ __forceinline__ bool rx_xg_rendezvous(const XgDev& x, unsigned seq) {
     if (p == x.rank) continue;
     while ((int)(__hip_atomic_load(mine + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
       if ((unsigned long long)(wall_clock64() - t0) > x.spin_ticks) {
-        __hip_atomic_store(x.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        rx_xg_fail(x);
         return false;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -64,9 +86,51 @@ __device__ __forceinline__ bool rx_xg_rendezvous(const XgDev& x, unsigned seq) {
   return true;
 }
 
+// Launch-wide rendezvous: `nblocks` workgroups of this launch call it (all threads). The last
+// workgroup to arrive meets the peers; the others wait on the local go word. Returns false on
+// every workgroup when the exchange failed. All `nblocks` workgroups must be able to be
+// resident together (callers launch at most a few hundred small workgroups).
+__device__ __forceinline__ bool rx_xg_grid_rendezvous(const XgDev& x, unsigned seq, unsigned nblocks) {
+  __shared__ int ok_s;
+  __syncthreads();  // this workgroup's slot writes are done
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope) my part of the slot
+    const unsigned old = __hip_atomic_fetch_add(x.ctl + kXgArrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == nblocks - 1) {
+      __hip_atomic_store(x.ctl + kXgArrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = rx_xg_rendezvous(x, seq) ? 1 : 0;
+      // open the gate even on failure (the others read the error word next)
+      __hip_atomic_store(x.ctl + kXgGo, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const long long t0 = wall_clock64();
+      while ((int)(__hip_atomic_load(x.ctl + kXgGo, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
+        if ((unsigned long long)(wall_clock64() - t0) > x.spin_ticks) {
+          rx_xg_fail(x);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (system scope) the peers' slots
+    }
+    if (ok && __hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) ok = 0;
+    ok_s = ok;
+  }
+  __syncthreads();
+  return ok_s != 0;
+}
+
+// 16-byte system-coherent load from a (possibly peer-mapped) region: sc0|sc1, never a stale
+// line of this device's caches.
+__device__ __forceinline__ float4 rx_xg_load4(const float* base, size_t idx4) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7ffffff0, 0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(idx4 * 16), 0, 17);
+  return __builtin_bit_cast(float4, v);
+}
+
 // Sum of element idx of slot `par` over all ranks, always in rank order so every rank computes
-// bit-identical sums (replicas stay identical, as under DDP). Peer lines are read with
-// system-scope loads: they must come from the peer's memory, never from a cache here.
+// bit-identical sums (replicas stay identical, as under DDP).
 __device__ __forceinline__ float rx_xg_sum(const XgDev& x, int par, int idx) {
   const size_t off = (size_t)par * x.nf + idx;
   float s = 0.f;

@@ -6,9 +6,14 @@
 //   rx_xg_handle   -> 64-byte IPC handle of the region (exchanged over torch.distributed)
 //   rx_xg_open     -> map every peer's region (hipIpcOpenMemHandle, lazy peer access)
 // Use:
-//   rx_xg_allreduce            -> in-place sum of a device fp32 buffer (copy into slot, one kernel)
+//   rx_xg_allreduce            -> in-place sum of a device fp32 buffer: ONE kernel (copy into the
+//                                 slot, one launch-wide rendezvous, 16-B peer reads, sum), with
+//                                 its sequence number kept on the device: the launch is
+//                                 identical every call, so a HIP graph can capture and replay it
 //   rx_xg_devdesc/take_seq/slot -> the fused step loop (csrc/hip/fused_mlp.hip) reduces inside
-//                                 its optimizer kernel instead
+//                                 its optimizer kernel instead (host-side sequence numbers)
+//   rx_xg_vote                 -> epoch-end agreement for the fused loop: every rank's error word
+//                                 summed into a double the host reads with the epoch metrics
 //   rx_xg_error                -> nonzero once any wait timed out (a peer never arrived)
 //
 // Reference role: the small-bucket gradient all-reduce of DDP / Horovod
@@ -16,6 +21,7 @@
 // §2.11 K2 and §5.8 (one-shot P2P all-reduce for <= 1 MB buckets).
 #include "comm/xgmi.h"
 
+#include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -28,24 +34,91 @@ struct XgHost {
   hipIpcMemHandle_t handle;
   unsigned seq = 0;
   int device = 0;
+  bool host_seq = false;  // sequence numbers taken on the host (fused step loop) or on the device
   bool opened[RX_XG_MAXR] = {false};
 };
 
 constexpr int kThreads = 256;
-constexpr int kPerThread = 4;
+// Workgroups per launch: every one must be resident at once (the launch-wide rendezvous), also
+// when several ranks share one device in a rehearsal, and the work is xGMI-link bound, not
+// compute bound -- 128 x 256 threads keep ~2 MB of 16-B peer loads in flight.
+constexpr int kMaxBlocks = 128;
 
-__global__ __launch_bounds__(kThreads) void xg_reduce_kernel(XgDev x, float* __restrict__ out, int n, unsigned seq) {
-  __shared__ int ok;
-  if (threadIdx.x == 0) ok = rx_xg_rendezvous(x, seq) ? 1 : 0;
-  __syncthreads();
-  if (!ok) return;
+// In-place all-reduce of n floats. VEC: buf is 16-B aligned (n / 4 float4 plus a scalar tail),
+// otherwise scalar. Each element is owned by one thread in both phases (same grid-stride
+// mapping), so the rank's own contribution is re-read from buf before the thread overwrites
+// it with the sum.
+// hseq: the host-chosen sequence number of a host-sequenced communicator, or 0 (device-sequenced:
+// the number is ctl[kXgDevSeq] + 1 and this launch's last workgroup stores it back).
+template <bool VEC>
+__global__ __launch_bounds__(kThreads) void xg_allreduce_kernel(XgDev x, float* __restrict__ buf, int n,
+                                                                unsigned hseq, float scale) {
+  const unsigned seq =
+      hseq ? hseq : __hip_atomic_load(x.ctl + kXgDevSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const int par = (int)(seq & 1u);
-  const int base = blockIdx.x * kThreads * kPerThread + threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < kPerThread; ++k) {
-    const int idx = base + k * kThreads;
-    if (idx < n) out[idx] = rx_xg_sum(x, par, idx);
+  float* mine = x.region[x.rank] + (size_t)par * x.nf;
+  const int stride = gridDim.x * kThreads;
+  const int t = blockIdx.x * kThreads + threadIdx.x;
+  if (VEC) {
+    const int n4 = n >> 2;
+    const int tail = n & 3;
+    for (int i = t; i < n4; i += stride) reinterpret_cast<float4*>(mine)[i] = reinterpret_cast<const float4*>(buf)[i];
+    if (blockIdx.x == 0 && threadIdx.x < tail) mine[(n4 << 2) + threadIdx.x] = buf[(n4 << 2) + threadIdx.x];
+    if (!rx_xg_grid_rendezvous(x, seq, gridDim.x)) return;
+    for (int i = t; i < n4; i += stride) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int p = 0; p < x.world; ++p) {   // rank order: bit-identical sums on every rank
+        const float4 v = p == x.rank ? reinterpret_cast<const float4*>(buf)[i]
+                                     : rx_xg_load4(x.region[p] + (size_t)par * x.nf, (size_t)i);
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+      }
+      s.x *= scale;
+      s.y *= scale;
+      s.z *= scale;
+      s.w *= scale;
+      reinterpret_cast<float4*>(buf)[i] = s;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < tail) {
+      const int i = (n4 << 2) + threadIdx.x;
+      buf[i] = rx_xg_sum(x, par, i) * scale;
+    }
+  } else {
+    for (int i = t; i < n; i += stride) mine[i] = buf[i];
+    if (!rx_xg_grid_rendezvous(x, seq, gridDim.x)) return;
+    for (int i = t; i < n; i += stride) buf[i] = rx_xg_sum(x, par, i) * scale;
   }
+  // the launch's last workgroup advances the device sequence number for the next launch
+  if (hseq) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(x.ctl + kXgDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(x.ctl + kXgDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(x.ctl + kXgDevSeq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Epoch-end vote of the fused step loop: publish this rank's error word into every peer's vote
+// array, meet them (one flag round of sequence `seq`), and write the sum of all ranks' error
+// words (+1 if this meeting itself timed out) into *out. Every rank that completes the meeting
+// computes the same value.
+__global__ __launch_bounds__(64) void xg_vote_kernel(XgDev x, unsigned seq, double* out) {
+  if (threadIdx.x != 0) return;
+  const unsigned mine = __hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int p = 0; p < x.world; ++p)
+    __hip_atomic_store(rx_xg_votes(x, p, seq) + x.rank, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  double sum = 0.0;
+  if (rx_xg_rendezvous(x, seq)) {
+    for (int p = 0; p < x.world; ++p)
+      sum += (double)__hip_atomic_load(rx_xg_votes(x, x.rank, seq) + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    sum = 1.0 + (double)mine;
+  }
+  *out = sum;
 }
 
 }  // namespace
@@ -60,16 +133,17 @@ void* rx_xg_create(int world, int rank, int device, int n, double timeout_s) {
   XgHost* h = new XgHost();
   h->device = device;
   const int nf = (n + 63) & ~63;
-  h->bytes = (2 * (size_t)nf + RX_XG_MAXR) * sizeof(float);
+  h->bytes = (2 * (size_t)nf + 3 * RX_XG_MAXR) * sizeof(float);
   if (hipExtMallocWithFlags(&h->base, h->bytes, hipDeviceMallocUncached) != hipSuccess) {
     delete h;
     return nullptr;
   }
-  unsigned* err = nullptr;
-  if (hipMalloc(&err, 64) != hipSuccess || hipMemset(err, 0, 64) != hipSuccess ||
+  unsigned* ctl = nullptr;
+  if (hipMalloc(&ctl, kXgCtlWords * sizeof(unsigned)) != hipSuccess ||
+      hipMemset(ctl, 0, kXgCtlWords * sizeof(unsigned)) != hipSuccess ||
       hipMemset(h->base, 0, h->bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
       hipIpcGetMemHandle(&h->handle, h->base) != hipSuccess) {
-    if (err) (void)hipFree(err);
+    if (ctl) (void)hipFree(ctl);
     (void)hipFree(h->base);
     delete h;
     return nullptr;
@@ -80,7 +154,8 @@ void* rx_xg_create(int world, int rank, int device, int n, double timeout_s) {
   h->dev.world = world;
   h->dev.rank = rank;
   h->dev.nf = nf;
-  h->dev.err = err;
+  h->dev.ctl = ctl;
+  h->dev.err = ctl + kXgErr;
   h->dev.spin_ticks = (unsigned long long)(timeout_s * khz * 1000.0);
   h->dev.region[rank] = (float*)h->base;
   return h;
@@ -130,18 +205,64 @@ float* rx_xg_slot(void* ctx, int parity) {
   return (float*)h->base + (size_t)(parity & 1) * h->dev.nf;
 }
 
+// Switch a fresh communicator to host-side sequence numbers (before its first use): required by
+// the fused step loop (rx_xg_take_seq) and rx_xg_vote; rx_xg_allreduce then takes its number on
+// the host too (not graph-replayable).
+int rx_xg_set_host_seq(void* ctx, int on) {
+  ((XgHost*)ctx)->host_seq = on != 0;
+  return 0;
+}
+
+// Largest n rx_xg_allreduce takes: the slot.
+int rx_xg_max_floats(void* ctx) { return ((XgHost*)ctx)->dev.nf; }
+
+// In-place all-reduce of n floats on `stream`, times `scale` (1/world: an average with no
+// extra pass): one launch whose arguments depend only on (buf, n, scale), so a captured graph
+// replays it correctly.
+int rx_xg_allreduce_scaled(float* buf, int n, float scale, void* ctx, hipStream_t stream) {
+  XgHost* h = (XgHost*)ctx;
+  if (n < 0 || n > rx_xg_max_floats(ctx)) return -2;
+  if (n == 0) return 0;
+  if (h->dev.world == 1) {
+    if (scale == 1.0f) return 0;
+  }
+  const bool vec = (reinterpret_cast<uintptr_t>(buf) & 15u) == 0;
+  const long units = vec ? (long)(n >> 2) : (long)n;
+  // ~4 units per thread before the grid grows, at most kMaxBlocks (then grid-stride)
+  long blocks = (units + (long)kThreads * 4 - 1) / ((long)kThreads * 4);
+  if (blocks < 1) blocks = 1;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  const unsigned hseq = h->host_seq ? rx_xg_take_seq(ctx, 1) : 0u;
+  if (vec)
+    hipLaunchKernelGGL(xg_allreduce_kernel<true>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, buf, n,
+                       hseq, scale);
+  else
+    hipLaunchKernelGGL(xg_allreduce_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, buf,
+                       n, hseq, scale);
+  return (int)hipGetLastError();
+}
+
 // In-place all-reduce (sum) of n floats on `stream`.
 int rx_xg_allreduce(float* buf, int n, void* ctx, hipStream_t stream) {
+  return rx_xg_allreduce_scaled(buf, n, 1.0f, ctx, stream);
+}
+
+// Epoch-end agreement for host-sequenced users (the fused step loop): *out (device double) =
+// sum over ranks of their error words, or > 0 when this meeting timed out.
+int rx_xg_vote(void* ctx, double* out, hipStream_t stream) {
   XgHost* h = (XgHost*)ctx;
-  if (n > h->dev.nf) return -2;
-  if (h->dev.world == 1) return 0;
+  if (!h->host_seq) return -3;
+  if (h->dev.world == 1) return (int)hipMemsetAsync(out, 0, sizeof(double), stream);
   const unsigned seq = rx_xg_take_seq(ctx, 1);
-  float* slot = rx_xg_slot(ctx, (int)(seq & 1u));
-  hipError_t e = hipMemcpyAsync(slot, buf, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, stream);
-  if (e != hipSuccess) return (int)e;
-  const int blocks = (n + kThreads * kPerThread - 1) / (kThreads * kPerThread);
-  hipLaunchKernelGGL(xg_reduce_kernel, dim3(blocks), dim3(kThreads), 0, stream, h->dev, buf, n, seq);
+  hipLaunchKernelGGL(xg_vote_kernel, dim3(1), dim3(64), 0, stream, h->dev, seq, out);
   return (int)hipGetLastError();
+}
+
+// Test hook: set this rank's error word (as a peer timeout would).
+int rx_xg_set_error(void* ctx, int v) {
+  XgHost* h = (XgHost*)ctx;
+  const unsigned u = (unsigned)v;
+  return (int)hipMemcpy(h->dev.err, &u, sizeof(u), hipMemcpyHostToDevice);
 }
 
 int rx_xg_error(void* ctx) {
@@ -158,7 +279,7 @@ int rx_xg_destroy(void* ctx) {
   (void)hipDeviceSynchronize();
   for (int p = 0; p < h->dev.world; ++p)
     if (h->opened[p]) (void)hipIpcCloseMemHandle(h->dev.region[p]);
-  (void)hipFree(h->dev.err);
+  (void)hipFree(h->dev.ctl);
   (void)hipFree(h->base);
   delete h;
   return 0;

@@ -22,12 +22,23 @@ constexpr int kMaxF = 32;  // interaction rows (1 + tables), padded
 
 // ---------------------------------------------------------------- embeddings --------------
 // X[b][1 + t][:] = W[offsets[t] + idx[b][t]][:]   (one 16-B chunk of D per thread)
+// and, with `head`, X[b][0][:] = head[b][:] (the bottom-MLP output: the interaction input is
+// written whole by this one launch, no separate concat copy)
 __global__ __launch_bounds__(256) void emb_gather_kernel(const float* __restrict__ W, const long long* __restrict__ offs,
                                                          const long long* __restrict__ idx, float* __restrict__ X,
-                                                         int B, int T, int D, int F, long long total_rows, int col0) {
+                                                         const float* __restrict__ head, int B, int T, int D, int F,
+                                                         long long total_rows, int col0) {
   const int chunks = D >> 2;
   const long long n = (long long)B * T * chunks;
-  for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += (long long)gridDim.x * blockDim.x) {
+  const long long nh = head != nullptr ? (long long)B * chunks : 0;
+  for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n + nh; g += (long long)gridDim.x * blockDim.x) {
+    if (g >= n) {
+      const long long h = g - n;
+      const int c = (int)(h % chunks);
+      const long long b = h / chunks;
+      *reinterpret_cast<f32x4*>(X + (b * F) * D + 4 * c) = *reinterpret_cast<const f32x4*>(head + b * D + 4 * c);
+      continue;
+    }
     const int c = (int)(g % chunks);
     const long long bt = g / chunks;
     const int t = (int)(bt % T);
@@ -176,11 +187,13 @@ int grid_for(long long n) {
 
 extern "C" {
 
-int rx_emb_gather(const float* W, const long long* offs, const long long* idx, float* X, int B, int T, int D, int F,
-                  long long total_rows, hipStream_t s) {
+// head (nullable, [B, D] fp32, 16-B aligned rows): copied into X[b][0] by the same launch.
+int rx_emb_gather(const float* W, const long long* offs, const long long* idx, float* X, const float* head, int B,
+                  int T, int D, int F, long long total_rows, hipStream_t s) {
   if (D % 4 != 0 || F < T + 1) return -1;
-  hipLaunchKernelGGL(emb_gather_kernel, dim3(grid_for((long long)B * T * (D / 4))), dim3(256), 0, s, W, offs, idx, X, B,
-                     T, D, F, total_rows, 1);
+  const long long units = (long long)B * (T + (head != nullptr ? 1 : 0)) * (D / 4);
+  hipLaunchKernelGGL(emb_gather_kernel, dim3(grid_for(units)), dim3(256), 0, s, W, offs, idx, X, head, B, T, D, F,
+                     total_rows, 1);
   return (int)hipGetLastError();
 }
 
@@ -189,8 +202,8 @@ int rx_emb_gather(const float* W, const long long* offs, const long long* idx, f
 int rx_emb_gather_rows(const float* W, const long long* offs, const long long* idx, float* Y, int B, int T, int D,
                        long long total_rows, hipStream_t s) {
   if (D % 4 != 0) return -1;
-  hipLaunchKernelGGL(emb_gather_kernel, dim3(grid_for((long long)B * T * (D / 4))), dim3(256), 0, s, W, offs, idx, Y, B,
-                     T, D, T, total_rows, 0);
+  hipLaunchKernelGGL(emb_gather_kernel, dim3(grid_for((long long)B * T * (D / 4))), dim3(256), 0, s, W, offs, idx, Y,
+                     (const float*)nullptr, B, T, D, T, total_rows, 0);
   return (int)hipGetLastError();
 }
 

@@ -108,7 +108,11 @@ def rocm_built() -> bool:
 
 
 def _reduce_op(op):
-    return {Average: dist.ReduceOp.SUM, Sum: dist.ReduceOp.SUM, Adasum: dist.ReduceOp.SUM,
+    if op == Adasum:
+        # Adasum combines gradients by projection (not a sum): returning a sum instead would
+        # silently train a different algorithm
+        raise NotImplementedError("hvd.Adasum is not implemented; use op=hvd.Average or hvd.Sum")
+    return {Average: dist.ReduceOp.SUM, Sum: dist.ReduceOp.SUM,
             Min: dist.ReduceOp.MIN, Max: dist.ReduceOp.MAX, Product: dist.ReduceOp.PRODUCT}[op]
 
 
@@ -305,7 +309,8 @@ class _Fusion:
     def __init__(self, params: List[torch.nn.Parameter], threshold: int, op, compression, gscale):
         self.op, self.compression, self.gscale = op, compression, gscale
         self._sum = None
-        if op in (Average, Sum, Adasum):
+        _reduce_op(op)      # unsupported ops fail at wrap time, not mid-step
+        if op in (Average, Sum):
             from raydp_amd.ops.comm import BucketAllreduce
             self._sum = BucketAllreduce()   # one-shot xGMI for small fp32 buckets
         self.buckets: List[List[torch.nn.Parameter]] = []
@@ -339,20 +344,23 @@ class _Fusion:
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in ps]
         flat = torch.cat([g.reshape(-1) for g in grads])
         flat, ctx = self.compression.compress(flat)
+        scaled = False
         if self._sum is not None:
-            work = self._sum(flat)
+            # the average's 1/size rides in the one-shot kernel's sum pass (uncompressed fp32)
+            scaled = ctx is None and self._sum.routes_to_xgmi(flat)
+            work = self._sum(flat, self.gscale) if scaled else self._sum(flat)
         else:
             work = dist.all_reduce(flat, op=_reduce_op(self.op), async_op=True)
-        self.pending.append((b, flat, ctx, work))
+        self.pending.append((b, flat, ctx, work, scaled))
 
     def finish(self):
         for b in range(len(self.buckets)):   # buckets never completed (unused params)
             if self.ready[b] != len(self.buckets[b]) and not any(x[0] == b for x in self.pending):
                 self._launch(b)
-        for b, flat, ctx, work in self.pending:
+        for b, flat, ctx, work, scaled in self.pending:
             work.wait()
             flat = self.compression.decompress(flat, ctx)
-            if self.gscale != 1.0:
+            if self.gscale != 1.0 and not scaled:
                 flat.mul_(self.gscale)
             off = 0
             for p in self.buckets[b]:
@@ -378,6 +386,7 @@ def DistributedOptimizer(optimizer, named_parameters=None, compression=None, bac
         missing = [p for p in params if id(p) not in names]
         if missing:
             raise ValueError("named_parameters does not cover every optimizer parameter")
+    _reduce_op(op)
     threshold = int(os.environ.get("HOROVOD_FUSION_THRESHOLD", str(64 << 20)))
     world = size()
     gscale = (1.0 / world if op in (Average, Adasum) else 1.0)

@@ -94,15 +94,19 @@ class XgmiComm:
     mapping is unavailable (e.g. ranks on different hosts or GPUs hidden per process).
     """
 
-    def __init__(self, world: int, rank: int, device: int, nfloats: int, timeout_s: float = 30.0):
+    def __init__(self, world: int, rank: int, device: int, nfloats: int, timeout_s: float = 30.0,
+                 host_seq: bool = False):
         L = _hip.lib()
         L.rx_xg_create.restype = ctypes.c_void_p
         L.rx_xg_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double]
         L.rx_xg_take_seq.restype = ctypes.c_uint
         self.lib, self.world, self.rank, self.nfloats = L, world, rank, nfloats
+        self.host_seq = host_seq
         self.ctx = L.rx_xg_create(world, rank, device, nfloats, timeout_s)
         if not self.ctx:
             raise RuntimeError("rx_xg_create failed (uncached exchange region / IPC handle)")
+        L.rx_xg_set_host_seq(ctypes.c_void_p(self.ctx), int(host_seq))
+        self.max_floats = int(L.rx_xg_max_floats(ctypes.c_void_p(self.ctx)))
         self.fn_ptr = ctypes.cast(L.rx_xg_allreduce, ctypes.c_void_p)
 
     def handle(self) -> bytes:
@@ -117,11 +121,28 @@ class XgmiComm:
     def error(self) -> int:
         return int(self.lib.rx_xg_error(ctypes.c_void_p(self.ctx)))
 
-    def allreduce_(self, t) -> None:
-        """In-place sum of a contiguous fp32 CUDA tensor (numel <= nfloats) on the current stream."""
-        rc = self.lib.rx_xg_allreduce(ctypes.c_void_p(t.data_ptr()), t.numel(), ctypes.c_void_p(self.ctx),
-                                      _hip.stream_ptr(t.device))
+    def _inject_error(self) -> None:
+        """Test hook: mark this rank as having missed a peer (as a timed-out wait does)."""
+        self.lib.rx_xg_set_error(ctypes.c_void_p(self.ctx), 1)
+
+    def allreduce_(self, t, scale: float = 1.0) -> None:
+        """In-place sum (times ``scale``) of a contiguous fp32 CUDA tensor (numel <= max_floats)
+        on the current stream. A device-sequenced communicator (the default) launches the same
+        kernel with the same arguments every call, so the call may be captured into a HIP graph
+        and replayed."""
+        if t.numel() > self.max_floats:
+            raise ValueError(f"xGMI one-shot all-reduce of {t.numel()} floats > {self.max_floats}")
+        rc = self.lib.rx_xg_allreduce_scaled(ctypes.c_void_p(t.data_ptr()), t.numel(), ctypes.c_float(scale),
+                                             ctypes.c_void_p(self.ctx), _hip.stream_ptr(t.device))
         _hip.check(rc, "rx_xg_allreduce")
+
+    def vote(self, out) -> None:
+        """Epoch-end agreement (host-sequenced communicators): ``out`` (a device float64
+        element) becomes the sum of every rank's error word, > 0 when any rank -- or this
+        meeting -- timed out. Read it together with the epoch's metrics (one D2H copy)."""
+        rc = self.lib.rx_xg_vote(ctypes.c_void_p(self.ctx), ctypes.c_void_p(out.data_ptr()),
+                                 _hip.stream_ptr(out.device))
+        _hip.check(rc, "rx_xg_vote")
 
     def check(self):
         if self.error():
@@ -134,7 +155,8 @@ class XgmiComm:
             self.ctx = None
 
     @classmethod
-    def create(cls, nfloats: int, group=None, timeout_s: float = 30.0) -> Optional["XgmiComm"]:
+    def create(cls, nfloats: int, group=None, timeout_s: float = 30.0,
+               host_seq: bool = False) -> Optional["XgmiComm"]:
         import socket
 
         import torch
@@ -144,12 +166,15 @@ class XgmiComm:
         world, rank = dist.get_world_size(group), dist.get_rank(group)
         if world < 2 or world > 16:
             return None
-        key = ("xg", id(group) if group is not None else "world", int(nfloats))
+        if _XGMI_DISABLED:
+            return None
+        # the two sequencing modes share the flag words, so they never share a communicator
+        key = ("xg", id(group) if group is not None else "world", int(nfloats), bool(host_seq))
         if key in _cache:
             return _cache[key]
         comm, err = None, None
         try:
-            comm = cls(world, rank, torch.cuda.current_device(), nfloats, timeout_s)
+            comm = cls(world, rank, torch.cuda.current_device(), nfloats, timeout_s, host_seq)
             h = comm.handle()
         except Exception as e:  # noqa: BLE001
             err, h = repr(e), b""
@@ -185,11 +210,18 @@ class XgmiComm:
             return False
 
 
-def forget_xgmi(comm) -> None:
-    """Retire a communicator whose peers missed a deadline: later users get a fresh decision."""
+_XGMI_DISABLED = False
+
+
+def forget_xgmi(comm, disable: bool = True) -> None:
+    """Retire a communicator whose peers missed a deadline. ``disable``: no xGMI communicator
+    is created in this process any more (the retried fit runs over RCCL)."""
+    global _XGMI_DISABLED
     for k, v in list(_cache.items()):
         if v is comm:
             _cache.pop(k, None)
+    if disable:
+        _XGMI_DISABLED = True
 
 
 def _agree(ok: bool, group=None) -> bool:
@@ -202,7 +234,16 @@ def _agree(ok: bool, group=None) -> bool:
     return int(t.item()) == 0
 
 
-XG_BUCKET_MAX_BYTES = 1 << 20  # one-shot threshold (<= 1 MB buckets)
+XG_BUCKET_MAX_BYTES = 16 << 20  # largest one-shot bucket the communicator is sized for
+
+
+def oneshot_max_bytes() -> int:
+    """Buckets up to this many bytes take the one-shot kernel (``spark.ray.mi355x.allreduce.
+    oneshot_max_mb``, capped at the communicator's ``XG_BUCKET_MAX_BYTES``). One-shot: each rank
+    reads the N-1 peer buckets concurrently, one per xGMI link, so it moves S bytes per link
+    whatever N; a ring moves 2(N-1)/N x S through every hop and pays 2(N-1) hand-offs."""
+    from raydp_amd.utils.config import get as conf_get
+    return int(min(float(conf_get("spark.ray.mi355x.allreduce.oneshot_max_mb")) * (1 << 20), XG_BUCKET_MAX_BYTES))
 
 
 class _Done:
@@ -216,10 +257,11 @@ class _Done:
 
 
 class BucketAllreduce:
-    """Sum-all-reduce of gradient buckets for the DDP and Horovod wrappers.
+    """All-reduce of gradient buckets for the DDP and Horovod wrappers.
 
-    Buckets of at most ``XG_BUCKET_MAX_BYTES`` fp32 go through the one-shot xGMI kernel
-    (stream-ordered, latency-bound sizes); larger ones, other dtypes and non-RCCL groups use
+    fp32 buckets up to :func:`oneshot_max_bytes` go through the one-shot xGMI kernel
+    (stream-ordered, device-sequenced: capturable into a HIP graph, and the 1/world average
+    folded into the same pass); larger ones, other dtypes and non-RCCL groups use
     ``torch.distributed.all_reduce``. Construct it on every rank at the same point (it runs
     the collective xGMI set-up)."""
 
@@ -229,11 +271,13 @@ class BucketAllreduce:
         from raydp_amd.utils.config import get as conf_get
         self.group = group
         self.xg = None
+        self.limit = oneshot_max_bytes()
         try:
             # gloo groups qualify too when the tensors are on the GPU (a rehearsal with several
             # ranks per device): the peer regions are bootstrapped over whatever group is given
             if (dist.is_initialized() and dist.get_backend(group) in ("nccl", "gloo") and torch.cuda.is_available()
-                    and torch.cuda.is_initialized() and conf_get("spark.ray.mi355x.allreduce") != "rccl"):
+                    and torch.cuda.is_initialized() and conf_get("spark.ray.mi355x.allreduce") != "rccl"
+                    and self.limit > 0):
                 self.xg = XgmiComm.create(XG_BUCKET_MAX_BYTES // 4, group=group,
                                           timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
         except Exception:  # noqa: BLE001
@@ -241,20 +285,40 @@ class BucketAllreduce:
 
     @property
     def kind(self) -> str:
-        """What the buckets ride on: the one-shot xGMI kernel for buckets <= 1 MiB (when the peer
+        """What the buckets ride on: the one-shot xGMI kernel for small buckets (when the peer
         mapping is up) and torch.distributed (RCCL / gloo) for the rest."""
         import torch.distributed as dist
         base = f"torch.distributed:{dist.get_backend(self.group)}" if dist.is_initialized() else "none"
-        return f"xgmi_oneshot(<=1MiB)+{base}" if self.xg is not None else base
+        if self.xg is None:
+            return base
+        return f"xgmi_oneshot(<={self.limit / (1 << 20):g}MiB)+{base}"
 
     def routes_to_xgmi(self, flat) -> bool:
         import torch
         return (self.xg is not None and flat.is_cuda and flat.dtype == torch.float32 and flat.is_contiguous()
-                and flat.numel() * 4 <= XG_BUCKET_MAX_BYTES and not torch.cuda.is_current_stream_capturing())
+                and flat.numel() * 4 <= self.limit and flat.numel() <= self.xg.max_floats)
 
-    def __call__(self, flat):
+    def __call__(self, flat, scale: float = 1.0):
+        """Sum ``flat`` over ranks in place, times ``scale``. Returns a handle whose ``wait()``
+        orders the result before later work on the current stream."""
         import torch.distributed as dist
         if self.routes_to_xgmi(flat):
-            self.xg.allreduce_(flat)
+            self.xg.allreduce_(flat, scale)
             return _Done()
-        return dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if scale == 1.0:
+            return work
+        return _Scaled(work, flat, scale)
+
+
+class _Scaled:
+    def __init__(self, work, flat, scale):
+        self.work, self.flat, self.scale = work, flat, scale
+
+    def wait(self):
+        self.work.wait()
+        self.flat.mul_(self.scale)
+        return True
+
+    def is_completed(self):
+        return self.work.is_completed()

@@ -21,7 +21,7 @@ def _lib():
     L = _hip.lib()
     if not _bound:
         vp, i, f, ll = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_longlong
-        L.rx_emb_gather.argtypes = [vp, vp, vp, vp, i, i, i, i, ll, vp]
+        L.rx_emb_gather.argtypes = [vp, vp, vp, vp, vp, i, i, i, i, ll, vp]
         L.rx_emb_sgd.argtypes = [vp, vp, vp, vp, i, i, i, i, f, ll, vp]
         L.rx_emb_gather_rows.argtypes = [vp, vp, vp, vp, i, i, i, ll, vp]
         L.rx_emb_sgd_rows.argtypes = [vp, vp, vp, vp, i, i, i, f, ll, vp]
@@ -119,10 +119,13 @@ class _EmbedConcat(torch.autograd.Function):
         B, T = idx.shape
         D = weight.shape[1]
         X = torch.empty(B, T + 1, D, dtype=torch.float32, device=weight.device)
-        X[:, 0] = mlp_out
         idx = idx.contiguous().long()
-        _hip.check(_lib().rx_emb_gather(_p(weight), _p(offsets), _p(idx), _p(X), B, T, D, T + 1, weight.shape[0],
-                                        _hip.stream_ptr(weight.device)), "rx_emb_gather")
+        head = mlp_out.contiguous()
+        if head.shape != (B, D) or head.dtype != torch.float32:
+            raise ValueError(f"bottom-MLP output must be fp32 [{B}, {D}]")
+        # one launch writes the whole interaction input: X[:, 0] = mlp_out, X[:, 1:] = rows
+        _hip.check(_lib().rx_emb_gather(_p(weight), _p(offsets), _p(idx), _p(X), _p(head), B, T, D, T + 1,
+                                        weight.shape[0], _hip.stream_ptr(weight.device)), "rx_emb_gather")
         ctx.save_for_backward(weight, offsets, idx)
         ctx.fused_lr = fused_lr
         return X

@@ -456,9 +456,14 @@ class FusedMLPTrainer:
                 _hip.check(rc, "rx_opt_step")
         self.step_count += nsteps
         self.steps_in_epoch = nsteps
-        out = self._read_metrics()
         if xg is not None:
-            xg.check()
+            # epoch-end agreement over xGMI, read with the metrics (one D2H copy)
+            xg.vote(self.metrics[7:8])
+        out = self._read_metrics()
+        if xg is not None and out["xg_vote"] != 0.0:
+            from raydp_amd.exceptions import CollectiveError
+            raise CollectiveError("xGMI all-reduce: a peer did not arrive within the timeout "
+                                  f"(vote {out['xg_vote']:g})")
         return out
 
     def snapshot(self):
@@ -577,7 +582,8 @@ class FusedMLPTrainer:
         nb = max(m[4], 1.0)
         cnt = max(m[3], 1.0)
         return {"loss": float(m[0] / nb), "mae": float(m[1] / cnt), "mse": float(m[2] / cnt),
-                "acc": float(m[5] / cnt), "count": float(m[3]), "batches": float(m[4])}
+                "acc": float(m[5] / cnt), "count": float(m[3]), "batches": float(m[4]),
+                "xg_vote": float(m[7])}
 
     # ----------------------------------------------------------------------- state --------
     @torch.no_grad()

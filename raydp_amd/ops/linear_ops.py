@@ -262,12 +262,42 @@ class FusedLinearTower:
         self.out_f32 = out_f32
         self.images: List[Optional[torch.Tensor]] = [None] * len(self.linears)
         self._versions = [None] * len(self.linears)
+        # images the multi-tensor optimizer writes itself (raydp_amd/ops/fused_optim.py): not
+        # re-derived before a forward, not even inside a graph capture
+        self._managed = [False] * len(self.linears)
+        self._register()
+
+    def _register(self):
+        from raydp_amd.ops.fused_optim import register_image
+        for li, lin in enumerate(self.linears):
+            register_image(lin.weight, self, li)
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+        self._managed = [False] * len(self.linears)
+        self._register()
+
+    def image_for(self, li: int) -> torch.Tensor:
+        """The bf16 image buffer of layer ``li`` (allocated on first use)."""
+        w = self.linears[li].weight
+        img = self.images[li]
+        if img is None or img.device != w.device or img.shape != w.shape:
+            img = self.images[li] = torch.empty(w.shape, dtype=torch.bfloat16, device=w.device)
+            self._versions[li] = None
+        return img
+
+    def image_updated(self, li: int):
+        """The optimizer kernel just wrote layer ``li``'s image from the updated weight."""
+        w = self.linears[li].weight
+        self._versions[li] = (w.data_ptr(), w._version)
+        self._managed[li] = True
 
     def __getstate__(self):
         # device images are caches: a copied / pickled tower rebuilds them from its weights
         st = dict(self.__dict__)
         st["images"] = [None] * len(self.linears)
         st["_versions"] = [None] * len(self.linears)
+        st["_managed"] = [False] * len(self.linears)
         return st
 
     def _refresh_images(self):
@@ -282,7 +312,7 @@ class FusedLinearTower:
                 img = self.images[li] = torch.empty(w.shape, dtype=torch.bfloat16, device=w.device)
                 self._versions[li] = None
             key = (w.data_ptr(), w._version)
-            if self._versions[li] != key or capturing:
+            if self._versions[li] != key or (capturing and not self._managed[li]):
                 stale.append(li)
                 self._versions[li] = key
         if not stale:

@@ -4,17 +4,27 @@ Replaces the DDP that Ray Train's ``prepare_model`` applies in the reference
 (``python/raydp/torch/estimator.py:243``; collectives K1-K3 of SURVEY §2.11). Design for
 MI355X over RCCL/xGMI:
 
-* gradients are packed into flat buckets in *reverse* parameter order (the order backward
-  produces them); a bucket's all-reduce is launched asynchronously on the communication stream
-  the moment its last gradient is accumulated, so communication overlaps the rest of backward;
-* bucket size defaults to 32 MiB (``RAYDP_DDP_BUCKET_MB``): xGMI rings are per-link bound
-  (~153 GB/s per link), so fewer, larger messages amortise the ~10-20 µs collective latency;
+* gradients LIVE in flat buckets: every dense parameter's ``.grad`` is a view of its bucket
+  (reverse parameter order = the order backward produces them), so autograd accumulates
+  straight into the buffer that is all-reduced -- no per-step copy in, no copy back out. A
+  bucket's all-reduce is launched the moment its last gradient is accumulated, so
+  communication overlaps the rest of backward;
+* fp32 buckets up to ``spark.ray.mi355x.allreduce.oneshot_max_mb`` (16 MiB) ride the one-shot
+  xGMI kernel with the 1/world average folded into its sum pass; larger ones go to RCCL;
+* bucket size defaults to 32 MiB (``RAYDP_DDP_BUCKET_MB``): xGMI links are per-link bound
+  (~153 GB/s per link), so fewer, larger messages amortise the ~10-20 us collective latency;
   tiny models (NYC_Model: 194 KB) end up in one bucket = one collective per step;
-* averaging is folded into one ``div_`` on the flat bucket (not per tensor);
-* parameters and buffers are broadcast from rank 0 at wrap time; buffers (BatchNorm running
-  stats) are re-broadcast before each forward when ``broadcast_buffers`` (torch semantics).
+* parameters are broadcast from rank 0 at wrap time (one collective per bucket); replicated
+  floating-point buffers (BatchNorm running statistics) are re-pointed into one flat tensor
+  and re-broadcast before each forward with ONE collective (torch's ``broadcast_buffers``);
+* with every bucket and the buffer broadcast on the one-shot kernel (device-sequenced, no
+  host bookkeeping) the whole step can be captured into a HIP graph (``capturable()``;
+  ``raydp_amd/torch/graphs.py``).
+
+``zero_grad()`` zeroes the buckets in place (one fill per bucket) and keeps the views; an
+optimizer's ``zero_grad(set_to_none=True)`` is tolerated (the hook copies the fresh gradient
+into the bucket and re-points ``.grad``).
 """
-import os
 from typing import List
 
 import torch
@@ -31,9 +41,11 @@ class _Bucket:
         self.pending = len(params)
         self.work = None
         self.offsets = []
+        self.views = []
         off = 0
         for p in params:
             self.offsets.append(off)
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
             off += p.numel()
 
     def reset(self):
@@ -48,6 +60,7 @@ class DistributedDataParallel(nn.Module):
         self.module = module
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
+        self.rank = dist.get_rank(process_group)
         self.broadcast_buffers = broadcast_buffers
         from raydp_amd.utils.config import get as conf_get
         cap = float(bucket_cap_mb or conf_get("spark.ray.mi355x.ddp.bucket_mb")) * (1 << 20)
@@ -70,11 +83,8 @@ class DistributedDataParallel(nn.Module):
             if getattr(m, "_raydp_model_parallel", False):
                 local_ids.update(id(t) for t in list(m.parameters()) + list(m.buffers()))
         self._local_ids = local_ids
-        with torch.no_grad():
-            for t in list(module.parameters()) + list(module.buffers()):
-                if getattr(t, "_raydp_model_parallel", False) or id(t) in local_ids:
-                    continue
-                dist.broadcast(t.data, 0, group=process_group)
+        from raydp_amd.ops.comm import BucketAllreduce
+        self._allreduce = BucketAllreduce(process_group)
         # reverse order ~= gradient production order
         self.buckets: List[_Bucket] = []
         cur, size = [], 0
@@ -87,18 +97,61 @@ class DistributedDataParallel(nn.Module):
             size += nbytes
         if cur:
             self.buckets.append(_Bucket(cur))
+        self._broadcast_state(params)
         self._where = {}
         for bi, b in enumerate(self.buckets):
             for pi, p in enumerate(b.params):
                 self._where[p] = (bi, pi)
+                p.grad = b.views[pi]          # gradient-as-bucket-view (zeros)
                 p.register_post_accumulate_grad_hook(self._make_hook(p))
         for p in self.sparse_params:
             p.register_post_accumulate_grad_hook(self._sparse_hook)
         self._finalize_queued = False
         self.require_backward_grad_sync = True
-        from raydp_amd.ops.comm import BucketAllreduce
-        self._allreduce = BucketAllreduce(process_group)
 
+    # ------------------------------------------------------------------ wrap-time state
+    def _replicated(self, t) -> bool:
+        return not (getattr(t, "_raydp_model_parallel", False) or id(t) in self._local_ids)
+
+    @torch.no_grad()
+    def _broadcast_state(self, params):
+        """Rank 0's parameters and buffers everywhere (one collective per bucket of params, one
+        per buffer dtype). Floating-point replicated buffers are re-pointed into one flat
+        tensor per dtype so the per-forward broadcast is one collective."""
+        from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+        groups = {}
+        for p in params + [p for p in self.module.parameters() if p not in set(params)]:
+            if self._replicated(p):
+                groups.setdefault((p.dtype, p.device), []).append(p.data)
+        for ts in groups.values():
+            flat = _flatten_dense_tensors(ts)
+            dist.broadcast(flat, 0, group=self.pg)
+            for t, v in zip(ts, _unflatten_dense_tensors(flat, ts)):
+                t.copy_(v)
+        self._buf_flats = []     # (flat, [(module, name)]) per floating dtype
+        bufs = {}
+        for m in self.module.modules():
+            if getattr(m, "_raydp_model_parallel", False):
+                continue
+            for name, t in m._buffers.items():
+                if t is None or not self._replicated(t):
+                    continue
+                bufs.setdefault((t.dtype, t.device), []).append((m, name, t))
+        for (dtype, dev), ents in bufs.items():
+            ts = [t for _, _, t in ents]
+            flat = _flatten_dense_tensors(ts)
+            dist.broadcast(flat, 0, group=self.pg)
+            if dtype.is_floating_point:
+                off = 0
+                for m, name, t in ents:
+                    m._buffers[name] = flat[off:off + t.numel()].view_as(t)
+                    off += t.numel()
+                self._buf_flats.append(flat)
+            else:   # integer counters (num_batches_tracked) agree by construction after this
+                for (m, name, t), v in zip(ents, _unflatten_dense_tensors(flat, ts)):
+                    t.copy_(v)
+
+    # ------------------------------------------------------------------ hooks
     def _sparse_hook(self, param):
         if self.require_backward_grad_sync and not self._finalize_queued:
             self._finalize_queued = True
@@ -134,14 +187,18 @@ class DistributedDataParallel(nn.Module):
                 return
             bi, pi = self._where[param]
             b = self.buckets[bi]
-            off = b.offsets[pi]
-            b.flat[off:off + param.numel()].copy_(param.grad.reshape(-1))
+            view = b.views[pi]
+            if param.grad is not view:
+                # a fresh gradient tensor (the optimizer set .grad to None): move it into the
+                # bucket and re-point .grad, so the next steps accumulate in place
+                view.copy_(param.grad)
+                param.grad = view
             b.pending -= 1
             if not self._finalize_queued:
                 self._finalize_queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
             if b.pending == 0:
-                b.work = self._allreduce(b.flat)
+                b.work = self._allreduce(b.flat, 1.0 / self.world)
         return hook
 
     def _finalize(self):
@@ -153,28 +210,46 @@ class DistributedDataParallel(nn.Module):
                 # parameters unused in this forward: reduce the zeros they contributed
                 for pi, p in enumerate(b.params):
                     if p.grad is None:
-                        off = b.offsets[pi]
-                        b.flat[off:off + p.numel()].zero_()
-                b.work = self._allreduce(b.flat)
+                        b.views[pi].zero_()
+                        p.grad = b.views[pi]
+                b.work = self._allreduce(b.flat, 1.0 / self.world)
             b.work.wait()
-            b.flat.div_(self.world)
-            for pi, p in enumerate(b.params):
-                off = b.offsets[pi]
-                g = b.flat[off:off + p.numel()].view_as(p)
-                if p.grad is None:
-                    p.grad = g.clone()
-                else:
-                    p.grad.copy_(g)
             b.reset()
 
+    # ------------------------------------------------------------------ API
+    def zero_grad(self, set_to_none: bool = False):
+        """Zero every bucket in place (one fill per bucket); ``.grad`` stays a bucket view."""
+        for b in self.buckets:
+            b.flat.zero_()
+            for pi, p in enumerate(b.params):
+                if p.grad is not b.views[pi]:
+                    p.grad = b.views[pi]
+        for p in self.sparse_params:
+            p.grad = None
+
+    def capturable(self) -> bool:
+        """True when one training step issues no host-synchronising collective: every
+        gradient bucket and the buffer broadcast ride the one-shot xGMI kernel and no
+        parameter has sparse gradients."""
+        if self.sparse_params:
+            return False
+        if not all(self._allreduce.routes_to_xgmi(b.flat) for b in self.buckets):
+            return False
+        if self.broadcast_buffers and not all(self._allreduce.routes_to_xgmi(f) for f in self._buf_flats):
+            return False
+        return True
+
     def forward(self, *args, **kw):
-        if self.broadcast_buffers and self.world > 1:
+        if self.broadcast_buffers and self.world > 1 and self._buf_flats:
             with torch.no_grad():
-                for m in self.module.modules():   # replicated buffers only (rank-local ones stay)
-                    if getattr(m, "_raydp_model_parallel", False):
-                        continue
-                    for t in m.buffers(recurse=False):
-                        dist.broadcast(t.data, 0, group=self.pg)
+                for flat in self._buf_flats:
+                    if self._allreduce.routes_to_xgmi(flat):
+                        # broadcast as a one-shot sum where every rank but 0 adds zeros (exact)
+                        if self.rank != 0:
+                            flat.zero_()
+                        self._allreduce(flat).wait()
+                    else:
+                        dist.broadcast(flat, 0, group=self.pg)
         return self.module(*args, **kw)
 
     def state_dict(self, *a, **kw):

@@ -279,7 +279,8 @@ class ActorManager:
         ra, rk = _resolve_args(args, kwargs)
         clean = {k: v for k, v in opts.items() if k not in ("scheduling_strategy", "placement_group")}
         a.opts = dict(opts, _class_name=getattr(cls, "__name__", str(cls)))
-        a.gpu_ids = self._take_gpus(vnode, res.get("GPU", 0.0))
+        a.gpu_take = self._take_gpus(vnode, res.get("GPU", 0.0))
+        a.gpu_ids = [g for g, _ in a.gpu_take]
         if a.gpu_ids:
             a.opts["_gpu_ids"] = a.gpu_ids
         with open(a.spec_path + ".tmp", "wb") as f:
@@ -324,23 +325,36 @@ class ActorManager:
 
     @staticmethod
     def _take_gpus(vnode, n: float):
-        """Whole-GPU assignment: the actor sees exactly these devices (HIP_VISIBLE_DEVICES)."""
+        """GPU assignment: the actor sees exactly these devices (HIP_VISIBLE_DEVICES). A
+        fractional request (``num_gpus=0.5``: several workers rehearsing on one card) packs onto
+        the most-used GPU that still has that much capacity left; a whole request takes idle
+        GPUs. Returns ``[(gpu id, share)]``."""
         import math
         if vnode is None or not n:
             return []
-        if not hasattr(vnode, "gpu_free"):
-            vnode.gpu_free = list(range(int(vnode.total.get("GPU", 0))))
-        k = max(1, int(math.ceil(n)))
-        ids, vnode.gpu_free = vnode.gpu_free[:k], vnode.gpu_free[k:]
-        return ids
+        if not hasattr(vnode, "gpu_cap"):
+            vnode.gpu_cap = [1.0] * int(vnode.total.get("GPU", 0))
+        cap = vnode.gpu_cap
+        if n < 1.0:
+            fits = [i for i, c in enumerate(cap) if c + 1e-9 >= n]
+            if not fits:
+                return []
+            i = min(fits, key=lambda j: (cap[j], j))
+            cap[i] -= n
+            return [(i, float(n))]
+        idle = [i for i, c in enumerate(cap) if c >= 1.0 - 1e-9][:int(math.ceil(n))]
+        for i in idle:
+            cap[i] = 0.0
+        return [(i, 1.0) for i in idle]
 
     def release(self, a: ProcessActor):
         with self._lock:
             if getattr(a, "_released", False):
                 return
             a._released = True
-        if getattr(a, "gpu_ids", None) and a.vnode is not None:
-            a.vnode.gpu_free = sorted(set(getattr(a.vnode, "gpu_free", [])) | set(a.gpu_ids))
+        if getattr(a, "gpu_take", None) and a.vnode is not None and hasattr(a.vnode, "gpu_cap"):
+            for g, share in a.gpu_take:
+                a.vnode.gpu_cap[g] = min(1.0, a.vnode.gpu_cap[g] + share)
         cl = self.node.cluster
         with cl.lock:
             if a.pg is not None:

@@ -137,6 +137,10 @@ def init(address=None, num_cpus=None, num_gpus=None, resources=None, object_stor
 
 def shutdown():
     global _node
+    import sys
+    tr = sys.modules.get("raydp_amd.train.trainer")
+    if tr is not None:      # warm training worker groups are actors of this node
+        tr.release_worker_groups()
     with _lock:
         n = _node
         _node = None

@@ -163,14 +163,50 @@ class FusedMLPEngine:
                                        acc_thr=acc_thr)
         self.optimizer = optimizer
         self.trainer.load_optimizer_state(optimizer)
+        self.xg, self.comm, self.ar = None, None, None
+        self.allreduce_kind = None
+        self.max_steps = None
         if self.world > 1:
-            import torch.distributed as dist
-            dist.broadcast(self.trainer.params, 0)
-            self.trainer.refresh_images()
+            self._setup_collectives()
         self.drop_last = bool(config.get("drop_last", False))
         self.shuffle = bool(config.get("shuffle", True))
         self.seed = _epoch_seed_base(config)
+        self.equal_shards = bool(config.get("_equal_shards", False))
         self.epoch = 0
+
+    def _setup_collectives(self):
+        """World > 1, once per fit: pick the gradient path (xGMI one-shot fused into the
+        optimizer kernel, else the native RCCL communicator inside the C++ step loop, else
+        ``torch.distributed``) and make every rank start from rank 0's parameters (DDP's
+        constructor broadcast, reference ``train.torch.prepare_model`` at
+        ``python/raydp/torch/estimator.py:243``) -- over xGMI that broadcast is one one-shot
+        all-reduce where every rank but 0 contributes zeros (exact: x + 0 = x)."""
+        import torch.distributed as dist
+        from raydp_amd.ops.comm import NativeComm
+        tr = self.trainer
+        self.xg = _xgmi_for(tr)
+        if self.xg is not None:
+            self.allreduce_kind = "xgmi_oneshot"
+            if tr.params.numel() <= self.xg.max_floats:
+                if dist.get_rank() != 0:
+                    tr.params.zero_()
+                self.xg.allreduce_(tr.params)
+            else:
+                dist.broadcast(tr.params, 0)
+        else:
+            if dist.get_backend() == "nccl":
+                self.comm = NativeComm.from_process_group()
+            if self.comm is not None:
+                self.allreduce_kind = "rccl_native"
+                self.comm.broadcast_(tr.params, 0)
+            else:
+                self.allreduce_kind = f"torch.distributed:{dist.get_backend()}"
+                dist.broadcast(tr.params, 0)
+
+                def ar(g):
+                    dist.all_reduce(g)
+                self.ar = ar
+        tr.refresh_images()
 
     def load(self, train_ds, eval_ds, config):
         fc, ft = config["feature_columns"], config["feature_types"]
@@ -179,6 +215,17 @@ class FusedMLPEngine:
                                    self.device, fused_stride=k)
         self.eval = _ShardTensors(eval_ds, fc, ft, config["label_column"], torch.float32, self.device,
                                   fused_stride=k) if eval_ds is not None else None
+        if self.world > 1 and not self.equal_shards:
+            # ranks that brought their own data (SPMD local shards) agree once per fit on the
+            # step count, so every per-step collective is matched; shards split by the trainer
+            # are equal by construction and skip this
+            import torch.distributed as dist
+            b = self.trainer.batch
+            mine = self.train.n // b if self.drop_last else -(-self.train.n // b)
+            dev = self.device if dist.get_backend() == "nccl" else "cpu"
+            s = torch.tensor([mine], device=dev, dtype=torch.int64)
+            dist.all_reduce(s, op=dist.ReduceOp.MIN)
+            self.max_steps = int(s.item())
 
     def _res(self, m):
         out = {}
@@ -192,71 +239,33 @@ class FusedMLPEngine:
         return out
 
     def train_epoch(self):
+        """One epoch = one native call. World > 1 adds no host synchronisation of its own: the
+        only device read per epoch is the metrics vector, which on the xGMI path also carries
+        the epoch-end vote (every rank's peer-timeout word, summed over xGMI). A nonzero vote
+        -- seen identically by every rank -- fails this worker (``CollectiveError``): the group
+        restarts from the newest epoch checkpoint, with the xGMI path disabled in this
+        process (``FailureConfig`` semantics, reference ``torch/estimator.py:331-334``)."""
         t = self.train
         perm = None
         if self.shuffle:
             perm = random_permutation(t.n, self.seed + self.epoch, self.device)
         self.epoch += 1
-        ar, comm, max_steps, xg = None, None, None, None
-        if self.world > 1:
-            import torch.distributed as dist
-            from raydp_amd.ops.comm import NativeComm
-            # every rank must run the same number of steps (matched collectives)
-            b = self.trainer.batch
-            mine = t.n // b if self.drop_last else -(-t.n // b)
-            s = torch.tensor([mine], device=self.device, dtype=torch.int64)
-            dist.all_reduce(s, op=dist.ReduceOp.MIN)
-            max_steps = int(s.item())
-            xg = None if getattr(self, "_xgmi_broken", False) else _xgmi_for(self.trainer)
-            comm = None
-            if xg is None:
-                comm = NativeComm.from_process_group() if dist.get_backend() == "nccl" else None
-            self.allreduce_kind = "xgmi_oneshot" if xg is not None else (
-                "rccl_native" if comm is not None else f"torch.distributed:{dist.get_backend()}")
-            if comm is None and xg is None:
-                def ar(g):
-                    dist.all_reduce(g)
-        if xg is None:
-            m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, allreduce=ar,
-                                         world_size=self.world, drop_last=self.drop_last, comm=comm,
-                                         max_steps=max_steps)
+        if self.xg is not None:
+            from raydp_amd.exceptions import CollectiveError
+            from raydp_amd.ops.comm import forget_xgmi
+            try:
+                m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, world_size=self.world,
+                                             drop_last=self.drop_last, max_steps=self.max_steps, xg=self.xg)
+            except CollectiveError:
+                forget_xgmi(self.xg, disable=True)
+                self.xg = None
+                raise
         else:
-            m = self._xgmi_epoch(xg, t, perm, max_steps)
+            m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, allreduce=self.ar,
+                                         world_size=self.world, drop_last=self.drop_last, comm=self.comm,
+                                         max_steps=self.max_steps)
         self.trainer.note_steps(self.trainer.steps_in_epoch)
         return self._res(m), m["loss"]
-
-    def _xgmi_epoch(self, xg, t, perm, max_steps):
-        """One epoch with the one-shot xGMI all-reduce fused into the optimizer kernel. Every
-        peer wait in that kernel is bounded; if any rank saw a timeout, all ranks roll back to
-        the epoch-start snapshot, drop the xGMI path for good and rerun the epoch over RCCL
-        (matched on every rank by one agreement collective per epoch)."""
-        import torch.distributed as dist
-        from raydp_amd.exceptions import CollectiveError
-        from raydp_amd.ops.comm import NativeComm, _agree, forget_xgmi
-        snap = self.trainer.snapshot()
-        ok = True
-        try:
-            m = self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, world_size=self.world,
-                                         drop_last=self.drop_last, max_steps=max_steps, xg=xg)
-        except CollectiveError:
-            ok = False
-        if _agree(ok):
-            return m
-        import warnings
-        warnings.warn("xGMI one-shot all-reduce timed out on some rank: rolled back, rerunning "
-                      "the epoch over RCCL and staying on it")
-        forget_xgmi(xg)
-        self._xgmi_broken = True
-        self.trainer.restore(snap)
-        comm = NativeComm.from_process_group() if dist.get_backend() == "nccl" else None
-        ar = None
-        if comm is None:
-            def ar(g):
-                dist.all_reduce(g)
-        self.allreduce_kind = "rccl_native" if comm is not None else f"torch.distributed:{dist.get_backend()}"
-        return self.trainer.train_epoch(t.feats_bf16, t.labels, t.n, perm, allreduce=ar,
-                                        world_size=self.world, drop_last=self.drop_last, comm=comm,
-                                        max_steps=max_steps)
 
     def evaluate_epoch(self):
         e = self.eval
@@ -313,7 +322,8 @@ def _xgmi_for(trainer):
     if mode == "rccl" or not torch.cuda.is_available():
         return None
     # the exchange slot is the whole gradient buffer (flat gradient + exported activations)
-    xg = XgmiComm.create(trainer.grads.numel(), timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
+    xg = XgmiComm.create(trainer.grads.numel(), timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"),
+                         host_seq=True)
     if xg is None and mode == "xgmi":
         raise RuntimeError("spark.ray.mi355x.allreduce=xgmi but the xGMI peer mapping is unavailable")
     return xg
@@ -327,12 +337,6 @@ class TorchLoopEngine:
         self.world = session.get_world_size()
         self.raw_model = model.to(device)
         self.allreduce_kind = None
-        if self.world > 1:
-            from raydp_amd.parallel.ddp import DistributedDataParallel
-            self.model = DistributedDataParallel(self.raw_model)
-            self.allreduce_kind = self.model._allreduce.kind
-        else:
-            self.model = self.raw_model
         # optimizer state may reference CPU tensors; move them
         for st in optimizer.state.values():
             for k, v in list(st.items()):
@@ -340,6 +344,16 @@ class TorchLoopEngine:
                     st[k] = v.to(device)
         self.optimizer, self.loss, self.metrics = optimizer, loss, metrics
         self.scheduler = lr_scheduler
+        self._fused_sgd = None          # decided at the first step (needs the gradients)
+        self.fusions = []
+        if device.type == "cuda":
+            self._fuse_hot_ops()        # before DDP sees which parameters have sparse gradients
+        if self.world > 1:
+            from raydp_amd.parallel.ddp import DistributedDataParallel
+            self.model = DistributedDataParallel(self.raw_model)
+            self.allreduce_kind = self.model._allreduce.kind
+        else:
+            self.model = self.raw_model
         self.batch = int(config["batch_size"])
         self.drop_last = bool(config.get("drop_last", False))
         self.shuffle = bool(config.get("shuffle", True))
@@ -356,6 +370,55 @@ class TorchLoopEngine:
             self.graph_status = why or "enabled"
         else:
             self.graph_status = "disabled (RAYDP_TORCH_GRAPHS=0)"
+
+    def _fuse_hot_ops(self):
+        """Swap the step's eager tails for HIP kernels where the semantics are identical:
+        ``BCEWithLogitsLoss()`` -> :class:`raydp_amd.ops.fused_optim.FusedBCEWithLogits`;
+        plain-SGD DLRM tables (replicated on one GPU, or sharded) -> the sparse SGD fused into
+        the embedding backward (``rx_emb_sgd``: no sparse gradient tensor, no index_add)."""
+        from raydp_amd.ops import fused_optim
+        if fused_optim.fusable_bce(self.loss):
+            self.loss = fused_optim.FusedBCEWithLogits()
+            self.fusions.append("bce_with_logits")
+        opt = self.optimizer
+        if type(opt) is torch.optim.SGD and self.scheduler is None and all(
+                float(g["momentum"]) == 0.0 and float(g["weight_decay"]) == 0.0 and not g.get("maximize", False)
+                and not isinstance(g["lr"], torch.Tensor) for g in opt.param_groups):
+            from raydp_amd.ops.dlrm_ops import FusedEmbeddings
+            lr_of = {id(p): float(g["lr"]) for g in opt.param_groups for p in g["params"]}
+            for m in self.raw_model.modules():
+                sharded = hasattr(m, "start") and hasattr(m, "finish")
+                if isinstance(m, FusedEmbeddings) or sharded:
+                    w = getattr(m, "weight", None)
+                    if getattr(m, "fused_sgd_lr", 0) is not None or w is None or id(w) not in lr_of:
+                        continue
+                    if not sharded and self.world > 1:
+                        continue   # replicated tables updated locally would diverge across ranks
+                    m.fused_sgd_lr = lr_of[id(w)]
+                    w._raydp_sparse_grad = False
+                    self.fusions.append("embedding_sgd")
+
+    def opt_step(self):
+        """``optimizer.step()``, on the multi-tensor SGD kernel when it reproduces it (one launch
+        per 24 tensors, fused-tower bf16 images written in the same pass)."""
+        if self._fused_sgd is None:
+            from raydp_amd.ops import fused_optim
+            self._fused_sgd = self.device.type == "cuda" and fused_optim.sgd_supported(self.optimizer) is None
+            if self._fused_sgd:
+                self.fusions.append("multi_tensor_sgd")
+        if self._fused_sgd:
+            from raydp_amd.ops.fused_optim import sgd_step
+            sgd_step(self.optimizer)
+        else:
+            self.optimizer.step()
+
+    def zero_grad(self):
+        """DDP: zero the gradient buckets in place (``.grad`` stays a bucket view, autograd
+        accumulates straight into the all-reduced buffer); else drop the gradients."""
+        if self.world > 1 and hasattr(self.model, "buckets"):
+            self.model.zero_grad()
+        else:
+            self.optimizer.zero_grad(set_to_none=True)
 
     def load(self, train_ds, eval_ds, config):
         fc, ft = config["feature_columns"], config["feature_types"]
@@ -392,9 +455,9 @@ class TorchLoopEngine:
             loss = self.loss(outputs, targets)
             total += loss.detach()
             self.metrics.update(outputs, targets)
-            self.optimizer.zero_grad(set_to_none=True)
+            self.zero_grad()
             loss.backward()
-            self.optimizer.step()
+            self.opt_step()
             if self.scheduler is not None:
                 self.scheduler.step()
             nb += 1

@@ -374,6 +374,9 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             # per-epoch checkpoints (model.pt + optim.pt) every N epochs; 0 = only the final
             # model.pt, as the reference
             "checkpoint_frequency": int(self._extra_config.get("checkpoint_frequency", 0) or 0),
+            # the trainer splits the datasets into equal shards (every rank runs the same step
+            # count without asking); SPMD ranks that bring their own rows agree once per fit
+            "_equal_shards": not bool(self._extra_config.get("spmd_local_shards")),
         }
         use_gpu = self._extra_config.get("use_gpu")
         if self._resources_per_worker and "GPU" in self._resources_per_worker:

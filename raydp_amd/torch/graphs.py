@@ -48,7 +48,9 @@ def supported(engine) -> Optional[str]:
     if engine.device.type != "cuda":
         return "not on a GPU"
     if engine.world != 1:
-        return "world_size > 1 (collectives stay eager)"
+        cap = getattr(engine.model, "capturable", None)
+        if cap is None or not cap():
+            return "world_size > 1 with a collective that is not capturable (RCCL bucket, sparse gradients)"
     if not engine.metrics.graph_safe():
         return "non built-in metric"
     if type(engine.optimizer) not in _SAFE_OPT:
@@ -116,9 +118,9 @@ class GraphedTrainLoop:
         loss = e.loss(out, lab)
         self.total += loss.detach()
         e.metrics.update(out, lab)
-        e.optimizer.zero_grad(set_to_none=True)
+        e.zero_grad()
         loss.backward()
-        e.optimizer.step()
+        e.opt_step()
 
     def _gather(self, sel):
         d = self.e.train
@@ -133,7 +135,7 @@ class GraphedTrainLoop:
         b = self.e.batch
         win = torch.empty(steps * b, dtype=torch.int64, device=self.e.device)
         g = torch.cuda.CUDAGraph()
-        self.e.optimizer.zero_grad(set_to_none=True)
+        self.e.zero_grad()
         with torch.cuda.graph(g, pool=self.pool), _CaptureSafeIndexing(self.index_cache):
             for j in range(steps):
                 self._forward_step(*self._gather(win[j * b:(j + 1) * b]))
@@ -151,7 +153,7 @@ class GraphedTrainLoop:
                 self.failed = f"{type(exc).__name__}: {exc}\n" + "".join(traceback.format_tb(exc.__traceback__)[-4:])
                 self.graphs.clear()
                 torch.cuda.synchronize(self.e.device)
-                self.e.optimizer.zero_grad(set_to_none=True)
+                self.e.zero_grad()
                 b = self.e.batch
                 for j in range(steps):
                     self._eager(sel[j * b:(j + 1) * b])

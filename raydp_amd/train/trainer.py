@@ -24,6 +24,7 @@ import socket
 import tempfile
 import time
 import traceback
+import uuid
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
@@ -96,16 +97,34 @@ def _backend(torch_config, use_gpu: bool) -> str:
     oneCCL there) -> the process-group backend: RCCL (``"nccl"``) on GPU workers, gloo on CPU."""
     if torch_config is not None:
         return torch_config.resolve(use_gpu)
+    forced = os.environ.get("RAYDP_TRAIN_BACKEND")
+    if forced:      # rehearsals: several GPU workers sharing one card cannot form an RCCL ring
+        return forced
     return "nccl" if use_gpu else "gloo"
 
 
-def latest_checkpoint(storage: str) -> Optional[str]:
-    """Newest ``checkpoint_*`` directory under a run's storage path (reported by rank 0)."""
+def _checkpoint_names(storage: str) -> List[str]:
     try:
-        names = sorted(n for n in os.listdir(storage) if n.startswith("checkpoint_") and ".tmp" not in n)
+        return sorted(n for n in os.listdir(storage) if n.startswith("checkpoint_") and ".tmp" not in n)
     except OSError:
-        return None
-    return os.path.join(storage, names[-1]) if names else None
+        return []
+
+
+def latest_checkpoint(storage: str, exclude=(), resumable_only: bool = False) -> Optional[str]:
+    """Newest ``checkpoint_*`` directory under a run's storage path (reported by rank 0).
+
+    ``exclude``: names that existed before this fit started (a reused ``RunConfig.name``);
+    ``resumable_only``: only per-epoch checkpoints, which carry ``meta.json`` (the epoch they
+    follow) -- the final ``model.pt`` of a finished attempt is not a point to resume from."""
+    skip = set(exclude)
+    for n in reversed(_checkpoint_names(storage)):
+        if n in skip:
+            continue
+        path = os.path.join(storage, n)
+        if resumable_only and not os.path.exists(os.path.join(path, "meta.json")):
+            continue
+        return path
+    return None
 
 
 def _worker_entry(rank, world, port, payload, queue):
@@ -179,7 +198,9 @@ class DataParallelTrainer:
         base = self.run_config.storage_path or os.path.join(tempfile.gettempdir(), "raydp_results")
         if base.startswith("file://"):
             base = base[len("file://"):]
-        name = self.run_config.name or f"TorchTrainer_{time.strftime('%Y-%m-%d_%H-%M-%S')}_{os.getpid()}"
+        # unique per fit: two fits started in the same second must never share checkpoints
+        name = self.run_config.name or \
+            f"TorchTrainer_{time.strftime('%Y-%m-%d_%H-%M-%S')}_{os.getpid()}_{uuid.uuid4().hex[:8]}"
         path = os.path.join(base, name)
         os.makedirs(path, exist_ok=True)
         return path
@@ -191,6 +212,7 @@ class DataParallelTrainer:
         failures = 0
         max_f = self.run_config.failure_config.max_failures
         storage = self._storage()
+        preexisting = _checkpoint_names(storage)   # a reused RunConfig.name: not this fit's
         restored = []
         while True:
             try:
@@ -201,7 +223,9 @@ class DataParallelTrainer:
                 failures += 1
                 if max_f >= 0 and failures > max_f:
                     raise TrainingFailedError(f"training failed after {failures} attempt(s):\n{e}") from None
-                ck = latest_checkpoint(storage)
+                # only a per-epoch checkpoint this fit wrote (meta.json): never the final
+                # model.pt of an attempt whose peer died afterwards, never an earlier fit's
+                ck = latest_checkpoint(storage, exclude=preexisting, resumable_only=True)
                 if ck is not None:
                     self.resume = Checkpoint(ck)
                     restored.append(ck)
@@ -269,49 +293,42 @@ class DataParallelTrainer:
 
     def _run_spawned(self, world, use_gpu, storage, reporter):
         """Worker group of ``world`` process actors (one per rank, GPUs assigned by the
-        runtime), joined into one ``torch.distributed`` group (RCCL when they own GPUs)."""
+        runtime), joined into one ``torch.distributed`` group (RCCL when they own GPUs).
+
+        Ray Train starts fresh worker actors per fit, but Ray prestarts its worker processes,
+        so that costs milliseconds there. Here an actor is a new Python process that imports
+        torch and initialises HIP (seconds), so a group that finished a fit cleanly is kept
+        warm -- process group, RCCL / xGMI communicators, loaded kernels -- and the next fit
+        with the same shape reuses it (``_GROUPS``). A failed attempt kills its group."""
         import cloudpickle
         from raydp_amd import runtime
-        from raydp_amd.runtime import pgroup
         res = dict(self.scaling.resources_per_worker or {})
         cpus = float(res.pop("CPU", 1))
         gpus = float(res.pop("GPU", 1 if use_gpu else 0)) if use_gpu else 0.0
-        bundle = {"CPU": cpus}
-        if gpus:
-            bundle["GPU"] = gpus
-        bundle.update(res)
         strategy = self.scaling.placement_strategy if isinstance(self.scaling.placement_strategy, str) else "PACK"
-        pg = pgroup.placement_group([dict(bundle) for _ in range(world)], strategy=strategy)
-        port = _free_port()
-        cls = runtime.remote(_TrainWorker)
-        workers = []
         from raydp_amd.utils.config import env_for_workers
         wenv = env_for_workers()   # spark.ray.mi355x.* settings of the driver's session
+        backend = _backend(self.torch_config, use_gpu)
+        tmo = self.torch_config.timeout_s if self.torch_config is not None else None
+        # a warm group keeps the environment it was started with: the RAYDP_* variables (the
+        # env-var form of the spark.ray.mi355x.* settings) are part of its identity
+        renv = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("RAYDP_")))
+        key = (world, use_gpu, cpus, gpus, tuple(sorted(res.items())), strategy, backend, tmo,
+               tuple(sorted(wenv.items())) if wenv else (), renv)
+        group = _GROUPS.take(key)
+        if group is None:
+            group = _WorkerGroup.start(world, use_gpu, cpus, gpus, res, strategy, wenv, backend, tmo, storage)
+        ok = False
         try:
-            for r in range(world):
-                opts = {"num_cpus": cpus, "num_gpus": gpus, "placement_group": pg,
-                        "placement_group_bundle_index": r, "max_concurrency": 2}
-                if wenv:
-                    opts["runtime_env"] = {"env_vars": dict(wenv)}
-                if res:
-                    opts["resources"] = res
-                workers.append(cls.options(**opts).remote(r, world, storage, use_gpu))
-            # Like Ray Train's shared CUDA_VISIBLE_DEVICES: every worker of a node sees all of
-            # that node's worker GPUs and binds cuda:<local_rank>, so RCCL and the xGMI one-shot
-            # path can map peer memory (a worker that saw only its own GPU could not)
-            layout = _local_layout(workers)
-            backend = _backend(self.torch_config, use_gpu)
-            tmo = self.torch_config.timeout_s if self.torch_config is not None else None
-            runtime.get([w.setup.remote("127.0.0.1", port, *layout[r], backend=backend, timeout_s=tmo)
-                         for r, w in enumerate(workers)])
+            workers = group.workers
             refs = []
             for r, w in enumerate(workers):
                 shards = _shard(self.datasets, r, world)
-                payload = cloudpickle.dumps((self.fn, self.config, shards, self.resume))
+                payload = cloudpickle.dumps((self.fn, self.config, shards, self.resume, storage))
                 refs.append(w.run.remote(payload))
             # wait on all ranks at once: when one dies, its peers are blocked in a collective
-            # that will never complete -- fail the attempt at the first error (the finally
-            # block below kills the survivors) instead of waiting on rank 0 forever
+            # that will never complete -- fail the attempt at the first error (the group is
+            # killed below) instead of waiting on rank 0 forever
             outs, error = [None] * world, None
             pending = list(refs)
             while pending and error is None:
@@ -327,17 +344,120 @@ class DataParallelTrainer:
             for r, reports in enumerate(outs):
                 for metrics, ckpt in reports:
                     reporter(r, metrics, ckpt)
+            ok = True
         finally:
-            for w in workers:
-                try:
-                    runtime.kill(w, no_restart=True)
-                except Exception:  # noqa: BLE001
-                    pass
-            pgroup.remove_placement_group(pg)
+            if ok and _GROUPS.enabled():
+                _GROUPS.put(key, group)
+            else:
+                group.kill()
+
+
+class _WorkerGroup:
+    """``world`` live ``_TrainWorker`` actors joined in one process group, plus their
+    placement group."""
+
+    def __init__(self, workers, pg):
+        self.workers, self.pg = workers, pg
+        from raydp_amd.runtime import core
+        self.node = core.current_node()
+
+    @classmethod
+    def start(cls, world, use_gpu, cpus, gpus, res, strategy, wenv, backend, tmo, storage):
+        from raydp_amd import runtime
+        from raydp_amd.runtime import pgroup
+        bundle = {"CPU": cpus}
+        if gpus:
+            bundle["GPU"] = gpus
+        bundle.update(res)
+        pg = pgroup.placement_group([dict(bundle) for _ in range(world)], strategy=strategy)
+        port = _free_port()
+        actor = runtime.remote(_TrainWorker)
+        workers = []
+        try:
+            for r in range(world):
+                opts = {"num_cpus": cpus, "num_gpus": gpus, "placement_group": pg,
+                        "placement_group_bundle_index": r, "max_concurrency": 2}
+                if wenv:
+                    opts["runtime_env"] = {"env_vars": dict(wenv)}
+                if res:
+                    opts["resources"] = res
+                workers.append(actor.options(**opts).remote(r, world, storage, use_gpu))
+            # Like Ray Train's shared CUDA_VISIBLE_DEVICES: every worker of a node sees all of
+            # that node's worker GPUs and binds its own device, so RCCL and the xGMI one-shot
+            # path can map peer memory (a worker that saw only its own GPU could not)
+            layout = _local_layout(workers)
+            runtime.get([w.setup.remote("127.0.0.1", port, *layout[r], backend=backend, timeout_s=tmo)
+                         for r, w in enumerate(workers)])
+        except BaseException:
+            cls(workers, pg).kill()
+            raise
+        return cls(workers, pg)
+
+    def alive(self) -> bool:
+        from raydp_amd.runtime import core
+        return core.current_node() is self.node and all(
+            not getattr(getattr(w, "_impl", None), "dead", True) for w in self.workers)
+
+    def kill(self):
+        from raydp_amd import runtime
+        from raydp_amd.runtime import pgroup
+        for w in self.workers:
+            try:
+                runtime.kill(w, no_restart=True)
+            except Exception:  # noqa: BLE001
+                pass
+        try:
+            pgroup.remove_placement_group(self.pg)
+        except Exception:  # noqa: BLE001
+            pass
+        self.workers = []
+
+
+class _GroupPool:
+    """Warm worker groups keyed by their shape (at most one per key)."""
+
+    def __init__(self):
+        self._groups: Dict[Any, _WorkerGroup] = {}
+
+    @staticmethod
+    def enabled() -> bool:
+        return os.environ.get("RAYDP_TRAIN_REUSE_WORKERS", "1") != "0"
+
+    def take(self, key) -> Optional[_WorkerGroup]:
+        g = self._groups.pop(key, None)
+        if g is not None and not g.alive():
+            g.kill()
+            g = None
+        return g
+
+    def put(self, key, group: _WorkerGroup):
+        old = self._groups.pop(key, None)
+        if old is not None and old is not group:
+            old.kill()
+        self._groups[key] = group
+
+    def clear(self):
+        groups, self._groups = list(self._groups.values()), {}
+        for g in groups:
+            g.kill()
+
+    def __len__(self):
+        return len(self._groups)
+
+
+_GROUPS = _GroupPool()
+
+
+def release_worker_groups():
+    """Stop the warm training worker groups (``runtime.shutdown`` does this too)."""
+    _GROUPS.clear()
 
 
 def _local_layout(workers):
-    """Per worker: (visible GPU ids of its node, local rank, local world size, node rank)."""
+    """Per worker: (visible GPU ids of its node, local rank, local world size, node rank,
+    device index). The local rank is the worker's position among its node's workers -- unique
+    even when several workers share one GPU (fractional GPUs) -- and the device index is its
+    GPU's position in the node's visible list."""
     nodes, order = {}, []
     for w in workers:
         impl = getattr(w, "_impl", None)
@@ -355,20 +475,23 @@ def _local_layout(workers):
         peers = nodes[node]
         gpus = sorted({g for p in peers for g in (getattr(getattr(p, "_impl", None), "gpu_ids", None) or [])})
         mine = getattr(impl, "gpu_ids", None) or []
-        local = gpus.index(mine[0]) if mine and mine[0] in gpus else peers.index(w)
-        out.append((gpus or None, local, len(peers), order.index(node)))
+        local = peers.index(w)
+        dev = gpus.index(mine[0]) if mine and mine[0] in gpus else local
+        out.append((gpus or None, local, len(peers), order.index(node), dev))
     return out
 
 
 class _TrainWorker:
-    """One rank of a spawned worker group (a process actor)."""
+    """One rank of a spawned worker group (a process actor). Stays alive between fits while
+    its group is warm; its process group is torn down with the process."""
 
     def __init__(self, rank: int, world: int, storage: str, use_gpu: bool):
         self.rank, self.world, self.storage, self.use_gpu = rank, world, storage, use_gpu
         self.local_rank, self.local_world, self.node_rank = 0, 1, rank
 
     def setup(self, addr: str, port: int, visible=None, local_rank: int = 0, local_world: int = 1,
-              node_rank: int = 0, backend: Optional[str] = None, timeout_s: Optional[float] = None):
+              node_rank: int = 0, device_index: Optional[int] = None, backend: Optional[str] = None,
+              timeout_s: Optional[float] = None):
         if visible and self.use_gpu:
             # before the first HIP call of this process: the node's worker GPUs, in order
             os.environ["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in visible)
@@ -377,7 +500,7 @@ class _TrainWorker:
         self.local_rank, self.local_world, self.node_rank = local_rank, local_world, node_rank
         self.device = torch.device("cpu")
         if self.use_gpu and torch.cuda.is_available():
-            dev = local_rank % max(1, torch.cuda.device_count())
+            dev = (local_rank if device_index is None else device_index) % max(1, torch.cuda.device_count())
             torch.cuda.set_device(dev)
             self.device = torch.device("cuda", dev)
         os.environ.update({"RANK": str(self.rank), "WORLD_SIZE": str(self.world),
@@ -385,12 +508,21 @@ class _TrainWorker:
                            "MASTER_ADDR": addr, "MASTER_PORT": str(port)})
         if backend is None or (backend == "nccl" and self.device.type != "cuda"):
             backend = "nccl" if self.device.type == "cuda" else "gloo"
-        _init_dist(backend, self.rank, self.world, addr, port, timeout_s)
+        if backend == "nccl":
+            import datetime
+            import torch.distributed as dist
+            kw = {"timeout": datetime.timedelta(seconds=float(timeout_s))} if timeout_s else {}
+            # device_id: RCCL binds its communicator now (no lazy init inside the first step)
+            dist.init_process_group(backend, init_method=f"tcp://{addr}:{port}", rank=self.rank,
+                                    world_size=self.world, device_id=self.device, **kw)
+        else:
+            _init_dist(backend, self.rank, self.world, addr, port, timeout_s)
         return True
 
     def run(self, payload: bytes):
         import cloudpickle
-        fn, config, shards, resume = cloudpickle.loads(payload)
+        fn, config, shards, resume, storage = cloudpickle.loads(payload)
+        self.storage = storage
         reports = []
 
         def reporter(r, metrics, ckpt):
@@ -402,9 +534,6 @@ class _TrainWorker:
             fn(config) if _accepts_arg(fn) else fn()
         finally:
             S._set_session(None)
-            import torch.distributed as dist
-            if dist.is_initialized():
-                dist.destroy_process_group()
         return reports
 
 

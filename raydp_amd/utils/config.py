@@ -125,6 +125,10 @@ register("spark.ray.mi355x.allreduce", "str", "auto",
 register("spark.ray.mi355x.allreduce.timeout_s", "float", 30.0,
          "bound on every xGMI flag wait before the kernel gives up and reports an error",
          env="RAYDP_ALLREDUCE_TIMEOUT_S")
+register("spark.ray.mi355x.allreduce.oneshot_max_mb", "float", 16.0,
+         "DDP / Horovod buckets up to this size take the one-shot xGMI kernel (every rank reads the "
+         "N-1 peer buckets at once, one per link: S / 153 GB/s whatever N); larger ones go to RCCL",
+         env="RAYDP_ALLREDUCE_ONESHOT_MAX_MB")
 register("spark.ray.mi355x.fused", "str", "auto",
          "TorchEstimator engine: auto (fused HIP MLP when the model is an MLP), on (required), off",
          env="RAYDP_FUSED", choices=["auto", "on", "off"])

@@ -1,0 +1,76 @@
+"""The reference topology on the GPU: ONE driver, ``TorchEstimator(num_workers=2)`` whose two
+worker processes are spawned by the worker-group trainer (``_run_spawned``; reference
+``python/raydp/torch/estimator.py:331-355`` -> Ray Train ``TorchTrainer``), each binding the
+GPU, ingesting its equal shard into HBM and training on the fused HIP engine with the gradient
+all-reduced over the one-shot xGMI path.
+
+gpurun gives one MI355X, so both workers share it (``resources_per_worker={"GPU": 0.5}``) and
+their process group bootstraps over gloo (two ranks on one device cannot form an RCCL ring);
+the xGMI peer mapping between the two processes is the same code that runs across 8 GPUs.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _model():
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Linear(20, 64), nn.ReLU(), nn.BatchNorm1d(64), nn.Linear(64, 16), nn.ReLU(),
+                         nn.Linear(16, 1))
+
+
+def _fit(tmp_path, tag):
+    import pandas as pd
+    from raydp_amd.data import from_pandas
+    from raydp_amd.torch import TorchEstimator
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((64 * 16, 20)).astype(np.float32)
+    df = pd.DataFrame({f"f{i}": x[:, i] for i in range(20)})
+    df["y"] = x[:, :4].sum(1) * 0.5 + 1.0
+    model = _model()
+    est = TorchEstimator(num_workers=2, resources_per_worker={"CPU": 1, "GPU": 0.5}, model=model,
+                         optimizer=torch.optim.Adam(model.parameters(), lr=3e-3), loss=nn.MSELoss(),
+                         feature_columns=[f"f{i}" for i in range(20)], label_column="y", batch_size=64,
+                         num_epochs=3, fused="on", shuffle_seed=5, storage_path=str(tmp_path / tag),
+                         metrics_name=["MeanAbsoluteError"])
+    res = est.fit(from_pandas(df))
+    return est, res
+
+
+def test_spawned_workers_train_fused_over_xgmi_and_stay_warm(runtime_local, tmp_path, monkeypatch):
+    from raydp_amd.train import trainer as T
+    monkeypatch.setenv("RAYDP_TRAIN_BACKEND", "gloo")
+    est, res = _fit(tmp_path, "a")
+    hist = [m for m in res.metrics_history if "train_loss" in m]
+    assert [m["epoch"] for m in hist] == [0, 1, 2]
+    assert hist[0]["engine"] == "fused_mlp_hip", hist[0]
+    assert hist[0]["allreduce"] == "xgmi_oneshot", hist[0]
+    assert hist[-1]["train_loss"] < hist[0]["train_loss"]
+    assert len(T._GROUPS) == 1, "a group that finished cleanly is kept warm"
+    group = next(iter(T._GROUPS._groups.values()))
+    # the second fit of the same shape reuses the warm workers (no process start, no HIP init)
+    est2, res2 = _fit(tmp_path, "b")
+    assert next(iter(T._GROUPS._groups.values())) is group
+    a = est.get_model().state_dict()
+    b = est2.get_model().state_dict()
+    for k in a:        # same data, same seeds, same reduction order: the same model
+        torch.testing.assert_close(a[k].float(), b[k].float(), atol=0, rtol=0)
+    # the same fit with the gradient on the process group (gloo) instead of xGMI
+    monkeypatch.setenv("RAYDP_ALLREDUCE", "rccl")
+    est3, res3 = _fit(tmp_path, "c")
+    h3 = [m for m in res3.metrics_history if "train_loss" in m]
+    assert h3[0]["allreduce"] == "torch.distributed:gloo", h3[0]
+    assert len(T._GROUPS) == 2          # a different environment is a different group
+    c = est3.get_model().state_dict()
+    for k in a:
+        if not a[k].dtype.is_floating_point:
+            continue
+        # the xGMI path sums the ranks inside the dW MFMA (rank-concatenated batch), the other
+        # path adds materialised per-rank dW: fp32 summation order only
+        rel = float((a[k].float() - c[k].float()).abs().max()) / max(1e-6, float(c[k].float().abs().max()))
+        assert rel < 5e-3, (k, rel)
+    T.release_worker_groups()
+    assert len(T._GROUPS) == 0

@@ -32,22 +32,31 @@ def _allreduce_main(rank, world, port, q):
     _init(rank, world, port)
     try:
         from raydp_amd.ops.comm import XgmiComm
-        n = 50_000
-        comm = XgmiComm.create(n, timeout_s=20.0)
+        # NYC gradient (194 KB), a 1 MiB bucket, the DLRM dense gradient (8.7 MB), an odd size
+        sizes = [48_513, 262_144, 2_177_185, 50_001]
+        comm = XgmiComm.create(max(sizes), timeout_s=20.0)
         if comm is None:
             q.put((rank, "create failed", 0.0))
             return
         worst = 0.0
-        for it in range(12):
+        for it in range(8):
+            n = sizes[it % len(sizes)]
             data = [torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + r)).cuda()
                     for r in range(world)]
             want = torch.zeros(n, device="cuda")
-            for r in range(world):
+            for r in range(world):       # rank order: the kernel's summation order
                 want = want + data[r]
-            t = data[rank].clone()
-            comm.allreduce_(t)
+            scale = 1.0 / world if it % 2 else 1.0
+            if it == 5:
+                # unaligned (scalar) path: a view starting one float into its storage
+                buf = torch.zeros(n + 1, device="cuda")
+                buf[1:] = data[rank]
+                t = buf[1:]
+            else:
+                t = data[rank].clone()
+            comm.allreduce_(t, scale)
             torch.cuda.synchronize()
-            worst = max(worst, float((t - want).abs().max()))
+            worst = max(worst, float((t - want * scale).abs().max()))
         q.put((rank, "ok" if comm.error() == 0 else "error word set", worst))
         torch.cuda.synchronize()
         dist.barrier()
@@ -95,7 +104,7 @@ def _fused_main(rank, world, port, q):
             labels = torch.randn(n, 1, generator=g)
             feats, labels = feats.to(dev), labels.to(dev)
             if mode == "xgmi":
-                xg = XgmiComm.create(tr.grads.numel(), timeout_s=20.0)
+                xg = XgmiComm.create(tr.grads.numel(), timeout_s=20.0, host_seq=True)
                 if xg is None:
                     q.put((rank, "create failed", None, None))
                     return
@@ -120,7 +129,7 @@ def _fused_main(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _run(target, world=2):
+def _run(target, world=2, timeout=100):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -128,7 +137,7 @@ def _run(target, world=2):
     for p in ps:
         p.start()
     try:
-        res = sorted(q.get(timeout=100) for _ in ps)
+        res = sorted(q.get(timeout=timeout) for _ in ps)
     finally:
         for p in ps:
             p.join(timeout=30)
@@ -137,10 +146,11 @@ def _run(target, world=2):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_allreduce_ranks_share_one_gpu(world):
-    """World 4 exercises the N-1 = 3 peer read fan-out and the flag protocol with more than
-    one remote writer per slot."""
+    """World 8 is a full MI355X node's fan-out: 7 peer reads per element and 7 remote flag
+    writers per region, one launch-wide rendezvous per call, 16-B peer loads (and the scalar
+    path for an unaligned buffer), buckets from 194 KB to 8.7 MB, sum and average."""
     res = _run(_allreduce_main, world)
     assert len(res) == world
     for rank, status, worst in res:
@@ -148,8 +158,9 @@ def test_xgmi_allreduce_ranks_share_one_gpu(world):
         assert worst < 1e-5, (rank, worst)
 
 
-def test_fused_step_loop_with_xgmi_reduce_matches_gloo_allreduce():
-    res = _run(_fused_main)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_fused_step_loop_with_xgmi_reduce_matches_gloo_allreduce(world):
+    res = _run(_fused_main, world)
     for rank, status, same, rel in res:
         assert status == "ok", (rank, status)
         assert same, "replicas diverged across ranks"
@@ -213,55 +224,124 @@ def _fallback_main(rank, world, port, q):
     try:
         from raydp_amd.exceptions import CollectiveError
         from raydp_amd.models.mlp_spec import extract_mlp_spec
-        from raydp_amd.ops.comm import XgmiComm
+        from raydp_amd.ops import comm as C
         from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
         from raydp_amd.torch.engine import FusedMLPEngine
         dev = torch.device("cuda", 0)
-
-        def trainer():
-            torch.manual_seed(0)
-            model = _nyc()
-            opt = torch.optim.Adam(model.parameters(), lr=1e-2)
-            return FusedMLPTrainer(extract_mlp_spec(model), optimizer_config(opt), loss_code(nn.MSELoss()), 64, dev)
-        tr = trainer()
+        torch.manual_seed(0)
+        model = _nyc()
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+        tr = FusedMLPTrainer(extract_mlp_spec(model), optimizer_config(opt), loss_code(nn.MSELoss()), 64, dev)
         g = torch.Generator().manual_seed(7 + rank)
         n = 64 * 16
         feats = torch.zeros(n, tr.feat_k, dtype=torch.bfloat16)
         feats[:, :20] = torch.randn(n, 20, generator=g).to(torch.bfloat16)
         labels = torch.randn(n, 1, generator=g)
         feats, labels = feats.to(dev), labels.to(dev)
-        xg = XgmiComm.create(tr.grads.numel(), timeout_s=20.0)
+        xg = C.XgmiComm.create(tr.grads.numel(), timeout_s=20.0, host_seq=True)
         if xg is None:
             q.put((rank, "create failed", None, None))
             return
-        real = tr.train_epoch
-
-        def flaky(*a, **k):
-            out = real(*a, **k)      # the epoch really ran (and mutated the state) ...
-            if k.get("xg") is not None and rank == 1:
-                raise CollectiveError("injected peer timeout")   # ... then one rank reports a miss
-            return out
-        tr.train_epoch = flaky
-        eng = types.SimpleNamespace(trainer=tr, world=world, drop_last=False, allreduce_kind="xgmi_oneshot")
-        FusedMLPEngine._xgmi_epoch(eng, xg, types.SimpleNamespace(feats_bf16=feats, labels=labels, n=n),
-                                   None, None)
+        eng = types.SimpleNamespace(trainer=tr, world=world, drop_last=False, xg=xg, ar=None, comm=None,
+                                    max_steps=None, shuffle=False, epoch=0, metrics_names=[],
+                                    train=types.SimpleNamespace(feats_bf16=feats, labels=labels, n=n))
+        eng._res = lambda m: {}
+        outcomes = []
+        for ep in range(2):
+            if ep == 1 and rank == 1:
+                xg._inject_error()          # rank 1 "missed a peer" during epoch 1
+            try:
+                FusedMLPEngine.train_epoch(eng)
+                outcomes.append("ok")
+            except CollectiveError:
+                outcomes.append("collective_error")
         torch.cuda.synchronize()
-        # reference: the same epoch from the same start over gloo
-        ref = trainer()
-
-        def ar(gr):
-            dist.all_reduce(gr)
-        ref.train_epoch(feats, labels, n, None, allreduce=ar, world_size=world)
-        torch.cuda.synchronize()
-        q.put((rank, eng.allreduce_kind, bool(eng._xgmi_broken),
-               bool(torch.equal(tr.params, ref.params)) and tr.step_count == ref.step_count))
+        # the process dropped the xGMI path: a new communicator is refused on every rank
+        again = C.XgmiComm.create(tr.grads.numel(), timeout_s=20.0, host_seq=True)
+        q.put((rank, tuple(outcomes), eng.xg is None, again is None))
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def test_xgmi_epoch_timeout_rolls_back_and_reruns_over_the_process_group():
+def test_xgmi_timeout_on_one_rank_fails_every_rank_in_the_same_epoch():
+    """A peer miss on ONE rank reaches every rank through the epoch-end vote (read with the
+    metrics, no extra host sync): all ranks raise CollectiveError in the same epoch -- a worker
+    failure, so the trainer restarts the group from its newest checkpoint -- and the process
+    stops using xGMI."""
     res = _run(_fallback_main)
-    for rank, kind, broken, same in res:
-        assert kind == "torch.distributed:gloo", (rank, kind)
-        assert broken and same, (rank, broken, same)
+    for rank, outcomes, dropped, refused in res:
+        assert outcomes == ("ok", "collective_error"), (rank, outcomes)
+        assert dropped and refused, (rank, dropped, refused)
+
+
+def _ddp_graph_main(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    import torch.nn as nn
+    _init(rank, world, port)
+    try:
+        from raydp_amd.ops import comm as C
+        from raydp_amd.parallel.ddp import DistributedDataParallel
+        dev = torch.device("cuda", 0)
+        g = torch.Generator().manual_seed(11 + rank)
+        xs = [torch.randn(64, 20, generator=g).to(dev) for _ in range(6)]
+        ys = [torch.randn(64, 1, generator=g).to(dev) for _ in range(6)]
+        outs = {}
+        for mode in ("eager", "graph"):
+            torch.manual_seed(0)
+            net = nn.Sequential(nn.Linear(20, 64), nn.ReLU(), nn.BatchNorm1d(64), nn.Linear(64, 1)).to(dev)
+            ddp = DistributedDataParallel(net)
+            assert ddp.capturable(), "NYC-sized DDP buckets must ride the capturable one-shot kernel"
+            opt = torch.optim.Adam(ddp.parameters(), lr=1e-2, capturable=True)
+            sx, sy = torch.zeros_like(xs[0]), torch.zeros_like(ys[0])
+
+            def step():
+                ddp.zero_grad()
+                loss = nn.functional.mse_loss(ddp(sx), sy)
+                loss.backward()
+                opt.step()
+            # two eager steps on a side stream (optimizer state, workspaces), then capture
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for i in range(2):
+                    sx.copy_(xs[i])
+                    sy.copy_(ys[i])
+                    step()
+            torch.cuda.current_stream().wait_stream(side)
+            if mode == "eager":
+                for i in range(2, 6):
+                    sx.copy_(xs[i])
+                    sy.copy_(ys[i])
+                    step()
+            else:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    step()
+                for i in range(2, 6):
+                    sx.copy_(xs[i])
+                    sy.copy_(ys[i])
+                    graph.replay()
+            torch.cuda.synchronize()
+            outs[mode] = torch.cat([t.detach().reshape(-1) for t in list(net.parameters()) + list(net.buffers())
+                                    if t.dtype.is_floating_point]).cpu()
+        gathered = [None] * world
+        dist.all_gather_object(gathered, outs["graph"])
+        same_ranks = all(bool(torch.equal(gathered[0], t)) for t in gathered)
+        q.put((rank, bool(torch.equal(outs["eager"], outs["graph"])), same_ranks))
+        dist.barrier()
+        C.reset_cache()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ddp_step_graph_replay_over_xgmi_matches_eager_bitwise(world):
+    """A whole DDP step (BN buffer broadcast, backward with the bucket all-reduce, average,
+    Adam) captured into one HIP graph and replayed at world > 1 trains bit for bit like the
+    eager loop, and every replica stays identical."""
+    res = _run(_ddp_graph_main, world)
+    for rank, same_as_eager, same_ranks in res:
+        assert same_as_eager, f"rank {rank}: graph replay diverged from the eager DDP loop"
+        assert same_ranks, "replicas diverged"

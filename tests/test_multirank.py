@@ -206,8 +206,10 @@ def test_gbdt_world_stages_cpu_tensors_through_gpu_for_rccl(monkeypatch):
     assert w._comm_device(torch.zeros(1)) == torch.device("cpu")
 
 
-def test_bucket_allreduce_never_routes_large_buckets_to_xgmi():
-    """The one-shot xGMI kernel is for latency-bound buckets: > 1 MiB goes to RCCL."""
+def test_bucket_allreduce_routing_threshold():
+    """One-shot xGMI for fp32 buckets up to spark.ray.mi355x.allreduce.oneshot_max_mb (16 MiB:
+    the DLRM dense gradient, 8.7 MB, is one one-shot bucket); larger ones and other dtypes go
+    to RCCL, and nothing routes to xGMI without a communicator."""
     from raydp_amd.ops import comm
 
     class FakeFlat:
@@ -219,14 +221,19 @@ def test_bucket_allreduce_never_routes_large_buckets_to_xgmi():
 
         def is_contiguous(self):
             return True
+
+    class FakeXg:
+        max_floats = comm.XG_BUCKET_MAX_BYTES // 4
     b = comm.BucketAllreduce.__new__(comm.BucketAllreduce)
-    b.group, b.xg = None, object()
-    limit = comm.XG_BUCKET_MAX_BYTES // 4
-    assert comm.XG_BUCKET_MAX_BYTES == 1 << 20
-    assert b.routes_to_xgmi(FakeFlat(limit)) if torch.cuda.is_available() else True
+    b.group, b.xg, b.limit = None, FakeXg(), comm.oneshot_max_bytes()
+    assert comm.oneshot_max_bytes() == 16 << 20
+    limit = b.limit // 4
+    assert b.routes_to_xgmi(FakeFlat(limit))
     assert not b.routes_to_xgmi(FakeFlat(limit + 1))
-    assert not b.routes_to_xgmi(FakeFlat(2_177_185))          # DLRM dense gradient (8.7 MB)
+    assert b.routes_to_xgmi(FakeFlat(2_177_185))              # DLRM dense gradient (8.7 MB)
     assert not b.routes_to_xgmi(FakeFlat(1024, torch.bfloat16))
+    b.limit = 1 << 20                                        # a lowered threshold is honoured
+    assert not b.routes_to_xgmi(FakeFlat(2_177_185))
     b.xg = None
     assert not b.routes_to_xgmi(FakeFlat(16))
 
@@ -287,3 +294,48 @@ def test_sharded_embeddings_exchange_batch_sizes_only_on_change():
     for r in res:
         assert r[1], r
         assert r[2] == 2, r       # first step and the step where the size changed
+
+
+def test_fused_engine_adds_no_host_sync_per_epoch_at_world_2(monkeypatch):
+    """World > 1 costs of the fused engine's epoch: no collective and no host read of its own
+    (the step count is agreed once at load -- and not at all for trainer-split equal shards;
+    the xGMI vote rides in the metrics read inside the native epoch). Counted with the
+    distributed API and Tensor.item instrumented around FusedMLPEngine.train_epoch / load."""
+    import types
+
+    import torch.distributed as dist
+    from raydp_amd.torch import engine as E
+
+    calls = []
+    for name in ("all_reduce", "broadcast", "all_gather", "all_gather_object", "barrier", "broadcast_object_list"):
+        monkeypatch.setattr(dist, name, lambda *a, _n=name, **k: calls.append(_n))
+    real_item = torch.Tensor.item
+    monkeypatch.setattr(torch.Tensor, "item", lambda self: (calls.append("item"), real_item(self))[1])
+    monkeypatch.setattr(dist, "get_backend", lambda *a, **k: "gloo")
+
+    class FakeTrainer:
+        batch, steps_in_epoch = 64, 4
+
+        def train_epoch(self, *a, **k):
+            return {"loss": 0.5, "mae": 0.1, "mse": 0.2, "acc": 0.0, "xg_vote": 0.0}
+
+        def note_steps(self, n):
+            pass
+    shard = types.SimpleNamespace(feats_bf16=None, labels=None, n=256)
+    eng = types.SimpleNamespace(trainer=FakeTrainer(), world=2, drop_last=True, xg=None, ar=None, comm=None,
+                                max_steps=None, shuffle=False, epoch=0, metrics_names=["MeanAbsoluteError"],
+                                train=shard)
+    eng._res = lambda m: E.FusedMLPEngine._res(eng, m)
+    for _ in range(3):
+        E.FusedMLPEngine.train_epoch(eng)
+    assert calls == [], calls
+    # load(): trainer-split shards are equal -> nothing; SPMD local shards -> one agreement
+    monkeypatch.setattr(E, "_ShardTensors", lambda *a, **k: shard)
+    eng.trainer.feat_k, eng.device = 24, torch.device("cpu")
+    cfg = {"feature_columns": ["a"], "feature_types": None, "label_column": "y"}
+    eng.equal_shards = True
+    E.FusedMLPEngine.load(eng, None, None, cfg)
+    assert calls == [], calls
+    eng.equal_shards = False
+    E.FusedMLPEngine.load(eng, None, None, cfg)
+    assert calls == ["all_reduce", "item"], calls
