@@ -37,6 +37,7 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.local_exec_bytes", "RAYDP_LOCAL_EXEC_BYTES", "4m"},
     {"spark.ray.mi355x.xg_opt_stride", "RAYDP_XG_OPT_STRIDE", "1"},
     {"spark.ray.mi355x.overlap_conversion", "RAYDP_OVERLAP_CONVERSION", "1"},
+    {"spark.ray.mi355x.udf_verify", "RAYDP_UDF_VERIFY", "sampled"},
 };
 
 // Value of a key: its environment variable when set and non-empty, else the default.

@@ -53,6 +53,8 @@ enum BinKind : int32_t {
   B_MOD_PY = 5,      // numpy np.mod (sign of divisor)
   B_FLOORDIV_PY = 6, // numpy np.floor_divide
   B_POW = 7, B_MIN = 8, B_MAX = 9,
+  B_PYMIN = 10,      // Python builtin min(a, b): b if b < a else a (NaN order-dependent, as Python)
+  B_PYMAX = 11,      // Python builtin max(a, b): b if b > a else a
 };
 
 enum CmpKind : int32_t { C_LT = 0, C_LE = 1, C_GT = 2, C_GE = 3, C_EQ = 4, C_NE = 5 };
@@ -391,6 +393,12 @@ template <typename T> void run_bin(Regs& R, const Instr& I, int n) {
       break;
     case B_MAX:
       for (int i = 0; i < n; ++i) o[i] = (a[i] != a[i]) ? a[i] : (b[i] != b[i]) ? b[i] : (b[i] > a[i] ? b[i] : a[i]);
+      break;
+    case B_PYMIN:
+      for (int i = 0; i < n; ++i) o[i] = b[i] < a[i] ? b[i] : a[i];
+      break;
+    case B_PYMAX:
+      for (int i = 0; i < n; ++i) o[i] = b[i] > a[i] ? b[i] : a[i];
       break;
     default: break;
   }

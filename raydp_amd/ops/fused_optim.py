@@ -54,17 +54,14 @@ def _lib():
     return L
 
 
-# weight -> (tower, layer index): fused Linear towers register the weights whose bf16 image
-# they read, so the optimizer kernel can keep the image current
-_IMAGE_OWNERS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
-
-
 def register_image(weight: torch.Tensor, tower, layer: int):
-    _IMAGE_OWNERS[weight] = (weakref.ref(tower), layer)
+    """A fused Linear tower reads a bf16 image of ``weight``: remember (on the parameter itself,
+    weakly) who owns it, so the optimizer kernel can keep the image current."""
+    weight._raydp_image_owner = (weakref.ref(tower), layer)
 
 
 def _image_of(p):
-    ent = _IMAGE_OWNERS.get(p)
+    ent = getattr(p, "_raydp_image_owner", None)
     if ent is None:
         return None, None, None
     tower = ent[0]()

@@ -44,7 +44,7 @@ from raydp_amd.spark import column as C
 T_BOOL, T_I32, T_I64, T_F32, T_F64 = 0, 1, 2, 3, 4
 OP_LOAD, OP_CONST, OP_CAST, OP_BIN, OP_CMP, OP_UN, OP_AND, OP_OR, OP_IFELSE, OP_DT, OP_FILTER, \
     OP_ISNULL, OP_FILLNULL = range(1, 14)
-B_ADD, B_SUB, B_MUL, B_DIV, B_MOD_SPARK, B_MOD_PY, B_FLOORDIV_PY, B_POW, B_MIN, B_MAX = range(10)
+B_ADD, B_SUB, B_MUL, B_DIV, B_MOD_SPARK, B_MOD_PY, B_FLOORDIV_PY, B_POW, B_MIN, B_MAX, B_PYMIN, B_PYMAX = range(12)
 C_LT, C_LE, C_GT, C_GE, C_EQ, C_NE = range(6)
 U_NEG, U_ABS, U_NOT, U_SQRT, U_FLOOR, U_CEIL, U_TRUNC, U_ISNAN = range(8)
 D_FIELDS = {"year": 0, "month": 1, "dayofmonth": 2, "hour": 3, "minute": 4, "second": 5,
@@ -56,7 +56,8 @@ _ARROW_OF = {T_BOOL: pa.bool_(), T_I32: pa.int32(), T_I64: pa.int64(), T_F32: pa
              T_F64: pa.float64()}
 
 _VERIFY_FIRST, _VERIFY_LATER = 64, 4
-STATS = {"fused_partitions": 0, "fallback_partitions": 0, "compiles": 0, "udf_retired": 0}
+STATS = {"fused_partitions": 0, "fallback_partitions": 0, "compiles": 0, "udf_retired": 0,
+         "udf_guard_fallbacks": 0}
 
 
 class _Unsupported(Exception):
@@ -458,8 +459,9 @@ class _ChainCompiler:
         for a in args:
             if not (_is_num(a.atype) or a.ct == T_BOOL):
                 raise _Unsupported("udf arg type")
-        res = _UdfCompiler(self.b, u).compile(args)
-        self.b.taps.append((u, res, args))
+        uc = _UdfCompiler(self.b, u)
+        res = uc.compile(args)
+        self.b.taps.append((u, res, args, uc.guards))
         return res
 
     # -- operators ----------------------------------------------------------------------
@@ -580,6 +582,11 @@ class _UdfCompiler:
             raise _Unsupported("signature")
         self.fdef = fdef
         self.arg_names = [a.arg for a in fdef.args.args]
+        # rows where Python raises but the VM computes a number (zero divisor, negative base of
+        # a fractional power, math.sqrt of a negative, int() of NaN/inf, int64 overflow): each
+        # guard is checked on the partition's values and sends the partition to the per-row
+        # path instead of letting an inf/NaN/wrapped value through
+        self.guards: List[tuple] = []
         self.globals = dict(fn.__globals__)
         if fn.__closure__:
             for name, cell in zip(fn.__code__.co_freevars, fn.__closure__):
@@ -708,6 +715,7 @@ class _UdfCompiler:
                 raise _Unsupported("integer power")
             xv = b.cast(self._strong(x, y if isinstance(y, Val) else None), ct)
             yv = b.cast(self._strong(y, x if isinstance(x, Val) else None), ct)
+            self._guard_binop(k, x, y, xv, yv, ct)
             return b.bin(k, xv, yv, ct)
         if isinstance(node, ast.UnaryOp):
             v = self._expr(node.operand, env)
@@ -754,15 +762,47 @@ class _UdfCompiler:
             return self._call(name, args)
         raise _Unsupported(type(node).__name__)
 
+    def _guard_binop(self, k, x, y, xv, yv, ct):
+        if k in (B_DIV, B_FLOORDIV_PY, B_MOD_PY):
+            if isinstance(y, Weak):
+                if y.v == 0:
+                    raise _Unsupported("constant zero divisor")   # Python raises on every row
+            else:
+                self.guards.append(("nz", yv))
+        elif k == B_POW:
+            if isinstance(y, Weak):
+                if float(y.v) == int(y.v) and y.v >= 0:
+                    return                                           # x ** n, n >= 0: defined
+                if float(y.v) != int(y.v) and y.v > 0:
+                    if not isinstance(x, Weak):
+                        self.guards.append(("nonneg", xv))           # fractional: base >= 0
+                    return
+            self.guards.append(("pow", xv, yv))
+        elif ct in (T_I32, T_I64) and k in (B_ADD, B_SUB, B_MUL):
+            # Python ints do not wrap: keep the operands where int64 cannot overflow
+            bound = (1 << 31) if k == B_MUL else (1 << 62)
+            for w, v in ((x, xv), (y, yv)):
+                if isinstance(w, Weak):
+                    if k == B_MUL and w.v not in (0, 1, -1):
+                        bound = min(bound, (1 << 62) // max(1, abs(int(w.v))))
+                    continue
+            for w, v in ((x, xv), (y, yv)):
+                if not isinstance(w, Weak):
+                    self.guards.append(("absle", v, bound))
+
     def _callable(self, fnode) -> str:
         if isinstance(fnode, ast.Name):
             obj = self.globals.get(fnode.id, getattr(builtins, fnode.id, None))
-            for nm in ("int", "float", "abs", "bool", "min", "max"):
+            for nm in ("int", "float", "abs", "bool"):
                 if obj is getattr(builtins, nm):
                     return nm
+            if obj is builtins.min or obj is builtins.max:
+                return "pymin" if obj is builtins.min else "pymax"
             if obj is math.fabs or obj is np.abs or obj is np.absolute:
                 return "abs"
-            if obj is math.sqrt or obj is np.sqrt:
+            if obj is math.sqrt:
+                return "msqrt"        # raises on a negative argument (np.sqrt gives NaN)
+            if obj is np.sqrt:
                 return "sqrt"
             raise _Unsupported(f"call {fnode.id}")
         if isinstance(fnode, ast.Attribute) and isinstance(fnode.value, ast.Name):
@@ -772,7 +812,7 @@ class _UdfCompiler:
             if mod is np and fnode.attr in ("sqrt", "minimum", "maximum"):
                 return {"minimum": "min", "maximum": "max"}.get(fnode.attr, fnode.attr)
             if mod is math and fnode.attr in ("fabs", "sqrt"):
-                return "abs" if fnode.attr == "fabs" else "sqrt"
+                return "abs" if fnode.attr == "fabs" else "msqrt"
         raise _Unsupported("callable")
 
     def _call(self, name, args):
@@ -791,13 +831,15 @@ class _UdfCompiler:
                 return b.const(bool(vs[0]), pa.bool_())
             if name == "abs":
                 return Weak(abs(vs[0]))
-            if name in ("min", "max") and len(vs) >= 2:
-                return Weak(min(vs) if name == "min" else max(vs))
+            if name in ("min", "max", "pymin", "pymax") and len(vs) >= 2:
+                return Weak(min(vs) if name in ("min", "pymin") else max(vs))
             raise _Unsupported("constant call")
         args = [self._strong(a, next((x for x in args if isinstance(x, Val)), None)) for a in args]
         if name == "int":
             (v,) = args
             if v.ct in (T_F32, T_F64):
+                self.guards.append(("finite", v))      # int(nan) / int(inf) raise
+                self.guards.append(("absle", v, float(1 << 62)))
                 v = b.un(U_TRUNC, v)
             return b.cast(v, T_I64)
         if name == "float":
@@ -811,21 +853,26 @@ class _UdfCompiler:
             if v.ct == T_BOOL:
                 raise _Unsupported("abs bool")
             return b.un(U_ABS, v)
-        if name == "sqrt":
+        if name in ("sqrt", "msqrt"):
             (v,) = args
             ct = v.ct if v.ct in (T_F32, T_F64) else T_F64
             if v.ct == T_BOOL:
                 raise _Unsupported("sqrt bool")
+            if name == "msqrt":
+                self.guards.append(("nonneg", v))
             return b.un(U_SQRT, b.cast(v, ct))
-        if name in ("min", "max"):
+        if name in ("min", "max", "pymin", "pymax"):
             if len(args) < 2:
                 raise _Unsupported("min/max arity")
+            # numpy minimum/maximum propagate NaN; Python's builtins keep the running value
+            # unless the next item compares smaller/greater (a left fold, NaN order-dependent)
+            op = {"min": B_MIN, "max": B_MAX, "pymin": B_PYMIN, "pymax": B_PYMAX}[name]
             out = args[0]
             for y in args[1:]:
                 ct = _np_promote(out, y)
                 xv = b.cast(self._strong(out, y if isinstance(y, Val) else None), ct)
                 yv = b.cast(self._strong(y, out if isinstance(out, Val) else None), ct)
-                out = b.bin(B_MIN if name == "min" else B_MAX, xv, yv, ct)
+                out = b.bin(op, xv, yv, ct)
             return out
         raise _Unsupported(name)
 
@@ -856,9 +903,12 @@ class Program:
             else:
                 self.columns.append((name, ref))
         self.taps = []
-        for u, res, args in b.taps:
+        for u, res, args, guards in b.taps:
+            gs = [(g[0], [("k", v.const) if v.const is not None else ("o", export(v)) for v in g[1:]
+                          if isinstance(v, Val)], [v for v in g[1:] if not isinstance(v, Val)])
+                  for g in guards]
             self.taps.append((u, export(res), [("k", a.const) if a.const is not None else ("o", export(a))
-                                               for a in args]))
+                                               for a in args], gs))
         self.out_types = [v.atype for v in outs]
         self.out_ct = [v.ct for v in outs]
         self._allocate(b, outs)
@@ -1014,8 +1064,11 @@ class Program:
                     st = ()
                 stats[j] = st
             return st
-        for k, (u, r, argix) in enumerate(self.taps):
+        for k, (u, r, argix, guards) in enumerate(self.taps):
             if any(a[0] == "o" and outs[a[1]].null_count for a in argix):
+                return None
+            if guards and _guard_trips(guards, view):
+                STATS["udf_guard_fallbacks"] += 1
                 return None
             args = [view(a[1]) if a[0] == "o" else a[1] for a in argix]
             ext = [extremes(a[1]) if a[0] == "o" else () for a in argix]
@@ -1047,6 +1100,9 @@ class Program:
         first = not self.verified[k]
         cnt = min(m, _VERIFY_FIRST if first else _VERIFY_LATER)
         idx = {(j * (m - 1)) // max(1, cnt - 1) for j in range(cnt)}
+        from raydp_amd.utils.config import get as conf_get
+        if conf_get("spark.ray.mi355x.udf_verify") == "full":
+            idx = set(range(m))           # every row against the Python function
         seen = self.__dict__.setdefault("_ranges", {}).get(k)
         grow = []
         for j, e in enumerate(ext):
@@ -1082,6 +1138,35 @@ class Program:
                 cur[j] = (lo, hi) if r is None else (min(r[0], lo), max(r[1], hi))
             self._ranges[k] = cur
         return True
+
+
+def _guard_trips(guards, view) -> bool:
+    """True when some row of this partition makes Python raise where the VM would not."""
+    with np.errstate(all="ignore"):
+        for kind, refs, params in guards:
+            vals = [view(r[1]) if r[0] == "o" else np.asarray(r[1]) for r in refs]
+            if kind == "nz":
+                if (vals[0] == 0).any():
+                    return True
+            elif kind == "nonneg":
+                if (vals[0] < 0).any():
+                    return True
+            elif kind == "finite":
+                if not np.isfinite(vals[0]).all():
+                    return True
+            elif kind == "absle":
+                v = vals[0]
+                if v.dtype.kind == "f":
+                    if (np.abs(v) > params[0]).any():
+                        return True
+                elif ((v > params[0]) | (v < -params[0])).any():
+                    return True
+            elif kind == "pow":
+                base, ex = (vals + [np.asarray(p) for p in params])[:2]
+                frac = np.floor(ex) != ex if np.asarray(ex).dtype.kind == "f" else False
+                if ((base < 0) & frac).any() or ((base == 0) & (ex < 0)).any():
+                    return True
+    return False
 
 
 def _argmin(a):

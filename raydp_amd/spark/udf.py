@@ -188,10 +188,10 @@ class _Vectorizer:
                 return np.abs
             if obj is builtins.bool:
                 return lambda x: np.asarray(x).astype(bool)
-            if obj is builtins.min:
-                return lambda *a: _reduce(np.minimum, a)
+            if obj is builtins.min:      # Python's fold: keep the running value unless y < it
+                return lambda *a: _reduce(lambda x, y: np.where(np.less(y, x), y, x), a)
             if obj is builtins.max:
-                return lambda *a: _reduce(np.maximum, a)
+                return lambda *a: _reduce(lambda x, y: np.where(np.greater(y, x), y, x), a)
             if obj is builtins.round:
                 return lambda x, d=0: np.round(x, d)
             if isinstance(obj, np.ufunc):
@@ -275,8 +275,13 @@ class UserDefinedFunction:
             if self._vec is None:
                 self._vec = _Vectorizer(self.func)
             nps = [a.to_numpy(zero_copy_only=False) for a in arrays]
-            res = self._vec(nps, n)
+            # numpy returns inf/nan (or a warning) where Python raises -- a zero divisor, 0/0,
+            # an invalid power: such a batch runs per row, with Python's semantics
+            with np.errstate(divide="raise", invalid="raise", over="raise"):
+                res = self._vec(nps, n)
             res = np.broadcast_to(np.asarray(res), (n,)).astype(np_dtype)
+        except FloatingPointError:
+            return None                    # this batch only: the UDF stays vectorised
         except Exception:  # noqa: BLE001 - any failure means "not vectorizable"
             self._vec_state = "failed"
             return None
@@ -310,7 +315,12 @@ class UserDefinedFunction:
         cols = [a.to_pylist() for a in arrays]
         f = self.func
         out = [f(*row) for row in zip(*cols)] if cols else [f() for _ in range(n)]
-        return pa.array(out, type=out_type, from_pandas=True)
+        if pa.types.is_floating(out_type):
+            # a Python int returned for a floating column converts like float(x) (Arrow refuses
+            # ints beyond 2**53 that the vectorised paths cast without complaint)
+            out = [float(v) if isinstance(v, (int, np.integer)) and not isinstance(v, (bool, np.bool_)) else v
+                   for v in out]
+        return pa.array(out, type=out_type, from_pandas=False)
 
     @property
     def vectorized(self) -> bool:

@@ -172,6 +172,10 @@ register("spark.ray.mi355x.local_exec_bytes", "bytes", "4m",
 register("spark.ray.mi355x.xg_opt_stride", "int", 1,
          "workgroup stride of the fused reduce+optimizer kernel (1: every XCD pulls peer lines)",
          env="RAYDP_XG_OPT_STRIDE")
+register("spark.ray.mi355x.udf_verify", "str", "sampled",
+         "inlined Python UDFs: sampled (spread rows + every argument's new extreme rows per partition) "
+         "or full (every row checked against the Python function)", env="RAYDP_UDF_VERIFY",
+         choices=["sampled", "full"])
 register("spark.ray.mi355x.overlap_conversion", "bool", True,
          "fit_on_spark: the training engine is built (device buffers, kernels, parameter upload) while "
          "the conversion stage runs on the executors; the dataset blocks are awaited at first use",

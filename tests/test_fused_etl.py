@@ -211,43 +211,77 @@ def _complexish(x):
     return x ** 0.5
 
 
-def test_udf_verification_retires_mismatching_udf(spark, monkeypatch):
+def test_python_raising_rows_take_the_row_path(spark, monkeypatch):
     # numpy gives NaN for a negative base, Python a complex number (an error for a double UDF):
-    # the per-partition check sees the minimum row, retires the UDF, and the Arrow path raises
+    # the compile-time guard (base >= 0 of a fractional power) sends the partition holding the
+    # negative row to the per-row path, which raises like Spark would
     u = udf(_complexish, "double")
     t = pa.table({"x": pa.array(np.concatenate([np.linspace(1, 9, 50), [-4.0]]))})
     df = spark.createDataFrame(t).withColumn("r", u("x"))
     monkeypatch.setenv("RAYDP_FUSED_ETL", "1")
-    before = exprc.STATS["udf_retired"]
+    before = exprc.STATS["udf_guard_fallbacks"]
     with pytest.raises((TypeError, pa.ArrowInvalid)):
         [df._plan.compute(i) for i in range(df._plan.num_partitions())]
-    assert exprc.STATS["udf_retired"] > before
+    assert exprc.STATS["udf_guard_fallbacks"] > before
+
+
+def _ratio(a, b):
+    return a / b + a // b + a % b
+
+
+def test_zero_divisor_mid_range_takes_the_row_path(spark, monkeypatch):
+    """A zero divisor in the middle of the value range (never a sampled extreme) must not come
+    back as inf/nan: Python raises ZeroDivisionError there."""
+    u = udf(_ratio, "double")
+    x = np.arange(-3, 4, dtype=np.int64).repeat(30)          # divisor -3..3, zeros mid-range
+    t = pa.table({"a": pa.array(np.arange(len(x), dtype=np.int64) + 7), "b": pa.array(x)})
+    df = spark.createDataFrame(t).withColumn("r", u("a", "b"))
+    monkeypatch.setenv("RAYDP_FUSED_ETL", "1")
+    before = exprc.STATS["udf_guard_fallbacks"]
+    with pytest.raises(Exception) as ei:
+        [df._plan.compute(i) for i in range(df._plan.num_partitions())]
+    assert "ZeroDivision" in repr(ei.value) or "division" in str(ei.value)
+    assert exprc.STATS["udf_guard_fallbacks"] > before
+    # without zeros the same UDF stays inlined and matches the row path exactly
+    t2 = pa.table({"a": pa.array(np.arange(200, dtype=np.int64) - 50),
+                   "b": pa.array(np.where(np.arange(200) % 2, 3, -2).astype(np.int64))})
+    d = _same(spark.createDataFrame(t2).withColumn("r", u("a", "b")), monkeypatch)
+    assert d["fused_partitions"] > 0
+
+
+LIMIT = 100.0
+
+
+def _clip(x):
+    return x if x < LIMIT else -x
 
 
 def test_udf_verification_follows_new_value_ranges(spark, monkeypatch):
     """Partitions inside the value range already checked at a call site only get spread rows
-    checked; a later partition that leaves that range has its extreme rows checked: the
-    mismatch (negative base) is caught there and the UDF retired."""
-    def _root2(x):          # its own function: retirement is remembered per function
-        return x ** 0.5
-    u = udf(_root2, "double")
-    good = np.linspace(1, 9, 200)
-    parts = [pa.table({"x": pa.array(good)}), pa.table({"x": pa.array(good[::-1].copy())}),
-             pa.table({"x": pa.array(np.concatenate([good[:150], [-4.0], good[150:]]))})]
+    checked; a later partition that leaves that range has its extreme rows checked. Here the
+    Python function's behaviour changes above x = 5 after compilation (a module global the
+    compiled program captured), which only rows beyond the checked range expose: the
+    mismatch is caught there and the UDF retired to the row path."""
+    global LIMIT
+    u = udf(_clip, "double")
+    good = np.linspace(1, 4.9, 200)
     monkeypatch.setenv("RAYDP_FUSED_ETL", "1")
     before = exprc.STATS["udf_retired"]
 
     def run(t):   # same chain structure: the same compiled program (and checked ranges) serves all
         df = spark.createDataFrame(t).withColumn("r", u("x"))
         return pa.concat_tables([df._plan.compute(i) for i in range(df._plan.num_partitions())])
-    for t in parts[:2]:
-        np.testing.assert_allclose(np.asarray(run(t).column("r")), np.sqrt(np.asarray(t.column("x"))))
-    assert exprc.STATS["udf_retired"] == before
-    fused = exprc.STATS["fused_partitions"]
-    assert fused > 0
-    with pytest.raises((TypeError, pa.ArrowInvalid)):
-        run(parts[2])
-    assert exprc.STATS["udf_retired"] > before
+    try:
+        for t in (pa.table({"x": pa.array(good)}), pa.table({"x": pa.array(good[::-1].copy())})):
+            np.testing.assert_allclose(np.asarray(run(t).column("r")), np.asarray(t.column("x")))
+        assert exprc.STATS["udf_retired"] == before
+        LIMIT = 5.0
+        t3 = pa.table({"x": pa.array(np.concatenate([good[:150], [9.0], good[150:]]))})
+        r = np.asarray(run(t3).column("r"))
+        assert r[150] == -9.0            # the row path's answer, not the stale program's
+        assert exprc.STATS["udf_retired"] > before
+    finally:
+        LIMIT = 100.0
 
 
 def test_all_rows_filtered_and_empty_input(spark, monkeypatch):
