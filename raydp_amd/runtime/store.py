@@ -236,7 +236,19 @@ def _shm_dir() -> str:
     return d if os.path.isdir(d) and os.access(d, os.W_OK) else None
 
 
+def colocated_stores() -> int:
+    """How many object stores this node's processes open side by side: one per local rank of
+    an SPMD job (``LOCAL_WORLD_SIZE``, set by torchrun and by bench.py's self-launch), else 1."""
+    try:
+        return max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    except ValueError:
+        return 1
+
+
 def default_capacity() -> int:
+    """Arena size: 30% of the free shared memory, split between the stores co-located on this
+    node (8 SPMD ranks must not each claim 30% -- 240% of /dev/shm, a SIGBUS at data scale),
+    at most 64 GiB each."""
     env = os.environ.get("RAYDP_OBJECT_STORE_BYTES")
     if env:
         return int(env)
@@ -245,7 +257,8 @@ def default_capacity() -> int:
         avail = st.f_bavail * st.f_frsize
     except OSError:
         avail = 8 << 30
-    return int(min(max(avail * 0.3, 256 << 20), 64 << 30))
+    share = avail * 0.3 / colocated_stores()
+    return int(min(max(share, 16 << 20), 64 << 30))
 
 
 def open_store(node_id: str, capacity: Optional[int], session_dir: str) -> SharedObjectStore:

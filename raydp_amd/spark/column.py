@@ -478,6 +478,26 @@ class WindowExpr(Expr):
         return f"{self.fn}() OVER (...)"
 
 
+def map_children(e: Expr, fn) -> Expr:
+    """A shallow copy of ``e`` whose child expressions are replaced by ``fn(child)`` (every
+    Expr-valued attribute, list element and tuple element; other state is shared)."""
+    import copy
+
+    def conv(v):
+        if isinstance(v, Expr):
+            return fn(v)
+        if isinstance(v, list):
+            return [conv(x) for x in v]
+        if isinstance(v, tuple):
+            return tuple(conv(x) for x in v)
+        return v
+    out = copy.copy(e)
+    for k, v in list(vars(out).items()):
+        if isinstance(v, (Expr, list, tuple)):
+            setattr(out, k, conv(v))
+    return out
+
+
 def _to_expr(v, name_is_col=False) -> Expr:
     if isinstance(v, Column):
         return v._expr

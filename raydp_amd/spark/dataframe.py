@@ -20,7 +20,7 @@ import pyarrow.compute as pc
 from raydp_amd.spark import plan as P
 from raydp_amd.spark import wide as W
 from raydp_amd.spark.column import (AggExpr, Alias, ColRef, Column, Expr, Func, Lit, SortOrder,
-                                    WindowExpr, _to_expr, as_array)
+                                    WindowExpr, _to_expr, as_array, map_children)
 from raydp_amd.spark.row import Row
 from raydp_amd.spark.types import StructType, from_arrow_schema
 
@@ -155,16 +155,34 @@ class GroupedData:
         if len(exprs) == 1 and isinstance(exprs[0], dict):
             from raydp_amd.spark import functions as F
             exprs = [getattr(F, fn if fn != "mean" else "avg")(c) for c, fn in exprs[0].items()]
-        aggs = []
+        aggs, post, hidden = [], [], {}
+
+        def lift(e):
+            # an aggregate inside a larger expression (round(avg(x), 2), sum(a) / count(b)):
+            # aggregate it under a hidden name, evaluate the expression on the grouped rows
+            if isinstance(e, AggExpr):
+                nm = e.name()
+                if nm not in hidden:
+                    hidden[nm] = f"__agg{len(hidden)}"
+                    aggs.append((e, hidden[nm]))
+                return ColRef(hidden[nm])
+            return map_children(e, lift)
         for c in exprs:
             e = c._expr
             name = e.name()
             if isinstance(e, Alias):
                 e = e.child
-            if not isinstance(e, AggExpr):
+            if isinstance(e, AggExpr):
+                aggs.append((e, name))
+                post.append(name)
+            elif e.is_aggregate():
+                post.append(Column(Alias(lift(e), name)))
+            else:
                 raise ValueError(f"{name} is not an aggregate expression")
-            aggs.append((e, name))
-        return DataFrame(W.AggregatePlan(self._df._plan, self._keys, aggs), self._df._session)
+        out = DataFrame(W.AggregatePlan(self._df._plan, self._keys, aggs), self._df._session)
+        if hidden:
+            out = out.select(*self._keys, *post)
+        return out
 
     def _simple(self, fn, cols):
         from raydp_amd.spark import functions as F
@@ -440,10 +458,19 @@ class DataFrame:
         return self._map(lambda t, i: P.sort_table(t, keys), "sortWithinPartitions")
 
     def groupBy(self, *cols):
-        keys = []
+        keys, df = [], self
         for c in _names_of(cols):
-            keys.append(c if isinstance(c, str) else c._expr.name())
-        return GroupedData(self, keys)
+            if isinstance(c, str):
+                keys.append(c)
+                continue
+            e = c._expr
+            inner = e.child if isinstance(e, Alias) else e
+            if isinstance(inner, ColRef) and not isinstance(e, Alias):
+                keys.append(inner.col_name)
+            else:     # an expression key: materialise it under its name first
+                df = df.withColumn(e.name(), c)
+                keys.append(e.name())
+        return GroupedData(df, keys)
 
     groupby = groupBy
 

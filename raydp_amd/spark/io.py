@@ -196,5 +196,15 @@ class DataFrameWriter:
         self._df._session._run(P.MapPlan(self._df._src(), write, "writeJson"))
         open(os.path.join(d, "_SUCCESS"), "w").close()
 
-    def saveAsTable(self, name):
-        self._df.createOrReplaceTempView(name)
+    def saveAsTable(self, name, format=None, mode=None, **kw):  # noqa: A002
+        """Persist as a parquet table of the session's warehouse (``spark.sql.warehouse.dir``);
+        ``spark.table(name)`` / ``spark.sql("select ... from name")`` read it back, from this
+        session or a later one."""
+        from raydp_amd.spark.sql import save_as_table
+        if format and format.lower() != "parquet":
+            raise NotImplementedError("saveAsTable stores parquet tables")
+        save_as_table(self._df._session, name, self._df, mode or self._mode)
+
+    def insertInto(self, tableName, overwrite=False):
+        from raydp_amd.spark.sql import _catalog
+        _catalog(self._df._session).save(tableName, self._df, "overwrite" if overwrite else "append")

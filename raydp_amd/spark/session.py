@@ -300,14 +300,23 @@ class SparkSession:
         return list(self._catalog)
 
     def table(self, name):
-        return self._catalog[name]
+        from raydp_amd.spark.sql import _catalog
+        return _catalog(self).lookup(name)
 
-    def sql(self, query: str):
-        q = query.strip().rstrip(";")
-        low = q.lower()
-        if low.startswith("select * from "):
-            return self._catalog[q[len("select * from "):].strip()]
-        raise NotImplementedError("only 'SELECT * FROM <view>' SQL is supported")
+    def tableExists(self, name) -> bool:
+        from raydp_amd.spark.sql import _catalog
+        return _catalog(self).exists(name)
+
+    def dropTempView(self, name) -> bool:
+        return self._catalog.pop(name, None) is not None
+
+    def sql(self, query: str, args=None):
+        """Run a Spark SQL statement (``raydp_amd/spark/sql.py``): queries over temp views and
+        warehouse tables, views, CTAS / INSERT, databases."""
+        from raydp_amd.spark.sql import execute
+        if args:
+            raise NotImplementedError("parameterised SQL (args=) is not supported")
+        return execute(self, query)
 
     def newSession(self):
         return self

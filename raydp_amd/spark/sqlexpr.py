@@ -269,7 +269,25 @@ class _Parser:
         fn = getattr(F, alias, None) or getattr(F, name, None)
         if fn is None:
             raise ValueError(f"unknown SQL function {name}")
+        # SQL passes every argument as an expression; the Python API takes some as plain
+        # values (round's scale, substring's positions, a date format, ...)
+        scalar_at = _SCALAR_ARGS.get(alias)
+        if scalar_at is not None:
+            args = [self._literal_value(a) if (i in scalar_at or (-1 in scalar_at and i > 0))
+                    and hasattr(a, "_expr") else a for i, a in enumerate(args)]
         return fn(*args)
+
+
+# argument positions the Python function API takes as values, not Columns (-1: every argument
+# after the first)
+_SCALAR_ARGS = {
+    "round": {-1}, "bround": {-1}, "substring": {-1}, "left": {-1}, "right": {-1}, "lpad": {1, 2},
+    "rpad": {1, 2}, "repeat": {-1}, "split": {-1}, "regexp_replace": {-1}, "regexp_extract": {-1},
+    "date_format": {-1}, "date_add": {-1}, "date_sub": {-1}, "add_months": {-1}, "format_number": {-1},
+    "locate": {0, 2}, "instr": {-1}, "translate": {-1}, "trunc": {-1}, "date_trunc": {0},
+    "from_unixtime": {-1}, "to_date": {-1}, "to_timestamp": {-1}, "unix_timestamp": {-1}, "sha2": {-1},
+    "conv": {-1}, "concat_ws": {0}, "percentile_approx": {-1}, "ntile": {0},
+}
 
 
 def parse(s: str):

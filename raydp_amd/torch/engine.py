@@ -281,8 +281,9 @@ class FusedMLPEngine:
     def optimizer_state_dict(self):
         opt = self.optimizer
         if self.detached:
-            # export into a private optimizer over the same parameters, never the caller's
-            priv = type(opt)(self.model.parameters(), lr=0.1)
+            # export into a private optimizer over the same parameter groups, never the caller's
+            # (its groups may cover a subset of the model, or several groups)
+            priv = type(opt)([dict(g, params=list(g["params"])) for g in opt.param_groups])
             priv.load_state_dict(opt.state_dict())
             opt = priv
         return self.trainer.export_optimizer_state(opt)

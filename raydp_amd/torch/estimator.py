@@ -456,6 +456,9 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             sys.setswitchinterval(min(switch, 2e-4))
             try:
                 fut = _conversion_pool().submit(convert)
+                # the short switch interval is only for the overlap: back to normal the moment
+                # the conversion is done, not after the whole training run
+                fut.add_done_callback(lambda _f: sys.setswitchinterval(switch))
                 train_ds = Dataset.deferred(_Pick(fut, 0))
                 evaluate_ds = Dataset.deferred(_Pick(fut, 1)) if evaluate_df is not None else None
                 in_flight.wait()

@@ -77,7 +77,7 @@ def test_fused_bce_with_logits_matches_torch(n):
     (la * 3.0).backward()
     (lb * 3.0).backward()
     assert abs(float(lb) - float(la)) <= 1e-5 * max(1.0, abs(float(la))), (float(lb), float(la))
-    torch.testing.assert_close(xb.grad.double(), xa.grad, rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(xb.grad.double(), xa.grad.double(), rtol=1e-5, atol=1e-8)
 
 
 def test_dlrm_step_with_fused_tail_matches_eager():

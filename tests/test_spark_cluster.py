@@ -324,3 +324,31 @@ def test_fault_inject_helpers(spark_on_ray_2_executors):
     assert new != old
     assert spark.range(0, 500, numPartitions=5).count() == 500
     assert "0" in spark._cluster.restarted_executors().values()
+
+
+def test_colocated_stores_share_the_node_shm_budget(monkeypatch):
+    """Eight SPMD ranks of one node (LOCAL_WORLD_SIZE=8) each open an object store: together
+    they never reserve more than the free /dev/shm (30% of it, split eight ways)."""
+    import os
+    import tempfile
+
+    from raydp_amd.runtime import store as S
+    monkeypatch.delenv("RAYDP_OBJECT_STORE_BYTES", raising=False)
+    st = os.statvfs(S._shm_dir() or "/tmp")
+    avail = st.f_bavail * st.f_frsize
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    stores = []
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            for r in range(8):
+                stores.append(S.open_store(f"budget-test-{r}", None, d))
+            total = sum(s.capacity for s in stores)
+            assert total <= avail, (total, avail)
+            assert total <= 0.3 * avail + (8 << 24), (total, avail)
+    finally:
+        for s in stores:
+            s.destroy()
+    # a lone process keeps the whole 30% (unless the 64 GiB cap binds)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    one = S.default_capacity()
+    assert one >= min(64 << 30, 4 * max(s.capacity for s in stores)), one
