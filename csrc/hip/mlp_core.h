@@ -418,6 +418,72 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
 #pragma unroll
           for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
         }
+        if (lcode == 4) {
+          // Cross entropy over the out <= 16 classes of one tile (a row's logits live in the 16
+          // lanes sharing lg). Labels arrive as a weighted one-hot row (t_c = w[y] at c = y,
+          // else 0; an ignored row is all zeros): with W = sum of the rows' weights,
+          //   loss = sum_rows (w_y * logsumexp(x) - w_y * x_y) / W
+          //   dL/dx_c = (w_y * softmax(x)_c - t_c) / W      (torch's weighted mean)
+          // and the row counts as correct when argmax_c x (first index on ties) is y.
+          float wsum = 0.f;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = mt * 16 + lg * 4 + r;
+              const float x = acc[j * MT + mt][r];
+              const float t = (colok && row < nvalid) ? tl[mt * 4 + r] : 0.f;
+              float mx = colok ? x : -INFINITY;
+              int bi = colok ? c : 1 << 20;
+#pragma unroll
+              for (int o = 1; o < 16; o <<= 1) {
+                const float om = __shfl_xor(mx, o);
+                const int oi = __shfl_xor(bi, o);
+                if (om > mx || (om == mx && oi < bi)) {
+                  mx = om;
+                  bi = oi;
+                }
+              }
+              const float ex = colok ? __expf(x - mx) : 0.f;
+              float se = ex, wr = t, tx = t * (colok ? x : 0.f);
+#pragma unroll
+              for (int o = 1; o < 16; o <<= 1) {
+                se += __shfl_xor(se, o);
+                wr += __shfl_xor(wr, o);
+                tx += __shfl_xor(tx, o);
+              }
+              const bool head = lr == 0 && row < nvalid;   // one lane per row
+              if (head) {
+                lsum += wr * (mx + __logf(se)) - tx;
+                wsum += wr;
+              }
+              if (t > 0.f && c == bi) csum += 1.f;          // the label's lane of a correct row
+              acc[j * MT + mt][r] = (colok && row < nvalid) ? wr * (ex / se) - t : 0.f;
+            }
+          const float wt = rx_wavesum(wsum);
+          const float invw = wt > 0.f ? 1.f / wt : 0.f;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              acc[j * MT + mt][r] *= invw;
+              gsum += acc[j * MT + mt][r];
+            }
+          lsum = rx_wavesum(lsum) * invw;
+          csum = rx_wavesum(csum);
+          if (lane == 0) {
+            atomicAdd(&metrics[0], (double)lsum);
+            atomicAdd(&metrics[5], (double)csum);
+            if (n == 0) {
+              atomicAdd(&metrics[3], (double)nvalid);
+              atomicAdd(&metrics[4], 1.0);
+            }
+          }
+          if (TRAIN) {
+            gsum = rx_colsum16(gsum);
+            if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum;
+          }
+        } else {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -434,8 +500,16 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
                 csum += ((acc[j * MT + mt][r] > d.acc_thr ? 1 : 0) == (int)t) ? 1.f : 0.f;
               const float sgn = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
               const bool quad = ae < beta;
-              lsum += quad ? 0.5f * e * e / beta : ae - 0.5f * beta;  // smooth-L1 term
-              g = lcode == 0 ? 2.f * e : (lcode == 1 && quad ? e / beta : sgn);
+              if (lcode == 3) {
+                // BCE with logits, softplus form (stable for either sign):
+                //   l = max(x, 0) - x t + log1p(exp(-|x|)),  dl/dx = sigmoid(x) - t
+                const float x = acc[j * MT + mt][r];
+                lsum += fmaxf(x, 0.f) - x * t + log1pf(__expf(-fabsf(x)));
+                g = 1.f / (1.f + __expf(-x)) - t;
+              } else {
+                lsum += quad ? 0.5f * e * e / beta : ae - 0.5f * beta;  // smooth-L1 term
+                g = lcode == 0 ? 2.f * e : (lcode == 1 && quad ? e / beta : sgn);
+              }
               g *= inv_n;
             }
             acc[j * MT + mt][r] = g;  // acc now holds G_{L-1}
@@ -461,6 +535,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
           gsum = rx_colsum16(gsum);
           if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum;
         }
+        }  // regression / BCE losses
       }
     }
   }

@@ -27,7 +27,8 @@ def _ru(x, m):
 
 
 def loss_code(loss) -> Optional[tuple]:
-    """(code, beta) for a supported mean-reduced regression loss, else None."""
+    """(code, beta) for a supported mean-reduced loss (MSE 0, SmoothL1 1, L1 2, BCE-with-logits
+    3, weighted cross entropy 4), else None."""
     if isinstance(loss, type) and issubclass(loss, nn.Module):
         try:
             loss = loss()
@@ -36,7 +37,35 @@ def loss_code(loss) -> Optional[tuple]:
     for cls, code in _LOSSES.items():
         if type(loss) is cls and getattr(loss, "reduction", "mean") == "mean":
             return code, float(getattr(loss, "beta", 1.0))
+    # BCEWithLogitsLoss() (mean, no weight / pos_weight): code 3, in the last layer's epilogue
+    if type(loss) is nn.BCEWithLogitsLoss and loss.reduction == "mean" and loss.weight is None \
+            and loss.pos_weight is None:
+        return 3, 1.0
+    # CrossEntropyLoss(weight=w) over class-index labels (mean, no label smoothing): code 4 --
+    # the engine feeds w[y]-weighted one-hot label rows (fused_labels)
+    if type(loss) is nn.CrossEntropyLoss and loss.reduction == "mean" and float(loss.label_smoothing) == 0.0:
+        w = loss.weight
+        if w is not None and (w.dim() != 1 or not bool((w > 0).all())):
+            return None
+        return 4, 1.0
     return None
+
+
+def fused_labels(loss, labels: torch.Tensor, classes: int) -> torch.Tensor:
+    """The label matrix the fused kernel reads for ``loss``: the ingested column as is, or for
+    cross entropy the ``[N, classes]`` one-hot rows scaled by the class weight (an
+    ``ignore_index`` row is all zeros: it adds nothing to the loss or the weight sum, as in
+    torch)."""
+    if type(loss) is not nn.CrossEntropyLoss:
+        return labels
+    y = labels.reshape(-1).round().long()
+    w = loss.weight.to(labels.device, torch.float32) if loss.weight is not None else \
+        torch.ones(classes, device=labels.device)
+    valid = (y >= 0) & (y < classes)
+    out = torch.zeros(y.numel(), classes, dtype=torch.float32, device=labels.device)
+    idx = torch.arange(y.numel(), device=labels.device)[valid]
+    out[idx, y[valid]] = w[y[valid]]
+    return out.contiguous()
 
 
 def optimizer_config(opt) -> Optional[dict]:

@@ -7,8 +7,9 @@
   the kernel's row gather. Used when the model is a fusable MLP (``models/mlp_spec.py``) --
   optionally behind an embedding front (per-column ``nn.Embedding`` lookups concatenated with
   dense columns, the stroke tutorial's NET_Model: the kernel gathers the table rows and stores
-  their gradients itself) -- the loss is MSE/SmoothL1/L1, the optimizer Adam/AdamW/SGD and the
-  metrics are MAE/MSE/binary Accuracy.
+  their gradients itself) -- the loss is MSE/SmoothL1/L1/BCE-with-logits (metrics MAE/MSE/binary
+  Accuracy) or class-weighted CrossEntropy over <= 16 classes (argmax Accuracy), the optimizer
+  Adam/AdamW/SGD.
 * ``TorchLoopEngine`` — any other model. Still device-resident (data ingested once, batches are
   device slices of a permuted index), loss and metrics accumulated on the device and read once
   per epoch; DDP via ``raydp_amd.parallel.ddp`` when ``world_size > 1``. On one GPU the whole
@@ -136,9 +137,6 @@ class FusedMLPEngine:
             return None
         if isinstance(feature_types, (list, tuple)) and len({t for t in feature_types}) > 1:
             return None
-        acc_thr = _binary_accuracy_threshold(metrics)
-        if acc_thr is False:
-            return None
         spec = extract_mlp_spec(model)
         lc = loss_code(loss)
         oc = optimizer_config(optimizer)
@@ -146,18 +144,28 @@ class FusedMLPEngine:
             return None
         if (spec.raw_features or spec.in_features) != len(feature_columns):
             return None
+        if lc[0] == 4:
+            # cross entropy: the classes of one 16-wide output tile; accuracy is the argmax,
+            # counted by the kernel (regression metrics do not apply)
+            if not 2 <= spec.out_features <= 16 or not _argmax_accuracy_only(metrics, spec.out_features):
+                return None
+            return spec, lc, oc, None
+        acc_thr = _binary_accuracy_threshold(metrics)
+        if acc_thr is False:
+            return None
         if acc_thr is not None and spec.out_features != 1:
             return None
         return spec, lc, oc, acc_thr
 
     def __init__(self, model, optimizer, spec, lc, oc, acc_thr, metrics, device, config, lr_scheduler_fn,
-                 detached: bool = False):
+                 detached: bool = False, loss=None):
         """``detached``: ``model`` / ``optimizer`` are the caller's own objects, only read here
         (parameters, running statistics, hyper-parameters and moments are copied to the device
         once); results are exported from the device buffers and the objects are never written."""
         from raydp_amd.ops.fused_mlp import FusedMLPTrainer
         self.model, self.metrics_names, self.device = model, metrics.names, device
         self.detached = detached
+        self.loss = loss if loss is not None else config.get("loss")   # label encoding (fused_labels)
         self.world = session.get_world_size()
         self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn,
                                        acc_thr=acc_thr)
@@ -209,12 +217,17 @@ class FusedMLPEngine:
         tr.refresh_images()
 
     def load(self, train_ds, eval_ds, config):
+        from raydp_amd.ops.fused_mlp import fused_labels
         fc, ft = config["feature_columns"], config["feature_types"]
         k = self.trainer.feat_k
         self.train = _ShardTensors(train_ds, fc, ft, config["label_column"], torch.float32,
                                    self.device, fused_stride=k)
         self.eval = _ShardTensors(eval_ds, fc, ft, config["label_column"], torch.float32, self.device,
                                   fused_stride=k) if eval_ds is not None else None
+        classes = self.trainer.desc.out_dim
+        for sh in (self.train, self.eval):
+            if sh is not None and sh.labels is not None:
+                sh.labels = fused_labels(self.loss, sh.labels, classes)
         if self.world > 1 and not self.equal_shards:
             # ranks that brought their own data (SPMD local shards) agree once per fit on the
             # step count, so every per-step collective is matched; shards split by the trainer
@@ -287,6 +300,21 @@ class FusedMLPEngine:
             priv.load_state_dict(opt.state_dict())
             opt = priv
         return self.trainer.export_optimizer_state(opt)
+
+
+def _argmax_accuracy_only(metrics, classes: int) -> bool:
+    """Every requested metric is an Accuracy the fused cross-entropy epilogue counts (argmax of
+    the logits == label): multiclass with ``classes`` classes, or unspecified."""
+    from raydp_amd.torch import metrics as M
+    for n in metrics.names:
+        m = metrics._metrics.get(n)
+        if n not in ("Accuracy", "MulticlassAccuracy") or type(m) not in (M.Accuracy,):
+            return False
+        kw = getattr(m, "kwargs", {})
+        if kw.get("task", "multiclass") != "multiclass" or kw.get("num_classes") not in (None, classes) \
+                or kw.get("average", "micro") != "micro" or kw.get("top_k", 1) != 1:
+            return False
+    return True
 
 
 def _binary_accuracy_threshold(metrics):

@@ -244,7 +244,8 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             lr_fn = None
             if config["lr_scheduler_creator"]:
                 lr_fn = _make_lr_schedule(optimizer, config["lr_scheduler_creator"], config)
-            engine = FusedMLPEngine(model, optimizer, spec, lc, oc, acc_thr, metrics, device, config, lr_fn)
+            engine = FusedMLPEngine(model, optimizer, spec, lc, oc, acc_thr, metrics, device, config, lr_fn,
+                                    loss=loss)
         else:
             model = model.to(device)       # in place: the optimizer keeps its parameter objects
             sched = config["lr_scheduler_creator"](optimizer, config) if config["lr_scheduler_creator"] else None
@@ -285,7 +286,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             return None
         spec, lc, oc, acc_thr = fused
         return FusedMLPEngine(model, opt, spec, lc, oc, acc_thr, metrics, device, config, None,
-                              detached=True)
+                              detached=True, loss=loss)
 
     @staticmethod
     def _train_loop(config, engine, start_epoch, device):

@@ -103,12 +103,15 @@ def make_train_func(features):
         from ray import train
         from ray.train import get_dataset_shard
         bs = config["batch_size"]
+        # device=DEVICE: on a GPU the shard is ingested into HBM once and batches are slices of it
         train_ds = get_dataset_shard("train").to_torch(feature_columns=features, label_column="stroke",
                                                        label_column_dtype=torch.long,
-                                                       feature_column_dtypes=feature_dtype, batch_size=bs)
+                                                       feature_column_dtypes=feature_dtype, batch_size=bs,
+                                                       device=DEVICE)
         test_ds = get_dataset_shard("test").to_torch(feature_columns=features, label_column="stroke",
                                                      label_column_dtype=torch.long,
-                                                     feature_column_dtypes=feature_dtype, batch_size=bs)
+                                                     feature_column_dtypes=feature_dtype, batch_size=bs,
+                                                     device=DEVICE)
         model = NET_Model(len(features))
         model = train.torch.prepare_model(model).to(DEVICE)
         criterion = nn.CrossEntropyLoss(weight=torch.tensor([0.35, 0.65], device=DEVICE))
