@@ -31,12 +31,6 @@
 // the persistent epoch kernel. Fused multiply-adds are written out (fmaf) where they pay.
 #pragma clang fp contract(off)
 
-// timing experiments only (raydp_amd/ops/mlp_jit.py RAYDP_MLP_EXPERIMENT): drop a store class
-#ifdef RX_EXP_NOSCRATCH
-constexpr bool kExpNoScratch = true;
-#else
-constexpr bool kExpNoScratch = false;
-#endif
 // Saved forward values (BN inputs / ReLU mask sources) stay fp32: a bf16 copy halves their
 // bytes but the BN gamma/beta gradients cancel to near zero for some channels, and Adam turns
 // their rounding error into sign flips of the update (measured: 12 % parameter error).
@@ -49,16 +43,6 @@ __device__ __forceinline__ int frag_off(int base, int n, int mt, int lane) {
   return base + ((n * MT + mt) * 64 + lane) * 4;
 }
 
-#ifdef RX_EXP_WTSTORE
-constexpr bool kWtStores = true;   // measured: no gain over plain 16-B stores here
-#else
-constexpr bool kWtStores = false;
-#endif
-#ifdef RX_EXP_NOWGRAD
-constexpr bool kExpNoWgrad = true;
-#else
-constexpr bool kExpNoWgrad = false;
-#endif
 
 // Row pad (elements) of the row-major LDS activations R: a row stride of max_k + 16 elements is
 // 2 (mod 4) 16-B units, which keeps the ds_read_b128 A-fragment reads (16 rows x 4 k-chunks per
@@ -197,11 +181,7 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restric
 // The first PK k-steps of a tile's weight fragments, fetched ahead of time (before the work
 // that precedes the GEMM) so their global round trip overlaps that work.
 constexpr int RX_PJ = 2;  // tiles per wave prefetched
-#ifdef RX_EXP_PK8
-constexpr int RX_PK = 8;  // measured: no gain over 4 (27.95 vs 27.80 us per persistent step)
-#else
-constexpr int RX_PK = 4;  // k-steps per tile prefetched
-#endif
+constexpr int RX_PK = 4;  // k-steps per tile prefetched (8 measured no faster: 27.95 vs 27.80 us/step)
 template <bool PS>
 __device__ __forceinline__ void gemm_prefetch(bf16x8 (&pre)[RX_PK], const u16* __restrict__ img, int boff, int K,
                                               int lg) {
@@ -371,8 +351,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
           // save the BN input for the backward pass (fragment-major, see frag_off)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            if (!kExpNoScratch)
-              *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) = acc[j * MT + mt];
+            *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) = acc[j * MT + mt];
         } else {
           mean = colok ? pr[3 * ly.out_n + c] : 0.f;
           invstd = colok ? rsqrtf(pr[4 * ly.out_n + c] + ly.eps) : 0.f;
@@ -644,12 +623,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       if (o < ly.out) {
         float* dst = Gr + ly.w_off + o * ly.in + i0;
         if (vec && i0 + 3 < ly.in) {
-          if (!kExpNoWgrad) {
-            if (kWtStores)
-              rx_store16_wt(Gr, (ly.w_off + o * ly.in + i0) * 4, a4);
-            else
-              *reinterpret_cast<f32x4*>(dst) = a4;
-          }
+          *reinterpret_cast<f32x4*>(dst) = a4;   // (write-through sc1 stores measured no faster)
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)

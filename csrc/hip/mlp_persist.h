@@ -245,10 +245,8 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     if (rx_tid() == 0)
       __hip_atomic_store(sync + RX_PS_FLAG(0), (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     stamp(s, 4);
-#ifndef RX_EXP_NOVEC
     ps_vector_update<C>(d, o, smem, Gr, m, v, rx_g(sched)[s], rx_g(sched)[nsteps + s], rx_g(sched)[2 * nsteps + s],
                         (opt_first && s == 0) ? 1 : 0);
-#endif
     stamp(s, 6);
     __syncthreads();
     stamp(s, 5);

@@ -43,9 +43,6 @@ def _f(x: float) -> str:
 def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
     L = desc.L
     out = ['#include "mlp_persist.h"', "", "namespace {", "", "struct JD {"]
-    exp = os.environ.get("RAYDP_MLP_EXPERIMENT")   # timing experiments only (wrong numerics)
-    if exp:
-        out = [f"#define RX_EXP_{e}" for e in exp.split(",")] + out
     for k in _DESC_INT:
         out.append(f"  static constexpr int {k} = {int(getattr(desc, k))};")
     out.append(f"  static constexpr float beta = {_f(desc.beta)};")

@@ -1,0 +1,71 @@
+#!/bin/bash
+# One entry point for the GPU-box work (run through gpurun). Every GPU step has its own time
+# limit and the script stops at the first failure.
+#   scripts/gpu.sh tests [pytest -k expr]        GPU test suite, then smoke()
+#   scripts/gpu.sh bench [N] [STEPS] [WARM] [REPS]  bench.py runs -> gpurun_out/bench.jsonl
+#   scripts/gpu.sh rehearse [N] [STEPS] [WARM]   N ranks on the one GPU: SPMD self-launch (gloo
+#                                                 bootstrap, xGMI gradients) + estimator topology
+#   scripts/gpu.sh prof NAME CMD...              rocprofv3 kernel trace + stats -> gpurun_out/prof/NAME
+#   scripts/gpu.sh pmc PASS bench|lin            one PMC counter pass (1..3) -> gpurun_out/pmc
+#   scripts/gpu.sh dlrm [BATCH...]               DLRM train bench (graph + eager) -> gpurun_out/dlrm.jsonl
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+T="python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider"
+cmd=$1; shift
+case $cmd in
+  tests)
+    K=${1:+-k "$1"}
+    timeout -k 10 900 $T tests/ -m gpu $K > gpurun_out/gpu_tests.log 2>&1
+    rc=$?; echo "gpu tests rc=$rc"; grep -E "passed|failed|^E  " gpurun_out/gpu_tests.log | tail -15
+    [ $rc -ne 0 ] && exit $rc
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+    rc=$?; tail -1 gpurun_out/smoke.log; exit $rc;;
+  bench)
+    N=${1:-1}; S=${2:-20}; W=${3:-5}; REPS=${4:-3}
+    for i in $(seq $REPS); do
+      timeout -k 10 300 python bench.py --gpus $N --steps $S --warmup $W >> gpurun_out/bench.jsonl 2>> gpurun_out/bench.err || exit 9
+    done
+    tail -c 1500 gpurun_out/bench.jsonl;;
+  rehearse)
+    N=${1:-2}; S=${2:-20}; W=${3:-5}
+    RAYDP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus $N --steps $S --warmup $W \
+      >> gpurun_out/rehearse_spmd.jsonl 2>> gpurun_out/rehearse.err || exit 12
+    timeout -k 10 300 python bench.py --gpus $N --gpu-share $(python -c "print(1/$N)") --topology estimator \
+      --steps $S --warmup $W >> gpurun_out/rehearse_estimator.jsonl 2>> gpurun_out/rehearse.err || exit 13
+    tail -c 900 gpurun_out/rehearse_spmd.jsonl; tail -c 900 gpurun_out/rehearse_estimator.jsonl;;
+  prof)
+    NAME=$1; shift
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/$NAME -o run \
+      -- "$@" > $R/gpurun_out/prof/$NAME.log 2>&1
+    rc=$?; echo "prof rc=$rc"; exit $rc;;
+  pmc)
+    mkdir -p gpurun_out/pmc
+    cd /tmp && export TMPDIR=/tmp
+    case $1 in
+      1) P="SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE";;
+      2) P="FETCH_SIZE TCC_HIT_sum SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES";;
+      3) P="WRITE_SIZE TCC_MISS_sum SQ_INSTS_VALU SQ_INSTS_SALU";;
+      *) echo "pass 1..3"; exit 2;;
+    esac
+    REGEX="rx_jit_persist|mlp_persist|lin_gemm|arrow_ingest|xg_allreduce|mt_sgd"
+    if [ "$2" = bench ]; then
+      CMD="python3 $R/bench.py --steps 200 --warmup 5 --no-reference-config"
+    else
+      CMD="python3 $R/benchmarks/linear_gemm_bench.py --reps 3"
+    fi
+    timeout -s KILL 150 rocprofv3 --pmc $P --kernel-include-regex "$REGEX" --output-format csv \
+      -d $R/gpurun_out/pmc -o $2_p$1 -- $CMD > $R/gpurun_out/pmc/$2_p$1.log 2>&1
+    rc=$?; echo "pmc rc=$rc"; exit $rc;;
+  dlrm)
+    for B in ${@:-2048 128}; do
+      timeout -k 10 200 python benchmarks/dlrm_bench.py --batch $B --steps 400 --warmup 40 --graph \
+        >> gpurun_out/dlrm.jsonl 2>> gpurun_out/dlrm.err || exit 14
+      timeout -k 10 200 python benchmarks/dlrm_bench.py --batch $B --steps 400 --warmup 40 \
+        >> gpurun_out/dlrm.jsonl 2>> gpurun_out/dlrm.err || exit 15
+    done
+    cat gpurun_out/dlrm.jsonl;;
+  *) echo "usage: scripts/gpu.sh tests|bench|rehearse|prof|pmc|dlrm ..."; exit 2;;
+esac
