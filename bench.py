@@ -279,6 +279,12 @@ def main():
     import gc
     gc.collect()
     gc.freeze()
+    from raydp_amd.utils.devmon import DeviceMonitor
+    # power / HBM / activity of the node's GPUs during the timed region, sampled by a child
+    # process (rank 0 only; it touches no HIP context and no Python state of the pipeline)
+    mon = DeviceMonitor(interval_s=0.005) if local == 0 else None
+    if mon is not None:
+        mon.__enter__()
     barrier()
     from raydp_amd.utils import tracing
     prof = None
@@ -291,6 +297,8 @@ def main():
         res = run_pipeline(spark, main_csv, args.steps, n_train, storage, **kw)
         barrier()
     dt = time.perf_counter() - t0
+    if mon is not None:
+        mon.__exit__(None, None, None)
     if prof is not None:
         prof.disable()
         import io
@@ -332,6 +340,9 @@ def main():
                        "timed_region": "csv read+ETL+from_spark+shuffle+HBM ingest+train+checkpoint",
                        "final_train_loss": res.metrics_history[0].get("train_loss")
                        if res.metrics_history else None,
+                       "step_time_us": res.metrics_history[0].get("step_time_us") if res.metrics_history else None,
+                       "device_telemetry": mon.summary() if mon is not None else None,
+                       "hbm_peak_allocated_mib": round(torch.cuda.max_memory_allocated() / 2 ** 20, 1),
                        "rank0_breakdown_s": dict({k: round(v, 4) for k, v in LAST_TIMINGS.items()},
                                                  **{k: round(v, 4) for k, v in DRIVER_TIMINGS.items()},
                                                  other=round(dt - sum(v for k, v in LAST_TIMINGS.items()

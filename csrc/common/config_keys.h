@@ -26,7 +26,6 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.mlp_wgrad", "RAYDP_MLP_WGRAD", "opt"},
     {"spark.ray.mi355x.mlp_persistent", "RAYDP_MLP_PERSISTENT", "1"},
     {"spark.ray.mi355x.mlp_persistent.timeout_s", "RAYDP_MLP_PERSISTENT_TIMEOUT_S", "5"},
-    {"spark.ray.mi355x.mlp_persistent.cooperative", "RAYDP_MLP_COOPERATIVE", "0"},
     {"spark.ray.mi355x.fused_linear", "RAYDP_FUSED_LINEAR", "1"},
     {"spark.ray.mi355x.ddp.bucket_mb", "RAYDP_DDP_BUCKET_MB", "32"},
     {"spark.ray.mi355x.object_store_bytes", "RAYDP_OBJECT_STORE_BYTES", "0"},
@@ -37,6 +36,7 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.local_exec_bytes", "RAYDP_LOCAL_EXEC_BYTES", "4m"},
     {"spark.ray.mi355x.xg_opt_stride", "RAYDP_XG_OPT_STRIDE", "1"},
     {"spark.ray.mi355x.overlap_conversion", "RAYDP_OVERLAP_CONVERSION", "1"},
+    {"spark.ray.mi355x.step_times", "RAYDP_STEP_TIMES", "1"},
     {"spark.ray.mi355x.udf_verify", "RAYDP_UDF_VERIFY", "sampled"},
 };
 

@@ -148,6 +148,10 @@ __device__ __forceinline__ void ps_store_vectors(const D& d, const char* smem, f
   });
 }
 
+// stamps[0..31]: phase stamps of the middle step (diagnostics); stamps[32 + s]: start of step s,
+// stamps[32 + nsteps]: end of the last step
+#define RX_PS_STEP_STAMPS 32
+
 template <class C, int MT>
 __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const OptDesc& o, const u16* __restrict__ img,
                                            float* __restrict__ rstats, float* __restrict__ P, float* __restrict__ Gr,
@@ -184,6 +188,9 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
   const bool ps_wt = flag_lds[1] != 0;
   for (int s = 0; s < nsteps; ++s) {
     stamp(s, 0);
+    // per-step start times (stamps[32 + s], one lane, one vector store): the step-time
+    // histogram of raydp_amd/utils/devmon.py
+    if (stamps != nullptr && rx_tid() == 0) rx_g(stamps)[RX_PS_STEP_STAMPS + s] = wall_clock64();
     const int row0 = s * batch;
     const int nvalid = min(batch, n_rows - row0);
     for (int i = rx_tid(); i < Tile<MT>::BP; i += RX_THREADS)
@@ -251,6 +258,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     __syncthreads();
     stamp(s, 5);
   }
+  if (stamps != nullptr && rx_tid() == 0) rx_g(stamps)[RX_PS_STEP_STAMPS + nsteps] = wall_clock64();
   ps_store_vectors<C>(d, smem, P);
   store_running_stats<C>(d, smem, rstats);
 }

@@ -136,6 +136,7 @@ class FusedMLPTrainer:
         self.loss_code, self.beta = loss
         self.lr_schedule = lr_schedule
         self.acc_thr = acc_thr           # binary accuracy threshold (None: not counted)
+        self.record_steps = False        # per-step device times of persistent epochs
         self.step_count = 0
         self.lib = _hip.lib()
         self._build()
@@ -495,6 +496,16 @@ class FusedMLPTrainer:
                                   f"(vote {out['xg_vote']:g})")
         return out
 
+    def step_times_us(self) -> Optional[np.ndarray]:
+        """Device time of every step of the last persistent epoch (microseconds; the 100 MHz
+        wall clock), or None when it was not recorded (``record_steps``)."""
+        st = getattr(self, "_step_stamps", None)
+        if st is None:
+            return None
+        self._step_stamps = None
+        t = st.cpu().numpy()[32:].astype(np.float64)
+        return np.diff(t) * 0.01 if t.size > 1 else None
+
     def snapshot(self):
         """Device copy of everything an epoch mutates (see :meth:`restore`)."""
         return ([t.clone() for t in (self.params, self.m, self.v, self.rstats, self.img)],
@@ -530,15 +541,22 @@ class FusedMLPTrainer:
         # admitted but a co-tenant still starved a workgroup) rolls back and reruns the epoch on
         # the launch-per-step loop instead of failing the fit
         snap = [t.clone() for t in (self.params, self.m, self.v, self.rstats, self.img)]
+        stamps = None
+        if self.record_steps:
+            # device wall clock at every step start (csrc/hip/mlp_persist.h RX_PS_STEP_STAMPS)
+            stamps = torch.zeros(32 + nsteps + 1, dtype=torch.int64, device=self.device)
+            self.bufs.stamps = stamps.data_ptr()
         rc = self.lib.rx_mlp_train_persistent(
             ctypes.byref(self.desc), ctypes.byref(self.bufs), ctypes.byref(self.opt), self._od, self.mt,
             pp(self.m.data_ptr()), pp(self.v.data_ptr()), pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p,
             n_rows, self.batch, nsteps, pp(sched.data_ptr()), int(self.step_count == 0),
             pp(self._ps_sync.data_ptr()), ctypes.c_double(timeout), stream)
+        self.bufs.stamps = 0
         if rc in (-3, -4):
             return False
         _hip.check(rc, "rx_mlp_train_persistent")
         self._ps_sched = sched   # kept alive until the launch has consumed it
+        self._step_stamps = stamps
         if int(self._ps_sync[self._ps_err].item()) != 0:
             import warnings
             warnings.warn("persistent fused-MLP epoch: a workgroup wait timed out; rolled back and "

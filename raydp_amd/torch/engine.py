@@ -169,6 +169,9 @@ class FusedMLPEngine:
         self.world = session.get_world_size()
         self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn,
                                        acc_thr=acc_thr)
+        from raydp_amd.utils.config import get as conf_get
+        self.trainer.record_steps = bool(conf_get("spark.ray.mi355x.step_times"))
+        self.last_step_times = None
         self.optimizer = optimizer
         self.trainer.load_optimizer_state(optimizer)
         self.xg, self.comm, self.ar = None, None, None
@@ -278,6 +281,10 @@ class FusedMLPEngine:
                                          world_size=self.world, drop_last=self.drop_last, comm=self.comm,
                                          max_steps=self.max_steps)
         self.trainer.note_steps(self.trainer.steps_in_epoch)
+        st = self.trainer.step_times_us()
+        if st is not None:
+            from raydp_amd.utils.devmon import step_time_histogram
+            self.last_step_times = step_time_histogram(st)
         return self._res(m), m["loss"]
 
     def evaluate_epoch(self):

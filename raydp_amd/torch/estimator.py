@@ -329,6 +329,8 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                         "train_epoch_wall_s": wall}
                 if dev_s is not None:
                     perf["train_epoch_device_s"] = dev_s
+                if getattr(engine, "last_step_times", None):
+                    perf["step_time_us"] = engine.last_step_times    # device-timed, per step
             session.report(dict(epoch=epoch, train_res=train_res, train_loss=train_loss,
                                 engine=engine.name, allreduce=getattr(engine, "allreduce_kind", None), **perf))
             if eval_ds is not None:

@@ -143,10 +143,6 @@ register("spark.ray.mi355x.mlp_wgrad", "str", "opt",
 register("spark.ray.mi355x.mlp_persistent", "bool", True,
          "one GPU: run a whole fused-MLP epoch as one persistent launch with the optimizer beside the "
          "backward pass (csrc/hip/mlp_persist.h)", env="RAYDP_MLP_PERSISTENT")
-register("spark.ray.mi355x.mlp_persistent.cooperative", "bool", False,
-         "launch the persistent epoch kernel cooperatively (the runtime admits it only when the whole "
-         "grid is resident); default: plain launch after this process checked the occupancy (same "
-         "speed; the cooperative queue's teardown faults at exit under rocprofv3)", env="RAYDP_MLP_COOPERATIVE")
 register("spark.ray.mi355x.fused_linear", "bool", True,
          "run Linear(+ReLU) towers of the DLRM-class models (TorchMlp) on the fused MFMA GEMM kernels "
          "(csrc/hip/linear_act.hip) instead of eager torch", env="RAYDP_FUSED_LINEAR")
@@ -172,6 +168,9 @@ register("spark.ray.mi355x.local_exec_bytes", "bytes", "4m",
 register("spark.ray.mi355x.xg_opt_stride", "int", 1,
          "workgroup stride of the fused reduce+optimizer kernel (1: every XCD pulls peer lines)",
          env="RAYDP_XG_OPT_STRIDE")
+register("spark.ray.mi355x.step_times", "bool", True,
+         "record the device time of every fused-MLP step (one store per step) and report a step-time "
+         "histogram with each epoch", env="RAYDP_STEP_TIMES")
 register("spark.ray.mi355x.udf_verify", "str", "sampled",
          "inlined Python UDFs: sampled (spread rows + every argument's new extreme rows per partition) "
          "or full (every row checked against the Python function)", env="RAYDP_UDF_VERIFY",

@@ -67,3 +67,20 @@ def test_actor_log_files_carry_job_id_header():
         raydp_amd.stop_spark()
     finally:
         runtime.shutdown()
+
+
+def test_device_monitor_and_step_histogram():
+    """SURVEY §5.5 telemetry: the AMD SMI sampler never breaks the region it brackets (here no
+    driver: it reports why), and the step-time histogram has the percentiles and buckets."""
+    import time
+
+    from raydp_amd.utils.devmon import DeviceMonitor, step_time_histogram
+    with DeviceMonitor(interval_s=0.01) as mon:
+        time.sleep(0.03)
+    s = mon.summary()
+    assert isinstance(s, dict) and "available" in s
+    if not s["available"]:
+        assert s["reason"]
+    h = step_time_histogram([27.5, 28.0, 29.0, 31.0, 45.0, 1200.0])
+    assert h["steps"] == 6 and h["p50"] == 30.0 and h["max"] == 1200.0
+    assert sum(h["hist_us"].values()) == 6 and h["hist_us"]["1000-5000"] == 1
