@@ -74,6 +74,14 @@ def _relerr(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-4 * b.numel() ** 0.5))
 
 
+def _norm_ratio(a, b):
+    """||a|| / ||b|| with _relerr's floor: converts a tolerance relative to ``a`` into one
+    relative to ``b`` (for the triangle-inequality bound kernel-vs-fp32 <= kernel-vs-emulation
+    + emulation-vs-fp32)."""
+    a, b = a.float().cpu(), b.float().cpu()
+    return max(1.0, float(a.norm()) / max(float(b.norm()), 1e-4 * b.numel() ** 0.5))
+
+
 def _setup(model, loss, opt_cls, batch, n_rows, in_f, out_f, seed=0, **opt_kw):
     from raydp_amd.models.mlp_spec import extract_mlp_spec
     from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
@@ -123,7 +131,12 @@ def test_fused_mlp_one_step_matches_torch(nvalid, loss):
                 e_emu = _relerr(gmap[key], getattr(emods[name], attr).grad)
                 e_fp32 = _relerr(gmap[key], getattr(rmods[name], attr).grad)
                 assert e_emu < 2e-2, (name, attr, e_emu)
-                assert e_fp32 < 0.35, (name, attr, e_fp32)
+                # against fp32 the kernel may differ by exactly what bf16 GEMM operands cost
+                # (emulation vs fp32, measured on the same inputs) plus the emulation tolerance:
+                # a triangle-inequality bound instead of a fixed, loose constant
+                bf16_cost = _relerr(getattr(emods[name], attr).grad, getattr(rmods[name], attr).grad)
+                tol = 2e-2 * _norm_ratio(getattr(emods[name], attr).grad, getattr(rmods[name], attr).grad)
+                assert e_fp32 <= bf16_cost + tol + 1e-6, (name, attr, e_fp32, bf16_cost)
     # optimizer step against torch's Adam applied to the kernel's OWN gradient (a first Adam step
     # moves every element by ~lr * sign(g): comparing against the emulation's gradient would
     # flip on the near-zero BatchNorm channels, whose sign is noise in any reference)
