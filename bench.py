@@ -234,6 +234,12 @@ def main():
             raise SystemExit("--topology estimator runs as ONE driver process (it spawns the workers)")
     elif world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    cpus = int(os.environ.get("RAYDP_BENCH_CPUS", "4"))
+    if world > 1 and os.environ.get("RAYDP_BENCH_PIN", "1") != "0":
+        # each SPMD rank's pipeline (driver + its executor processes, all host-bound) on its own
+        # cores: ranks do not preempt each other, and the max over ranks stops paying for it
+        from raydp_amd.utils import pin_to_rank_slice
+        pin_to_rank_slice(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)), min_per_rank=cpus + 1)
     import torch
     import torch.distributed as dist
     # modulo: lets a rehearsal put several ranks on a 1-GPU box (RAYDP_BENCH_BACKEND=gloo)
@@ -257,7 +263,6 @@ def main():
     make_csv(warm_csv, max(1, args.warmup) * BATCH * rows_per, 1000 + rank)
     make_csv(main_csv, args.steps * BATCH * rows_per, 2000 + rank)
 
-    cpus = int(os.environ.get("RAYDP_BENCH_CPUS", "4"))
     # estimator topology: one CPU per training worker on top of the executors'
     runtime.init(num_cpus=cpus + (n_train if args.topology == "estimator" else 0))
     # one single-core executor process per CPU: Arrow ETL scales without sharing a GIL

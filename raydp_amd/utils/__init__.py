@@ -153,3 +153,33 @@ def divide_blocks(blocks: List[int], world_size: int, shuffle: bool = False,
             have = take(int(rng.choice(order)), have)
         results[rank] = chosen
     return results
+
+
+def partition_cpus(local_rank: int, local_world: int, min_per_rank: int = 2):
+    """The CPU slice of one local rank when ``local_world`` ranks share a node: contiguous,
+    equal slices of the cores this process may use (rank r -> the r-th slice, so with the usual
+    MI355X layout of GPUs 0-3 on socket 0 and 4-7 on socket 1 a rank's host work stays on its
+    GPU's socket). None when the node has fewer than ``min_per_rank`` cores per rank (then
+    overlapping slices would only add contention) or there is nothing to split."""
+    import os
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    if local_world <= 1 or len(cpus) < min_per_rank * local_world:
+        return None
+    per = len(cpus) // local_world
+    return cpus[local_rank * per:(local_rank + 1) * per]
+
+
+def pin_to_rank_slice(local_rank: int, local_world: int, min_per_rank: int = 2):
+    """Confine this process -- and every process it starts afterwards (the runtime supervisor,
+    executor and worker actors inherit it) -- to its rank's CPU slice. Returns the slice or None."""
+    import os
+    cpus = partition_cpus(local_rank, local_world, min_per_rank)
+    if cpus:
+        try:
+            os.sched_setaffinity(0, cpus)
+        except OSError:
+            return None
+    return cpus

@@ -77,3 +77,17 @@ def test_divide_blocks(blocks, world, shuffle):
 def test_divide_blocks_not_enough():
     with pytest.raises(Exception):
         utils.divide_blocks([1], 2)
+
+
+def test_partition_cpus_gives_disjoint_rank_slices(monkeypatch):
+    import os
+
+    from raydp_amd.utils import partition_cpus
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)))
+    slices = [partition_cpus(r, 8, 5) for r in range(8)]
+    assert all(len(s) == 8 for s in slices)
+    flat = [c for s in slices for c in s]
+    assert len(set(flat)) == 64                       # disjoint, covering every core
+    assert slices[0] == list(range(8)) and slices[7] == list(range(56, 64))
+    assert partition_cpus(0, 8, 9) is None            # too few cores: no pinning
+    assert partition_cpus(0, 1, 2) is None
