@@ -13,8 +13,9 @@ and one training step moves only the looked-up rows:
             sparse gradient of the owner's local table (SGD applies it without densifying).
 
 Collectives are ``torch.distributed.all_to_all_single`` (RCCL over xGMI on MI355X, gloo on
-CPU). The id exchange is issued ``async_op`` before the bottom MLP runs (``start`` / ``finish``,
-``Dlrm.forward``) and, with the fused embedding SGD, the reverse gradient exchange overlaps the
+CPU). The small id exchange and the owner gather run first; the row exchange back (16x the id
+bytes at D = 32 fp32) is issued ``async_op`` and overlaps the bottom MLP (``start`` / ``finish``,
+``Dlrm.forward``); with the fused embedding SGD the reverse gradient exchange overlaps the
 bottom MLP's backward (applied at the end of the backward pass). Batch sizes are exchanged only
 when they change. Dense parameters (the MLPs) stay data parallel.
 """
@@ -43,21 +44,24 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group):
 
 
 class _Pending:
-    """An id exchange in flight (``ShardedEmbeddings.start``): the all-to-all of the local
-    batch's category ids to the tables' owners, issued ``async_op`` so that the bottom MLP runs
-    while it moves."""
-    __slots__ = ("B", "T", "all_b", "in_splits", "out_splits", "recv", "work")
+    """A lookup in flight (``ShardedEmbeddings.start``): the ids have been exchanged and the
+    owners' rows gathered; the all-to-all returning the rows (the step's largest exchange,
+    B x T x D values) runs asynchronously while the bottom MLP is computed."""
+    __slots__ = ("B", "T", "all_b", "in_splits", "out_splits", "recv", "work", "back")
 
 
 class _ShardedLookup(torch.autograd.Function):
+    """Forward: id all-to-all, owner-side row gather, and the row all-to-all issued
+    ``async_op`` (its handle goes into ``pend.work``; ``finish`` waits -- a stream dependency,
+    no host block -- after the bottom MLP has been enqueued). Returns the received rows in
+    rank-blocked order."""
+
     @staticmethod
     def forward(ctx, weight, pend, mod):
         group, world = mod.group, mod.world
         B, T = pend.B, pend.T
         D = weight.shape[1]
         dev = weight.device
-        if pend.work is not None:
-            pend.work.wait()
         in_splits, out_splits = pend.in_splits, pend.out_splits
         # 2) owner-side gather for every source rank (HIP row gather on the GPU)
         nl = len(mod.local_tables)
@@ -65,32 +69,26 @@ class _ShardedLookup(torch.autograd.Function):
         lidx = pend.recv.view(-1, nl) if nl else pend.recv.view(0, 0)
         emb = gather_rows(weight, mod.local_offsets, lidx).view(-1, D) if nl else \
             torch.empty(0, D, device=dev, dtype=weight.dtype)
-        # 3) embeddings back to the requesting ranks
+        # 3) embeddings back to the requesting ranks, in flight while the bottom MLP runs
         back = torch.empty(sum(in_splits), D, dtype=weight.dtype, device=dev)
-        _a2a(back, emb, [s for s in in_splits], [s for s in out_splits], group)
-        out = torch.empty(B, T, D, dtype=weight.dtype, device=dev)
-        off = 0
-        for r in range(world):
-            n = len(mod.tables_of[r])
-            if n:
-                out[:, mod.tables_of[r]] = back[off:off + B * n].view(B, n, D)
-            off += B * n
+        pend.work = dist.all_to_all_single(back, emb.contiguous(), output_split_sizes=list(in_splits),
+                                           input_split_sizes=list(out_splits), group=group, async_op=True)
         ctx.save_for_backward(lidx, weight)
         ctx.meta = (mod, B, T, D, in_splits, out_splits, weight.shape)
-        return out
+        return back
 
     @staticmethod
     def backward(ctx, g):
         lidx, weight = ctx.saved_tensors
         mod, B, T, D, in_splits, out_splits, wshape = ctx.meta
-        send = torch.cat([g[:, mod.tables_of[r]].reshape(-1, D) for r in range(mod.world)]) if T else g.reshape(-1, D)
+        send = g.contiguous()          # already rank-blocked: the reverse of the forward exchange
         recv = torch.empty(sum(out_splits), D, dtype=g.dtype, device=g.device)
         nl = len(mod.local_tables)
         if mod.fused_sgd_lr is not None:
             # the reverse exchange runs while autograd continues with the bottom MLP's backward;
             # the rows are applied to the owner's tables at the end of the backward pass
-            work = dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=out_splits,
-                                          input_split_sizes=in_splits, group=mod.group, async_op=True)
+            work = dist.all_to_all_single(recv, send, output_split_sizes=list(out_splits),
+                                          input_split_sizes=list(in_splits), group=mod.group, async_op=True)
 
             def finish():
                 work.wait()
@@ -163,7 +161,8 @@ class ShardedEmbeddings(nn.Module):
         return self._all_b
 
     def start(self, idx: torch.Tensor) -> _Pending:
-        """Issue the id all-to-all of step 1 asynchronously; ``finish`` completes the lookup."""
+        """Exchange the ids, gather the owned rows and put the row all-to-all in flight; the
+        caller computes the bottom MLP next and ``finish`` completes the lookup."""
         idx = idx.long()
         B, T = idx.shape
         p = _Pending()
@@ -173,13 +172,36 @@ class ShardedEmbeddings(nn.Module):
         p.in_splits = [B * len(self.tables_of[r]) for r in range(self.world)]
         p.out_splits = [p.all_b[r] * len(self.local_tables) for r in range(self.world)]
         p.recv = torch.empty(sum(p.out_splits), dtype=idx.dtype, device=idx.device)
-        p.work = dist.all_to_all_single(p.recv, send.contiguous(), output_split_sizes=p.out_splits,
-                                        input_split_sizes=p.in_splits, group=self.group, async_op=True)
+        _a2a(p.recv, send, p.out_splits, p.in_splits, self.group)     # ids (8 B per lookup)
+        p.back = _ShardedLookup.apply(self.weight, p, self)             # rows: async
         return p
 
     def finish(self, pend: _Pending, mlp_out: torch.Tensor) -> torch.Tensor:
-        emb = _ShardedLookup.apply(self.weight, pend, self)
+        pend.work.wait()     # the compute stream waits for the rows (no host synchronisation)
+        B, T, D = pend.B, pend.T, self.dim
+        # rank-blocked rows -> [B, T, D] in table order (one gather through a cached index)
+        perm = self._row_order(B, T, mlp_out.device)
+        emb = pend.back.index_select(0, perm).view(B, T, D) if T else pend.back.view(B, 0, D)
         return torch.cat([mlp_out.unsqueeze(1).to(emb.dtype), emb], dim=1)
+
+    def _row_order(self, B: int, T: int, dev) -> torch.Tensor:
+        """Index that maps the received rank-blocked rows ([rank][b][its tables]) to
+        [b][table] order."""
+        key = (B, T, str(dev))
+        cached = getattr(self, "_order_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        pos = torch.empty(B, T, dtype=torch.long)
+        off = 0
+        for r in range(self.world):
+            ts = self.tables_of[r]
+            n = len(ts)
+            if n:
+                pos[:, ts] = off + torch.arange(B * n).view(B, n)
+            off += B * n
+        perm = pos.reshape(-1).to(dev)
+        self._order_cache = (key, perm)
+        return perm
 
     def forward(self, mlp_out: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
         return self.finish(self.start(idx), mlp_out)
