@@ -12,6 +12,8 @@
 //                                 identical every call, so a HIP graph can capture and replay it
 //   rx_xg_devdesc/take_seq/slot -> the fused step loop (csrc/hip/fused_mlp.hip) reduces inside
 //                                 its optimizer kernel instead (host-side sequence numbers)
+//   rx_xg_allgather            -> every rank's n words side by side (device-sequenced too):
+//                                 the replicated DLRM tables' sparse gradient rows and ids
 //   rx_xg_vote                 -> epoch-end agreement for the fused loop: every rank's error word
 //                                 summed into a double the host reads with the epoch metrics
 //   rx_xg_error                -> nonzero once any wait timed out (a peer never arrived)
@@ -92,6 +94,47 @@ __global__ __launch_bounds__(kThreads) void xg_allreduce_kernel(XgDev x, float* 
   }
   // the launch's last workgroup advances the device sequence number for the next launch
   if (hseq) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(x.ctl + kXgDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(x.ctl + kXgDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(x.ctl + kXgDevSeq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// All-gather of n floats (raw 4-byte words of any dtype) per rank: dst[p * n + i] = rank p's
+// src[i]. Device-sequenced like the all-reduce (capturable); VEC: src and dst 16-B aligned and
+// n a multiple of 4.
+template <bool VEC>
+__global__ __launch_bounds__(kThreads) void xg_allgather_kernel(XgDev x, const float* __restrict__ src,
+                                                                float* __restrict__ dst, int n) {
+  const unsigned seq = __hip_atomic_load(x.ctl + kXgDevSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int par = (int)(seq & 1u);
+  float* mine = x.region[x.rank] + (size_t)par * x.nf;
+  const int stride = gridDim.x * kThreads;
+  const int t = blockIdx.x * kThreads + threadIdx.x;
+  const int units = VEC ? n >> 2 : n;
+  for (int i = t; i < units; i += stride) {
+    if (VEC)
+      reinterpret_cast<float4*>(mine)[i] = reinterpret_cast<const float4*>(src)[i];
+    else
+      mine[i] = src[i];
+  }
+  if (!rx_xg_grid_rendezvous(x, seq, gridDim.x)) return;
+  for (int p = 0; p < x.world; ++p) {
+    const float* from = x.region[p] + (size_t)par * x.nf;
+    for (int i = t; i < units; i += stride) {
+      if (VEC) {
+        const float4 v = p == x.rank ? reinterpret_cast<const float4*>(src)[i] : rx_xg_load4(from, (size_t)i);
+        reinterpret_cast<float4*>(dst + (size_t)p * n)[i] = v;
+      } else {
+        dst[(size_t)p * n + i] = p == x.rank ? src[i]
+                                             : __hip_atomic_load(from + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned old = __hip_atomic_fetch_add(x.ctl + kXgDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -239,6 +282,25 @@ int rx_xg_allreduce_scaled(float* buf, int n, float scale, void* ctx, hipStream_
   else
     hipLaunchKernelGGL(xg_allreduce_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, buf,
                        n, hseq, scale);
+  return (int)hipGetLastError();
+}
+
+// All-gather of n 4-byte words per rank into dst (world * n words), device-sequenced.
+int rx_xg_allgather(const float* src, float* dst, int n, void* ctx, hipStream_t stream) {
+  XgHost* h = (XgHost*)ctx;
+  if (h->host_seq) return -3;
+  if (n < 0 || n > h->dev.nf) return -2;
+  if (n == 0) return 0;
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0 && (n & 3) == 0;
+  const long units = vec ? (long)(n >> 2) : (long)n;
+  long blocks = (units + (long)kThreads * 4 - 1) / ((long)kThreads * 4);
+  if (blocks < 1) blocks = 1;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (vec)
+    hipLaunchKernelGGL(xg_allgather_kernel<true>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, src, dst, n);
+  else
+    hipLaunchKernelGGL(xg_allgather_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, src, dst,
+                       n);
   return (int)hipGetLastError();
 }
 

@@ -136,6 +136,20 @@ class XgmiComm:
                                              ctypes.c_void_p(self.ctx), _hip.stream_ptr(t.device))
         _hip.check(rc, "rx_xg_allreduce")
 
+    def allgather_(self, src, dst) -> None:
+        """``dst`` (``world * src`` bytes, contiguous, same dtype family of 4-byte words or
+        int64) receives every rank's ``src`` in rank order: one device-sequenced launch
+        (capturable). ``src`` must have the same size on every rank."""
+        if src.element_size() * src.numel() % 4 or dst.numel() * dst.element_size() != \
+                self.world * src.numel() * src.element_size():
+            raise ValueError("allgather_: dst must hold world x src, in 4-byte words")
+        words = src.numel() * src.element_size() // 4
+        if words > self.max_floats:
+            raise ValueError(f"xGMI all-gather of {words} words > {self.max_floats}")
+        rc = self.lib.rx_xg_allgather(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), words,
+                                      ctypes.c_void_p(self.ctx), _hip.stream_ptr(src.device))
+        _hip.check(rc, "rx_xg_allgather")
+
     def vote(self, out) -> None:
         """Epoch-end agreement (host-sequenced communicators): ``out`` (a device float64
         element) becomes the sum of every rank's error word, > 0 when any rank -- or this

@@ -115,7 +115,7 @@ class _EmbedConcat(torch.autograd.Function):
     """X = [mlp_out; W[offs + idx]] ([B, 1 + T, D]); weight gradient sparse (or fused SGD)."""
 
     @staticmethod
-    def forward(ctx, mlp_out, weight, offsets, idx, fused_lr):
+    def forward(ctx, mlp_out, weight, offsets, idx, fused_lr, sync=None):
         B, T = idx.shape
         D = weight.shape[1]
         X = torch.empty(B, T + 1, D, dtype=torch.float32, device=weight.device)
@@ -128,6 +128,7 @@ class _EmbedConcat(torch.autograd.Function):
                                         weight.shape[0], _hip.stream_ptr(weight.device)), "rx_emb_gather")
         ctx.save_for_backward(weight, offsets, idx)
         ctx.fused_lr = fused_lr
+        ctx.sync = sync
         return X
 
     @staticmethod
@@ -138,13 +139,24 @@ class _EmbedConcat(torch.autograd.Function):
         dX = dX.contiguous()
         d_mlp = dX[:, 0]
         if ctx.fused_lr is not None:
-            _hip.check(_lib().rx_emb_sgd(_p(weight), _p(offsets), _p(idx), _p(dX), B, T, D, T + 1,
-                                         ctypes.c_float(ctx.fused_lr), weight.shape[0],
+            ids, rows_dx, n, lr = idx, dX, B, ctx.fused_lr
+            if ctx.sync is not None:
+                # replicated tables over W ranks: every rank applies every rank's rows (SGD is
+                # linear: the same update as all-reducing the sparse gradient and averaging),
+                # gathered over xGMI on the device -- no host round trip, capturable
+                comm, W = ctx.sync
+                ids = torch.empty((W,) + tuple(idx.shape), dtype=idx.dtype, device=idx.device)
+                comm.allgather_(idx, ids)
+                rows_dx = torch.empty((W,) + tuple(dX.shape), dtype=dX.dtype, device=dX.device)
+                comm.allgather_(dX, rows_dx)
+                n, lr = W * B, lr / W
+            _hip.check(_lib().rx_emb_sgd(_p(weight), _p(offsets), _p(ids), _p(rows_dx), n, T, D, T + 1,
+                                         ctypes.c_float(lr), weight.shape[0],
                                          _hip.stream_ptr(weight.device)), "rx_emb_sgd")
-            return d_mlp, None, None, None, None
+            return d_mlp, None, None, None, None, None
         rows = (idx + offsets.view(1, -1)).reshape(-1)
         grad = torch.sparse_coo_tensor(rows.unsqueeze(0), dX[:, 1:].reshape(-1, D), weight.shape)
-        return d_mlp, grad, None, None, None
+        return d_mlp, grad, None, None, None, None
 
 
 class FusedEmbeddings(nn.Module):
@@ -172,7 +184,8 @@ class FusedEmbeddings(nn.Module):
 
     def forward(self, mlp_out: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
         if self.weight.is_cuda:
-            return _EmbedConcat.apply(mlp_out.float(), self.weight, self.offsets, idx, self.fused_sgd_lr)
+            return _EmbedConcat.apply(mlp_out.float(), self.weight, self.offsets, idx, self.fused_sgd_lr,
+                                      getattr(self, "sync", None))
         rows = idx.long() + self.offsets.view(1, -1)
         emb = nn.functional.embedding(rows, self.weight, sparse=True)
         return torch.cat([mlp_out.unsqueeze(1).float(), emb], dim=1)

@@ -70,8 +70,12 @@ class DistributedDataParallel(nn.Module):
                 sparse_ids.add(id(m.weight))
         params, self.sparse_params = [], []
         for p in module.parameters():
-            if not p.requires_grad or getattr(p, "_raydp_model_parallel", False):
-                continue   # sharded tables (raydp_amd.parallel.embedding_mp) are not replicated
+            if not p.requires_grad or getattr(p, "_raydp_model_parallel", False) \
+                    or getattr(p, "_raydp_grad_synced", False):
+                # sharded tables (raydp_amd.parallel.embedding_mp) are not replicated; replicated
+                # tables whose module synchronises its own updates (FusedEmbeddings.sync) are
+                # broadcast at wrap time but never bucketed
+                continue
             if id(p) in sparse_ids or getattr(p, "_raydp_sparse_grad", False):
                 self.sparse_params.append(p)
             else:

@@ -383,7 +383,7 @@ class TorchLoopEngine:
         self._fused_sgd = None          # decided at the first step (needs the gradients)
         self.fusions = []
         if device.type == "cuda":
-            self._fuse_hot_ops()        # before DDP sees which parameters have sparse gradients
+            self._fuse_hot_ops(config)  # before DDP sees which parameters have sparse gradients
         if self.world > 1:
             from raydp_amd.parallel.ddp import DistributedDataParallel
             self.model = DistributedDataParallel(self.raw_model)
@@ -407,11 +407,15 @@ class TorchLoopEngine:
         else:
             self.graph_status = "disabled (RAYDP_TORCH_GRAPHS=0)"
 
-    def _fuse_hot_ops(self):
+    def _fuse_hot_ops(self, config=None):
         """Swap the step's eager tails for HIP kernels where the semantics are identical:
         ``BCEWithLogitsLoss()`` -> :class:`raydp_amd.ops.fused_optim.FusedBCEWithLogits`;
-        plain-SGD DLRM tables (replicated on one GPU, or sharded) -> the sparse SGD fused into
-        the embedding backward (``rx_emb_sgd``: no sparse gradient tensor, no index_add)."""
+        plain-SGD DLRM tables -> the sparse SGD fused into the embedding backward
+        (``rx_emb_sgd``: no sparse gradient tensor, no index_add) -- on one GPU, for sharded
+        tables, and for tables replicated over the ranks when the trainer's equal shards keep
+        every rank's batch the same size: each step's ids and gradient rows are then
+        all-gathered over xGMI on the device and every rank applies all of them (the DDP
+        sparse all-reduce without its host round trips)."""
         from raydp_amd.ops import fused_optim
         if fused_optim.fusable_bce(self.loss):
             self.loss = fused_optim.FusedBCEWithLogits()
@@ -429,10 +433,29 @@ class TorchLoopEngine:
                     if getattr(m, "fused_sgd_lr", 0) is not None or w is None or id(w) not in lr_of:
                         continue
                     if not sharded and self.world > 1:
-                        continue   # replicated tables updated locally would diverge across ranks
+                        # replicated tables updated locally would diverge: gather every rank's
+                        # rows (fixed size per step only with equal shards)
+                        sync = self._embedding_sync(m, config)
+                        if sync is None:
+                            continue
+                        m.sync = sync
+                        w._raydp_grad_synced = True
                     m.fused_sgd_lr = lr_of[id(w)]
                     w._raydp_sparse_grad = False
-                    self.fusions.append("embedding_sgd")
+                    self.fusions.append("embedding_sgd" if sharded or self.world == 1 else "embedding_sgd_xgmi_gather")
+
+    def _embedding_sync(self, m, config):
+        """(xGMI communicator, world) for a replicated table's row all-gather, or None."""
+        if not config or not config.get("_equal_shards") or not config.get("drop_last"):
+            return None     # ragged last batches would gather rows of different sizes
+        from raydp_amd.ops.comm import XgmiComm
+        from raydp_amd.utils.config import get as conf_get
+        if conf_get("spark.ray.mi355x.allreduce") == "rccl":
+            return None
+        b = int(config["batch_size"])
+        words = b * (len(m.table_sizes) + 1) * m.dim + 64
+        comm = XgmiComm.create(words, timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
+        return (comm, self.world) if comm is not None else None
 
     def opt_step(self):
         """``optimizer.step()``, on the multi-tensor SGD kernel when it reproduces it (one launch

@@ -317,7 +317,15 @@ class DataParallelTrainer:
                tuple(sorted(wenv.items())) if wenv else (), renv)
         group = _GROUPS.take(key)
         if group is None:
-            group = _WorkerGroup.start(world, use_gpu, cpus, gpus, res, strategy, wenv, backend, tmo, storage)
+            from raydp_amd.runtime.node import ResourceError
+            try:
+                group = _WorkerGroup.start(world, use_gpu, cpus, gpus, res, strategy, wenv, backend, tmo, storage)
+            except ResourceError:
+                # warm groups of other shapes hold their CPUs / GPUs: release them and retry
+                if not len(_GROUPS):
+                    raise
+                _GROUPS.clear()
+                group = _WorkerGroup.start(world, use_gpu, cpus, gpus, res, strategy, wenv, backend, tmo, storage)
         ok = False
         try:
             workers = group.workers

@@ -32,7 +32,7 @@ def _fit(tmp_path, tag):
     df["y"] = x[:, :4].sum(1) * 0.5 + 1.0
     model = _model()
     est = TorchEstimator(num_workers=2, resources_per_worker={"CPU": 1, "GPU": 0.5}, model=model,
-                         optimizer=torch.optim.Adam(model.parameters(), lr=3e-3), loss=nn.MSELoss(),
+                         optimizer=torch.optim.SGD(model.parameters(), lr=0.02, momentum=0.9), loss=nn.MSELoss(),
                          feature_columns=[f"f{i}" for i in range(20)], label_column="y", batch_size=64,
                          num_epochs=3, fused="on", shuffle_seed=5, storage_path=str(tmp_path / tag),
                          metrics_name=["MeanAbsoluteError"])
@@ -63,7 +63,9 @@ def test_spawned_workers_train_fused_over_xgmi_and_stay_warm(runtime_local, tmp_
     est3, res3 = _fit(tmp_path, "c")
     h3 = [m for m in res3.metrics_history if "train_loss" in m]
     assert h3[0]["allreduce"] == "torch.distributed:gloo", h3[0]
-    assert len(T._GROUPS) == 2          # a different environment is a different group
+    # a different environment is a different group; the card's GPU share was held by the warm
+    # group of the first shape, which was released to place this one
+    assert len(T._GROUPS) == 1 and next(iter(T._GROUPS._groups.values())) is not group
     c = est3.get_model().state_dict()
     for k in a:
         if not a[k].dtype.is_floating_point:
@@ -71,6 +73,6 @@ def test_spawned_workers_train_fused_over_xgmi_and_stay_warm(runtime_local, tmp_
         # the xGMI path sums the ranks inside the dW MFMA (rank-concatenated batch), the other
         # path adds materialised per-rank dW: fp32 summation order only
         rel = float((a[k].float() - c[k].float()).abs().max()) / max(1e-6, float(c[k].float().abs().max()))
-        assert rel < 5e-3, (k, rel)
+        assert rel < 1e-4, (k, rel)
     T.release_worker_groups()
     assert len(T._GROUPS) == 0

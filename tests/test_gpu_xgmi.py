@@ -350,3 +350,53 @@ def test_ddp_step_graph_replay_over_xgmi_matches_eager_bitwise(world):
     for rank, same_as_eager, same_ranks in res:
         assert same_as_eager, f"rank {rank}: graph replay diverged from the eager DDP loop"
         assert same_ranks, "replicas diverged"
+
+
+def _emb_sync_main(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    _init(rank, world, port)
+    try:
+        from raydp_amd.ops.comm import XgmiComm
+        from raydp_amd.ops.dlrm_ops import FusedEmbeddings
+        dev = torch.device("cuda", 0)
+        # the all-gather itself: int64 ids and fp32 rows, rank order
+        comm = XgmiComm.create(64 * 27 * 32 + 64, timeout_s=20.0)
+        src = torch.arange(10, dtype=torch.int64, device=dev) + 100 * rank
+        dst = torch.empty(world, 10, dtype=torch.int64, device=dev)
+        comm.allgather_(src, dst)
+        gathered_ok = bool(torch.equal(dst.cpu(), torch.stack([torch.arange(10) + 100 * r for r in range(world)])))
+        # replicated tables, SGD fused into backward, rows gathered over xGMI
+        sizes, D, B, lr = [50, 70, 30], 32, 64, 0.1
+        torch.manual_seed(0)
+        emb = FusedEmbeddings(sizes, D).to(dev)
+        w0 = emb.weight.detach().clone()
+        emb.fused_sgd_lr, emb.sync = lr, (comm, world)
+        g = torch.Generator().manual_seed(3)
+        ids = [torch.stack([torch.randint(0, s, (B,), generator=g) for s in sizes], 1) for _ in range(world)]
+        heads = [torch.randn(B, D, generator=g) for _ in range(world)]
+        X = emb(heads[rank].to(dev), ids[rank].to(dev))
+        (X[:, 1:] ** 2).sum().backward()
+        torch.cuda.synchronize()
+        # reference: the average over ranks of every rank's sparse gradient, one SGD step
+        ref = w0.cpu().clone()
+        offs = torch.tensor([0, 50, 120])
+        for r in range(world):
+            rows = (ids[r] + offs.view(1, -1)).reshape(-1)
+            grad_rows = 2 * w0.cpu()[rows]
+            ref.index_add_(0, rows, grad_rows, alpha=-lr / world)
+        err = float((emb.weight.detach().cpu() - ref).abs().max())
+        q.put((rank, gathered_ok, err))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_replicated_embedding_rows_gathered_over_xgmi():
+    """DLRM tables replicated over ranks with the fused SGD: every rank applies every rank's
+    gradient rows (all-gathered on the device over xGMI) -- the same table as the averaged
+    sparse all-reduce of DDP, on every rank."""
+    res = _run(_emb_sync_main, 2)
+    for rank, gathered_ok, err in res:
+        assert gathered_ok, rank
+        assert err < 1e-5, (rank, err)

@@ -339,3 +339,31 @@ def test_fused_engine_adds_no_host_sync_per_epoch_at_world_2(monkeypatch):
     eng.equal_shards = False
     E.FusedMLPEngine.load(eng, None, None, cfg)
     assert calls == ["all_reduce", "item"], calls
+
+
+def test_warm_worker_groups_are_reused_and_evicted_for_resources(runtime_local, tmp_path, monkeypatch):
+    """Spawned worker groups stay warm between fits of the same shape (no new processes), a
+    different shape that does not fit beside them evicts them, and runtime shutdown stops them."""
+    import pandas as pd
+    from raydp_amd.data import from_pandas
+    from raydp_amd.torch import TorchEstimator
+    from raydp_amd.train import trainer as T
+    df = pd.DataFrame({"a": np.arange(64.0), "y": np.arange(64.0) * 0.5})
+
+    def fit(workers, cpus):
+        torch.manual_seed(0)
+        m = nn.Linear(1, 1)
+        est = TorchEstimator(num_workers=workers, resources_per_worker={"CPU": cpus}, model=m,
+                             optimizer=torch.optim.SGD(m.parameters(), lr=1e-3), loss=nn.MSELoss(),
+                             feature_columns=["a"], label_column="y", batch_size=8, num_epochs=1, use_gpu=False,
+                             storage_path=str(tmp_path), fused="off")
+        return est.fit(from_pandas(df))
+    fit(2, 1)
+    g1 = next(iter(T._GROUPS._groups.values()))
+    pids = [w._impl.pid for w in g1.workers]
+    fit(2, 1)
+    assert next(iter(T._GROUPS._groups.values())) is g1 and [w._impl.pid for w in g1.workers] == pids
+    fit(2, 2.5)                 # 2 x 2.5 CPUs do not fit beside the warm group's 2 on 6 CPUs
+    assert len(T._GROUPS) == 1 and next(iter(T._GROUPS._groups.values())) is not g1
+    T.release_worker_groups()
+    assert len(T._GROUPS) == 0
