@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 T="python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider"
-timeout -k 10 700 $T tests/test_gpu_spawned.py tests/test_gpu_hvd.py tests/test_gpu_xgmi.py -k "spawned or hvd or embedding_rows" -m gpu > gpurun_out/r3_multi_tests.log 2>&1
+timeout -k 10 700 $T tests/test_gpu_hvd.py tests/test_gpu_xgmi.py -k "hvd or embedding_rows" -m gpu > gpurun_out/r3_multi_tests.log 2>&1
 rc=$?; echo "targeted rc=$rc"; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/r3_multi_tests.log | tail -30
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 $T tests/ -m gpu > gpurun_out/r3_gpu_suite.log 2>&1

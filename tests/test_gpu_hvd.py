@@ -10,6 +10,8 @@ import pytest
 import torch
 import torch.nn as nn
 
+import raydp  # noqa: F401 - installs the ray / horovod facades
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
