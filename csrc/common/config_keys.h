@@ -38,6 +38,7 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.overlap_conversion", "RAYDP_OVERLAP_CONVERSION", "1"},
     {"spark.ray.mi355x.step_times", "RAYDP_STEP_TIMES", "1"},
     {"spark.ray.mi355x.udf_verify", "RAYDP_UDF_VERIFY", "sampled"},
+    {"spark.ray.mi355x.native_executor", "RAYDP_NATIVE_EXECUTOR", "1"},
 };
 
 // Value of a key: its environment variable when set and non-empty, else the default.

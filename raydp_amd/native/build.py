@@ -44,6 +44,12 @@ LIBS = {
     "exec_kernels": dict(kind="cpu", sources=lambda: [os.path.join(CSRC, "exec", "exec_kernels.cc"),
                                                        os.path.join(CSRC, "exec", "expr", "expr_vm.cc")]),
     "raydp_runtime": dict(kind="cpu", sources=_runtime_sources, libs=["-lpthread", "-lrt", "-ldl"]),
+    # native executor core: task loop, CSV/stream sources, VM segments, IPC sink into the
+    # object store, partition cache (Arrow C++ from the pyarrow wheel; libraydp_runtime)
+    "raydp_executor": dict(kind="cpu", std="c++20", arrow=True,
+                           sources=lambda: [os.path.join(CSRC, "exec", "executor.cc"),
+                                            os.path.join(CSRC, "exec", "expr", "expr_vm.cc")],
+                           libs=["-L", HERE, "-lraydp_runtime", "-Wl,-rpath,$ORIGIN", "-lpthread"]),
     "hipkernels": dict(kind="hip", sources=_hip_sources),
     # executables: the per-node actor supervisor, the application master (native control
     # plane) and the per-node external shuffle-block service
@@ -51,6 +57,18 @@ LIBS = {
     "raydp_appmaster": dict(kind="exe", sources=lambda: [os.path.join(CSRC, "control", "app_master.cc")]),
     "raydp_shuffle_service": dict(kind="exe", sources=lambda: [os.path.join(CSRC, "exec", "shuffle_service.cc")]),
 }
+
+
+def _arrow_flags():
+    """Compile/link flags for Arrow C++ as shipped in the pyarrow wheel: the executor library
+    links the SAME libarrow the Python process already has loaded (one memory pool, one
+    type registry)."""
+    import pyarrow as pa
+    libdir = pa.get_library_dirs()[0]
+    so = sorted(f for f in os.listdir(libdir) if f.startswith("libarrow.so."))
+    if not so:
+        raise RuntimeError(f"no libarrow.so.* under {libdir}")
+    return ["-I", pa.get_include(), "-L", libdir, f"-l:{so[0]}", f"-Wl,-rpath,{libdir}"]
 
 
 def out_path(name: str) -> str:
@@ -69,7 +87,7 @@ def _newer(out, srcs):
         return False
     t = os.path.getmtime(out)
     deps = list(srcs)
-    for d in ("common", "hip", "runtime", "exec", "comm", "control"):
+    for d in ("common", "hip", "runtime", "exec", "exec/expr", "comm", "control"):
         p = os.path.join(CSRC, d)
         if os.path.isdir(p):
             deps += [os.path.join(p, f) for f in os.listdir(p) if f.endswith((".h", ".hpp", ".cuh"))]
@@ -89,8 +107,9 @@ def build_one(name: str, force: bool = False) -> str:
         _run([cxx, "-O2", "-std=c++17", "-Wall"] + inc + srcs + ["-o", tmp])
     elif spec["kind"] == "cpu":
         cxx = shutil.which("g++") or "c++"
-        cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-function"] + \
-            inc + srcs + ["-o", tmp] + spec.get("libs", [])
+        extra = _arrow_flags() if spec.get("arrow") else []
+        cmd = [cxx, "-O3", f"-std={spec.get('std', 'c++17')}", "-shared", "-fPIC", "-Wall",
+               "-Wno-unused-function"] + inc + srcs + ["-o", tmp] + spec.get("libs", []) + extra
         _run(cmd)
     else:
         hipcc = os.path.join(ROCM, "bin", "hipcc")

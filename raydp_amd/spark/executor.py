@@ -12,11 +12,18 @@ prepareRecoverableRDD`` + ``getRDDPartition`` (``RayDPExecutor.scala:312-355``):
 is computed and sealed into the executor node's store under a stable id; the driver turns
 those ids into ``ObjectRef``s whose lineage recomputes a lost partition. ``block_locations``
 / ``unpersist`` back ``getBlockLocations`` and ``release_spark_recoverable``.
+
+The task loop and the block cache are native (``csrc/exec/executor.cc`` through
+``raydp_amd/spark/native_exec.py``): a persisted stage whose operators all lower to the
+expression VM runs partition by partition on the C++ worker pool (CSV split or Arrow stream ->
+VM segments -> Arrow IPC straight into the store), with the Python UDF checks called back
+through the bridge; other stages, and any partition the native path hands back, run here in
+Python. ``spark.ray.mi355x.native_executor=0`` keeps every stage on the Python path.
 """
 import hashlib
 import os
 import threading
-from typing import Dict, List, Tuple
+from typing import Dict, List
 
 
 class RayDPExecutor:
@@ -33,8 +40,11 @@ class RayDPExecutor:
         self._fns: Dict[str, object] = {}
         self._fn_order: List[str] = []
         self._lock = threading.Lock()
-        self._cache: Dict[Tuple[str, int], str] = {}   # (rdd_id, partition) -> store object id
+        # native task loop (one worker per core) + the (rdd_id, partition) -> object id cache
+        from raydp_amd.spark import native_exec
+        self._native = native_exec.NativeExecutor(max(1, int(cores)))
         self.tasks_run = 0
+        self.native_tasks = 0
         from raydp_amd.runtime import core
         self._node = core.current_node()
         self._warm_up()
@@ -74,15 +84,19 @@ class RayDPExecutor:
                 "ip": get_node_ip_address(), "cores": self.cores, "tasks_run": self.tasks_run,
                 "restart_count": int(os.environ.get("RAYDP_ACTOR_RESTART_COUNT", "0")),
                 "spark_executor_id": self.spark_executor_id,
-                "shuffle_service": self.registration.shuffle_socket if self.registration else None}
+                "shuffle_service": self.registration.shuffle_socket if self.registration else None,
+                "native_tasks": self.native_tasks, "native_loop": self._native.stats()}
 
     # ------------------------------------------------------------------ tasks -----------
+    @staticmethod
+    def _key(payload) -> str:
+        if isinstance(payload, (bytes, bytearray)):
+            return hashlib.blake2b(payload, digest_size=16).hexdigest()
+        return payload[2]
+
     def _fn(self, payload):
         """Stage function from a store key ``(node_id, path, oid)`` (or raw pickled bytes)."""
-        if isinstance(payload, (bytes, bytearray)):
-            key = hashlib.blake2b(payload, digest_size=16).hexdigest()
-        else:
-            key = payload[2]
+        key = self._key(payload)
         with self._lock:
             fn = self._fns.get(key)
         if fn is None:
@@ -103,6 +117,17 @@ class RayDPExecutor:
                     self._fns.pop(self._fn_order.pop(0), None)
         return fn
 
+    @staticmethod
+    def _lower(fn):
+        """The stage's native form (``native_exec.lower``, cached on the stage's plan) or None."""
+        from raydp_amd.spark import native_exec
+        if not native_exec.enabled():
+            return None
+        try:
+            return native_exec.lower(fn)
+        except Exception:  # noqa: BLE001 - lowering is an optimisation: the Python path runs
+            return None
+
     def run_task(self, payload: bytes, index: int):
         fn = self._fn(payload)
         from raydp_amd.spark.plan import _PartitionScope
@@ -115,34 +140,69 @@ class RayDPExecutor:
     def persist_partitions(self, payload: bytes, rdd_id: str, indices: List[int]):
         """Compute ``indices`` and seal them in this node's store; returns
         ``[(index, object_id, node_id, store_path, num_rows)]``."""
-        import pyarrow as pa
+        from raydp_amd.spark import native_exec
         from raydp_amd.utils import tracing
         with tracing.span("stage unpickle", cat="executor"):
             fn = self._fn(payload)
         st = self._node.store
-        out = []
+        low = self._lower(fn)
+        oids = {}
         for i in indices:
-            with tracing.span("task", cat="executor", partition=i, persist=rdd_id):
-                t = fn(i)
-            if not isinstance(t, pa.Table):
-                raise TypeError(f"stage produced {type(t)} for a persisted partition")
-            t = t.replace_schema_metadata()
             oid = hashlib.blake2b(f"{rdd_id}:{i}".encode(), digest_size=16).hexdigest()
-            with self._lock:
-                old = self._cache.pop((rdd_id, i), None)
+            old = self._native.cache_pop(rdd_id, i)
             if old is not None or st.contains(oid):
                 st.delete(oid)
-            with tracing.span("store put", cat="executor", rows=t.num_rows):
-                st.put(oid, t)
-            with self._lock:
-                self._cache[(rdd_id, i)] = oid
-            out.append((i, oid, st.node_id, st.path, t.num_rows))
+            oids[i] = oid
+        rows: Dict[int, int] = {}
+        if low is not None:
+            # every partition of this call goes onto the native worker pool at once
+            with tracing.span("native tasks", cat="executor", tasks=len(indices), persist=rdd_id):
+                sub = []
+                for i in indices:
+                    tid, keep = self._native.submit(low, i, st, oids[i])
+                    sub.append((i, tid, keep))
+                for i, tid, keep in sub:
+                    if tid < 0:
+                        continue
+                    status, n, _, err = self._native.wait(tid)
+                    if status == native_exec.OK:
+                        rows[i] = n
+                        native_exec.STATS["native_tasks"] += 1
+                        continue
+                    # FALLBACK / RETRY (a UDF was retired) / ERROR (e.g. the store is full):
+                    # the Python path computes the partition and raises its own error if any
+                    kind = {native_exec.RETRY: "native_retries", native_exec.ERROR: "native_errors"}
+                    native_exec.STATS[kind.get(status, "native_fallbacks")] += 1
+                    if status == native_exec.ERROR:
+                        native_exec.LAST_ERROR[0] = err
+        out = []
+        for i in indices:
+            oid = oids[i]
+            if i in rows:
+                self.native_tasks += 1
+            else:
+                rows[i] = self._persist_python(fn, i, st, oid, rdd_id)
+            self._native.cache_put(rdd_id, i, oid)
+            out.append((i, oid, st.node_id, st.path, rows[i]))
             self.tasks_run += 1
         return out
 
+    def _persist_python(self, fn, i, st, oid, rdd_id) -> int:
+        import pyarrow as pa
+        from raydp_amd.utils import tracing
+        with tracing.span("task", cat="executor", partition=i, persist=rdd_id):
+            t = fn(i)
+        if not isinstance(t, pa.Table):
+            raise TypeError(f"stage produced {type(t)} for a persisted partition")
+        t = t.replace_schema_metadata()
+        if st.contains(oid):
+            st.delete(oid)
+        with tracing.span("store put", cat="executor", rows=t.num_rows):
+            st.put(oid, t)
+        return t.num_rows
+
     def get_rdd_partition(self, rdd_id: str, index: int):
-        with self._lock:
-            oid = self._cache.get((rdd_id, index))
+        oid = self._native.cache_get(rdd_id, index)
         if oid is None:
             # requestRecacheRDD (RayDPExecutor.scala:289-310): the driver agent re-materialises
             if self.registration is not None:
@@ -152,19 +212,11 @@ class RayDPExecutor:
         return t if found else None
 
     def block_locations(self, rdd_id: str) -> Dict[int, str]:
-        with self._lock:
-            return {i: self.executor_id for (r, i) in self._cache if r == rdd_id}
+        return {i: self.executor_id for i in self._native.cache_list(rdd_id)}
 
     def unpersist(self, rdd_id: str) -> int:
-        st = self._node.store
-        with self._lock:
-            keys = [k for k in self._cache if k[0] == rdd_id]
-            oids = [self._cache.pop(k) for k in keys]
-        for o in oids:
-            st.delete(o)
-        return len(oids)
+        return self._native.cache_unpersist(rdd_id, self._node.store)
 
     def stop(self):
-        for rdd in {k[0] for k in list(self._cache)}:
-            self.unpersist(rdd)
+        self._native.cache_unpersist(None, self._node.store)
         return True

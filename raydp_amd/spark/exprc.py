@@ -56,6 +56,8 @@ _ARROW_OF = {T_BOOL: pa.bool_(), T_I32: pa.int32(), T_I64: pa.int64(), T_F32: pa
              T_F64: pa.float64()}
 
 _VERIFY_FIRST, _VERIFY_LATER = 64, 4
+# Program.check_taps results (the same codes as csrc/exec/executor.cc Status)
+TAPS_OK, TAPS_FALLBACK, TAPS_RETRY = 0, 1, 2
 STATS = {"fused_partitions": 0, "fallback_partitions": 0, "compiles": 0, "udf_retired": 0,
          "udf_guard_fallbacks": 0}
 
@@ -1038,8 +1040,34 @@ class Program:
             validity = valid_bufs[j] if nulls[j] else None
             outs.append(pa.Array.from_buffers(typ, m, [validity, out_bufs[j]],
                                               null_count=int(nulls[j])))
-        # UDF call sites: null arguments -> Spark's per-row None semantics (Arrow path);
-        # otherwise check the Python function on a sample of rows
+        rc = self.check_taps(outs, out_bufs, m)
+        if rc == TAPS_FALLBACK:
+            return None
+        if rc == TAPS_RETRY:
+            raise _Retry()
+        cols, names = [], []
+        pass_idx = [ref[1] for _, ref in self.columns if ref[0] == "in"]
+        passed = {}
+        if pass_idx:
+            if self.has_filter:
+                sub = t.select(pass_idx).take(pa.array(sel[:m]))
+                for j, ix in enumerate(pass_idx):
+                    passed[ix] = sub.column(j)
+            else:
+                for ix in pass_idx:
+                    passed[ix] = t.column(ix)
+        for name, ref in self.columns:
+            cols.append(outs[ref[1]] if ref[0] == "vm" else passed[ref[1]])
+            names.append(name)
+        return pa.Table.from_arrays(cols, names=names)
+
+    def check_taps(self, outs, out_bufs, m: int) -> int:
+        """UDF call sites of one VM run over ``m`` rows (``outs``: the exported arrays,
+        ``out_bufs``: their value buffers). Null arguments -> Spark's per-row None semantics
+        (TAPS_FALLBACK: the Arrow path); a guard trip -> TAPS_FALLBACK; otherwise the Python
+        function is checked on a sample of rows, and a mismatch retires the UDF (TAPS_RETRY).
+        Shared by the Python path (``run``) and the native task loop's UDF bridge
+        (``raydp_amd/spark/native_exec.py``)."""
         views = {}
 
         def view(j):
@@ -1066,30 +1094,16 @@ class Program:
             return st
         for k, (u, r, argix, guards) in enumerate(self.taps):
             if any(a[0] == "o" and outs[a[1]].null_count for a in argix):
-                return None
+                return TAPS_FALLBACK
             if guards and _guard_trips(guards, view):
                 STATS["udf_guard_fallbacks"] += 1
-                return None
+                return TAPS_FALLBACK
             args = [view(a[1]) if a[0] == "o" else a[1] for a in argix]
             ext = [extremes(a[1]) if a[0] == "o" else () for a in argix]
             if not self._verify(k, u, view(r), args, m, ext):
                 _retire(u)
-                raise _Retry()
-        cols, names = [], []
-        pass_idx = [ref[1] for _, ref in self.columns if ref[0] == "in"]
-        passed = {}
-        if pass_idx:
-            if self.has_filter:
-                sub = t.select(pass_idx).take(pa.array(sel[:m]))
-                for j, ix in enumerate(pass_idx):
-                    passed[ix] = sub.column(j)
-            else:
-                for ix in pass_idx:
-                    passed[ix] = t.column(ix)
-        for name, ref in self.columns:
-            cols.append(outs[ref[1]] if ref[0] == "vm" else passed[ref[1]])
-            names.append(name)
-        return pa.Table.from_arrays(cols, names=names)
+                return TAPS_RETRY
+        return TAPS_OK
 
     def _verify(self, k, u, res: np.ndarray, args: list, m: int, ext: list) -> bool:
         """Python function vs VM result. First partition of a call site: 64 spread rows plus
@@ -1603,7 +1617,7 @@ def _relink_chain(tid: str, data: bytes, base):
     child = base
     for t in tmpl:
         n = object.__new__(type(t))
-        n.__dict__.update({k: v for k, v in t.__dict__.items() if k != "_fused_segs"})
+        n.__dict__.update({k: v for k, v in t.__dict__.items() if k not in ("_fused_segs", "_native_lowered")})
         n.child = child
         child = n
     return child

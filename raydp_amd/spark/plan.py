@@ -183,6 +183,7 @@ class MapPlan(Plan):
     def __getstate__(self):
         st = dict(self.__dict__)
         st.pop("_fused_segs", None)  # compiled programs are per process
+        st.pop("_native_lowered", None)  # native stage handle (spark/native_exec.py)
         if st.pop("_schema_static", False):
             st.pop("_schema", None)  # re-derived statically where needed: not worth shipping
         return st

@@ -175,6 +175,11 @@ register("spark.ray.mi355x.udf_verify", "str", "sampled",
          "inlined Python UDFs: sampled (spread rows + every argument's new extreme rows per partition) "
          "or full (every row checked against the Python function)", env="RAYDP_UDF_VERIFY",
          choices=["sampled", "full"])
+register("spark.ray.mi355x.native_executor", "bool", True,
+         "executors run persisted stages whose operators all lower to the expression VM on the native "
+         "task loop (csrc/exec/executor.cc: CSV split or Arrow stream -> VM -> IPC straight into the "
+         "object store); other stages and fallback partitions take the Python path",
+         env="RAYDP_NATIVE_EXECUTOR")
 register("spark.ray.mi355x.overlap_conversion", "bool", True,
          "fit_on_spark: the training engine is built (device buffers, kernels, parameter upload) while "
          "the conversion stage runs on the executors; the dataset blocks are awaited at first use",

@@ -112,12 +112,14 @@ def span(name: str, cat: str = "raydp", **args) -> Iterator[None]:
                    "pid": os.getpid(), "tid": threading.get_ident() % 100000, "args": args})
 
 
-def complete(name: str, t0_ns: int, cat: str = "raydp", **args):
-    """Record a span that started at ``t0_ns`` (``time.time_ns()``) and ends now."""
+def complete(name: str, t0_ns: int, cat: str = "raydp", t1_ns: Optional[int] = None, tid: Optional[int] = None,
+             **args):
+    """Record a span that started at ``t0_ns`` (``time.time_ns()``) and ends at ``t1_ns``
+    (default: now), on thread row ``tid`` (default: the calling thread)."""
     if _path():
-        t1 = time.time_ns()
+        t1 = time.time_ns() if t1_ns is None else t1_ns
         _emit({"name": name, "cat": cat, "ph": "X", "ts": t0_ns / 1000.0, "dur": (t1 - t0_ns) / 1000.0,
-               "pid": os.getpid(), "tid": threading.get_ident() % 100000, "args": args})
+               "pid": os.getpid(), "tid": threading.get_ident() % 100000 if tid is None else tid, "args": args})
 
 
 def instant(name: str, cat: str = "raydp", **args):

@@ -37,6 +37,7 @@ case $cmd in
     tail -c 900 gpurun_out/rehearse_spmd.jsonl; tail -c 900 gpurun_out/rehearse_estimator.jsonl;;
   prof)
     NAME=$1; shift
+    mkdir -p gpurun_out/prof
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/$NAME -o run \
       -- "$@" > $R/gpurun_out/prof/$NAME.log 2>&1
