@@ -127,14 +127,15 @@ def main():
 
 
 def _graph_step(net, lossf, opt, dense, cats, y, args):
-    """The training step of data slice k for capture: gradients are zeroed in place (a captured
-    memset) except on the cycle's first step, whose backward assigns them."""
+    """The training step of data slice k for capture. Every step drops the gradients before its
+    backward, so autograd ASSIGNS each parameter's gradient (from the graph's private pool; the
+    captured optimizer kernel reads that step's buffers) instead of a captured memset followed
+    by an accumulate-add per parameter. ``first`` is kept for callers that zero eagerly."""
     def run(k, first):
         s = k * args.batch
         out = net(dense[s:s + args.batch], cats[s:s + args.batch])
         loss = lossf(out.float(), y[s:s + args.batch])
-        if not first:
-            opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
         return loss
@@ -152,7 +153,6 @@ def _capture_cycle(run, opt, dev):
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
-        opt.zero_grad(set_to_none=True)    # the cycle's first captured backward assigns the grads
         with torch.cuda.graph(g):
             loss = None
             for k in range(8):
