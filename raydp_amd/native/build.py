@@ -48,6 +48,7 @@ LIBS = {
     # object store, partition cache (Arrow C++ from the pyarrow wheel; libraydp_runtime)
     "raydp_executor": dict(kind="cpu", std="c++20", arrow=True,
                            sources=lambda: [os.path.join(CSRC, "exec", "executor.cc"),
+                                            os.path.join(CSRC, "exec", "csv_infer.cc"),
                                             os.path.join(CSRC, "exec", "expr", "expr_vm.cc")],
                            libs=["-L", HERE, "-lraydp_runtime", "-Wl,-rpath,$ORIGIN", "-lpthread"]),
     "hipkernels": dict(kind="hip", sources=_hip_sources),

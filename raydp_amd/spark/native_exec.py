@@ -35,7 +35,7 @@ OK, FALLBACK, RETRY, ERROR = 0, 1, 2, -1
 _ERRLEN = 1024
 
 STATS = {"native_tasks": 0, "native_fallbacks": 0, "native_retries": 0, "native_errors": 0,
-         "lowered_stages": 0, "not_lowered": 0}
+         "lowered_stages": 0, "not_lowered": 0, "native_csv_reads": 0}
 LAST_ERROR = [None]     # message of the last native task that failed (then run in Python)
 
 _TAPFN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
@@ -79,6 +79,8 @@ def _lib():
             lib.rx_cache_unpersist.restype = c.c_int
             lib.rx_cache_rdds.argtypes = [c.c_void_p, c.c_char_p, c.c_int]
             lib.rx_cache_rdds.restype = c.c_int
+            lib.rx_csv_infer.argtypes = [c.c_char_p, c.c_int64, c.c_char, c.c_void_p]
+            lib.rx_csv_infer.restype = c.c_int
             _lib_handle = lib
     return _lib_handle
 
@@ -86,6 +88,19 @@ def _lib():
 def enabled() -> bool:
     from raydp_amd.utils.config import get as conf_get
     return bool(conf_get("spark.ray.mi355x.native_executor"))
+
+
+def read_csv_infer(data: bytes, sep: str = ",") -> Optional[pa.Table]:
+    """The table pyarrow's CSV reader with type inference (header row, null token "") returns
+    for ``data``, read natively in one pass (``csrc/exec/csv_infer.cc``), or None when the
+    bytes hold anything that reader does not decide exactly -- then read them with pyarrow."""
+    if len(sep) != 1 or not data:
+        return None
+    stream = ctypes.create_string_buffer(64)            # struct ArrowArrayStream
+    rc = _lib().rx_csv_infer(data, len(data), sep.encode(), ctypes.addressof(stream))
+    if rc != 1:
+        return None
+    return pa.RecordBatchReader._import_from_c(ctypes.addressof(stream)).read_all()
 
 
 # ------------------------------------------------------------------------------------------

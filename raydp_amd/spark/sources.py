@@ -117,6 +117,17 @@ def _downcast_ints(t: pa.Table) -> pa.Table:
     return pa.table(cols, names=t.column_names) if changed else t
 
 
+def _native_infer(head: bytes, sep: str) -> Optional[pa.Table]:
+    try:
+        from raydp_amd.spark import native_exec
+        t = native_exec.read_csv_infer(head, sep)
+    except Exception:  # noqa: BLE001 - the native reader is an optimisation: pyarrow reads
+        return None
+    if t is not None:
+        native_exec.STATS["native_csv_reads"] += 1
+    return t
+
+
 class CsvSource(Source):
     def __init__(self, path, header=True, infer_schema=False, sep=",", schema=None,
                  max_partition_bytes=128 * 1024 * 1024, null_value=None, parallelism=1,
@@ -165,9 +176,15 @@ class CsvSource(Source):
         nulls = [self.null_value] if self.null_value else [""]
         conv = pacsv.ConvertOptions(strings_can_be_null=True, null_values=nulls) if infer else \
             pacsv.ConvertOptions(column_types=None, null_values=nulls)
-        t = pacsv.read_csv(pa.BufferReader(pa.py_buffer(head)), read_options=self._read_opts(nbytes=len(head)),
-                           parse_options=pacsv.ParseOptions(delimiter=self.sep),
-                           convert_options=conv)
+        t = None
+        if infer and self.header and not self.null_value:
+            # one native pass that returns exactly pyarrow's inferred table, or None when the
+            # bytes hold anything it does not decide (csrc/exec/csv_infer.cc)
+            t = _native_infer(head, self.sep)
+        if t is None:
+            t = pacsv.read_csv(pa.BufferReader(pa.py_buffer(head)), read_options=self._read_opts(nbytes=len(head)),
+                               parse_options=pacsv.ParseOptions(delimiter=self.sep),
+                               convert_options=conv)
         if not infer:
             return pa.schema([pa.field(n, pa.string()) for n in t.column_names])
         t = _downcast_ints(t)
