@@ -81,18 +81,23 @@ bool word_is(const char* s, int32_t n, const char* w) {
   return true;
 }
 
-Kind classify(const Field& f) {
+// Classify one field; a number is parsed once, into *iv / *dv.
+Kind classify(const Field& f, int64_t* iv, double* dv) {
   const char* s = f.p;
   const int32_t n = f.n;
   if (n == 0) return kNull;
   if (s[0] == ' ' || s[0] == '\t' || s[n - 1] == ' ' || s[n - 1] == '\t') return kAmbiguous;
-  int64_t iv;
-  const bool ip = arrow::internal::ParseValue<arrow::Int64Type>(s, static_cast<size_t>(n), &iv);
-  if (int_shape(s, n)) return ip ? kInt : kAmbiguous;
-  double dv;
-  const bool dp = arrow::internal::StringToFloat(s, static_cast<size_t>(n), '.', &dv);
-  if (real_shape(s, n)) return dp ? kReal : kAmbiguous;
-  if (ip || dp) return kAmbiguous;           // Arrow reads it as a number in a form not vetted here
+  if (int_shape(s, n))
+    return arrow::internal::ParseValue<arrow::Int64Type>(s, static_cast<size_t>(n), iv) ? kInt : kAmbiguous;
+  if (real_shape(s, n))
+    return arrow::internal::StringToFloat(s, static_cast<size_t>(n), '.', dv) ? kReal : kAmbiguous;
+  // not a vetted number shape: ambiguous if Arrow would still read it as one (both parsers
+  // need a sign, a digit, '.', or the first letter of inf / nan up front)
+  const char c0 = (s[0] == '-' || s[0] == '+') && n > 1 ? s[1] : s[0];
+  if ((is_digit(c0) || c0 == '.' || c0 == 'i' || c0 == 'I' || c0 == 'n' || c0 == 'N') &&
+      (arrow::internal::ParseValue<arrow::Int64Type>(s, static_cast<size_t>(n), iv) ||
+       arrow::internal::StringToFloat(s, static_cast<size_t>(n), '.', dv)))
+    return kAmbiguous;
   // boolean / special float words
   const char* t = s;
   int32_t m = n;
@@ -111,26 +116,31 @@ Kind classify(const Field& f) {
   return kAmbiguous;
 }
 
-// Tokenise `data` into rows of fields. Returns false on anything the simple grammar does not
-// cover (the caller falls back to Arrow's reader).
-bool tokenize(const char* data, int64_t len, char delim, std::vector<std::vector<Field>>* rows) {
+// Tokenise `data` into a row-major field grid (`ncol` fields per row, header included).
+// Returns false on anything the simple grammar does not cover (the caller falls back to Arrow's
+// reader) or on a row whose field count differs from the header's (Arrow raises on it).
+bool tokenize(const char* data, int64_t len, char delim, std::vector<Field>* cells, size_t* ncol) {
   int64_t i = 0;
+  size_t row_start = 0;
+  *ncol = 0;
+  cells->reserve(static_cast<size_t>(len / 8 + 16));
   while (i < len) {
     int64_t e = i;
-    while (e < len && data[e] != '\n') ++e;
+    const void* nl = std::memchr(data + i, '\n', static_cast<size_t>(len - i));
+    e = nl ? static_cast<const char*>(nl) - data : len;
     if (e == i) {  // empty line: Arrow's ignore_empty_lines
       i = e + 1;
       continue;
     }
-    std::vector<Field> row;
+    row_start = cells->size();
     int64_t k = i;
     for (;;) {
       if (k < e && data[k] == '"') {
         int64_t q = k + 1;
         while (q < e && data[q] != '"') ++q;
-        if (q >= e) return false;                       // unterminated on this line
+        if (q >= e) return false;                              // unterminated on this line
         if (q + 1 < e && data[q + 1] != delim) return false;   // "" escape or text after quote
-        row.push_back(Field{data + k + 1, static_cast<int32_t>(q - k - 1)});
+        cells->push_back(Field{data + k + 1, static_cast<int32_t>(q - k - 1)});
         k = q + 1;
       } else {
         int64_t q = k;
@@ -138,20 +148,22 @@ bool tokenize(const char* data, int64_t len, char delim, std::vector<std::vector
           if (data[q] == '"' || data[q] == '\r') return false;
           ++q;
         }
-        row.push_back(Field{data + k, static_cast<int32_t>(q - k)});
+        cells->push_back(Field{data + k, static_cast<int32_t>(q - k)});
         k = q;
       }
       if (k >= e) break;
       ++k;  // delimiter
       if (k == e) {  // trailing delimiter: one more empty field
-        row.push_back(Field{data + k, 0});
+        cells->push_back(Field{data + k, 0});
         break;
       }
     }
-    rows->push_back(std::move(row));
+    const size_t nf = cells->size() - row_start;
+    if (*ncol == 0) *ncol = nf;
+    else if (nf != *ncol) return false;
     i = e + 1;
   }
-  return true;
+  return *ncol > 0;
 }
 
 }  // namespace
@@ -162,25 +174,26 @@ extern "C" {
 // type inference would. Returns 1 and exports the table as an ArrowArrayStream into `out`, 0 when
 // the input holds anything this reader does not decide (read it with Arrow), -1 on an error.
 int rx_csv_infer(const char* data, int64_t len, char delim, void* out) {
-  std::vector<std::vector<Field>> rows;
-  if (len <= 0 || !tokenize(data, len, delim, &rows) || rows.empty()) return 0;
-  const size_t ncol = rows[0].size();
-  const size_t nrow = rows.size() - 1;
-  if (ncol == 0 || nrow == 0) return 0;
-  for (size_t r = 1; r < rows.size(); ++r)
-    if (rows[r].size() != ncol) return 0;                   // ragged: Arrow raises
+  std::vector<Field> cells;
+  size_t ncol = 0;
+  if (len <= 0 || !tokenize(data, len, delim, &cells, &ncol)) return 0;
+  const size_t nrow = cells.size() / ncol - 1;
+  if (nrow == 0) return 0;
   std::vector<std::shared_ptr<arrow::Field>> fields;
   std::vector<std::shared_ptr<arrow::Array>> cols;
+  std::vector<Kind> kinds(nrow);
+  std::vector<int64_t> ivals(nrow);
+  std::vector<double> dvals(nrow);
   for (size_t c = 0; c < ncol; ++c) {
-    const Field& h = rows[0][c];
+    const Field& h = cells[c];
     for (int32_t j = 0; j < h.n; ++j)
       if (static_cast<unsigned char>(h.p[j]) >= 0x80) return 0;
-    bool any_int = false, any_real = false, any_text = false, any_value = false;
-    for (size_t r = 1; r <= nrow; ++r) {
-      const Kind k = classify(rows[r][c]);
+    bool any_real = false, any_text = false, any_value = false;
+    for (size_t r = 0; r < nrow; ++r) {
+      const Kind k = classify(cells[(r + 1) * ncol + c], &ivals[r], &dvals[r]);
       if (k == kAmbiguous) return 0;
+      kinds[r] = k;
       any_value |= k != kNull;
-      any_int |= k == kInt;
       any_real |= k == kReal;
       any_text |= k == kText;
     }
@@ -190,38 +203,31 @@ int rx_csv_infer(const char* data, int64_t len, char delim, void* out) {
     if (any_text) {
       arrow::StringBuilder b;
       st = b.Reserve(static_cast<int64_t>(nrow));
-      for (size_t r = 1; r <= nrow && st.ok(); ++r) {
-        const Field& f = rows[r][c];
+      for (size_t r = 0; r < nrow && st.ok(); ++r) {
+        const Field& f = cells[(r + 1) * ncol + c];
         st = f.n == 0 ? b.AppendNull() : b.Append(f.p, f.n);
       }
       if (st.ok()) st = b.Finish(&arr);
     } else if (any_real) {
+      // ints inside a double column: Arrow's real decoder parses their text as a double
+      for (size_t r = 0; r < nrow; ++r) {
+        if (kinds[r] != kInt) continue;
+        const Field& f = cells[(r + 1) * ncol + c];
+        if (!arrow::internal::StringToFloat(f.p, static_cast<size_t>(f.n), '.', &dvals[r])) return 0;
+      }
       arrow::DoubleBuilder b;
       st = b.Reserve(static_cast<int64_t>(nrow));
-      for (size_t r = 1; r <= nrow && st.ok(); ++r) {
-        const Field& f = rows[r][c];
-        double v = 0;
-        if (f.n == 0) {
-          b.UnsafeAppendNull();
-        } else {
-          if (!arrow::internal::StringToFloat(f.p, static_cast<size_t>(f.n), '.', &v)) return 0;
-          b.UnsafeAppend(v);
-        }
+      for (size_t r = 0; r < nrow && st.ok(); ++r) {
+        if (kinds[r] == kNull) b.UnsafeAppendNull();
+        else b.UnsafeAppend(dvals[r]);
       }
       if (st.ok()) st = b.Finish(&arr);
     } else {
-      (void)any_int;
       arrow::Int64Builder b;
       st = b.Reserve(static_cast<int64_t>(nrow));
-      for (size_t r = 1; r <= nrow && st.ok(); ++r) {
-        const Field& f = rows[r][c];
-        int64_t v = 0;
-        if (f.n == 0) {
-          b.UnsafeAppendNull();
-        } else {
-          if (!arrow::internal::ParseValue<arrow::Int64Type>(f.p, static_cast<size_t>(f.n), &v)) return 0;
-          b.UnsafeAppend(v);
-        }
+      for (size_t r = 0; r < nrow && st.ok(); ++r) {
+        if (kinds[r] == kNull) b.UnsafeAppendNull();
+        else b.UnsafeAppend(ivals[r]);
       }
       if (st.ok()) st = b.Finish(&arr);
     }

@@ -543,3 +543,10 @@ class TorchLoopEngine:
 
     def optimizer_state_dict(self):
         return self.optimizer.state_dict()
+
+    def close(self):
+        """End of the fit: destroy the captured graphs now. A warm worker keeps running fits;
+        left to the garbage collector, a previous fit's graph could be destroyed while the next
+        fit's capture is in progress, which HIP refuses (and torch turns into an abort)."""
+        if self.graphed is not None:
+            self.graphed.close()

@@ -345,6 +345,8 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         with tracing.span("checkpoint", cat="train"):
             states = engine.state_dict()
             states = {k: v.detach().cpu() for k, v in states.items()}
+            if hasattr(engine, "close"):
+                engine.close()
             checkpoint = None
             if session.get_world_rank() == 0:
                 # model.pt is written straight into a staging dir of the run's storage and

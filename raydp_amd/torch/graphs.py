@@ -26,6 +26,7 @@ Rules that keep it exact:
 * any capture failure (an op that synchronises, sparse gradients, ...) disables graphs for the
   engine and the same batch is re-run eagerly -- results never depend on whether capture worked.
 """
+import gc
 import os
 import traceback
 from typing import Optional
@@ -136,9 +137,18 @@ class GraphedTrainLoop:
         win = torch.empty(steps * b, dtype=torch.int64, device=self.e.device)
         g = torch.cuda.CUDAGraph()
         self.e.zero_grad()
-        with torch.cuda.graph(g, pool=self.pool), _CaptureSafeIndexing(self.index_cache):
-            for j in range(steps):
-                self._forward_step(*self._gather(win[j * b:(j + 1) * b]))
+        # no garbage collection while capturing: a collected object owning a graph (or any HIP
+        # resource whose release is not capture-safe) would be destroyed mid-capture
+        gc_was = gc.isenabled()
+        gc.collect()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g, pool=self.pool), _CaptureSafeIndexing(self.index_cache):
+                for j in range(steps):
+                    self._forward_step(*self._gather(win[j * b:(j + 1) * b]))
+        finally:
+            if gc_was:
+                gc.enable()
         if self.pool is None:
             self.pool = g.pool()
         self.graphs[steps] = (g, win)
@@ -163,6 +173,13 @@ class GraphedTrainLoop:
         g.replay()
         if self.e.scheduler is not None:
             self.e.scheduler.step()
+
+    def close(self):
+        """Destroy the captured graphs and their pool (no capture may be running)."""
+        if self.graphs:
+            torch.cuda.synchronize(self.e.device)
+        self.graphs.clear()
+        self.pool = None
 
     # ------------------------------------------------------------------ epoch
     def train_epoch(self):
