@@ -315,16 +315,20 @@ def test_fused_engine_adds_no_host_sync_per_epoch_at_world_2(monkeypatch):
 
     class FakeTrainer:
         batch, steps_in_epoch = 64, 4
+        desc = types.SimpleNamespace(out_dim=1)
 
         def train_epoch(self, *a, **k):
             return {"loss": 0.5, "mae": 0.1, "mse": 0.2, "acc": 0.0, "xg_vote": 0.0}
 
         def note_steps(self, n):
             pass
+
+        def step_times_us(self):
+            return None
     shard = types.SimpleNamespace(feats_bf16=None, labels=None, n=256)
     eng = types.SimpleNamespace(trainer=FakeTrainer(), world=2, drop_last=True, xg=None, ar=None, comm=None,
                                 max_steps=None, shuffle=False, epoch=0, metrics_names=["MeanAbsoluteError"],
-                                train=shard)
+                                train=shard, loss=None)
     eng._res = lambda m: E.FusedMLPEngine._res(eng, m)
     for _ in range(3):
         E.FusedMLPEngine.train_epoch(eng)
