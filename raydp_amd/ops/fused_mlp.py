@@ -311,23 +311,22 @@ class FusedMLPTrainer:
         act_floats = _ru((act + 1) // 2, 4)
         d.act_off, d.wgrad_mode = act_off, wmode
         self.total = total
-        self.params = torch.cat([f.detach().cpu() for f in flat]).to(dev).contiguous()
-        self.grads = torch.zeros(act_off + act_floats, dtype=torch.float32, device=dev)
-        self.m = torch.zeros_like(self.params)
-        self.v = torch.zeros_like(self.params)
-        self.scratch = torch.zeros(max(1, scratch_off), dtype=torch.float32, device=dev)
-        self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
-        self.img = torch.zeros(max(8, img_off), dtype=torch.bfloat16, device=dev)
-        rs_host = torch.zeros(max(1, rs_total), dtype=torch.float32)
+        # ONE device arena for every buffer of the trainer: [params | rstats | descriptors] are
+        # uploaded from one pinned host image in one copy, [grads | m | v | scratch | metrics |
+        # img] are zeroed by one fill (a fit's engine set-up is on the headline's critical path)
+        params_h = torch.cat([f.detach().reshape(-1).cpu().float() for f in flat]) if flat else \
+            torch.zeros(0)
+        rs_h = torch.zeros(max(1, rs_total), dtype=torch.float32)
         for bn, ro, n_ in rs_init:
-            rs_host[ro:ro + n_] = bn.running_mean.detach().cpu().float()
-            rs_host[ro + n_:ro + 2 * n_] = bn.running_var.detach().cpu().float()
-        self.rstats = rs_host.to(dev)
-        for bn, ro, n_ in rs_init:
-            self.run_bufs.append((bn, self.rstats[ro:ro + n_], self.rstats[ro + n_:ro + 2 * n_]))
-        base = self.img.data_ptr()
-        for si, wi, wti in seg_images:
-            o.seg[si].W, o.seg[si].Wt = base + 2 * wi, base + 2 * wti
+            rs_h[ro:ro + n_] = bn.running_mean.detach().cpu().float()
+            rs_h[ro + n_:ro + 2 * n_] = bn.running_var.detach().cpu().float()
+        self._arena_plan = {"params": (params_h.numel(), torch.float32), "rstats": (rs_h.numel(), torch.float32)}
+        self._arena_host = {"params": params_h, "rstats": rs_h}
+        self._arena_zero = [("grads", act_off + act_floats, torch.float32), ("m", params_h.numel(), torch.float32),
+                            ("v", params_h.numel(), torch.float32), ("scratch", max(1, scratch_off), torch.float32),
+                            ("metrics", 8, torch.float64), ("img", max(8, img_off), torch.bfloat16)]
+        self._arena_dev = dev
+        self._seg_images = seg_images
         cfg = self.cfg
         o.nseg, o.total, o.algo = nseg, total, cfg["algo"]
         o.b1, o.b2, o.eps = cfg.get("b1", 0.9), cfg.get("b2", 0.999), cfg.get("eps", 1e-8)
@@ -337,8 +336,7 @@ class FusedMLPTrainer:
         self.opt = o
         self.lds_bytes = lds
         # descriptors live in device memory: the kernels index them with runtime layer ids
-        self._desc_buf = torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8).to(dev)
-        self._opt_buf = torch.frombuffer(bytearray(bytes(o)), dtype=torch.uint8).to(dev)
+        self._materialize(bytes(d), bytes(o), rs_init)
         self._dd = ctypes.c_void_p(self._desc_buf.data_ptr())
         self._od = ctypes.c_void_p(self._opt_buf.data_ptr())
         b = _hip.StepBufs()
@@ -353,6 +351,58 @@ class FusedMLPTrainer:
             from raydp_amd.ops import mlp_jit
             self.jit = mlp_jit.load_specialized(self)
         self.refresh_images()
+
+    def _materialize(self, desc_bytes: bytes, opt_bytes: bytes, rs_init):
+        """Allocate the arena, point the optimizer descriptor's segments at their bf16 images,
+        and fill the arena with one zero fill + one host-to-device copy."""
+        dev = self._arena_dev
+        A = 256
+
+        def nbytes(n, dt):
+            return _ru(n * torch.tensor([], dtype=dt).element_size(), A)
+        up = [("params",) + self._arena_plan["params"], ("rstats",) + self._arena_plan["rstats"]]
+        off, where = 0, {}
+        for name, n, dt in up:
+            where[name] = (off, n, dt)
+            off += nbytes(n, dt)
+        desc_off = off
+        off += _ru(len(desc_bytes), A)
+        opt_off = off
+        off += _ru(len(opt_bytes), A)
+        up_end = off
+        for name, n, dt in self._arena_zero:
+            where[name] = (off, n, dt)
+            off += nbytes(n, dt)
+        arena = torch.empty(max(A, off), dtype=torch.uint8, device=dev)
+        self._arena = arena
+
+        def view(name):
+            o_, n, dt = where[name]
+            return arena[o_:o_ + n * torch.tensor([], dtype=dt).element_size()].view(dt)
+        self.params, self.rstats = view("params"), view("rstats")
+        self.grads, self.m, self.v = view("grads"), view("m"), view("v")
+        self.scratch, self.metrics, self.img = view("scratch"), view("metrics"), view("img")
+        self._desc_buf = arena[desc_off:desc_off + len(desc_bytes)]
+        base = self.img.data_ptr()
+        o = self.opt
+        for si, wi, wti in self._seg_images:
+            o.seg[si].W, o.seg[si].Wt = base + 2 * wi, base + 2 * wti
+        opt_bytes = bytes(o)
+        self._opt_buf = arena[opt_off:opt_off + len(opt_bytes)]
+        # host image of the uploaded part, pinned: one asynchronous copy
+        host = torch.empty(up_end, dtype=torch.uint8, pin_memory=dev.type == "cuda")
+        for name in ("params", "rstats"):
+            o_, n, dt = where[name]
+            src = self._arena_host[name]
+            host[o_:o_ + src.numel() * src.element_size()].view(dt).copy_(src)
+        host[desc_off:desc_off + len(desc_bytes)] = torch.frombuffer(bytearray(desc_bytes), dtype=torch.uint8)
+        host[opt_off:opt_off + len(opt_bytes)] = torch.frombuffer(bytearray(opt_bytes), dtype=torch.uint8)
+        arena[:up_end].copy_(host, non_blocking=True)
+        arena[up_end:].zero_()
+        self._arena_upload = host          # kept alive until the copy has run
+        self._arena_host = None
+        for bn, ro, n_ in rs_init:
+            self.run_bufs.append((bn, self.rstats[ro:ro + n_], self.rstats[ro + n_:ro + 2 * n_]))
 
     # ------------------------------------------------------------------- optimizer state ----
     def _param_of(self, kind, mod):
@@ -489,7 +539,8 @@ class FusedMLPTrainer:
         if xg is not None:
             # epoch-end agreement over xGMI, read with the metrics (one D2H copy)
             xg.vote(self.metrics[7:8])
-        out = self._read_metrics()
+        pre, self._metrics_np = getattr(self, "_metrics_np", None), None
+        out = self._read_metrics(pre)
         if xg is not None and out["xg_vote"] != 0.0:
             from raydp_amd.exceptions import CollectiveError
             raise CollectiveError("xGMI all-reduce: a peer did not arrive within the timeout "
@@ -503,7 +554,7 @@ class FusedMLPTrainer:
         if st is None:
             return None
         self._step_stamps = None
-        t = st.cpu().numpy()[32:].astype(np.float64)
+        t = np.asarray(st)[32:].astype(np.float64)
         return np.diff(t) * 0.01 if t.size > 1 else None
 
     def snapshot(self):
@@ -533,18 +584,28 @@ class FusedMLPTrainer:
             self._ps_ok = self._ps_grid <= int(props.multi_processor_count)
         if not self._ps_ok:
             return False
-        sched = torch.from_numpy(np.concatenate([lr_np, bc1_np, bc2_np])).to(self.device)
         pp = ctypes.c_void_p
+        # the per-step schedule goes up from a pinned staging buffer (no synchronous copy)
+        sched_h = self._host_buf("sched", 3 * nsteps, torch.float32)
+        sched_np = sched_h.numpy()
+        sched_np[:nsteps], sched_np[nsteps:2 * nsteps], sched_np[2 * nsteps:] = lr_np, bc1_np, bc2_np
+        sched = sched_h.to(self.device, non_blocking=True)
         from raydp_amd.utils.config import get as conf_get
         timeout = float(conf_get("spark.ray.mi355x.mlp_persistent.timeout_s"))
         # device-side snapshot of the state the epoch mutates: a wait that times out (the grid was
         # admitted but a co-tenant still starved a workgroup) rolls back and reruns the epoch on
-        # the launch-per-step loop instead of failing the fit
-        snap = [t.clone() for t in (self.params, self.m, self.v, self.rstats, self.img)]
+        # the launch-per-step loop instead of failing the fit. One multi-tensor copy into
+        # buffers kept across epochs.
+        live = [self.params, self.m, self.v, self.rstats, self.img]
+        snap = getattr(self, "_snap", None)
+        if snap is None:
+            snap = self._snap = [torch.empty_like(t) for t in live]
+        torch._foreach_copy_(snap, live)
         stamps = None
         if self.record_steps:
             # device wall clock at every step start (csrc/hip/mlp_persist.h RX_PS_STEP_STAMPS)
-            stamps = torch.zeros(32 + nsteps + 1, dtype=torch.int64, device=self.device)
+            stamps = self._dev_buf("stamps", 32 + nsteps + 1, torch.int64)
+            stamps.zero_()
             self.bufs.stamps = stamps.data_ptr()
         rc = self.lib.rx_mlp_train_persistent(
             ctypes.byref(self.desc), ctypes.byref(self.bufs), ctypes.byref(self.opt), self._od, self.mt,
@@ -556,18 +617,51 @@ class FusedMLPTrainer:
             return False
         _hip.check(rc, "rx_mlp_train_persistent")
         self._ps_sched = sched   # kept alive until the launch has consumed it
-        self._step_stamps = stamps
-        if int(self._ps_sync[self._ps_err].item()) != 0:
+        # ONE synchronisation for everything the epoch reports: the wait-timeout word, the
+        # metrics and the step stamps come back together
+        back = self._readback([self._ps_sync[self._ps_err:self._ps_err + 1], self.metrics] +
+                              ([stamps] if stamps is not None else []))
+        self._step_stamps = back[2].copy() if stamps is not None else None
+        if int(back[0][0]) != 0:
             import warnings
             warnings.warn("persistent fused-MLP epoch: a workgroup wait timed out; rolled back and "
                           "rerunning the epoch on the launch-per-step loop")
-            for dst, src in zip((self.params, self.m, self.v, self.rstats, self.img), snap):
-                dst.copy_(src)
+            torch._foreach_copy_(live, snap)
             self.metrics.zero_()
+            self._step_stamps = None
             self._ps_ok = False          # this trainer stays on the step loop from now on
             self.persistent_fallbacks = getattr(self, "persistent_fallbacks", 0) + 1
             return False
+        self._metrics_np = back[1].copy()
         return True
+
+    def _host_buf(self, key, n, dtype) -> torch.Tensor:
+        """A pinned host buffer of at least ``n`` elements kept across epochs (first ``n`` used)."""
+        bufs = self.__dict__.setdefault("_host_bufs", {})
+        b = bufs.get((key, dtype))
+        if b is None or b.numel() < n:
+            b = torch.empty(max(n, 64), dtype=dtype, pin_memory=self.device.type == "cuda")
+            bufs[(key, dtype)] = b
+        return b[:n]
+
+    def _dev_buf(self, key, n, dtype) -> torch.Tensor:
+        bufs = self.__dict__.setdefault("_dev_bufs", {})
+        b = bufs.get((key, dtype))
+        if b is None or b.numel() < n:
+            b = torch.empty(max(n, 64), dtype=dtype, device=self.device)
+            bufs[(key, dtype)] = b
+        return b[:n]
+
+    def _readback(self, tensors) -> List[np.ndarray]:
+        """Copy device tensors into pinned host buffers and synchronise once; the returned
+        arrays alias those buffers (valid until the next readback)."""
+        hs = []
+        for i, t in enumerate(tensors):
+            h = self._host_buf(f"rb{i}", t.numel(), t.dtype)
+            h.copy_(t.reshape(-1), non_blocking=True)
+            hs.append(h)
+        torch.cuda.current_stream(self.device).synchronize()
+        return [h.numpy() for h in hs]
 
     def _check_operands(self, feats, labels, n_rows, perm=None):
         """Host-side guard: the kernels index rows [0, n_rows) of feats / labels (through perm)
@@ -621,8 +715,9 @@ class FusedMLPTrainer:
         _hip.check(rc, "rx_mlp_eval")
         return self._read_metrics()
 
-    def _read_metrics(self) -> Dict[str, float]:
-        m = self.metrics.cpu().numpy()
+    def _read_metrics(self, m: Optional[np.ndarray] = None) -> Dict[str, float]:
+        if m is None:
+            m = self.metrics.cpu().numpy()
         if m[6] > 0:
             raise IndexError("embedding id out of range in the fused trainer's input "
                              f"({int(m[6])} batch(es) clamped)")

@@ -117,3 +117,52 @@ def test_use_ccl_reaches_the_trainer(runtime_local, tmp_path, monkeypatch):
 
 
 _ = pytest
+
+
+def _loop_dies_after_final_report(config):
+    """Per-epoch checkpoints with meta.json, then rank 0's final model-only checkpoint, then
+    rank 1 dies once -- after every report of the attempt."""
+    import json
+    from raydp_amd.train import Checkpoint, session
+    rank = session.get_world_rank()
+    start = 0
+    ck = session.get_checkpoint()
+    if ck is not None:
+        with open(os.path.join(ck.path, "meta.json")) as f:
+            start = json.load(f)["epoch"] + 1
+    for epoch in range(start, 3):
+        ckpt = None
+        if rank == 0:
+            d = session.staging_dir()
+            with open(os.path.join(d, "meta.json"), "w") as f:
+                json.dump({"epoch": epoch}, f)
+            ckpt = Checkpoint(d, movable=True)
+        session.report({"epoch": epoch, "start": start}, checkpoint=ckpt)
+    if rank == 0:
+        d = session.staging_dir()
+        with open(os.path.join(d, "model.pt"), "wb") as f:
+            f.write(b"final")
+        session.report({"final": True, "start": start}, checkpoint=Checkpoint(d, movable=True))
+    else:
+        session.report({"final": True, "start": start})
+    flag = config["flag"]
+    if rank == 1 and not os.path.exists(flag):
+        open(flag, "w").close()
+        os._exit(1)
+
+
+def test_rank_dying_after_the_final_report_resumes_from_the_last_epoch_checkpoint(runtime_local, tmp_path):
+    from raydp_amd.train import FailureConfig, RunConfig, ScalingConfig, TorchTrainer
+    flag = str(tmp_path / "died")
+    tr = TorchTrainer(_loop_dies_after_final_report, train_loop_config={"flag": flag},
+                      scaling_config=ScalingConfig(num_workers=2, use_gpu=False),
+                      run_config=RunConfig(storage_path=str(tmp_path / "runs"),
+                                           failure_config=FailureConfig(max_failures=1)))
+    res = tr.fit()
+    assert os.path.exists(flag)
+    assert len(res.restored_from) == 1
+    # the final model.pt of the failed attempt carries no meta.json: the retry resumes after
+    # epoch 2 (nothing re-trained), not from the trained final model at epoch 0
+    assert os.path.exists(os.path.join(res.restored_from[0], "meta.json"))
+    finals = [m for m in res.metrics_history if m.get("final")]
+    assert finals and finals[-1]["start"] == 3, res.metrics_history

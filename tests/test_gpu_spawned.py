@@ -76,3 +76,34 @@ def test_spawned_workers_train_fused_over_xgmi_and_stay_warm(runtime_local, tmp_
         assert rel < 1e-4, (k, rel)
     T.release_worker_groups()
     assert len(T._GROUPS) == 0
+
+
+def test_warm_workers_survive_consecutive_graph_captured_fits(runtime_local, tmp_path, monkeypatch):
+    """The torch-loop engine at world 2 captures its DDP step (xGMI buckets) into HIP graphs. A
+    warm worker group runs the next fit in the same processes: the previous fit's graphs must be
+    gone before the new capture (a graph destroyed mid-capture aborts the worker)."""
+    import pandas as pd
+    from raydp_amd.data import from_pandas
+    from raydp_amd.torch import TorchEstimator
+    from raydp_amd.train import trainer as T
+    monkeypatch.setenv("RAYDP_TRAIN_BACKEND", "gloo")
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((64 * 12, 8)).astype(np.float32)
+    df = pd.DataFrame({f"f{i}": x[:, i] for i in range(8)})
+    df["y"] = np.tanh(x[:, :3].sum(1))
+    groups, engines = [], []
+    for tag, hidden in (("a", 16), ("b", 24)):        # a different model each fit
+        torch.manual_seed(0)
+        model = nn.Sequential(nn.Linear(8, hidden), nn.Tanh(), nn.Linear(hidden, 1))
+        est = TorchEstimator(num_workers=2, resources_per_worker={"CPU": 1, "GPU": 0.5}, model=model,
+                             optimizer=torch.optim.SGD(model.parameters(), lr=0.05), loss=nn.MSELoss(),
+                             feature_columns=[f"f{i}" for i in range(8)], label_column="y", batch_size=64,
+                             num_epochs=2, fused="off", shuffle_seed=3, storage_path=str(tmp_path / tag))
+        res = est.fit(from_pandas(df))
+        hist = [m for m in res.metrics_history if "train_loss" in m]
+        engines.append(hist[0]["engine"])
+        groups.append(next(iter(T._GROUPS._groups.values())))
+        assert hist[-1]["train_loss"] < hist[0]["train_loss"]
+    assert engines == ["torch_loop_hipgraph"] * 2, engines
+    assert groups[0] is groups[1], "the second fit must run on the same warm workers (no restart)"
+    T.release_worker_groups()
