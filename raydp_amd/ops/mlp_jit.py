@@ -111,12 +111,20 @@ def _hipcc() -> str:
     return os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
 
 
+_headers_digest = None
+
+
 def _key(src: str) -> str:
+    global _headers_digest
+    if _headers_digest is None:      # the kernel headers a process compiles against: read once
+        h = hashlib.sha256()
+        for f in ("mlp_core.h", "mlp_opt.h", "mlp_persist.h", "rx_common.h"):
+            with open(os.path.join(CSRC_HIP, f), "rb") as fh:
+                h.update(fh.read())
+        h.update(ARCH.encode())
+        _headers_digest = h.digest()
     h = hashlib.sha256(src.encode())
-    for f in ("mlp_core.h", "mlp_opt.h", "mlp_persist.h", "rx_common.h"):
-        with open(os.path.join(CSRC_HIP, f), "rb") as fh:
-            h.update(fh.read())
-    h.update(ARCH.encode())
+    h.update(_headers_digest)
     return h.hexdigest()[:24]
 
 
@@ -140,8 +148,17 @@ def compile_source(src: str) -> str:
     return path
 
 
+_paths = {}     # (descriptor bytes, MT) -> code-object path: a refit of the same model shape
+               # neither regenerates nor re-hashes the specialised source
+
+
 def compile_for(trainer) -> str:
-    return compile_source(generate_source(trainer.desc, trainer.mt))
+    k = (bytes(trainer.desc), int(trainer.mt))
+    path = _paths.get(k)
+    if path is None or not os.path.exists(path):
+        path = compile_source(generate_source(trainer.desc, trainer.mt))
+        _paths[k] = path
+    return path
 
 
 def load_specialized(trainer) -> Optional[str]:

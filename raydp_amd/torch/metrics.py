@@ -153,3 +153,13 @@ class TorchMetric:
     def zero_(self):
         for m in self._metrics.values():
             m.zero_()
+
+    def clone(self) -> "TorchMetric":
+        """A fresh collection of the same metrics (state reset) for one fit: built-in metrics
+        are rebuilt from their config (a deepcopy costs ~0.2 ms per fit), others deep-copied."""
+        import copy
+        out = TorchMetric()
+        for k, m in self._metrics.items():
+            out._metrics[k] = type(m)(**m.kwargs) if type(m).__name__ in _BUILTIN and type(m) is _BUILTIN[
+                type(m).__name__] else copy.deepcopy(m)
+        return out
