@@ -92,7 +92,11 @@ def main():
     for i in range(args.warmup):
         step(i)
     graph, graph_err = None, None
-    if args.graph and not mp:
+    # model parallel: capturable when the DDP buckets and the sharded tables' exchanges all ride
+    # the one-shot xGMI kernels (no torch.distributed call inside a step)
+    mp_capturable = mp and net.capturable() and all(
+        getattr(m, "_xg", None) is not None for m in model.modules() if hasattr(m, "_xg_plan"))
+    if args.graph and (not mp or mp_capturable):
         graph, graph_err = _capture_cycle(_graph_step(net, lossf, opt, dense, cats, y, args), opt, dev)
     barrier()
     t = time.perf_counter()
@@ -121,7 +125,8 @@ def main():
                           "amp": args.amp, "loss": float(loss),
                           "mlp": "eager torch" if args.eager_mlp else "fused MFMA towers (csrc/hip/linear_act.hip)",
                           "tables": 26, "rows_per_table": args.rows_per_table, "scaling": "weak",
-                          "hip_graph": graph is not None, "graph_error": graph_err}), flush=True)
+                          "hip_graph": graph is not None, "graph_error": graph_err,
+                          "mp_capturable": bool(mp_capturable)}), flush=True)
     if mp:
         dist.destroy_process_group()
 

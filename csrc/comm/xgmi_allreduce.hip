@@ -14,6 +14,8 @@
 //                                 its optimizer kernel instead (host-side sequence numbers)
 //   rx_xg_allgather            -> every rank's n words side by side (device-sequenced too):
 //                                 the replicated DLRM tables' sparse gradient rows and ids
+//   rx_xg_alltoallv            -> variable-split all-to-all (device-sequenced): the sharded
+//                                 DLRM tables' id and row exchanges
 //   rx_xg_vote                 -> epoch-end agreement for the fused loop: every rank's error word
 //                                 summed into a double the host reads with the epoch metrics
 //   rx_xg_error                -> nonzero once any wait timed out (a peer never arrived)
@@ -132,6 +134,60 @@ __global__ __launch_bounds__(kThreads) void xg_allgather_kernel(XgDev x, const f
       } else {
         dst[(size_t)p * n + i] = p == x.rank ? src[i]
                                              : __hip_atomic_load(from + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(x.ctl + kXgDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(x.ctl + kXgDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(x.ctl + kXgDevSeq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Variable-split all-to-all of raw 4-byte words (the sharded-embedding id and row exchanges,
+// raydp_amd/parallel/embedding_mp.py): every rank publishes its whole send buffer (src_words) in
+// its slot; after the rendezvous, rank r copies len[p] words starting at from_off[p] of rank p's
+// buffer into dst + dst_off[p]. Device-sequenced like the all-reduce (capturable); VEC: every
+// count / offset a multiple of 4 and src / dst 16-B aligned.
+struct XgA2A {
+  int src_words;
+  int from_off[RX_XG_MAXR];
+  int len[RX_XG_MAXR];
+  int dst_off[RX_XG_MAXR];
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(kThreads) void xg_alltoallv_kernel(XgDev x, const float* __restrict__ src,
+                                                                float* __restrict__ dst, XgA2A a) {
+  const unsigned seq = __hip_atomic_load(x.ctl + kXgDevSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int par = (int)(seq & 1u);
+  float* mine = x.region[x.rank] + (size_t)par * x.nf;
+  const int stride = gridDim.x * kThreads;
+  const int t = blockIdx.x * kThreads + threadIdx.x;
+  const int su = VEC ? a.src_words >> 2 : a.src_words;
+  for (int i = t; i < su; i += stride) {
+    if (VEC)
+      reinterpret_cast<float4*>(mine)[i] = reinterpret_cast<const float4*>(src)[i];
+    else
+      mine[i] = src[i];
+  }
+  if (!rx_xg_grid_rendezvous(x, seq, gridDim.x)) return;
+  for (int p = 0; p < x.world; ++p) {
+    const int units = VEC ? a.len[p] >> 2 : a.len[p];
+    const int fo = VEC ? a.from_off[p] >> 2 : a.from_off[p];
+    const int dof = VEC ? a.dst_off[p] >> 2 : a.dst_off[p];
+    const float* from = x.region[p] + (size_t)par * x.nf;
+    for (int i = t; i < units; i += stride) {
+      if (VEC) {
+        const float4 v = p == x.rank ? reinterpret_cast<const float4*>(src)[fo + i]
+                                     : rx_xg_load4(from, (size_t)(fo + i));
+        reinterpret_cast<float4*>(dst)[dof + i] = v;
+      } else {
+        dst[dof + i] = p == x.rank ? src[fo + i]
+                                   : __hip_atomic_load(from + fo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
@@ -301,6 +357,37 @@ int rx_xg_allgather(const float* src, float* dst, int n, void* ctx, hipStream_t 
   else
     hipLaunchKernelGGL(xg_allgather_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, src, dst,
                        n);
+  return (int)hipGetLastError();
+}
+
+int rx_xg_a2a_size() { return (int)sizeof(XgA2A); }
+
+// Variable-split all-to-all (device-sequenced communicators only). -2: a count outside the slot
+// or negative; -3: host-sequenced communicator.
+int rx_xg_alltoallv(const float* src, float* dst, const XgA2A* a, void* ctx, hipStream_t stream) {
+  XgHost* h = (XgHost*)ctx;
+  if (h->host_seq) return -3;
+  const int world = h->dev.world;
+  if (a->src_words < 0 || a->src_words > h->dev.nf) return -2;
+  long most = a->src_words;
+  unsigned bits = (unsigned)a->src_words | (unsigned)(reinterpret_cast<uintptr_t>(src) & 15u) |
+                  (unsigned)(reinterpret_cast<uintptr_t>(dst) & 15u);
+  for (int p = 0; p < world; ++p) {
+    if (a->len[p] < 0 || a->from_off[p] < 0 || a->dst_off[p] < 0 || (long)a->from_off[p] + a->len[p] > h->dev.nf)
+      return -2;
+    most = a->len[p] > most ? a->len[p] : most;
+    bits |= (unsigned)a->len[p] | (unsigned)a->from_off[p] | (unsigned)a->dst_off[p];
+  }
+  const bool vec = (bits & 3u) == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+  const long units = vec ? most >> 2 : most;
+  long blocks = (units + (long)kThreads * 4 - 1) / ((long)kThreads * 4);
+  if (blocks < 1) blocks = 1;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (vec)
+    hipLaunchKernelGGL(xg_alltoallv_kernel<true>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, src, dst, *a);
+  else
+    hipLaunchKernelGGL(xg_alltoallv_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, src, dst,
+                       *a);
   return (int)hipGetLastError();
 }
 

@@ -150,6 +150,27 @@ class XgmiComm:
                                       ctypes.c_void_p(self.ctx), _hip.stream_ptr(src.device))
         _hip.check(rc, "rx_xg_allgather")
 
+    def alltoallv_(self, src, dst, from_off, lens, dst_off) -> None:
+        """Variable-split all-to-all in 4-byte words (device-sequenced: capturable). This rank
+        publishes all of ``src``; it receives ``lens[p]`` words from rank ``p``, read at word
+        ``from_off[p]`` of that rank's ``src`` and written at word ``dst_off[p]`` of ``dst``.
+        Every rank must call it at the same point of its stream (like any collective)."""
+        if src.element_size() * src.numel() % 4 or not (src.is_contiguous() and dst.is_contiguous()):
+            raise ValueError("alltoallv_: contiguous tensors of whole 4-byte words")
+        words = src.numel() * src.element_size() // 4
+        if words > self.max_floats:
+            raise ValueError(f"xGMI all-to-all of {words} words > {self.max_floats}")
+        dwords = dst.numel() * dst.element_size() // 4
+        if len(lens) != self.world or any(o + n > dwords for o, n in zip(dst_off, lens)):
+            raise ValueError("alltoallv_: receive ranges outside dst")
+        if not getattr(XgmiComm, "_a2a_checked", False):
+            assert self.lib.rx_xg_a2a_size() == ctypes.sizeof(_XgA2A), "XgA2A layout mismatch"
+            XgmiComm._a2a_checked = True
+        a = _a2a_args(self.world, words, from_off, lens, dst_off)
+        rc = self.lib.rx_xg_alltoallv(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                                      ctypes.byref(a), ctypes.c_void_p(self.ctx), _hip.stream_ptr(src.device))
+        _hip.check(rc, "rx_xg_alltoallv")
+
     def vote(self, out) -> None:
         """Epoch-end agreement (host-sequenced communicators): ``out`` (a device float64
         element) becomes the sum of every rank's error word, > 0 when any rank -- or this
@@ -225,6 +246,20 @@ class XgmiComm:
 
 
 _XGMI_DISABLED = False
+
+
+class _XgA2A(ctypes.Structure):
+    """csrc/comm/xgmi_allreduce.hip XgA2A (RX_XG_MAXR = 16 ranks)."""
+    _fields_ = [("src_words", ctypes.c_int), ("from_off", ctypes.c_int * 16), ("len", ctypes.c_int * 16),
+                ("dst_off", ctypes.c_int * 16)]
+
+
+def _a2a_args(world, words, from_off, lens, dst_off) -> _XgA2A:
+    a = _XgA2A()
+    a.src_words = int(words)
+    for p in range(world):
+        a.from_off[p], a.len[p], a.dst_off[p] = int(from_off[p]), int(lens[p]), int(dst_off[p])
+    return a
 
 
 def forget_xgmi(comm, disable: bool = True) -> None:

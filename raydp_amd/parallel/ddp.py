@@ -112,6 +112,13 @@ class DistributedDataParallel(nn.Module):
             p.register_post_accumulate_grad_hook(self._sparse_hook)
         self._finalize_queued = False
         self.require_backward_grad_sync = True
+        # sharded embedding tables (raydp_amd.parallel.embedding_mp) set up their xGMI exchange
+        # here, at a point every rank reaches together, so capturable() can count on it
+        self._sharded = [m for m in module.modules() if hasattr(m, "_xg_plan")]
+        for m in self._sharded:
+            ps = list(m.parameters())
+            if ps:
+                m._xgmi(ps[0].device)
 
     # ------------------------------------------------------------------ wrap-time state
     def _replicated(self, t) -> bool:
@@ -237,6 +244,8 @@ class DistributedDataParallel(nn.Module):
         parameter has sparse gradients."""
         if self.sparse_params:
             return False
+        if any(m._xg is None for m in self._sharded):
+            return False        # a sharded table exchanges over torch.distributed
         if not all(self._allreduce.routes_to_xgmi(b.flat) for b in self.buckets):
             return False
         if self.broadcast_buffers and not all(self._allreduce.routes_to_xgmi(f) for f in self._buf_flats):

@@ -12,8 +12,11 @@ and one training step moves only the looked-up rows:
   backward  the embedding gradient rows travel back over the reverse all-to-all and become a
             sparse gradient of the owner's local table (SGD applies it without densifying).
 
-Collectives are ``torch.distributed.all_to_all_single`` (RCCL over xGMI on MI355X, gloo on
-CPU). The small id exchange and the owner gather run first; the row exchange back (16x the id
+Collectives: on GPUs whose ranks map each other's memory (one node, xGMI) the three exchanges are
+the one-shot xGMI all-to-all kernel (``XgmiComm.alltoallv_``, csrc/comm/xgmi_allreduce.hip):
+stream-ordered and device-sequenced, so a whole model-parallel step can be captured into a HIP
+graph; otherwise ``torch.distributed.all_to_all_single`` (RCCL, gloo on CPU). The small id
+exchange and the owner gather run first; the row exchange back (16x the id
 bytes at D = 32 fp32) is issued ``async_op`` and overlaps the bottom MLP (``start`` / ``finish``,
 ``Dlrm.forward``); with the fused embedding SGD the reverse gradient exchange overlaps the
 bottom MLP's backward (applied at the end of the backward pass). Batch sizes are exchanged only
@@ -47,7 +50,7 @@ class _Pending:
     """A lookup in flight (``ShardedEmbeddings.start``): the ids have been exchanged and the
     owners' rows gathered; the all-to-all returning the rows (the step's largest exchange,
     B x T x D values) runs asynchronously while the bottom MLP is computed."""
-    __slots__ = ("B", "T", "all_b", "in_splits", "out_splits", "recv", "work", "back")
+    __slots__ = ("B", "T", "all_b", "in_splits", "out_splits", "recv", "work", "back", "xg")
 
 
 class _ShardedLookup(torch.autograd.Function):
@@ -71,19 +74,37 @@ class _ShardedLookup(torch.autograd.Function):
             torch.empty(0, D, device=dev, dtype=weight.dtype)
         # 3) embeddings back to the requesting ranks, in flight while the bottom MLP runs
         back = torch.empty(sum(in_splits), D, dtype=weight.dtype, device=dev)
-        pend.work = dist.all_to_all_single(back, emb.contiguous(), output_split_sizes=list(in_splits),
-                                           input_split_sizes=list(out_splits), group=group, async_op=True)
+        if pend.xg is not None:
+            fo, ln, do = pend.xg["rows"]
+            mod._xg.alltoallv_(emb.contiguous(), back, fo, ln, do)
+            from raydp_amd.ops.comm import _Done
+            pend.work = _Done()
+        else:
+            pend.work = dist.all_to_all_single(back, emb.contiguous(), output_split_sizes=list(in_splits),
+                                               input_split_sizes=list(out_splits), group=group, async_op=True)
         ctx.save_for_backward(lidx, weight)
-        ctx.meta = (mod, B, T, D, in_splits, out_splits, weight.shape)
+        ctx.meta = (mod, B, T, D, in_splits, out_splits, weight.shape, pend.xg)
         return back
 
     @staticmethod
     def backward(ctx, g):
         lidx, weight = ctx.saved_tensors
-        mod, B, T, D, in_splits, out_splits, wshape = ctx.meta
+        mod, B, T, D, in_splits, out_splits, wshape, xg = ctx.meta
         send = g.contiguous()          # already rank-blocked: the reverse of the forward exchange
         recv = torch.empty(sum(out_splits), D, dtype=g.dtype, device=g.device)
         nl = len(mod.local_tables)
+        if xg is not None:
+            fo, ln, do = xg["grads"]
+            mod._xg.alltoallv_(send, recv, fo, ln, do)
+            if mod.fused_sgd_lr is not None:
+                if nl:
+                    from raydp_amd.ops.dlrm_ops import sgd_rows_
+                    sgd_rows_(weight, mod.local_offsets, lidx, recv.view(-1, nl, D), mod.fused_sgd_lr)
+                return None, None, None
+            if not nl:
+                return None, None, None
+            rows = (lidx + mod.local_offsets.view(1, -1)).reshape(-1)
+            return torch.sparse_coo_tensor(rows.unsqueeze(0), recv, wshape), None, None
         if mod.fused_sgd_lr is not None:
             # the reverse exchange runs while autograd continues with the bottom MLP's backward;
             # the rows are applied to the owner's tables at the end of the backward pass
@@ -133,6 +154,7 @@ class ShardedEmbeddings(nn.Module):
         self.register_buffer("local_offsets", torch.tensor(offs[:len(local_sizes)], dtype=torch.int64))
         self.weight = nn.Parameter(torch.empty(max(1, sum(local_sizes)), dim))
         self.weight._raydp_model_parallel = True   # owned by this rank only: DDP leaves it alone
+        self._xg, self._xg_tried, self._xg_plans = None, False, {}
         # with fused_sgd_lr the weight still requires grad (so backward runs the reverse
         # all-to-all) but its .grad stays None: optimizers skip it
         self._raydp_model_parallel = True          # ... and every buffer of this module (offsets)
@@ -160,6 +182,48 @@ class ShardedEmbeddings(nn.Module):
         self._last_b = B
         return self._all_b
 
+    def _xgmi(self, dev):
+        """The one-shot xGMI communicator of this group (shared with the DDP buckets), created
+        collectively on the first GPU lookup; None keeps torch.distributed."""
+        if not self._xg_tried:
+            self._xg_tried = True
+            if dev.type == "cuda" and self.world > 1:
+                from raydp_amd.ops.comm import XG_BUCKET_MAX_BYTES, XgmiComm
+                from raydp_amd.utils.config import get as conf_get
+                if conf_get("spark.ray.mi355x.allreduce") != "rccl":
+                    self._xg = XgmiComm.create(XG_BUCKET_MAX_BYTES // 4, group=self.group,
+                                               timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
+        return self._xg
+
+    def _xg_plan(self, all_b, D: int):
+        """Word offsets of the three exchanges for batch sizes ``all_b`` (rank order):
+        ids (int64, 2 words), rows back and row gradients (fp32, D words)."""
+        key = (tuple(all_b), D)
+        plan = self._xg_plans.get(key)
+        if plan is not None:
+            return plan
+        W, me = self.world, self.rank
+        nt = [len(self.tables_of[r]) for r in range(W)]
+        cum = [sum(nt[:r]) for r in range(W)]
+        nl = nt[me]
+        Bme = all_b[me]
+
+        def prefix(v):
+            return [sum(v[:p]) for p in range(len(v))]
+        # forward ids: rank p's send buffer is [q][B_p][nt[q]]; mine starts at B_p * cum[me]
+        ids_len = [all_b[p] * nl for p in range(W)]
+        ids = ([2 * all_b[p] * cum[me] for p in range(W)], [2 * n for n in ids_len], [2 * o for o in prefix(ids_len)])
+        # rows back: owner p's buffer is [q][B_q][nt[p]] rows; mine at sum_{q<me} B_q * nt[p]
+        rows_len = [Bme * nt[p] for p in range(W)]
+        rows = ([D * sum(all_b[q] for q in range(me)) * nt[p] for p in range(W)], [D * n for n in rows_len],
+                [D * o for o in prefix(rows_len)])
+        # gradients: rank q's buffer is [owner p][B_q][nt[p]] rows; mine (owner) at B_q * cum[me]
+        g_len = [all_b[q] * nl for q in range(W)]
+        grads = ([D * all_b[q] * cum[me] for q in range(W)], [D * n for n in g_len], [D * o for o in prefix(g_len)])
+        plan = {"ids": ids, "rows": rows, "grads": grads}
+        self._xg_plans[key] = plan
+        return plan
+
     def start(self, idx: torch.Tensor) -> _Pending:
         """Exchange the ids, gather the owned rows and put the row all-to-all in flight; the
         caller computes the bottom MLP next and ``finish`` completes the lookup."""
@@ -168,11 +232,23 @@ class ShardedEmbeddings(nn.Module):
         p = _Pending()
         p.B, p.T = B, T
         p.all_b = self._batch_sizes(B, idx.device)
-        send = torch.cat([idx[:, self.tables_of[r]].reshape(-1) for r in range(self.world)]) if T else idx.reshape(-1)
+        # [owner q][b][q's tables] through one cached device gather (capturable: no host index)
+        send = idx.reshape(-1).index_select(0, self._send_order(B, T, idx.device)) if T else idx.reshape(-1)
         p.in_splits = [B * len(self.tables_of[r]) for r in range(self.world)]
         p.out_splits = [p.all_b[r] * len(self.local_tables) for r in range(self.world)]
         p.recv = torch.empty(sum(p.out_splits), dtype=idx.dtype, device=idx.device)
-        _a2a(p.recv, send, p.out_splits, p.in_splits, self.group)     # ids (8 B per lookup)
+        p.xg = None
+        xg = self._xgmi(idx.device)
+        if xg is not None and T:
+            plan = self._xg_plan(p.all_b, self.dim)
+            most = max(2 * send.numel(), self.dim * max(sum(p.out_splits), sum(p.in_splits)))
+            if most <= xg.max_floats:
+                p.xg = plan
+        if p.xg is not None:
+            fo, ln, do = p.xg["ids"]
+            self._xg.alltoallv_(send.contiguous(), p.recv, fo, ln, do)     # ids (8 B per lookup)
+        else:
+            _a2a(p.recv, send, p.out_splits, p.in_splits, self.group)
         p.back = _ShardedLookup.apply(self.weight, p, self)             # rows: async
         return p
 
@@ -183,6 +259,19 @@ class ShardedEmbeddings(nn.Module):
         perm = self._row_order(B, T, mlp_out.device)
         emb = pend.back.index_select(0, perm).view(B, T, D) if T else pend.back.view(B, 0, D)
         return torch.cat([mlp_out.unsqueeze(1).to(emb.dtype), emb], dim=1)
+
+    def _send_order(self, B: int, T: int, dev) -> torch.Tensor:
+        """Flat index of the local [B, T] ids in send order: for every owner q, the batch's
+        ids of q's tables, row major."""
+        key = (B, T, str(dev))
+        cached = getattr(self, "_send_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        cols = [torch.tensor(self.tables_of[r], dtype=torch.long) for r in range(self.world)]
+        order = torch.cat([(torch.arange(B).view(B, 1) * T + c.view(1, -1)).reshape(-1) for c in cols])
+        order = order.to(dev)
+        self._send_cache = (key, order)
+        return order
 
     def _row_order(self, B: int, T: int, dev) -> torch.Tensor:
         """Index that maps the received rank-blocked rows ([rank][b][its tables]) to
