@@ -158,6 +158,11 @@ class _Pickler(cloudpickle.CloudPickler):
         self.store = _store()
 
     def reducer_override(self, obj):
+        t = _torch_tensor_type()
+        if t is not None and type(obj) is t:
+            red = _reduce_cpu_tensor(self, obj)
+            if red is not None:
+                return red
         if isinstance(obj, pa.Schema):
             # one IPC message instead of pyarrow's field-by-field reduction (plans cache their
             # output schema on every node: ~25 fields x 20 nodes per stage closure)
@@ -184,6 +189,57 @@ class _Pickler(cloudpickle.CloudPickler):
             self.oids.append(oid)
             return _load_shared, key
         return super().reducer_override(obj)
+
+
+def _torch_tensor_type():
+    """torch.Tensor when torch is already imported (never imports it)."""
+    m = sys.modules.get("torch")
+    return getattr(m, "Tensor", None) if m is not None else None
+
+
+class _StorageBox:
+    """One CPU storage's bytes in a pickle stream, pickled once however many tensors view it
+    (the pickler memoises the box): torch's own tensor pickling runs a whole ``torch.save``
+    per storage, ~60 us each -- a model + optimizer payload pays that per parameter."""
+    __slots__ = ("st",)
+
+    def __init__(self, st):
+        self.st = st
+
+    def __reduce__(self):
+        import numpy as np
+        n = self.st.nbytes()
+        import torch
+        raw = torch.empty(0, dtype=torch.uint8).set_(self.st, 0, (n,), (1,)).numpy() if n else np.zeros(0, np.uint8)
+        return _storage_from_bytes, (raw,)
+
+
+def _storage_from_bytes(raw):
+    import torch
+    return torch.from_numpy(raw.copy() if not raw.flags.writeable else raw).untyped_storage()
+
+
+def _reduce_cpu_tensor(pickler, obj):
+    if obj.device.type != "cpu" or obj.layout.__repr__() != "torch.strided" or obj.is_quantized or \
+            obj.is_conj() or obj.is_neg() or obj.requires_grad and obj.grad_fn is not None or \
+            obj._backward_hooks:
+        return None
+    st = obj.untyped_storage()
+    boxes = pickler.__dict__.setdefault("_storages", {})
+    key = (st.data_ptr(), st.nbytes())
+    box = boxes.get(key)
+    if box is None:
+        box = boxes[key] = _StorageBox(st)
+    return _tensor_from_storage, (box, str(obj.dtype).split(".")[-1], obj.storage_offset(), tuple(obj.size()),
+                                  tuple(obj.stride()), bool(obj.requires_grad))
+
+
+def _tensor_from_storage(st, dtype: str, offset: int, size, stride, requires_grad: bool):
+    import torch
+    t = torch.empty(0, dtype=getattr(torch, dtype)).set_(st, offset, size, stride)
+    if requires_grad:
+        t.requires_grad_(True)
+    return t
 
 
 def _schema_from_ipc(data: bytes) -> pa.Schema:

@@ -334,7 +334,13 @@ class DataParallelTrainer:
             # the loop, its config (model, optimizer, ...) and the resume point are the same for
             # every rank: pickled once, not once per worker (~2 ms each for the NYC model)
             with tracing.span("pickle fit payload", cat="train", world=world):
-                common = cloudpickle.dumps((self.fn, self.config, self.resume, storage))
+                from raydp_amd.runtime import serialization as S
+                try:
+                    # the runtime pickler: CPU tensors as raw storage bytes (not a torch.save
+                    # per storage), large Arrow tables by store reference
+                    common = S.dumps((self.fn, self.config, self.resume, storage), transfer=False)
+                except ValueError:
+                    common = cloudpickle.dumps((self.fn, self.config, self.resume, storage))
             for r, w in enumerate(workers):
                 shards = _shard(self.datasets, r, world)
                 refs.append(w.run.remote(common, cloudpickle.dumps(shards)))
