@@ -42,7 +42,7 @@ class RayDPExecutor:
         self._lock = threading.Lock()
         # native task loop (one worker per core) + the (rdd_id, partition) -> object id cache
         from raydp_amd.spark import native_exec
-        self._native = native_exec.NativeExecutor(max(1, int(cores)))
+        self._native = native_exec.make_executor(max(1, int(cores)))
         self.tasks_run = 0
         self.native_tasks = 0
         from raydp_amd.runtime import core
@@ -117,11 +117,10 @@ class RayDPExecutor:
                     self._fns.pop(self._fn_order.pop(0), None)
         return fn
 
-    @staticmethod
-    def _lower(fn):
+    def _lower(self, fn):
         """The stage's native form (``native_exec.lower``, cached on the stage's plan) or None."""
         from raydp_amd.spark import native_exec
-        if not native_exec.enabled():
+        if not native_exec.enabled() or not self._native.available:
             return None
         try:
             return native_exec.lower(fn)

@@ -304,7 +304,67 @@ _TAP = _TAPFN(_tap_impl)
 # ------------------------------------------------------------------------------------------
 # the per-process task loop + partition cache
 # ------------------------------------------------------------------------------------------
+def make_executor(threads: int):
+    """The native task loop + cache, or -- when the library cannot be loaded on this host (no
+    compiler, an Arrow C++ ABI that does not match the installed pyarrow) -- a Python cache
+    with the same interface whose ``available`` is False (every stage takes the Python path)."""
+    try:
+        return NativeExecutor(threads)
+    except Exception as e:  # noqa: BLE001
+        import logging
+        logging.getLogger(__name__).warning("native executor unavailable (%s); Python task path only", e)
+        return PyCache()
+
+
+class PyCache:
+    """Pure-Python stand-in for the partition cache of :class:`NativeExecutor`."""
+    available = False
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._c: Dict[Tuple[str, int], str] = {}
+
+    def stats(self):
+        return {"ok": 0, "fallback": 0, "error": 0, "rows": 0, "bytes": 0}
+
+    def cache_put(self, rdd, i, oid):
+        with self._lock:
+            old = self._c.get((rdd, int(i)))
+            self._c[(rdd, int(i))] = oid
+        return old
+
+    def cache_get(self, rdd, i):
+        with self._lock:
+            return self._c.get((rdd, int(i)))
+
+    def cache_pop(self, rdd, i):
+        with self._lock:
+            return self._c.pop((rdd, int(i)), None)
+
+    def cache_list(self, rdd):
+        with self._lock:
+            return sorted(i for (r, i) in self._c if r == rdd)
+
+    def cache_unpersist(self, rdd, store):
+        with self._lock:
+            keys = [k for k in self._c if rdd is None or k[0] == rdd]
+            oids = [self._c.pop(k) for k in keys]
+        if store is not None:
+            for o in oids:
+                store.delete(o)
+        return len(oids)
+
+    def cached_rdds(self):
+        with self._lock:
+            return sorted({r for r, _ in self._c})
+
+    def close(self):
+        pass
+
+
 class NativeExecutor:
+    available = True
+
     def __init__(self, threads: int):
         self._lib = _lib()
         self._h = self._lib.rx_exec_create(max(1, int(threads)))

@@ -216,3 +216,13 @@ def test_disabled_keeps_python_path(monkeypatch):
     monkeypatch.setenv("RAYDP_NATIVE_EXECUTOR", "0")
     assert not native_exec.enabled()
     assert exprc.TAPS_OK == native_exec.OK and exprc.TAPS_FALLBACK == native_exec.FALLBACK
+
+
+def test_python_cache_fallback_has_the_same_interface(store):
+    c = native_exec.PyCache()
+    oid = uuid.uuid4().hex
+    store.put(oid, pa.table({"x": [1]}))
+    assert c.cache_put("r", 0, oid) is None and c.cache_get("r", 0) == oid
+    assert c.cache_list("r") == [0] and c.cached_rdds() == ["r"]
+    assert c.cache_unpersist("r", store) == 1 and not store.contains(oid)
+    assert not c.available and native_exec.NativeExecutor.available
