@@ -156,6 +156,13 @@ def build_sanitized(kind: str, out_dir: str, names=("raydp_supervisor", "raydp_a
              [os.path.join(CSRC, "tests", "expr_vm_fuzz.cc"), os.path.join(CSRC, "exec", "expr", "expr_vm.cc"),
               "-o", p])
         out["expr_vm_fuzz"] = p
+        # the native executor core: task loop + partition cache + CSV reader, many threads
+        p = os.path.join(out_dir, "executor_stress")
+        _run([cxx, "-O1", "-g", "-std=c++20"] + flags + inc +
+             [os.path.join(CSRC, "tests", "executor_stress.cc"), os.path.join(CSRC, "exec", "executor.cc"),
+              os.path.join(CSRC, "exec", "csv_infer.cc"), os.path.join(CSRC, "exec", "expr", "expr_vm.cc"),
+              os.path.join(CSRC, "runtime", "objstore.cc"), "-o", p, "-lpthread", "-lrt"] + _arrow_flags())
+        out["executor_stress"] = p
     return out
 
 

@@ -12,4 +12,6 @@ python -m raydp_amd.native.build --sanitize tsan "$OUT/tsan"
 "$OUT/asan/runtime_stress" 4 3 3000
 "$OUT/tsan/runtime_stress" 4 1 2000
 "$OUT/asan/expr_vm_fuzz" 1000 1
+"$OUT/asan/executor_stress" 4 8 5000
+"$OUT/tsan/executor_stress" 4 40 5000 sync
 python -m pytest tests/test_sanitizers.py -q -p no:cacheprovider

@@ -104,3 +104,19 @@ def test_services_under_asan(monkeypatch):
     time.sleep(0.3)  # shuffle service is SIGTERMed by the master on shutdown
     _no_reports(os.path.join(work, "logs", "appmaster.err"))
     _no_reports(os.path.join(work, "logs", "supervisor.err"))
+
+
+@pytest.mark.parametrize("kind,mode", [("asan", "full"), ("tsan", "sync")])
+def test_native_executor_core_under_sanitizer(kind, mode):
+    """csrc/tests/executor_stress.cc: four driver threads submit CSV-split tasks of one stage to
+    the native task loop and wait on them while another thread reads the block cache and the
+    CSV inference reader. ASan+UBSan runs the whole data path; ThreadSanitizer runs the queue,
+    waits and cache alone (Arrow's uninstrumented thread pool and allocator only add noise)."""
+    exe = os.path.join(_built(kind), "executor_stress")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", TSAN_OPTIONS="halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    args = ["4", "5", "3000"] + (["sync"] if mode == "sync" else [])
+    r = subprocess.run([exe] + args, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert "failures 0" in r.stdout and "Sanitizer" not in r.stdout and "runtime error" not in r.stdout
