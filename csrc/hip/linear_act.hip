@@ -13,22 +13,30 @@
 // fp32 operands (the dense features, the dot-interaction output) are converted to bf16 while
 // they are staged into LDS (no cast kernels).
 //
-// Tiling: 64x64 output tile per 256-thread workgroup (4 waves as 2x2, 32x32 per wave = 2x2
-// MFMA tiles), 64-deep K stages double-buffered in LDS. Each operand tile is staged in its
-// memory orientation with 16-B row chunks; operands whose reduction index is the slow one in
-// memory are read with gfx950's transposing LDS read (ds_read_b64_tr_b16), so no layout needs a
-// transposed copy in HBM. Edges (any M, N, K, any leading dimension) are zero-filled on load
-// and masked on store.
+// Tiling: TM x TN output tile per 256-thread workgroup (4 waves as 2x2; each wave owns a
+// (TM/2) x (TN/2) block = (TM/32) x (TN/32) MFMA tiles), 64-deep K stages double-buffered in LDS.
+// Two tile shapes are built: 64x64 (narrow layers, ragged edges) and 128x128 (the wide tower
+// GEMMs: 4x the MFMAs per staged byte and per barrier -- a 64x64 tile moves 32 FLOP per L2 byte
+// and spends its K loop waiting on loads, profiles/r2_linear_gemm_kernel_times.txt), plus the
+// two mixed 128x64 / 64x128 shapes; rx_lin_plan picks the shape and split-K factor per GEMM.
+// Each operand tile is staged in its memory orientation with 16-B row chunks; operands whose
+// reduction index is the slow one in memory are read with gfx950's transposing LDS read
+// (ds_read_b64_tr_b16), so no layout needs a transposed copy in HBM. Edges (any M, N, K, any
+// leading dimension) are zero-filled on load and masked on store; a stage whose whole tile is
+// in bounds and 16-B aligned takes unchecked vector loads.
 #include "rx_common.h"
 
 #include <string.h>
 
-#define LIN_T 64    // output tile edge and K-stage depth
-#define LIN_S 80    // LDS image row stride in elements (160 B = 10 16-B units: ds_read_b128 fragment reads
+#define LIN_BK 64   // K-stage depth
+#define LIN_S 80    // ROW image row stride in elements (160 B = 10 16-B units: ds_read_b128 fragment reads
                     // conflict-free for gfx950's lane groups {0-3,12-15,20-27}, ... ; 144 B was 2-way)
+#define LIN_TMAX 128
 
 enum { LIN_ROW = 0, LIN_RED = 1 };
 enum { LIN_FWD = 0, LIN_DGRAD = 1, LIN_WGRAD = 2 };
+// tile shapes (LinArgs.tile): 0 = planned by rx_lin_plan
+enum { LIN_TILE_AUTO = 0, LIN_TILE_64x64 = 1, LIN_TILE_128x128 = 2, LIN_TILE_128x64 = 3, LIN_TILE_64x128 = 4 };
 
 struct LinOperand {
   const void* p;
@@ -53,94 +61,147 @@ struct LinArgs {
   float* dbias;  // WGRAD: [M] row sums of A (bias gradient)
   float beta;    // WGRAD: out = beta * out + acc (same for dbias)
   int splits;    // split-K factor (grid.z); > 1 needs ws + counters
-  float* ws;     // [tiles][splits][64*64 + 64] fp32 partial tiles (+ partial row sums)
+  float* ws;     // [tiles][splits][TM*TN + TM] fp32 partial tiles (+ partial row sums)
   unsigned* counters;  // [tiles], zero between calls (the last block of a tile resets it)
+  int tile;            // LIN_TILE_*
+  int pad_;
 };
 
 typedef short rx_v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) rx_v4s rx_lds_v4s;
 
-// Load the 8 consecutive elements (i, j .. j+7) of an operand as bf16 (zero outside [0, I) x [0, J)).
-template <int F32>
-__device__ __forceinline__ uint4 lin_load8(const LinOperand& o, long long i, long long j, long long I, long long J) {
-  uint4 r = make_uint4(0, 0, 0, 0);
-  if (i >= I || j >= J) return r;
-  if constexpr (F32) {
-    const float* p = reinterpret_cast<const float*>(o.p) + i * o.ld + j;
-    float v[8];
-    if (j + 8 <= J && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
-      const float4 x = *reinterpret_cast<const float4*>(p);
-      const float4 y = *reinterpret_cast<const float4*>(p + 4);
-      v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w, v[4] = y.x, v[5] = y.y, v[6] = y.z, v[7] = y.w;
+// LDS image of one operand tile of T rows: ROW -> [T][LIN_S] (row-major, k fastest);
+// RED -> [LIN_BK][T + 16] (k-major, rows fastest)
+template <int LAY, int T>
+struct LinImg {
+  static constexpr int stride = LAY == LIN_ROW ? LIN_S : T + 16;
+  static constexpr int elems = LAY == LIN_ROW ? T * LIN_S : LIN_BK * (T + 16);
+};
+
+// ---- operand staging: global -> registers -> LDS, branch-free ----
+// Every stage issues the same loads in the same order whatever the tile position: the loads of
+// stage k+2 stay in flight (counted vmcnt) while stage k is multiplied and stage k+1 is written
+// to LDS. Edges need no branches: each load goes through a buffer resource whose num_records
+// is the operand's extent, and a chunk outside [0, I) x [0, J) gets an offset past it, which the
+// hardware answers with zeros. (A data-dependent branch around a load makes hipcc wait for
+// vmcnt(0) -- the whole prefetch pipeline then drains every stage.)
+// Staging modes (host-selected per operand, LinArgs operand f32 / alignment):
+//   LIN_V16: bf16, 16-B aligned rows, J % 8 == 0   -> one 16-B load per 8-element chunk
+//   LIN_V32: fp32, same conditions                  -> two 16-B loads, converted at the LDS write
+//   LIN_G16 / LIN_G32: any leading dimension / edge -> eight 2- / 4-byte loads per chunk
+enum { LIN_V16 = 0, LIN_V32 = 1, LIN_G16 = 2, LIN_G32 = 3 };
+#define LIN_OOB 0x80000000u  // byte offset past every operand extent (extents are < 2^31 bytes)
+
+template <int MODE, int CH>
+struct LinStage;  // CH chunks of 8 elements per thread
+template <int CH>
+struct LinStage<LIN_V16, CH> { u32x4 v[CH]; };
+template <int CH>
+struct LinStage<LIN_V32, CH> { u32x4 v[2 * CH]; };
+template <int CH>
+struct LinStage<LIN_G16, CH> { u16 v[8 * CH]; };
+template <int CH>
+struct LinStage<LIN_G32, CH> { uint32_t v[8 * CH]; };
+
+// buffer resource over one operand: [I][ld] elements in memory, J valid along the fast index
+template <int MODE>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t lin_rsrc(const LinOperand& o, long long I, long long J) {
+  const long long esz = (MODE == LIN_V32 || MODE == LIN_G32) ? 4 : 2;
+  const long long ext = I > 0 && J > 0 ? ((I - 1) * o.ld + J) * esz : 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(o.p), 0, (int)ext, 0x00020000);
+}
+
+// The T/32 chunks a thread stages for one operand tile of T rows: tile rows r0..r0+T-1,
+// reduction k0..k0+63 (memory orientation: ROW -> (i, j) = (row, k); RED -> (i, j) = (k, row)).
+template <int MODE, int LAY, int T>
+__device__ __forceinline__ void lin_fetch(__amdgpu_buffer_rsrc_t rs, long long ld, long long r0, long long k0,
+                                          long long R, long long Kd, int tid, LinStage<MODE, T / 32>& st) {
+  constexpr int CPR = LAY == LIN_ROW ? LIN_BK / 8 : T / 8;  // chunks per memory row of the tile
+  const long long I = LAY == LIN_ROW ? R : Kd, J = LAY == LIN_ROW ? Kd : R;
+#pragma unroll
+  for (int t = 0; t < T / 32; ++t) {
+    const int c = tid + 256 * t;
+    const int ci = c / CPR, cj = (c % CPR) * 8;
+    const long long i = LAY == LIN_ROW ? r0 + ci : k0 + ci;
+    const long long j = LAY == LIN_ROW ? k0 + cj : r0 + cj;
+    const long long e0 = i * ld + j;  // element offset of the chunk
+    if constexpr (MODE == LIN_V16) {
+      const unsigned off = (i < I && j < J) ? (unsigned)(e0 * 2) : LIN_OOB;
+      st.v[t] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+    } else if constexpr (MODE == LIN_V32) {
+      const unsigned off = (i < I && j < J) ? (unsigned)(e0 * 4) : LIN_OOB;
+      st.v[2 * t] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+      st.v[2 * t + 1] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u), 0, 0);
     } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = j + e < J ? p[e] : 0.f;
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = i < I && j + e < J;
+        if constexpr (MODE == LIN_G16)
+          st.v[8 * t + e] = __builtin_amdgcn_raw_buffer_load_b16(rs, (int)(ok ? (unsigned)((e0 + e) * 2) : LIN_OOB), 0, 0);
+        else
+          st.v[8 * t + e] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(ok ? (unsigned)((e0 + e) * 4) : LIN_OOB), 0, 0);
+      }
     }
-    r.x = rx_f2bf2(v[0], v[1]);
-    r.y = rx_f2bf2(v[2], v[3]);
-    r.z = rx_f2bf2(v[4], v[5]);
-    r.w = rx_f2bf2(v[6], v[7]);
-  } else {
-    const u16* p = reinterpret_cast<const u16*>(o.p) + i * o.ld + j;
-    if (j + 8 <= J && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
-      r = *reinterpret_cast<const uint4*>(p);
-    } else {
-      u16 v[8];
+  }
+}
+
+// Write a staged tile into its LDS image as bf16 (fp32 operands converted here, after their
+// loads have landed -- converting at the load would make the stage wait for them).
+template <int MODE, int LAY, int T>
+__device__ __forceinline__ void lin_stash(u16* img, int tid, const LinStage<MODE, T / 32>& st) {
+  constexpr int CPR = LAY == LIN_ROW ? LIN_BK / 8 : T / 8;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = j + e < J ? p[e] : (u16)0;
+  for (int t = 0; t < T / 32; ++t) {
+    const int c = tid + 256 * t;
+    const int ci = c / CPR, cj = (c % CPR) * 8;
+    uint4 r;
+    if constexpr (MODE == LIN_V16) {
+      r = make_uint4(st.v[t][0], st.v[t][1], st.v[t][2], st.v[t][3]);
+    } else if constexpr (MODE == LIN_V32) {
+      const u32x4 x = st.v[2 * t], y = st.v[2 * t + 1];
+      r.x = rx_f2bf2(__uint_as_float(x[0]), __uint_as_float(x[1]));
+      r.y = rx_f2bf2(__uint_as_float(x[2]), __uint_as_float(x[3]));
+      r.z = rx_f2bf2(__uint_as_float(y[0]), __uint_as_float(y[1]));
+      r.w = rx_f2bf2(__uint_as_float(y[2]), __uint_as_float(y[3]));
+    } else if constexpr (MODE == LIN_G16) {
+      const u16* v = st.v + 8 * t;
       r.x = v[0] | ((uint32_t)v[1] << 16);
       r.y = v[2] | ((uint32_t)v[3] << 16);
       r.z = v[4] | ((uint32_t)v[5] << 16);
       r.w = v[6] | ((uint32_t)v[7] << 16);
+    } else {
+      const uint32_t* v = st.v + 8 * t;
+      r.x = rx_f2bf2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+      r.y = rx_f2bf2(__uint_as_float(v[2]), __uint_as_float(v[3]));
+      r.z = rx_f2bf2(__uint_as_float(v[4]), __uint_as_float(v[5]));
+      r.w = rx_f2bf2(__uint_as_float(v[6]), __uint_as_float(v[7]));
     }
-  }
-  return r;
-}
-
-// The two 16-B chunks a thread stages for one operand tile: tile rows r0.., reduction k0..
-// (memory orientation: ROW -> (i, j) = (row, k); RED -> (i, j) = (k, row)).
-template <int F32, int LAY>
-__device__ __forceinline__ void lin_fetch(const LinOperand& o, long long r0, long long k0, long long R, long long Kd,
-                                          int tid, uint4 (&v)[2]) {
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int c = tid + 256 * t;
-    const int i = c >> 3, jc = (c & 7) * 8;
-    if (LAY == LIN_ROW)
-      v[t] = lin_load8<F32>(o, r0 + i, k0 + jc, R, Kd);
-    else
-      v[t] = lin_load8<F32>(o, k0 + i, r0 + jc, Kd, R);
-  }
-}
-
-__device__ __forceinline__ void lin_stash(u16* img, int tid, const uint4 (&v)[2]) {
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int c = tid + 256 * t;
-    const int i = c >> 3, jc = (c & 7) * 8;
-    *reinterpret_cast<uint4*>(img + i * LIN_S + jc) = v[t];
+    *reinterpret_cast<uint4*>(img + ci * LinImg<LAY, T>::stride + cj) = r;
   }
 }
 
 // MFMA operand fragment for tile rows rb..rb+15, reduction ks..ks+31 (lane l: row rb + (l & 15),
 // k = ks + 8 (l >> 4) + e).
-__device__ __forceinline__ bf16x8 lin_frag(const u16* img, int lay, int rb, int ks, int lane) {
-  if (lay == LIN_ROW) {
-    const uint4 x = *reinterpret_cast<const uint4*>(img + (rb + (lane & 15)) * LIN_S + ks + 8 * (lane >> 4));
+template <int LAY, int T>
+__device__ __forceinline__ bf16x8 lin_frag(const u16* img, int rb, int ks, int lane) {
+  constexpr int S = LinImg<LAY, T>::stride;
+  if constexpr (LAY == LIN_ROW) {
+    const uint4 x = *reinterpret_cast<const uint4*>(img + (rb + (lane & 15)) * S + ks + 8 * (lane >> 4));
     return __builtin_bit_cast(bf16x8, x);
+  } else {
+    // [k][row] image: each 16-lane group h reads rows k = ks + 8h + {0..3} and {4..7}; lane 4q+p
+    // addresses row q, columns rb + 4p .. +3; lane i receives column rb + i
+    const int h = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const u16* a0 = img + (ks + 8 * h + q) * S + rb + 4 * p;
+    const u16* a1 = a0 + 4 * S;
+    const rx_v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (rx_lds_v4s*)((__attribute__((address_space(3))) char*)(uintptr_t)(a0)));
+    const rx_v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (rx_lds_v4s*)((__attribute__((address_space(3))) char*)(uintptr_t)(a1)));
+    typedef short rx_v8s __attribute__((ext_vector_type(8)));
+    const rx_v8s all = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, all);
   }
-  // [k][row] image: each 16-lane group h reads rows k = ks + 8h + {0..3} and {4..7}; lane 4q+p
-  // addresses row q, columns rb + 4p .. +3; lane i receives column rb + i
-  const int h = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const u16* a0 = img + (ks + 8 * h + q) * LIN_S + rb + 4 * p;
-  const u16* a1 = a0 + 4 * LIN_S;
-  const rx_v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (rx_lds_v4s*)((__attribute__((address_space(3))) char*)(uintptr_t)(a0)));
-  const rx_v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (rx_lds_v4s*)((__attribute__((address_space(3))) char*)(uintptr_t)(a1)));
-  typedef short rx_v8s __attribute__((ext_vector_type(8)));
-  const rx_v8s all = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, all);
 }
 
 __device__ __forceinline__ float lin_bsum(const bf16x8& f) {
@@ -153,75 +214,89 @@ __device__ __forceinline__ float lin_bsum(const bf16x8& f) {
 // LA / LB: the operands' memory orientations as template constants (FWD: ROW x ROW, DGRAD:
 // ROW x RED, WGRAD: RED x RED), so the fragment reads compile to straight-line ds_reads the
 // scheduler can batch ahead of the MFMAs instead of layout branches between them.
-template <int AF32, int BF32, int LA, int LB>
+template <int AM, int BM, int LA, int LB, int TM, int TN>
 __global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 lds[2][2][LIN_T * LIN_S];  // [buffer][A|B]
+  constexpr int FM = TM / 32, FN = TN / 32;  // MFMA tiles per wave along M / N
+  constexpr int IA = LinImg<LA, TM>::elems, IB = LinImg<LB, TN>::elems;
+  // ONE __shared__ array: [buffer][A image | B image]
+  __shared__ __attribute__((aligned(16))) u16 lds[2 * (IA + IB)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const long long m0 = (long long)blockIdx.x * LIN_T, n0 = (long long)blockIdx.y * LIN_T;
+  const long long m0 = (long long)blockIdx.x * TM, n0 = (long long)blockIdx.y * TN;
   // split-K: this block reduces K stages [k_begin, k_end)
-  const int nk_all = (a.K + LIN_T - 1) / LIN_T;
+  const int nk_all = (a.K + LIN_BK - 1) / LIN_BK;
   const int per = (nk_all + a.splits - 1) / a.splits;
   const int k_begin = blockIdx.z * per;
   const int k_end = min(nk_all, k_begin + per);
   const int nk = max(0, k_end - k_begin);
   const bool want_db = a.epi == LIN_WGRAD && a.dbias != nullptr && blockIdx.y == 0 && wn == 0;
 
-  f32x4 acc[2][2];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < FM; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float asum[2] = {0.f, 0.f};
+    for (int y = 0; y < FN; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float asum[FM];
+#pragma unroll
+  for (int x = 0; x < FM; ++x) asum[x] = 0.f;
 
+  const auto rsa = lin_rsrc<AM>(a.a, LA == LIN_ROW ? a.M : a.K, LA == LIN_ROW ? a.K : a.M);
+  const auto rsb = lin_rsrc<BM>(a.b, LB == LIN_ROW ? a.N : a.K, LB == LIN_ROW ? a.K : a.N);
   // Global -> register -> LDS pipeline two stages deep: while stage kt is multiplied out of LDS,
-  // stage kt+1 sits in one register set (loaded an iteration ago, stashed after the MFMAs) and
+  // stage kt+1 sits in one register set (loaded a stage ago, written to LDS after the MFMAs) and
   // stage kt+2's loads are in flight into the other set -- each load has two stages of MFMAs to
-  // arrive in. The loop is unrolled by two so the sets swap roles without register copies
-  // (a copy would wait for the loads it copies).
-  uint4 ra[2], rb[2], qa[2], qb[2];
-  auto fetch = [&](int kt, uint4 (&fa_)[2], uint4 (&fb_)[2]) {
-    lin_fetch<AF32, LA>(a.a, m0, (long long)(k_begin + kt) * LIN_T, a.M, a.K, tid, fa_);
-    lin_fetch<BF32, LB>(a.b, n0, (long long)(k_begin + kt) * LIN_T, a.N, a.K, tid, fb_);
+  // arrive in. The loop is unrolled by two so the sets swap roles without register copies.
+  // The prefetch index is clamped (the last stages re-load stage nk-1 into a set nobody
+  // reads) so every stage issues the same loads: no branch, counted waits.
+  LinStage<AM, TM / 32> ra, qa;
+  LinStage<BM, TN / 32> rb, qb;
+  auto fetch = [&](int kt, LinStage<AM, TM / 32>& fa_, LinStage<BM, TN / 32>& fb_) {
+    const long long k0 = (long long)(k_begin + kt) * LIN_BK;
+    lin_fetch<AM, LA, TM>(rsa, a.a.ld, m0, k0, a.M, a.K, tid, fa_);
+    lin_fetch<BM, LB, TN>(rsb, a.b.ld, n0, k0, a.N, a.K, tid, fb_);
   };
-  auto stage = [&](int kt, uint4 (&sa)[2], uint4 (&sb)[2], uint4 (&la)[2], uint4 (&lb)[2]) {
+  auto img_a = [&](int buf) { return lds + buf * (IA + IB); };
+  auto img_b = [&](int buf) { return lds + buf * (IA + IB) + IA; };
+  auto stage = [&](int kt, const LinStage<AM, TM / 32>& sa, const LinStage<BM, TN / 32>& sb,
+                   LinStage<AM, TM / 32>& la, LinStage<BM, TN / 32>& lb) {
     const int cur = kt & 1;
-    if (kt + 2 < nk) fetch(kt + 2, la, lb);
-    const u16* ia = lds[cur][0];
-    const u16* ib = lds[cur][1];
+    fetch(min(kt + 2, nk - 1), la, lb);
+    const u16* ia = img_a(cur);
+    const u16* ib = img_b(cur);
 #pragma unroll
-    for (int ks = 0; ks < LIN_T; ks += 32) {
-      bf16x8 fa[2], fb[2];
+    for (int ks = 0; ks < LIN_BK; ks += 32) {
+      bf16x8 fa[FM], fb[FN];
 #pragma unroll
-      for (int x = 0; x < 2; ++x) fa[x] = lin_frag(ia, LA, wm * 32 + 16 * x, ks, lane);
+      for (int x = 0; x < FM; ++x) fa[x] = lin_frag<LA, TM>(ia, wm * (TM / 2) + 16 * x, ks, lane);
 #pragma unroll
-      for (int y = 0; y < 2; ++y) fb[y] = lin_frag(ib, LB, wn * 32 + 16 * y, ks, lane);
+      for (int y = 0; y < FN; ++y) fb[y] = lin_frag<LB, TN>(ib, wn * (TN / 2) + 16 * y, ks, lane);
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int x = 0; x < FM; ++x)
 #pragma unroll
-        for (int y = 0; y < 2; ++y) acc[x][y] = rx_mfma16(fa[x], fb[y], acc[x][y]);
+        for (int y = 0; y < FN; ++y) acc[x][y] = rx_mfma16(fa[x], fb[y], acc[x][y]);
       if (want_db) {
 #pragma unroll
-        for (int x = 0; x < 2; ++x) asum[x] += lin_bsum(fa[x]);
+        for (int x = 0; x < FM; ++x) asum[x] += lin_bsum(fa[x]);
       }
     }
-    if (kt + 1 < nk) {
-      lin_stash(lds[cur ^ 1][0], tid, sa);
-      lin_stash(lds[cur ^ 1][1], tid, sb);
-    }
+    // stage kt+1 into the other buffer (after the last stage: a re-loaded copy nobody reads)
+    lin_stash<AM, LA, TM>(img_a(cur ^ 1), tid, sa);
+    lin_stash<BM, LB, TN>(img_b(cur ^ 1), tid, sb);
     __syncthreads();
   };
   if (nk > 0) {
     fetch(0, ra, rb);
-    lin_stash(lds[0][0], tid, ra);
-    lin_stash(lds[0][1], tid, rb);
-    if (nk > 1) fetch(1, ra, rb);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; kt += 2) {
-    stage(kt, ra, rb, qa, qb);                  // stash stage kt+1 from r*, load kt+2 into q*
-    if (kt + 1 < nk) stage(kt + 1, qa, qb, ra, rb);
+    lin_stash<AM, LA, TM>(img_a(0), tid, ra);
+    lin_stash<BM, LB, TN>(img_b(0), tid, rb);
+    fetch(min(1, nk - 1), ra, rb);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      stage(kt, ra, rb, qa, qb);      // write stage kt+1 from r*, load kt+2 into q*
+      stage(kt + 1, qa, qb, ra, rb);  // write stage kt+2 from q*, load kt+3 into r*
+    }
+    if (kt < nk) stage(kt, ra, rb, qa, qb);
   }
 
   if (a.splits > 1) {
@@ -232,28 +307,28 @@ __global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
     // barrier, ONE agent-scope counter add; the last block reads the payload with sc1 loads only
     // (they bypass its L1), so no release / acquire fence is needed.
     const int tile = blockIdx.x * gridDim.y + blockIdx.y;
-    const int TW = LIN_T * LIN_T + LIN_T;
+    const int TW = TM * TN + TM;
     float* mine = a.ws + ((long long)tile * a.splits + blockIdx.z) * TW;
-    const int slot = ((wave * 64 + lane) * 16) * 4;  // byte offset of this lane's 16 floats
+    const int slot = ((wave * 64 + lane) * (FM * FN * 4)) * 4;  // byte offset of this lane's floats
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < FM; ++x)
 #pragma unroll
-      for (int y = 0; y < 2; ++y)
-        rx_store16_sc1(mine, slot + 16 * (2 * x + y), __builtin_bit_cast(u32x4, acc[x][y]));
+      for (int y = 0; y < FN; ++y)
+        rx_store16_sc1(mine, slot + 16 * (FN * x + y), __builtin_bit_cast(u32x4, acc[x][y]));
     if (want_db) {
 #pragma unroll
-      for (int x = 0; x < 2; ++x) {
+      for (int x = 0; x < FM; ++x) {
         const float sx = rx_colsum16(asum[x]);
         if (lane < 16)
-          __hip_atomic_store(mine + LIN_T * LIN_T + wm * 32 + 16 * x + lane, sx, __ATOMIC_RELAXED,
+          __hip_atomic_store(mine + TM * TN + wm * (TM / 2) + 16 * x + lane, sx, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
-    // the flag lives in the (now idle) operand images: a separate __shared__ word would push the
-    // block past 40 KiB of LDS and cost a fourth resident workgroup per CU
-    unsigned* last_flag = reinterpret_cast<unsigned*>(&lds[0][0][0]);
+    // the flag lives in the (now idle) operand images: a separate __shared__ word would add a
+    // second LDS object (and push the 64x64 block past 40 KiB: one resident workgroup less per CU)
+    unsigned* last_flag = reinterpret_cast<unsigned*>(&lds[0]);
     if (tid == 0) {
       const unsigned done = __hip_atomic_fetch_add(a.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *last_flag = done + 1 == (unsigned)a.splits;
@@ -262,72 +337,178 @@ __global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
     if (!*last_flag) return;
     const float* base = a.ws + (long long)tile * a.splits * TW;
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < FM; ++x)
 #pragma unroll
-      for (int y = 0; y < 2; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float dsum[2] = {0.f, 0.f};
+      for (int y = 0; y < FN; ++y) acc[x][y] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float dsum[FM];
+#pragma unroll
+    for (int x = 0; x < FM; ++x) dsum[x] = 0.f;
     for (int sp = 0; sp < a.splits; ++sp) {
       const float* ps = base + (long long)sp * TW;
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int x = 0; x < FM; ++x)
 #pragma unroll
-        for (int y = 0; y < 2; ++y)
-          acc[x][y] += __builtin_bit_cast(f32x4, rx_load16_sc1(ps, slot + 16 * (2 * x + y)));
+        for (int y = 0; y < FN; ++y)
+          acc[x][y] += __builtin_bit_cast(f32x4, rx_load16_sc1(ps, slot + 16 * (FN * x + y)));
       if (want_db && lane < 16) {
 #pragma unroll
-        for (int x = 0; x < 2; ++x)
-          dsum[x] += __hip_atomic_load(ps + LIN_T * LIN_T + wm * 32 + 16 * x + lane, __ATOMIC_RELAXED,
+        for (int x = 0; x < FM; ++x)
+          dsum[x] += __hip_atomic_load(ps + TM * TN + wm * (TM / 2) + 16 * x + lane, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     if (tid == 0) __hip_atomic_store(a.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (want_db) {
 #pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        const long long m = m0 + wm * 32 + 16 * x + (lane & 15);
+      for (int x = 0; x < FM; ++x) {
+        const long long m = m0 + wm * (TM / 2) + 16 * x + (lane & 15);
         if (lane < 16 && m < a.M) a.dbias[m] = a.beta != 0.f ? a.beta * a.dbias[m] + dsum[x] : dsum[x];
       }
     }
   }
 
-  // epilogue: lane holds rows rb + 4 (lane >> 4) + r (r = 0..3), column cb + (lane & 15)
+  // Epilogue: lane holds rows rb + 4 (lane >> 4) + r (r = 0..3) of column cb + (lane & 15).
+  // Branch-free like the staging: every access goes through a buffer resource sized to its
+  // tensor (a null optional tensor gets num_records 0), out-of-range elements get an offset past
+  // it (loads answer 0, stores are dropped), all loads of the tile are issued before the first
+  // use, and index math is 32-bit (the host bounds every extent below 2^31 bytes).
+  const unsigned M = (unsigned)a.M, N = (unsigned)a.N;
+  const unsigned mb0 = (unsigned)m0 + wm * (TM / 2) + 4 * (lane >> 4), nb0 = (unsigned)n0 + wn * (TN / 2) + (lane & 15);
+  // element index (row offset + column) of every accumulator element, or ~0u when out of range
+  auto elem_idx = [&](unsigned ld, unsigned (&idx)[FM][FN][4]) {
 #pragma unroll
-  for (int x = 0; x < 2; ++x) {
-#pragma unroll
-    for (int y = 0; y < 2; ++y) {
-      const long long n = n0 + wn * 32 + 16 * y + (lane & 15);
-      if (n >= a.N) continue;
+    for (int x = 0; x < FM; ++x)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const long long m = m0 + wm * 32 + 16 * x + 4 * (lane >> 4) + r;
-        if (m >= a.M) continue;
-        float v = acc[x][y][r];
-        if (a.epi == LIN_FWD) {
-          if (a.bias != nullptr) v += a.bias[n];
-          if (a.relu) v = fmaxf(v, 0.f);
-          if (a.out_f32)
-            reinterpret_cast<float*>(a.out)[m * a.ldo + n] = v;
-          else
-            reinterpret_cast<u16*>(a.out)[m * a.ldo + n] = rx_f2bf(v);
-          if (a.out2 != nullptr) a.out2[m * a.ldo2 + n] = v;
-        } else if (a.epi == LIN_DGRAD) {
-          if (a.mask != nullptr && !(rx_bf2f(a.mask[m * a.ldm + n]) > 0.f)) v = 0.f;
-          if (a.out_f32)
-            reinterpret_cast<float*>(a.out)[m * a.ldo + n] = v;
-          else
-            reinterpret_cast<u16*>(a.out)[m * a.ldo + n] = rx_f2bf(v);
-        } else {
-          float* o = reinterpret_cast<float*>(a.out) + m * a.ldo + n;
-          *o = a.beta != 0.f ? a.beta * *o + v : v;
+        const unsigned m = mb0 + 16 * x + r;
+        const unsigned ro = m * ld;
+#pragma unroll
+        for (int y = 0; y < FN; ++y) {
+          const unsigned n = nb0 + 16 * y;
+          idx[x][y][r] = ((m < M) & (n < N)) ? ro + n : ~0u;
         }
       }
+  };
+  auto boff = [](unsigned i, unsigned esz) -> int { return (int)(i != ~0u ? i * esz : LIN_OOB); };
+  auto rsrc_of = [&](const void* p, long long ld, long long esz) {
+    const long long ext = p != nullptr ? ((long long)(a.M - 1) * ld + a.N) * esz : 0;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)ext, 0x00020000);
+  };
+  unsigned idx[FM][FN][4];
+  elem_idx((unsigned)a.ldo, idx);
+  if (a.epi == LIN_FWD) {
+    const auto rbias = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.bias), 0,
+                                                         a.bias != nullptr ? a.N * 4 : 0, 0x00020000);
+    float bv[FN];
+#pragma unroll
+    for (int y = 0; y < FN; ++y) {
+      const unsigned n = nb0 + 16 * y;
+      bv[y] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rbias, (int)(n < N ? n * 4 : LIN_OOB), 0, 0));
     }
+    const float lo = a.relu ? 0.f : -INFINITY;
+#pragma unroll
+    for (int x = 0; x < FM; ++x)
+#pragma unroll
+      for (int y = 0; y < FN; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[x][y][r] = fmaxf(acc[x][y][r] + bv[y], lo);
+    const auto ro = rsrc_of(a.out, a.ldo, a.out_f32 ? 4 : 2);
+    if (a.out_f32) {
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[x][y][r]), ro, boff(idx[x][y][r], 4), 0, 0);
+    } else {
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            __builtin_amdgcn_raw_buffer_store_b16(rx_f2bf(acc[x][y][r]), ro, boff(idx[x][y][r], 2), 0, 0);
+    }
+    if (a.out2 != nullptr) {
+      const auto ro2 = rsrc_of(a.out2, a.ldo2, 4);
+      elem_idx((unsigned)a.ldo2, idx);
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[x][y][r]), ro2, boff(idx[x][y][r], 4), 0, 0);
+    }
+  } else if (a.epi == LIN_DGRAD) {
+    if (a.mask != nullptr) {
+      const auto rm = rsrc_of(a.mask, a.ldm, 2);
+      unsigned mi[FM][FN][4];
+      elem_idx((unsigned)a.ldm, mi);
+      u16 mk[FM][FN][4];
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mk[x][y][r] = __builtin_amdgcn_raw_buffer_load_b16(rm, boff(mi[x][y][r], 2), 0, 0);
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[x][y][r] = rx_bf2f(mk[x][y][r]) > 0.f ? acc[x][y][r] : 0.f;
+    }
+    const auto ro = rsrc_of(a.out, a.ldo, a.out_f32 ? 4 : 2);
+    if (a.out_f32) {
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[x][y][r]), ro, boff(idx[x][y][r], 4), 0, 0);
+    } else {
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            __builtin_amdgcn_raw_buffer_store_b16(rx_f2bf(acc[x][y][r]), ro, boff(idx[x][y][r], 2), 0, 0);
+    }
+  } else {
+    const auto ro = rsrc_of(a.out, a.ldo, 4);
+    if (a.beta != 0.f) {
+      float old[FM][FN][4];
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            old[x][y][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ro, boff(idx[x][y][r], 4), 0, 0));
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[x][y][r] += a.beta * old[x][y][r];
+    }
+#pragma unroll
+    for (int x = 0; x < FM; ++x)
+#pragma unroll
+      for (int y = 0; y < FN; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[x][y][r]), ro, boff(idx[x][y][r], 4), 0, 0);
   }
   if (want_db && a.splits <= 1) {
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
+    for (int x = 0; x < FM; ++x) {
       const float s = rx_colsum16(asum[x]);  // the 4 lanes of row (lane & 15) hold k-quarters
-      const long long m = m0 + wm * 32 + 16 * x + (lane & 15);
+      const long long m = m0 + wm * (TM / 2) + 16 * x + (lane & 15);
       if (lane < 16 && m < a.M) a.dbias[m] = a.beta != 0.f ? a.beta * a.dbias[m] + s : s;
     }
   }
@@ -371,51 +552,141 @@ extern "C" {
 int rx_lin_args_size() { return (int)sizeof(LinArgs); }
 int rx_lin_refresh_size() { return (int)sizeof(LinRefresh); }
 
-// Split-K factor for a problem: about two workgroups per CU, each split at least four 64-deep
-// stages. Measured per DLRM tower GEMM (profiles/r2_linear_gemm_kernel_times.txt): the
-// split-K fix-up costs more than it hides once a problem has ~one tile per CU (the wide
-// forward / dgrad GEMMs run fastest unsplit), while the weight-gradient GEMMs (few output tiles,
-// K = batch) gain 2-3x from 2-8 splits.
-int rx_lin_splits(int M, int N, int K, int cus) {
-  const long long tiles = (long long)((M + LIN_T - 1) / LIN_T) * ((N + LIN_T - 1) / LIN_T);
-  const int nk = (K + LIN_T - 1) / LIN_T;
-  long long want = (2LL * cus + tiles - 1) / tiles;
-  long long mx = nk / 4;
+static void lin_tile_dims(int tile, int* tm, int* tn) {
+  *tm = (tile == LIN_TILE_128x128 || tile == LIN_TILE_128x64) ? 128 : 64;
+  *tn = (tile == LIN_TILE_128x128 || tile == LIN_TILE_64x128) ? 128 : 64;
+}
+
+static long long lin_tiles(int M, int N, int tile) {
+  int tm, tn;
+  lin_tile_dims(tile, &tm, &tn);
+  return (long long)((M + tm - 1) / tm) * ((N + tn - 1) / tn);
+}
+
+// Tile shape and split-K factor for one GEMM, fitted to a measured sweep of every shape x
+// split factor at the DLRM tower GEMMs (benchmarks/linear_gemm_bench.py --sweep,
+// profiles/r3_linear_gemm_sweep.txt):
+// * 64x64 tiles everywhere: at batch 2048 the 128-wide tiles leave half the CUs idle (128
+//   workgroups for a 2048x1024 output) and their one wave per SIMD exposes every LDS and barrier
+//   latency; splitting K to fill the chip costs more in the fix-up than it wins.
+// * split-K only for problems with few output tiles (the weight gradients, K = batch): about
+//   192 workgroups, each split at least eight 64-deep stages (s1 -> s4 is 17 -> 10.5 us at
+//   2 tiles; at 512 tiles any split doubles the time).
+// tile_force != 0 fixes the shape (sweeps / tests); the cus argument scales the target.
+int rx_lin_plan(int M, int N, int K, int cus, int tile_force, int* tile_out) {
+  const int tile = tile_force != LIN_TILE_AUTO ? tile_force : LIN_TILE_64x64;
+  if (tile_out) *tile_out = tile;
+  const long long tiles = lin_tiles(M, N, tile);
+  const int nk = (K + LIN_BK - 1) / LIN_BK;
+  const long long target = (3LL * (cus > 0 ? cus : 256)) / 4;  // 192 on MI355X
+  long long want = (target + tiles - 1) / tiles;
+  long long mx = nk / 8;
   if (want > mx) want = mx;
   if (want > 64) want = 64;
   return want < 1 ? 1 : (int)want;
 }
 
-int rx_lin_ws_floats(int M, int N, int splits) {
-  const long long tiles = (long long)((M + LIN_T - 1) / LIN_T) * ((N + LIN_T - 1) / LIN_T);
-  return splits > 1 ? (int)(tiles * splits * (LIN_T * LIN_T + LIN_T)) : 0;
+int rx_lin_splits(int M, int N, int K, int cus) { return rx_lin_plan(M, N, K, cus, LIN_TILE_AUTO, nullptr); }
+
+int rx_lin_tile(int M, int N, int K, int cus) {
+  int t = 0;
+  rx_lin_plan(M, N, K, cus, LIN_TILE_AUTO, &t);
+  return t;
 }
 
+// Split-K workspace for `splits` splits under ANY tile shape.
+int rx_lin_ws_floats(int M, int N, int splits) {
+  if (splits <= 1) return 0;
+  long long need = 0;
+  for (int t = LIN_TILE_64x64; t <= LIN_TILE_64x128; ++t) {
+    int tm, tn;
+    lin_tile_dims(t, &tm, &tn);
+    const long long f = lin_tiles(M, N, t) * splits * (tm * tn + tm);
+    need = f > need ? f : need;
+  }
+  return (int)need;
+}
+
+}  // extern "C"
+
+template <int AM, int BM, int TM, int TN>
+static void lin_launch_lay(const LinArgs* a, dim3 grid, hipStream_t stream) {
+  if (a->a.lay == LIN_ROW && a->b.lay == LIN_ROW)
+    hipLaunchKernelGGL((lin_gemm_kernel<AM, BM, LIN_ROW, LIN_ROW, TM, TN>), grid, dim3(256), 0, stream, *a);
+  else if (a->a.lay == LIN_ROW)
+    hipLaunchKernelGGL((lin_gemm_kernel<AM, BM, LIN_ROW, LIN_RED, TM, TN>), grid, dim3(256), 0, stream, *a);
+  else if (a->b.lay == LIN_ROW)
+    hipLaunchKernelGGL((lin_gemm_kernel<AM, BM, LIN_RED, LIN_ROW, TM, TN>), grid, dim3(256), 0, stream, *a);
+  else
+    hipLaunchKernelGGL((lin_gemm_kernel<AM, BM, LIN_RED, LIN_RED, TM, TN>), grid, dim3(256), 0, stream, *a);
+}
+
+// Staging mode of one operand: vector loads when every row starts 16-B aligned and the fast
+// index's extent is a multiple of 8 (so no 8-element chunk straddles the edge).
+static int lin_mode(const LinOperand& o, long long J) {
+  const int esz = o.f32 ? 4 : 2;
+  const bool vec = ((uintptr_t)o.p & 15) == 0 && (o.ld * esz) % 16 == 0 && J % 8 == 0;
+  return (vec ? 0 : 2) + (o.f32 ? 1 : 0);
+}
+
+// the wider tiles are built for the vector modes only (the generic modes serve the narrow,
+// unaligned layers, e.g. the 13 dense features)
+template <int TM, int TN>
+static void lin_launch_vec(const LinArgs* a, int ma, int mb, hipStream_t stream) {
+  const dim3 grid((unsigned)((a->M + TM - 1) / TM), (unsigned)((a->N + TN - 1) / TN), (unsigned)a->splits);
+  if (ma == LIN_V16 && mb == LIN_V16)
+    lin_launch_lay<LIN_V16, LIN_V16, TM, TN>(a, grid, stream);
+  else if (ma == LIN_V16)
+    lin_launch_lay<LIN_V16, LIN_V32, TM, TN>(a, grid, stream);
+  else if (mb == LIN_V16)
+    lin_launch_lay<LIN_V32, LIN_V16, TM, TN>(a, grid, stream);
+  else
+    lin_launch_lay<LIN_V32, LIN_V32, TM, TN>(a, grid, stream);
+}
+
+template <int AM>
+static void lin_launch_64_b(const LinArgs* a, int mb, dim3 grid, hipStream_t stream) {
+  switch (mb) {
+    case LIN_V16: lin_launch_lay<AM, LIN_V16, 64, 64>(a, grid, stream); break;
+    case LIN_V32: lin_launch_lay<AM, LIN_V32, 64, 64>(a, grid, stream); break;
+    case LIN_G16: lin_launch_lay<AM, LIN_G16, 64, 64>(a, grid, stream); break;
+    default: lin_launch_lay<AM, LIN_G32, 64, 64>(a, grid, stream); break;
+  }
+}
+
+static void lin_launch_64(const LinArgs* a, int ma, int mb, hipStream_t stream) {
+  const dim3 grid((unsigned)((a->M + 63) / 64), (unsigned)((a->N + 63) / 64), (unsigned)a->splits);
+  switch (ma) {
+    case LIN_V16: lin_launch_64_b<LIN_V16>(a, mb, grid, stream); break;
+    case LIN_V32: lin_launch_64_b<LIN_V32>(a, mb, grid, stream); break;
+    case LIN_G16: lin_launch_64_b<LIN_G16>(a, mb, grid, stream); break;
+    default: lin_launch_64_b<LIN_G32>(a, mb, grid, stream); break;
+  }
+}
+
+extern "C" {
+
+// a->tile == LIN_TILE_AUTO: the shape rx_lin_plan picks (for the same M, N, K); a->splits is
+// used as given. Operands that need the generic (element-wise) staging run on 64x64 tiles.
 int rx_lin_gemm(const LinArgs* a, hipStream_t stream) {
   if (a->M <= 0 || a->N <= 0) return 0;
-  if (a->K < 0 || a->epi < 0 || a->epi > 2 || a->splits < 1) return -1;
+  if (a->K < 0 || a->epi < 0 || a->epi > 2 || a->splits < 1 || a->tile < 0 || a->tile > LIN_TILE_64x128) return -1;
   if (a->splits > 1 && (a->ws == nullptr || a->counters == nullptr)) return -1;
-  const dim3 grid((unsigned)((a->M + LIN_T - 1) / LIN_T), (unsigned)((a->N + LIN_T - 1) / LIN_T),
-                  (unsigned)a->splits);
-#define RX_LIN_LAY(AF, BF)                                                                          \
-  if (a->a.lay == LIN_ROW && a->b.lay == LIN_ROW)                                                  \
-    hipLaunchKernelGGL((lin_gemm_kernel<AF, BF, LIN_ROW, LIN_ROW>), grid, dim3(256), 0, stream, *a); \
-  else if (a->a.lay == LIN_ROW)                                                                    \
-    hipLaunchKernelGGL((lin_gemm_kernel<AF, BF, LIN_ROW, LIN_RED>), grid, dim3(256), 0, stream, *a); \
-  else if (a->b.lay == LIN_ROW)                                                                    \
-    hipLaunchKernelGGL((lin_gemm_kernel<AF, BF, LIN_RED, LIN_ROW>), grid, dim3(256), 0, stream, *a); \
-  else                                                                                             \
-    hipLaunchKernelGGL((lin_gemm_kernel<AF, BF, LIN_RED, LIN_RED>), grid, dim3(256), 0, stream, *a);
-  if (a->a.f32 && a->b.f32) {
-    RX_LIN_LAY(1, 1)
-  } else if (a->a.f32) {
-    RX_LIN_LAY(1, 0)
-  } else if (a->b.f32) {
-    RX_LIN_LAY(0, 1)
-  } else {
-    RX_LIN_LAY(0, 0)
+  // buffer-resource extents are 31-bit byte counts
+  const long long ea = (long long)(a->a.lay == LIN_ROW ? a->M : a->K) * a->a.ld * (a->a.f32 ? 4 : 2);
+  const long long eb = (long long)(a->b.lay == LIN_ROW ? a->N : a->K) * a->b.ld * (a->b.f32 ? 4 : 2);
+  if (ea >= (1LL << 31) || eb >= (1LL << 31)) return -2;
+  int tile = a->tile;
+  if (tile == LIN_TILE_AUTO) rx_lin_plan(a->M, a->N, a->K, 256, LIN_TILE_AUTO, &tile);
+  const int ma = lin_mode(a->a, a->a.lay == LIN_ROW ? a->K : a->M);
+  const int mb = lin_mode(a->b, a->b.lay == LIN_ROW ? a->K : a->N);
+  if (ma >= LIN_G16 || mb >= LIN_G16) tile = LIN_TILE_64x64;
+  switch (tile) {
+    case LIN_TILE_128x128: lin_launch_vec<128, 128>(a, ma, mb, stream); break;
+    case LIN_TILE_128x64: lin_launch_vec<128, 64>(a, ma, mb, stream); break;
+    case LIN_TILE_64x128: lin_launch_vec<64, 128>(a, ma, mb, stream); break;
+    default: lin_launch_64(a, ma, mb, stream); break;
   }
-#undef RX_LIN_LAY
   return (int)hipGetLastError();
 }
 
@@ -443,9 +714,11 @@ struct LinScratch {
 int rx_lin_mask_cast(const float* g, const u16* y, u16* out, long long n, hipStream_t stream);
 
 static int lin_run(LinArgs& a, const LinScratch& sc, hipStream_t stream) {
-  a.splits = rx_lin_splits(a.M, a.N, a.K, sc.cus);
-  const long long tiles = (long long)((a.M + LIN_T - 1) / LIN_T) * ((a.N + LIN_T - 1) / LIN_T);
-  if (a.splits > 1 && ((long long)rx_lin_ws_floats(a.M, a.N, a.splits) > sc.ws_floats || tiles > sc.counters_len))
+  int tile = LIN_TILE_AUTO;
+  a.splits = rx_lin_plan(a.M, a.N, a.K, sc.cus, LIN_TILE_AUTO, &tile);
+  a.tile = tile;
+  if (a.splits > 1 && ((long long)rx_lin_ws_floats(a.M, a.N, a.splits) > sc.ws_floats ||
+                       lin_tiles(a.M, a.N, tile) > sc.counters_len))
     a.splits = 1;  // scratch too small for this shape: run unsplit
   a.ws = a.splits > 1 ? sc.ws : nullptr;
   a.counters = a.splits > 1 ? sc.counters : nullptr;

@@ -114,14 +114,23 @@ def build_one(name: str, force: bool = False) -> str:
         _run(cmd)
     else:
         hipcc = os.path.join(ROCM, "bin", "hipcc")
-        objs = []
-        with tempfile.TemporaryDirectory() as td:
-            for s in srcs:
-                o = os.path.join(td, os.path.basename(s) + ".o")
-                _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                      "-munsafe-fp-atomics", "-c", s, "-o", o] + inc)
-                objs.append(o)
-            _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", tmp, "-ldl"])
+        # one object per source, kept between builds (a source is recompiled when it or any
+        # header is newer than its object) and compiled in parallel
+        od = os.path.join(os.path.dirname(CSRC), "build", "hipobj")
+        os.makedirs(od, exist_ok=True)
+        objs = [os.path.join(od, os.path.basename(s) + ".o") for s in srcs]
+        todo = [(s, o) for s, o in zip(srcs, objs) if force or not _newer(o, [s])]
+        from concurrent.futures import ThreadPoolExecutor
+        jobs = max(1, min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+        def compile_one(so):
+            src, obj = so
+            _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
+                  "-c", src, "-o", obj + ".tmp"] + inc)
+            os.replace(obj + ".tmp", obj)
+
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(compile_one, todo))
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", tmp, "-ldl"])
     os.replace(tmp, out)
     return out
 

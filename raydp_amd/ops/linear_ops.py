@@ -38,8 +38,12 @@ class LinArgs(ctypes.Structure):
         ("out2", ctypes.c_void_p), ("ldo2", ctypes.c_longlong),
         ("mask", ctypes.c_void_p), ("ldm", ctypes.c_longlong),
         ("dbias", ctypes.c_void_p), ("beta", ctypes.c_float), ("splits", ctypes.c_int),
-        ("ws", ctypes.c_void_p), ("counters", ctypes.c_void_p),
+        ("ws", ctypes.c_void_p), ("counters", ctypes.c_void_p), ("tile", ctypes.c_int), ("pad_", ctypes.c_int),
     ]
+
+
+# LinArgs.tile (csrc/hip/linear_act.hip LIN_TILE_*): 0 = the shape rx_lin_plan picks
+TILE_AUTO, TILE_64x64, TILE_128x128, TILE_128x64, TILE_64x128 = 0, 1, 2, 3, 4
 
 
 class LinRefresh(ctypes.Structure):
@@ -61,6 +65,8 @@ def _lib():
         L.rx_lin_splits.argtypes = [ctypes.c_int] * 4
         L.rx_lin_ws_floats.argtypes = [ctypes.c_int] * 3
         L.rx_lin_splits.restype = L.rx_lin_ws_floats.restype = ctypes.c_int
+        L.rx_lin_plan.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_int)]
+        L.rx_lin_plan.restype = ctypes.c_int
         i = ctypes.c_int
         L.rx_lin_tower_fwd.argtypes = [vp, i, i, vp, i, ll, vp, vp, vp, vp]
         L.rx_lin_tower_bwd.argtypes = [vp, i, i, vp, i, ll, vp, vp, vp, vp, vp, vp, vp]
@@ -83,15 +89,24 @@ _sizes = {}     # (device, GEMM shapes) -> (workspace floats, tiles)
 _cus = {}
 
 
-def _split_ws(device, M, N, K, force: Optional[int] = None):
-    """Split-K factor and (workspace, counters) for one GEMM on ``device``."""
+def plan(M: int, N: int, K: int, cus: int = 256, tile: int = TILE_AUTO):
+    """(tile shape, split-K factor) the kernel library picks for one GEMM (``rx_lin_plan``)."""
+    t = ctypes.c_int(0)
+    sp = int(_lib().rx_lin_plan(M, N, K, cus, int(tile), ctypes.byref(t)))
+    return t.value, sp
+
+
+def _split_ws(device, M, N, K, force: Optional[int] = None, tile: int = TILE_AUTO):
+    """(tile, split-K factor, workspace, counters) for one GEMM on ``device``."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     if idx not in _cus:
         _cus[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
     L = _lib()
-    sp = int(force) if force is not None else int(L.rx_lin_splits(M, N, K, _cus[idx]))
+    tile, sp = plan(M, N, K, _cus[idx], tile)
+    if force is not None:
+        sp = int(force)
     if sp <= 1:
-        return 1, None, None
+        return tile, 1, None, None
     need = int(L.rx_lin_ws_floats(M, N, sp))
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
     ws, cnt = _scratch.get(idx, (None, None))
@@ -100,7 +115,7 @@ def _split_ws(device, M, N, K, force: Optional[int] = None):
     if cnt is None or cnt.numel() < tiles:
         cnt = torch.zeros(max(tiles, 1024), dtype=torch.int32, device=device)
     _scratch[idx] = (ws, cnt)
-    return sp, ws, cnt
+    return tile, sp, ws, cnt
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -117,9 +132,10 @@ def _operand(t: torch.Tensor, lay: int) -> LinOperand:
 
 def gemm(epi: int, M: int, N: int, K: int, a: torch.Tensor, a_lay: int, b: torch.Tensor, b_lay: int,
          out: torch.Tensor, bias=None, relu=False, out2=None, mask=None, dbias=None, beta=0.0,
-         splits: Optional[int] = None):
+         splits: Optional[int] = None, tile: int = TILE_AUTO):
     """One launch of the fused GEMM (host-side shape checks: the kernel itself only bounds
-    rows / columns by M, N, K)."""
+    rows / columns by M, N, K). ``splits`` / ``tile`` force the split-K factor / tile shape
+    (default: ``plan``)."""
     def rows_cols(t, lay, rows):
         # ROW: [rows][K]; RED: [K][rows]
         want = (rows, K) if lay == ROW else (K, rows)
@@ -146,8 +162,8 @@ def gemm(epi: int, M: int, N: int, K: int, a: torch.Tensor, a_lay: int, b: torch
     args.out2, args.ldo2 = _ptr(out2), out2.stride(0) if out2 is not None else 0
     args.mask, args.ldm = _ptr(mask), mask.stride(0) if mask is not None else 0
     args.dbias, args.beta = _ptr(dbias), float(beta)
-    sp, ws, cnt = _split_ws(out.device, M, N, K, splits)
-    args.splits, args.ws, args.counters = sp, _ptr(ws), _ptr(cnt)
+    tl, sp, ws, cnt = _split_ws(out.device, M, N, K, splits, tile)
+    args.splits, args.ws, args.counters, args.tile = sp, _ptr(ws), _ptr(cnt), tl
     _hip.check(_lib().rx_lin_gemm(ctypes.byref(args), _hip.stream_ptr(out.device)), "rx_lin_gemm")
     return out
 

@@ -148,8 +148,9 @@ def test_dlrm_fused_towers_match_eager_and_train(monkeypatch):
     np.testing.assert_allclose(traj["1"], traj["0"], rtol=2e-2)
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
 @pytest.mark.parametrize("splits", [1, 3, 8])
-def test_split_k_is_deterministic_and_exact(splits):
+def test_split_k_is_deterministic_and_exact(splits, tile):
     """The split-K fix-up sums the partial tiles in split order: bitwise identical across runs,
     and equal (to fp32 reassociation) to the unsplit kernel, bias gradient included."""
     from raydp_amd.ops import linear_ops as L
@@ -161,7 +162,7 @@ def test_split_k_is_deterministic_and_exact(splits):
     for _ in range(2):
         dW = torch.empty(M, N, device="cuda")
         db = torch.empty(M, device="cuda")
-        L.gemm(L.WGRAD, M, N, K, G, L.RED, X, L.RED, dW, dbias=db, splits=splits)
+        L.gemm(L.WGRAD, M, N, K, G, L.RED, X, L.RED, dW, dbias=db, splits=splits, tile=tile)
         outs.append((dW, db))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     ref = G.float().T @ X.float()
@@ -169,20 +170,23 @@ def test_split_k_is_deterministic_and_exact(splits):
     assert _rel(outs[0][1], G.float().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
 @pytest.mark.parametrize("splits", [1, 3])
-def test_gemm_all_epilogues_ragged(splits):
+@pytest.mark.parametrize("shape", [(777, 333, 1000), (512, 384, 1024)])
+def test_gemm_all_epilogues_ragged(splits, tile, shape):
     """Every epilogue on ragged edges in every dimension (M, N, K not multiples of the 64-wide
-    tiles), bf16 and fp32 operands in both memory orientations, split and unsplit, against fp32
-    references of the bf16-rounded operands."""
+    tiles), bf16 and fp32 operands in both memory orientations, split and unsplit, every tile
+    shape, against fp32 references of the bf16-rounded operands. The second shape is whole
+    128-tiles with aligned rows (the unchecked-load fast path of every stage)."""
     from raydp_amd.ops import linear_ops as L
     g = torch.Generator(device="cuda").manual_seed(11)
-    M, N, K = 777, 333, 1000
+    M, N, K = shape
     X = torch.randn(M, K, device="cuda", generator=g)                        # fp32, ROW
     W = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)     # bf16, ROW
     b = torch.randn(N, device="cuda", generator=g)
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     y32 = torch.empty(M, N, device="cuda")
-    L.gemm(L.FWD, M, N, K, X, L.ROW, W, L.ROW, y, bias=b, relu=True, out2=y32, splits=splits)
+    L.gemm(L.FWD, M, N, K, X, L.ROW, W, L.ROW, y, bias=b, relu=True, out2=y32, splits=splits, tile=tile)
     ref = torch.relu(_bf(X) @ W.float().T + b)
     assert _rel(y32, ref) < 1e-5 and _rel(y.float(), ref) < 1e-2
     # dgrad: dX = (G W) * mask with W read transposed ([K][N] memory = RED)
@@ -190,13 +194,13 @@ def test_gemm_all_epilogues_ragged(splits):
     Wt = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)   # memory [N][K] = [red][rows]
     mask = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
     dx = torch.empty(M, K, device="cuda")
-    L.gemm(L.DGRAD, M, K, N, G, L.ROW, Wt, L.RED, dx, mask=mask, splits=splits)
+    L.gemm(L.DGRAD, M, K, N, G, L.ROW, Wt, L.RED, dx, mask=mask, splits=splits, tile=tile)
     ref = (G.float() @ Wt.float()) * (mask.float() > 0).float()
     assert _rel(dx, ref) < 1e-5
     # wgrad: dW = G^T X over the batch (both stored [batch][rows] = RED), bias-gradient row sums
     Xb = torch.randn(M, K, device="cuda", generator=g)                       # fp32 RED operand
     dW = torch.empty(K, N, device="cuda")
     db = torch.empty(K, device="cuda")
-    L.gemm(L.WGRAD, K, N, M, Xb, L.RED, G, L.RED, dW, dbias=db, splits=splits)
+    L.gemm(L.WGRAD, K, N, M, Xb, L.RED, G, L.RED, dW, dbias=db, splits=splits, tile=tile)
     assert _rel(dW, _bf(Xb).T @ G.float()) < 1e-5
     assert _rel(db, _bf(Xb).sum(0)) < 1e-5
