@@ -166,6 +166,138 @@ __global__ __launch_bounds__(256) void dot_bwd_kernel(const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------- gather + interaction -----
+// The replicated-table forward in ONE launch: each wave gathers its sample's interaction input
+// straight from the tables (row 0 = the bottom-MLP output `head`, row 1 + t = W[offs[t] +
+// idx[b][t]]), 16-B chunks), writes it to X (fp32: the backward's operand) and keeps its bf16
+// image in LDS for the MFMA interaction -- the emb_gather launch and the interaction kernel's
+// re-read of X are gone.
+template <int D>
+__global__ __launch_bounds__(256) void emb_dot_fwd_kernel(const float* __restrict__ W, const long long* __restrict__ offs,
+                                                          const long long* __restrict__ idx,
+                                                          const float* __restrict__ head, float* __restrict__ X,
+                                                          float* __restrict__ out, int B, int F,
+                                                          long long total_rows) {
+  constexpr int RS = D + 8, CH = D / 4;
+  __shared__ __attribute__((aligned(16))) u16 lds[4][kMaxF * RS];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + wave;
+  const bool valid = b < B;
+  const int T = F - 1;
+  u16* Xs = lds[wave];
+  if (valid) {
+    float* x = X + (long long)b * F * D;
+    for (int e = lane; e < kMaxF * CH; e += 64) {
+      const int r = e / CH, c = e % CH;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (r == 0) {
+        v = *reinterpret_cast<const f32x4*>(head + (long long)b * D + 4 * c);
+      } else if (r < F) {
+        long long row = offs[r - 1] + idx[(long long)b * T + r - 1];
+        row = row < 0 ? 0 : (row >= total_rows ? total_rows - 1 : row);  // never read out of bounds
+        v = *reinterpret_cast<const f32x4*>(W + row * D + 4 * c);
+      }
+      if (r < F) *reinterpret_cast<f32x4*>(x + r * D + 4 * c) = v;
+      uint2 pk;
+      pk.x = rx_f2bf2(v[0], v[1]);
+      pk.y = rx_f2bf2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(Xs + r * RS + 4 * c) = pk;
+    }
+  }
+  __syncthreads();
+  if (!valid) return;
+  const int lr = lane & 15, lg = lane >> 4;
+  f32x4 acc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int k0 = 0; k0 < D; k0 += 32) {
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Xs + lr * RS + k0 + 8 * lg);
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Xs + (16 + lr) * RS + k0 + 8 * lg);
+    acc[0] = rx_mfma16(a0, a0, acc[0]);
+    acc[1] = rx_mfma16(a1, a0, acc[1]);
+    acc[2] = rx_mfma16(a1, a1, acc[2]);
+  }
+  float* o = out + (long long)b * (D + F * (F - 1) / 2 + 1);
+  for (int k = lane; k < D; k += 64) o[k] = head[(long long)b * D + k];
+#pragma unroll
+  for (int blk = 0; blk < 3; ++blk) {
+    const int I = blk == 0 ? 0 : 1, J = blk == 2 ? 1 : 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = I * 16 + 4 * lg + r, j = J * 16 + lr;
+      if (i < F && j < i) o[D + i * (i - 1) / 2 + j] = acc[blk][r];
+    }
+  }
+  if (lane == 0) o[D + F * (F - 1) / 2] = 0.f;
+}
+
+// Interaction backward with the embedding SGD applied in its epilogue: dX = S X as in
+// dot_bwd_kernel, but only row 0 (the bottom-MLP gradient) is stored, to dmlp [B][D]; the
+// embedding rows' gradients go straight into the tables, W[row] -= lr * dX[b][1 + t] (fp32
+// atomics, as emb_sgd_kernel) -- no dX buffer, no second launch. relu_mask: row 0 of X is the
+// output of a ReLU (the bottom MLP's last layer), so dmlp is stored already multiplied by
+// relu'(.) = (X[b][0] > 0): the bottom tower's backward then skips its mask kernel.
+// One workgroup per sample (4 waves): the operand staging is spread over 256 threads (16-B
+// loads of X) and each wave owns MFMA tiles of dX, so the per-sample dependent chain (load ->
+// LDS -> MFMA -> atomics) is a quarter as long as with one wave per sample; at the notebook's
+// batch 128 that one-wave chain, not bandwidth, was the kernel's time.
+template <int D>
+__global__ __launch_bounds__(256) void dot_bwd_sgd_kernel(const float* __restrict__ X, const float* __restrict__ dO,
+                                                          float* __restrict__ dmlp, float* __restrict__ W,
+                                                          const long long* __restrict__ offs,
+                                                          const long long* __restrict__ idx, int B, int F, float lr,
+                                                          long long total_rows, int relu_mask) {
+  constexpr int XS = kMaxF + 8, CH = D / 4;
+  __shared__ __attribute__((aligned(16))) u16 XT[D * XS];
+  __shared__ __attribute__((aligned(16))) u16 S[kMaxF * XS];
+  __shared__ long long rows_s[kMaxF];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int T = F - 1;
+  const float* x = X + (long long)b * F * D;
+  const float* g = dO + (long long)b * (D + F * (F - 1) / 2 + 1);
+  for (int e = tid; e < kMaxF * CH; e += 256) {
+    const int r = e / CH, c = (e % CH) * 4;
+    const f32x4 v = r < F ? *reinterpret_cast<const f32x4*>(x + r * D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) XT[(c + q) * XS + r] = rx_f2bf(v[q]);
+  }
+  for (int e = tid; e < kMaxF * kMaxF; e += 256) {
+    const int i = e / kMaxF, j = e % kMaxF;
+    float v = 0.f;
+    if (i < F && j < F && i != j) {
+      const int hi = i > j ? i : j, lo = i > j ? j : i;
+      v = g[D + hi * (hi - 1) / 2 + lo];
+    }
+    S[i * XS + j] = rx_f2bf(v);
+  }
+  if (tid < kMaxF) {
+    long long row = -1;
+    if (tid >= 1 && tid < F) {
+      row = offs[tid - 1] + idx[(long long)b * T + tid - 1];
+      if (row < 0 || row >= total_rows) row = -1;
+    }
+    rows_s[tid] = row;
+  }
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63, lr_ = lane & 15, lg = lane >> 4;
+  constexpr int NT = 2 * (D / 16);  // (row tile mi) x (column tile nd) of dX [32 x D]
+  for (int t = wave; t < NT; t += 4) {
+    const int mi = t / (D / 16), nd = t % (D / 16);
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(S + (mi * 16 + lr_) * XS + 8 * lg);
+    const bf16x8 bb = *reinterpret_cast<const bf16x8*>(XT + (nd * 16 + lr_) * XS + 8 * lg);
+    const f32x4 c = rx_mfma16(a, bb, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = mi * 16 + 4 * lg + r, d = nd * 16 + lr_;
+      if (i == 0) {
+        dmlp[(long long)b * D + d] = (relu_mask && !(x[d] > 0.f)) ? 0.f : c[r] + g[d];
+      } else if (i < F) {
+        const long long row = rows_s[i];
+        if (row >= 0) atomicAdd(W + row * D + d, -lr * c[r]);
+      }
+    }
+  }
+}
+
 template <int D>
 int launch_fwd(const float* X, float* out, int B, int F, hipStream_t s) {
   hipLaunchKernelGGL(dot_fwd_kernel<D>, dim3((B + 3) / 4), dim3(256), 0, s, X, out, B, F);
@@ -231,6 +363,37 @@ int rx_dot_interaction_fwd(const float* X, float* out, int B, int F, int D, hipS
     case 128: return launch_fwd<128>(X, out, B, F, s);
     default: return -1;
   }
+}
+
+// Gather + interaction in one launch (replicated tables): X [B][F][D] written for the backward,
+// out = the interaction output. head: [B][D] fp32, 16-B aligned rows.
+int rx_emb_dot_fwd(const float* W, const long long* offs, const long long* idx, const float* head, float* X,
+                   float* out, int B, int F, int D, long long total_rows, hipStream_t s) {
+  if (F > kMaxF || F < 2) return -1;
+  const dim3 grid((B + 3) / 4);
+  switch (D) {
+    case 32: hipLaunchKernelGGL(emb_dot_fwd_kernel<32>, grid, dim3(256), 0, s, W, offs, idx, head, X, out, B, F, total_rows); break;
+    case 64: hipLaunchKernelGGL(emb_dot_fwd_kernel<64>, grid, dim3(256), 0, s, W, offs, idx, head, X, out, B, F, total_rows); break;
+    case 128: hipLaunchKernelGGL(emb_dot_fwd_kernel<128>, grid, dim3(256), 0, s, W, offs, idx, head, X, out, B, F, total_rows); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+// Interaction backward + fused embedding SGD: dmlp [B][D] = the bottom-MLP gradient; the table
+// rows are updated in place.
+int rx_dot_bwd_sgd(const float* X, const float* dO, float* dmlp, float* W, const long long* offs, const long long* idx,
+                   int B, int F, int D, float lr, long long total_rows, int relu_mask, hipStream_t s) {
+  if (F > kMaxF || F < 2) return -1;
+  if (B <= 0) return 0;
+  const dim3 grid(B);
+  switch (D) {
+    case 32: hipLaunchKernelGGL(dot_bwd_sgd_kernel<32>, grid, dim3(256), 0, s, X, dO, dmlp, W, offs, idx, B, F, lr, total_rows, relu_mask); break;
+    case 64: hipLaunchKernelGGL(dot_bwd_sgd_kernel<64>, grid, dim3(256), 0, s, X, dO, dmlp, W, offs, idx, B, F, lr, total_rows, relu_mask); break;
+    case 128: hipLaunchKernelGGL(dot_bwd_sgd_kernel<128>, grid, dim3(256), 0, s, X, dO, dmlp, W, offs, idx, B, F, lr, total_rows, relu_mask); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
 }
 
 int rx_dot_interaction_bwd(const float* X, const float* dO, float* dX, int B, int F, int D, hipStream_t s) {

@@ -214,23 +214,30 @@ __device__ __forceinline__ float lin_bsum(const bf16x8& f) {
 // LA / LB: the operands' memory orientations as template constants (FWD: ROW x ROW, DGRAD:
 // ROW x RED, WGRAD: RED x RED), so the fragment reads compile to straight-line ds_reads the
 // scheduler can batch ahead of the MFMAs instead of layout branches between them.
+// LDS of one GEMM block: [buffer][A image | B image] (u16 elements)
+template <int LA, int LB, int TM, int TN>
+struct LinLds {
+  static constexpr int IA = LinImg<LA, TM>::elems, IB = LinImg<LB, TN>::elems;
+  static constexpr int elems = 2 * (IA + IB);
+};
+
+// One output tile (bx, by) / K split bz of a GEMM whose tile grid has gy columns. Shared by the
+// single-GEMM kernel and the paired kernel (two independent GEMMs in one launch).
 template <int AM, int BM, int LA, int LB, int TM, int TN>
-__global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
+__device__ __forceinline__ void lin_gemm_body(const LinArgs& a, u16* lds, int bx, int by, int bz, int gy) {
   constexpr int FM = TM / 32, FN = TN / 32;  // MFMA tiles per wave along M / N
-  constexpr int IA = LinImg<LA, TM>::elems, IB = LinImg<LB, TN>::elems;
-  // ONE __shared__ array: [buffer][A image | B image]
-  __shared__ __attribute__((aligned(16))) u16 lds[2 * (IA + IB)];
+  constexpr int IA = LinLds<LA, LB, TM, TN>::IA, IB = LinLds<LA, LB, TM, TN>::IB;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const long long m0 = (long long)blockIdx.x * TM, n0 = (long long)blockIdx.y * TN;
+  const long long m0 = (long long)bx * TM, n0 = (long long)by * TN;
   // split-K: this block reduces K stages [k_begin, k_end)
   const int nk_all = (a.K + LIN_BK - 1) / LIN_BK;
   const int per = (nk_all + a.splits - 1) / a.splits;
-  const int k_begin = blockIdx.z * per;
+  const int k_begin = bz * per;
   const int k_end = min(nk_all, k_begin + per);
   const int nk = max(0, k_end - k_begin);
-  const bool want_db = a.epi == LIN_WGRAD && a.dbias != nullptr && blockIdx.y == 0 && wn == 0;
+  const bool want_db = a.epi == LIN_WGRAD && a.dbias != nullptr && by == 0 && wn == 0;
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -306,9 +313,9 @@ __global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
     // (MI355X: per-XCD L2s): write-through sc1 payload stores drained by every storing wave, a
     // barrier, ONE agent-scope counter add; the last block reads the payload with sc1 loads only
     // (they bypass its L1), so no release / acquire fence is needed.
-    const int tile = blockIdx.x * gridDim.y + blockIdx.y;
+    const int tile = bx * gy + by;
     const int TW = TM * TN + TM;
-    float* mine = a.ws + ((long long)tile * a.splits + blockIdx.z) * TW;
+    float* mine = a.ws + ((long long)tile * a.splits + bz) * TW;
     const int slot = ((wave * 64 + lane) * (FM * FN * 4)) * 4;  // byte offset of this lane's floats
 #pragma unroll
     for (int x = 0; x < FM; ++x)
@@ -514,11 +521,49 @@ __global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
   }
 }
 
+template <int AM, int BM, int LA, int LB, int TM, int TN>
+__global__ __launch_bounds__(256) void lin_gemm_kernel(LinArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 lds[LinLds<LA, LB, TM, TN>::elems];
+  lin_gemm_body<AM, BM, LA, LB, TM, TN>(a, lds, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.y);
+}
+
+// Two independent 64x64-tiled GEMMs in ONE launch: a layer's dgrad (ROW x RED, critical path of
+// the backward) and its wgrad (RED x RED, needed only by the optimizer) both read only that
+// layer's output gradient, so the tower backward issues one launch per layer instead of two
+// (the DLRM step at the notebook's batch 128 is launch bound: ~5 us per dependent launch).
+// Blocks [0, nb0) run problem 0, the rest problem 1; each problem's blocks are numbered
+// (split, row tile, column tile) like the single kernel's grid. One LDS array of the larger size.
+struct LinPair {
+  LinArgs p[2];
+  int gy[2];  // column tiles of each problem's grid
+  int gxy[2]; // tiles per split of each problem
+  int nb0;    // blocks of problem 0 (tiles x splits)
+  int pad_;
+};
+
+template <int AM0, int BM0, int AM1, int BM1>
+__global__ __launch_bounds__(256) void lin_pair_kernel(LinPair q) {
+  constexpr int E0 = LinLds<LIN_ROW, LIN_RED, 64, 64>::elems, E1 = LinLds<LIN_RED, LIN_RED, 64, 64>::elems;
+  __shared__ __attribute__((aligned(16))) u16 lds[E0 > E1 ? E0 : E1];
+  int id = blockIdx.x;
+  if (id < q.nb0) {
+    const int bz = id / q.gxy[0], r = id - bz * q.gxy[0];
+    lin_gemm_body<AM0, BM0, LIN_ROW, LIN_RED, 64, 64>(q.p[0], lds, r / q.gy[0], r % q.gy[0], bz, q.gy[0]);
+  } else {
+    id -= q.nb0;
+    const int bz = id / q.gxy[1], r = id - bz * q.gxy[1];
+    lin_gemm_body<AM1, BM1, LIN_RED, LIN_RED, 64, 64>(q.p[1], lds, r / q.gy[1], r % q.gy[1], bz, q.gy[1]);
+  }
+}
+
 // G = gY * (Y > 0) (relu) or G = gY, fp32 -> bf16 (the tower's top-layer output gradient).
+// gY rows are ldg floats apart (a column slice of a wider gradient, e.g. the DLRM interaction's
+// bottom-MLP slot, is read in place); Y and G are dense [n / cols][cols].
 __global__ __launch_bounds__(256) void lin_mask_cast_kernel(const float* __restrict__ g, const u16* __restrict__ y,
-                                                            u16* __restrict__ out, long long n) {
+                                                            u16* __restrict__ out, long long n, int cols, long long ldg) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    float v = g[i];
+    const long long r = i / cols;
+    float v = g[r * ldg + (i - r * cols)];
     if (y != nullptr && !(rx_bf2f(y[i]) > 0.f)) v = 0.f;
     out[i] = rx_f2bf(v);
   }
@@ -569,9 +614,12 @@ static long long lin_tiles(int M, int N, int tile) {
 // * 64x64 tiles everywhere: at batch 2048 the 128-wide tiles leave half the CUs idle (128
 //   workgroups for a 2048x1024 output) and their one wave per SIMD exposes every LDS and barrier
 //   latency; splitting K to fill the chip costs more in the fix-up than it wins.
-// * split-K only for problems with few output tiles (the weight gradients, K = batch): about
-//   192 workgroups, each split at least eight 64-deep stages (s1 -> s4 is 17 -> 10.5 us at
-//   2 tiles; at 512 tiles any split doubles the time).
+// * split-K only for problems with few output tiles AND a deep K (the weight gradients at
+//   batch 2048, K = batch): about 192 workgroups, each split at least eight 64-deep stages
+//   (s1 -> s4 is 17 -> 10.5 us at 2 tiles; at 512 tiles any split doubles the time). Below 24
+//   stages the fix-up costs more than the shorter K loop saves: at the notebook's batch 128 the
+//   1024-deep forward GEMMs run 8.06 / 7.95 us unsplit vs 8.83 / 8.64 us at s2
+//   (profiles/r3_linear_gemm_sweep_batch128.txt).
 // tile_force != 0 fixes the shape (sweeps / tests); the cus argument scales the target.
 int rx_lin_plan(int M, int N, int K, int cus, int tile_force, int* tile_out) {
   const int tile = tile_force != LIN_TILE_AUTO ? tile_force : LIN_TILE_64x64;
@@ -580,7 +628,7 @@ int rx_lin_plan(int M, int N, int K, int cus, int tile_force, int* tile_out) {
   const int nk = (K + LIN_BK - 1) / LIN_BK;
   const long long target = (3LL * (cus > 0 ? cus : 256)) / 4;  // 192 on MI355X
   long long want = (target + tiles - 1) / tiles;
-  long long mx = nk / 8;
+  long long mx = nk >= 24 ? nk / 8 : 1;
   if (want > mx) want = mx;
   if (want > 64) want = 64;
   return want < 1 ? 1 : (int)want;
@@ -709,9 +757,14 @@ struct LinScratch {
   long long ws_floats;
   int counters_len;
   int cus;
+  int pair;  // 1: the backward pairs each layer's dgrad and wgrad in one launch (needs the
+             //    workspace / counters sized for two problems: each gets one half)
+  int pad_;
 };
 
 int rx_lin_mask_cast(const float* g, const u16* y, u16* out, long long n, hipStream_t stream);
+static int lin_mask_cast2(const float* g, long long ldg, const u16* y, u16* out, int rows, int cols,
+                          hipStream_t stream);
 
 static int lin_run(LinArgs& a, const LinScratch& sc, hipStream_t stream) {
   int tile = LIN_TILE_AUTO;
@@ -723,6 +776,64 @@ static int lin_run(LinArgs& a, const LinScratch& sc, hipStream_t stream) {
   a.ws = a.splits > 1 ? sc.ws : nullptr;
   a.counters = a.splits > 1 ? sc.counters : nullptr;
   return rx_lin_gemm(&a, stream);
+}
+
+// Plan one problem of a pair into its half of the scratch.
+static void lin_plan_half(LinArgs& a, const LinScratch& sc, int half) {
+  int tile = LIN_TILE_AUTO;
+  a.splits = rx_lin_plan(a.M, a.N, a.K, sc.cus, LIN_TILE_AUTO, &tile);
+  a.tile = LIN_TILE_64x64;
+  const long long wsh = sc.ws_floats / 2, ch = sc.counters_len / 2;
+  if (a.splits > 1 && ((long long)rx_lin_ws_floats(a.M, a.N, a.splits) > wsh || lin_tiles(a.M, a.N, LIN_TILE_64x64) > ch))
+    a.splits = 1;
+  a.ws = a.splits > 1 ? sc.ws + half * wsh : nullptr;
+  a.counters = a.splits > 1 ? sc.counters + half * ch : nullptr;
+}
+
+// dgrad d (ROW x RED) and wgrad w (RED x RED) of one layer in one launch when both take the
+// 64x64 tile and the staging modes the paired kernel is built for (bf16 vector operands; the
+// wgrad's activation operand bf16 or fp32 vector); otherwise two launches.
+static int lin_run_pair(LinArgs& d, LinArgs& w, const LinScratch& sc, hipStream_t stream) {
+  const int dma = lin_mode(d.a, d.K), dmb = lin_mode(d.b, d.N);
+  const int wma = lin_mode(w.a, w.M), wmb = lin_mode(w.b, w.N);
+  int td = 0, tw = 0;
+  rx_lin_plan(d.M, d.N, d.K, sc.cus, LIN_TILE_AUTO, &td);
+  rx_lin_plan(w.M, w.N, w.K, sc.cus, LIN_TILE_AUTO, &tw);
+  // built pairs (A modes = the layer gradient G, staged the same way by both problems):
+  //   G bf16:  <V16, V16 | V16, V16 or V32>   (any layer below the top; X bf16 or fp32 input)
+  //   G fp32:  <V32, V16 | V32, V16>          (top layer of a tower whose gradient arrives fp32)
+  //            <G32, V16 | G32, V16>          (the same with an unaligned width, e.g. the logit)
+  const bool gv16 = dma == LIN_V16 && wma == LIN_V16 && (wmb == LIN_V16 || wmb == LIN_V32);
+  const bool gf32 = ((dma == LIN_V32 && wma == LIN_V32) || (dma == LIN_G32 && wma == LIN_G32)) && wmb == LIN_V16;
+  const bool ok = sc.pair && d.M > 0 && d.N > 0 && w.M > 0 && w.N > 0 && td == LIN_TILE_64x64 &&
+                  tw == LIN_TILE_64x64 && dmb == LIN_V16 && (gv16 || gf32);
+  if (!ok) {
+    int rc = lin_run(w, sc, stream);
+    return rc ? rc : lin_run(d, sc, stream);
+  }
+  const long long ed = (long long)d.M * d.a.ld * (d.a.f32 ? 4 : 2), eb = (long long)d.K * d.b.ld * 2;
+  const long long ewa = (long long)w.K * w.a.ld * (w.a.f32 ? 4 : 2), ewb = (long long)w.K * w.b.ld * (w.b.f32 ? 4 : 2);
+  if (ed >= (1LL << 31) || eb >= (1LL << 31) || ewa >= (1LL << 31) || ewb >= (1LL << 31)) return -2;
+  LinPair q;
+  memset(&q, 0, sizeof(q));
+  lin_plan_half(d, sc, 0);
+  lin_plan_half(w, sc, 1);
+  q.p[0] = d;
+  q.p[1] = w;
+  const int gx0 = (d.M + 63) / 64, gy0 = (d.N + 63) / 64, gx1 = (w.M + 63) / 64, gy1 = (w.N + 63) / 64;
+  q.gy[0] = gy0, q.gy[1] = gy1;
+  q.gxy[0] = gx0 * gy0, q.gxy[1] = gx1 * gy1;
+  q.nb0 = q.gxy[0] * d.splits;
+  const unsigned blocks = (unsigned)(q.nb0 + q.gxy[1] * w.splits);
+  if (dma == LIN_V32)
+    hipLaunchKernelGGL((lin_pair_kernel<LIN_V32, LIN_V16, LIN_V32, LIN_V16>), dim3(blocks), dim3(256), 0, stream, q);
+  else if (dma == LIN_G32)
+    hipLaunchKernelGGL((lin_pair_kernel<LIN_G32, LIN_V16, LIN_G32, LIN_V16>), dim3(blocks), dim3(256), 0, stream, q);
+  else if (wmb == LIN_V16)
+    hipLaunchKernelGGL((lin_pair_kernel<LIN_V16, LIN_V16, LIN_V16, LIN_V16>), dim3(blocks), dim3(256), 0, stream, q);
+  else
+    hipLaunchKernelGGL((lin_pair_kernel<LIN_V16, LIN_V16, LIN_V16, LIN_V32>), dim3(blocks), dim3(256), 0, stream, q);
+  return (int)hipGetLastError();
 }
 
 static LinArgs lin_args0() {
@@ -762,27 +873,36 @@ int rx_lin_tower_fwd(const LinLayer* L, int nl, int M, const void* x, int x_f32,
 // layer with a dW, and dx (nullable; fp32 when x_f32 else bf16). g0 / g1: bf16 ping-pong buffers
 // of M * max(N_l) elements.
 int rx_lin_tower_bwd(const LinLayer* L, int nl, int M, const void* x, int x_f32, long long ldx, u16* const* acts,
-                     const float* gout, void* dx, u16* g0, u16* g1, const LinScratch* sc, hipStream_t stream) {
-  u16* G = g0;
-  int rc = rx_lin_mask_cast(gout, L[nl - 1].relu ? acts[nl - 1] : nullptr, G, (long long)M * L[nl - 1].N, stream);
-  if (rc) return rc;
+                     const float* gout, long long ldg, int gout_masked, void* dx, u16* g0, u16* g1,
+                     const LinScratch* sc, hipStream_t stream) {
+  // the top layer's gradient: without a ReLU (or with the ReLU mask already applied by the
+  // producer of gout: gout_masked) it is gout itself (fp32, converted to bf16 while the GEMMs
+  // stage it); otherwise one mask+cast launch
+  const void* G = gout;
+  int g_f32 = 1;
+  int rc = 0;
+  if (L[nl - 1].relu && !gout_masked) {
+    if ((rc = lin_mask_cast2(gout, ldg, acts[nl - 1], g0, M, L[nl - 1].N, stream))) return rc;
+    G = g0;
+    g_f32 = 0;
+  }
   for (int l = nl - 1; l >= 0; --l) {
     const int N = L[l].N, K = L[l].K;
     const LinOperand Xl = l == 0 ? LinOperand{x, ldx, x_f32, LIN_RED} : LinOperand{acts[l - 1], K, 0, LIN_RED};
-    if (L[l].dW != nullptr) {
-      LinArgs a = lin_args0();
-      a.M = N, a.N = K, a.K = M, a.epi = LIN_WGRAD;
-      a.a = LinOperand{G, N, 0, LIN_RED};
-      a.b = Xl;
-      a.out = L[l].dW;
-      a.ldo = K;
-      a.dbias = L[l].db;
-      if ((rc = lin_run(a, *sc, stream))) return rc;
+    LinArgs w = lin_args0();
+    const bool has_w = L[l].dW != nullptr;
+    if (has_w) {
+      w.M = N, w.N = K, w.K = M, w.epi = LIN_WGRAD;
+      w.a = LinOperand{G, g_f32 ? ldg : N, g_f32, LIN_RED};
+      w.b = Xl;
+      w.out = L[l].dW;
+      w.ldo = K;
+      w.dbias = L[l].db;
     }
     if (l > 0 || dx != nullptr) {
       LinArgs a = lin_args0();
       a.M = M, a.N = K, a.K = N, a.epi = LIN_DGRAD;
-      a.a = LinOperand{G, N, 0, LIN_ROW};
+      a.a = LinOperand{G, g_f32 ? ldg : N, g_f32, LIN_ROW};
       a.b = LinOperand{L[l].W, K, 0, LIN_RED};
       u16* nextG = G == g0 ? g1 : g0;
       if (l > 0) {
@@ -796,8 +916,12 @@ int rx_lin_tower_bwd(const LinLayer* L, int nl, int M, const void* x, int x_f32,
         a.out_f32 = x_f32;
       }
       a.ldo = K;
-      if ((rc = lin_run(a, *sc, stream))) return rc;
+      rc = has_w ? lin_run_pair(a, w, *sc, stream) : lin_run(a, *sc, stream);
+      if (rc) return rc;
       G = nextG;
+      g_f32 = 0;
+    } else if (has_w) {
+      if ((rc = lin_run(w, *sc, stream))) return rc;
     }
   }
   return 0;
@@ -809,9 +933,19 @@ int rx_lin_scratch_size() { return (int)sizeof(LinScratch); }
 int rx_lin_mask_cast(const float* g, const u16* y, u16* out, long long n, hipStream_t stream) {
   if (n <= 0) return 0;
   const long long blocks = (n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048;
-  hipLaunchKernelGGL(lin_mask_cast_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, g, y, out, n);
+  hipLaunchKernelGGL(lin_mask_cast_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, g, y, out, n, 1, 1LL);
   return (int)hipGetLastError();
 }
+
+static int lin_mask_cast2(const float* g, long long ldg, const u16* y, u16* out, int rows, int cols,
+                          hipStream_t stream) {
+  const long long n = (long long)rows * cols;
+  if (n <= 0) return 0;
+  const long long blocks = (n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048;
+  hipLaunchKernelGGL(lin_mask_cast_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, g, y, out, n, cols, ldg);
+  return (int)hipGetLastError();
+}
+
 
 int rx_lin_refresh(const LinRefresh* r, hipStream_t stream) {
   if (r->n <= 0) return 0;

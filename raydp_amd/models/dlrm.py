@@ -94,9 +94,10 @@ class Dlrm(nn.Module):
             # sharded tables: the id all-to-all is in flight while the bottom MLP runs
             pending = self.embeddings.start(cats)
         mlp_out = self.bottom_mlp(dense.float())
-        X = self.embeddings.finish(pending, mlp_out) if pending is not None else \
-            self.embeddings(mlp_out, cats.long())
-        Z = dot_interaction(X)
+        if pending is not None:
+            Z = dot_interaction(self.embeddings.finish(pending, mlp_out))
+        else:   # replicated tables: lookup + interaction fused (one kernel each way on the GPU)
+            Z = self.embeddings.interact(mlp_out, cats.long(), relu_head=True)   # TorchMlp ends in ReLU
         if Z.is_cuda and _fused_ok(Z):
             # the whole top tower including the output layer is one fused op: the last bf16
             # activation never leaves the chain and the logits come back fp32

@@ -27,8 +27,10 @@ def _lib():
         L.rx_emb_sgd_rows.argtypes = [vp, vp, vp, vp, i, i, i, f, ll, vp]
         L.rx_dot_interaction_fwd.argtypes = [vp, vp, i, i, i, vp]
         L.rx_dot_interaction_bwd.argtypes = [vp, vp, vp, i, i, i, vp]
+        L.rx_emb_dot_fwd.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, ll, vp]
+        L.rx_dot_bwd_sgd.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, f, ll, i, vp]
         for n in ("rx_emb_gather", "rx_emb_sgd", "rx_emb_gather_rows", "rx_emb_sgd_rows", "rx_dot_interaction_fwd",
-                  "rx_dot_interaction_bwd"):
+                  "rx_dot_interaction_bwd", "rx_emb_dot_fwd", "rx_dot_bwd_sgd"):
             getattr(L, n).restype = i
         _bound = True
     return L
@@ -133,30 +135,83 @@ class _EmbedConcat(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dX):
-        weight, offsets, idx = ctx.saved_tensors
+        weight, offsets, idx = ctx.saved_tensors[:3]
+        return _embed_backward(weight, offsets, idx, dX, ctx.fused_lr, ctx.sync)
+
+
+def _embed_backward(weight, offsets, idx, dX, fused_lr, sync):
+    """Gradients of X = [mlp_out; W[offs + idx]] from dX: (d_mlp, weight grad or None (fused
+    SGD applied in place), None x 4)."""
+    B, T = idx.shape
+    D = weight.shape[1]
+    dX = dX.contiguous()
+    d_mlp = dX[:, 0]
+    if fused_lr is not None:
+        ids, rows_dx, n, lr = idx, dX, B, fused_lr
+        if sync is not None:
+            # replicated tables over W ranks: every rank applies every rank's rows (SGD is
+            # linear: the same update as all-reducing the sparse gradient and averaging),
+            # gathered over xGMI on the device -- no host round trip, capturable
+            comm, W = sync
+            ids = torch.empty((W,) + tuple(idx.shape), dtype=idx.dtype, device=idx.device)
+            comm.allgather_(idx, ids)
+            rows_dx = torch.empty((W,) + tuple(dX.shape), dtype=dX.dtype, device=dX.device)
+            comm.allgather_(dX, rows_dx)
+            n, lr = W * B, lr / W
+        _hip.check(_lib().rx_emb_sgd(_p(weight), _p(offsets), _p(ids), _p(rows_dx), n, T, D, T + 1,
+                                     ctypes.c_float(lr), weight.shape[0],
+                                     _hip.stream_ptr(weight.device)), "rx_emb_sgd")
+        return d_mlp, None, None, None, None, None
+    rows = (idx + offsets.view(1, -1)).reshape(-1)
+    grad = torch.sparse_coo_tensor(rows.unsqueeze(0), dX[:, 1:].reshape(-1, D), weight.shape)
+    return d_mlp, grad, None, None, None, None
+
+
+class _EmbedDot(torch.autograd.Function):
+    """Z = dot_interaction([mlp_out; W[offs + idx]]) for replicated tables: forward ONE launch
+    (gather + interaction, ``rx_emb_dot_fwd``); backward ONE launch when the embedding SGD is
+    fused and the tables are not synchronised across ranks (``rx_dot_bwd_sgd``: interaction
+    backward, bottom-MLP gradient, table rows updated in its epilogue), else the interaction
+    backward followed by _EmbedConcat's backward (all-gathered rows / sparse gradient)."""
+
+    @staticmethod
+    def forward(ctx, mlp_out, weight, offsets, idx, fused_lr, sync=None, relu_head=False):
         B, T = idx.shape
         D = weight.shape[1]
-        dX = dX.contiguous()
-        d_mlp = dX[:, 0]
-        if ctx.fused_lr is not None:
-            ids, rows_dx, n, lr = idx, dX, B, ctx.fused_lr
-            if ctx.sync is not None:
-                # replicated tables over W ranks: every rank applies every rank's rows (SGD is
-                # linear: the same update as all-reducing the sparse gradient and averaging),
-                # gathered over xGMI on the device -- no host round trip, capturable
-                comm, W = ctx.sync
-                ids = torch.empty((W,) + tuple(idx.shape), dtype=idx.dtype, device=idx.device)
-                comm.allgather_(idx, ids)
-                rows_dx = torch.empty((W,) + tuple(dX.shape), dtype=dX.dtype, device=dX.device)
-                comm.allgather_(dX, rows_dx)
-                n, lr = W * B, lr / W
-            _hip.check(_lib().rx_emb_sgd(_p(weight), _p(offsets), _p(ids), _p(rows_dx), n, T, D, T + 1,
-                                         ctypes.c_float(lr), weight.shape[0],
-                                         _hip.stream_ptr(weight.device)), "rx_emb_sgd")
-            return d_mlp, None, None, None, None, None
-        rows = (idx + offsets.view(1, -1)).reshape(-1)
-        grad = torch.sparse_coo_tensor(rows.unsqueeze(0), dX[:, 1:].reshape(-1, D), weight.shape)
-        return d_mlp, grad, None, None, None, None
+        F = T + 1
+        idx = idx.contiguous().long()
+        head = mlp_out.contiguous()
+        if head.shape != (B, D) or head.dtype != torch.float32:
+            raise ValueError(f"bottom-MLP output must be fp32 [{B}, {D}]")
+        X = torch.empty(B, F, D, dtype=torch.float32, device=weight.device)
+        Z = torch.empty(B, D + F * (F - 1) // 2 + 1, dtype=torch.float32, device=weight.device)
+        _hip.check(_lib().rx_emb_dot_fwd(_p(weight), _p(offsets), _p(idx), _p(head), _p(X), _p(Z), B, F, D,
+                                         weight.shape[0], _hip.stream_ptr(weight.device)), "rx_emb_dot_fwd")
+        ctx.save_for_backward(weight, offsets, idx, X)
+        ctx.fused_lr = fused_lr
+        ctx.sync = sync
+        ctx.relu_head = bool(relu_head)
+        return Z
+
+    @staticmethod
+    def backward(ctx, g):
+        weight, offsets, idx, X = ctx.saved_tensors
+        B, F, D = X.shape
+        g = g.contiguous().float()
+        stream = _hip.stream_ptr(X.device)
+        if ctx.fused_lr is not None and ctx.sync is None:
+            d_mlp = torch.empty(B, D, dtype=torch.float32, device=X.device)
+            _hip.check(_lib().rx_dot_bwd_sgd(_p(X), _p(g), _p(d_mlp), _p(weight), _p(offsets), _p(idx), B, F, D,
+                                             ctypes.c_float(ctx.fused_lr), weight.shape[0], int(ctx.relu_head),
+                                             stream), "rx_dot_bwd_sgd")
+            if ctx.relu_head:
+                # already multiplied by the bottom MLP's output ReLU mask (raydp_amd.ops.linear_ops
+                # reads this mark and skips its mask kernel; masking again would change nothing)
+                d_mlp._raydp_relu_masked = True
+            return d_mlp, None, None, None, None, None, None
+        dX = torch.empty_like(X)
+        _hip.check(_lib().rx_dot_interaction_bwd(_p(X), _p(g), _p(dX), B, F, D, stream), "rx_dot_interaction_bwd")
+        return _embed_backward(weight, offsets, idx, dX, ctx.fused_lr, ctx.sync) + (None,)
 
 
 class FusedEmbeddings(nn.Module):
@@ -189,3 +244,13 @@ class FusedEmbeddings(nn.Module):
         rows = idx.long() + self.offsets.view(1, -1)
         emb = nn.functional.embedding(rows, self.weight, sparse=True)
         return torch.cat([mlp_out.unsqueeze(1).float(), emb], dim=1)
+
+    def interact(self, mlp_out: torch.Tensor, idx: torch.Tensor, relu_head: bool = False) -> torch.Tensor:
+        """``dot_interaction(self(mlp_out, idx))``; on the GPU the lookup and the interaction are
+        one kernel each way (``_EmbedDot``). ``relu_head``: mlp_out is a ReLU output (its
+        gradient may then leave the interaction backward already masked)."""
+        T = len(self.table_sizes)
+        if self.weight.is_cuda and T + 1 <= 32 and self.dim in (32, 64, 128):
+            return _EmbedDot.apply(mlp_out.float(), self.weight, self.offsets, idx, self.fused_sgd_lr,
+                                   getattr(self, "sync", None), relu_head)
+        return dot_interaction(self(mlp_out, idx))

@@ -69,7 +69,7 @@ def _lib():
         L.rx_lin_plan.restype = ctypes.c_int
         i = ctypes.c_int
         L.rx_lin_tower_fwd.argtypes = [vp, i, i, vp, i, ll, vp, vp, vp, vp]
-        L.rx_lin_tower_bwd.argtypes = [vp, i, i, vp, i, ll, vp, vp, vp, vp, vp, vp, vp]
+        L.rx_lin_tower_bwd.argtypes = [vp, i, i, vp, i, ll, vp, vp, ll, i, vp, vp, vp, vp, vp]
         L.rx_lin_tower_fwd.restype = L.rx_lin_tower_bwd.restype = i
         for name, cls in (("rx_lin_layer_size", LinLayer), ("rx_lin_scratch_size", LinScratch)):
             getattr(L, name).restype = i
@@ -175,11 +175,17 @@ class LinLayer(ctypes.Structure):
 
 class LinScratch(ctypes.Structure):
     _fields_ = [("ws", ctypes.c_void_p), ("counters", ctypes.c_void_p), ("ws_floats", ctypes.c_longlong),
-                ("counters_len", ctypes.c_int), ("cus", ctypes.c_int)]
+                ("counters_len", ctypes.c_int), ("cus", ctypes.c_int), ("pair", ctypes.c_int), ("pad_", ctypes.c_int)]
+
+
+# The tower backward runs each layer's dgrad and wgrad as ONE paired launch
+# (csrc/hip/linear_act.hip lin_pair_kernel); False: two launches per layer (A/B measurements).
+PAIR_BACKWARD = True
 
 
 def _scratch_for(device, shapes) -> LinScratch:
-    """Split-K workspace covering every (M, N, K) GEMM in ``shapes`` (grown on demand)."""
+    """Split-K workspace covering every (M, N, K) GEMM in ``shapes`` (grown on demand); twice
+    that when the backward pairs two split GEMMs in one launch (each takes one half)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     if idx not in _cus:
         _cus[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
@@ -192,7 +198,7 @@ def _scratch_for(device, shapes) -> LinScratch:
             sp = int(L.rx_lin_splits(M, N, K, _cus[idx]))
             need = max(need, int(L.rx_lin_ws_floats(M, N, sp)))
             tiles = max(tiles, ((M + 63) // 64) * ((N + 63) // 64))
-        hit = _sizes[key] = (need, tiles)
+        hit = _sizes[key] = (2 * need, 2 * tiles)
     need, tiles = hit
     ws, cnt = _scratch.get(idx, (None, None))
     if ws is None or ws.numel() < max(need, 1):
@@ -202,7 +208,7 @@ def _scratch_for(device, shapes) -> LinScratch:
     _scratch[idx] = (ws, cnt)
     sc = LinScratch()
     sc.ws, sc.counters, sc.ws_floats = ws.data_ptr(), cnt.data_ptr(), ws.numel()
-    sc.counters_len, sc.cus = cnt.numel(), _cus[idx]
+    sc.counters_len, sc.cus, sc.pair = cnt.numel(), _cus[idx], int(PAIR_BACKWARD)
     return sc
 
 
@@ -235,7 +241,13 @@ class _TowerFn(torch.autograd.Function):
         x, *acts = ctx.saved_tensors
         M = x.shape[0]
         dev = x.device
-        gout = gout.contiguous().float()
+        # a producer that already applied this tower's output ReLU mask marks its gradient
+        # (raydp_amd.ops.dlrm_ops: the interaction backward masks the bottom-MLP slot with X > 0)
+        masked = bool(getattr(gout, "_raydp_relu_masked", False)) and t.relus[-1]
+        if gout.dtype != torch.float32 or gout.dim() != 2 or gout.stride(1) != 1:
+            gout = gout.contiguous().float()
+        # rows of gout may be further apart than its width (a column slice of a wider gradient,
+        # e.g. the DLRM interaction input's bottom-MLP slot): read in place, no copy kernel
         dWs, dbs = [], []
         for lin in t.linears:
             dWs.append(torch.empty(lin.out_features, lin.in_features, dtype=torch.float32, device=dev)
@@ -250,7 +262,9 @@ class _TowerFn(torch.autograd.Function):
         ptrs = (ctypes.c_void_p * len(acts))(*[a.data_ptr() for a in acts])
         sc = _scratch_for(dev, t._shapes(M))
         _hip.check(_lib().rx_lin_tower_bwd(layers, len(acts), M, ctypes.c_void_p(x.data_ptr()),
-                                           int(x.dtype == torch.float32), x.stride(0), ptrs, _ptr(gout), _ptr(dx),
+                                           int(x.dtype == torch.float32), x.stride(0), ptrs, _ptr(gout),
+                                           gout.stride(0) if gout.shape[0] > 1 else gout.shape[1], int(masked),
+                                           _ptr(dx),
                                            _ptr(g0), _ptr(g1), ctypes.byref(sc), _hip.stream_ptr(dev)),
                    "rx_lin_tower_bwd")
         out = [dx]

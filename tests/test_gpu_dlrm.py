@@ -148,3 +148,25 @@ def test_dlrm_graph_cycle_matches_eager(fused_sgd):
     torch.cuda.synchronize()
     for (n, a), (_, b) in zip(m_e.state_dict().items(), m_g.state_dict().items()):
         assert torch.allclose(a.float(), b.float(), rtol=1e-3, atol=1e-4), n
+
+
+@pytest.mark.parametrize("D", [32, 128])
+def test_fused_lookup_interaction_matches_two_kernel_path(D):
+    """FusedEmbeddings.interact (gather + interaction in one kernel; interaction backward with the
+    embedding SGD in its epilogue) against the separate gather -> dot_interaction path."""
+    torch.manual_seed(4)
+    sizes = [40, 3, 77, 500]
+    a = FusedEmbeddings(sizes, D, fused_sgd_lr=0.1).cuda()
+    b = copy.deepcopy(a)
+    idx = torch.stack([torch.randint(0, s, (203,)) for s in sizes], dim=1).cuda()
+    idx[:9] = 1                                   # duplicate rows: atomic accumulation
+    mlp_a = torch.randn(203, D, device="cuda", requires_grad=True)
+    mlp_b = mlp_a.detach().clone().requires_grad_(True)
+    za = a.interact(mlp_a, idx)
+    zb = dot_interaction(b(mlp_b, idx))
+    assert torch.equal(za, zb)
+    g = torch.randn_like(za)
+    za.backward(g)
+    zb.backward(g)
+    torch.testing.assert_close(mlp_a.grad, mlp_b.grad, rtol=0, atol=0)
+    torch.testing.assert_close(a.weight.detach(), b.weight.detach(), rtol=1e-6, atol=1e-6)

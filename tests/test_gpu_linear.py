@@ -204,3 +204,24 @@ def test_gemm_all_epilogues_ragged(splits, tile, shape):
     L.gemm(L.WGRAD, K, N, M, Xb, L.RED, G, L.RED, dW, dbias=db, splits=splits, tile=tile)
     assert _rel(dW, _bf(Xb).T @ G.float()) < 1e-5
     assert _rel(db, _bf(Xb).sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("M", [128, 2048])
+def test_paired_backward_is_bitwise_the_two_launch_backward(M, monkeypatch):
+    """lin_pair_kernel (a layer's dgrad + wgrad in one launch) computes exactly what the two
+    separate launches compute: same tiles, same split-K order (each problem has its own half
+    of the workspace)."""
+    from raydp_amd.ops import linear_ops
+    from raydp_amd.ops.linear_ops import FusedLinearTower
+    dims, relus = [384, 1024, 1024, 512, 256, 1], [True] * 4 + [False]
+    out = {}
+    for pair in (False, True):
+        monkeypatch.setattr(linear_ops, "PAIR_BACKWARD", pair)
+        lins, _ = _tower(dims, relus, seed=7)
+        tower = FusedLinearTower(lins, relus, out_f32=True)
+        g = torch.Generator(device="cuda").manual_seed(5)
+        x = torch.randn(M, dims[0], device="cuda", generator=g).requires_grad_(True)
+        tower(x).backward(torch.randn(M, 1, device="cuda", generator=g))
+        out[pair] = [x.grad.clone()] + [t.grad.clone() for lin in lins for t in (lin.weight, lin.bias)]
+    for a, b in zip(out[False], out[True]):
+        assert torch.equal(a, b)
