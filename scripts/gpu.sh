@@ -8,6 +8,7 @@
 #   scripts/gpu.sh prof NAME CMD...              rocprofv3 kernel trace + stats -> gpurun_out/prof/NAME
 #   scripts/gpu.sh pmc PASS bench|lin            one PMC counter pass (1..3) -> gpurun_out/pmc
 #   scripts/gpu.sh dlrm [BATCH...]               DLRM train bench (graph + eager) -> gpurun_out/dlrm.jsonl
+#   scripts/gpu.sh e2e                           DLRM end-to-end bench (1/2 workers) -> gpurun_out/dlrm_e2e.jsonl
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 mkdir -p gpurun_out
@@ -68,5 +69,14 @@ case $cmd in
         >> gpurun_out/dlrm.jsonl 2>> gpurun_out/dlrm.err || exit 15
     done
     cat gpurun_out/dlrm.jsonl;;
-  *) echo "usage: scripts/gpu.sh tests|bench|rehearse|prof|pmc|dlrm ..."; exit 2;;
+  e2e)
+    # DLRM end to end (synthetic Criteo TSV -> preprocessing -> fit_on_spark): the notebook's
+    # batch 128 with 1 and 2 workers, and batch 2048 with 1 worker
+    for cfg in "128 50000 5000 2" "128 50000 5000 1" "2048 200000 20000 1"; do
+      set -- $cfg
+      timeout -k 10 400 python benchmarks/dlrm_e2e_bench.py --batch $1 --rows $2 --warmup-rows $3 --workers $4 \
+        >> gpurun_out/dlrm_e2e.jsonl 2>> gpurun_out/dlrm_e2e.err || exit 16
+    done
+    cut -c1-400 gpurun_out/dlrm_e2e.jsonl;;
+  *) echo "usage: scripts/gpu.sh tests|bench|rehearse|prof|pmc|dlrm|e2e ..."; exit 2;;
 esac
