@@ -9,6 +9,10 @@
 #   scripts/gpu.sh pmc PASS bench|lin            one PMC counter pass (1..3) -> gpurun_out/pmc
 #   scripts/gpu.sh dlrm [BATCH...]               DLRM train bench (graph + eager) -> gpurun_out/dlrm.jsonl
 #   scripts/gpu.sh e2e                           DLRM end-to-end bench (1/2 workers) -> gpurun_out/dlrm_e2e.jsonl
+#   scripts/gpu.sh trace [N]                     span timeline of the estimator topology, N workers on the
+#                                                 one GPU (RAYDP_TRACE) -> gpurun_out/tr, *_timeline.txt
+#   scripts/gpu.sh xgmi [WORLD...]               one-shot xGMI collective bench, ranks share the GPU
+#   scripts/gpu.sh warm [WARM] [RUNS]            headline pipeline: per-run walls/phases after warm-up
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 mkdir -p gpurun_out
@@ -78,5 +82,23 @@ case $cmd in
         >> gpurun_out/dlrm_e2e.jsonl 2>> gpurun_out/dlrm_e2e.err || exit 16
     done
     cut -c1-400 gpurun_out/dlrm_e2e.jsonl;;
-  *) echo "usage: scripts/gpu.sh tests|bench|rehearse|prof|pmc|dlrm|e2e ..."; exit 2;;
+  trace)
+    N=${1:-2}
+    mkdir -p gpurun_out/tr; rm -f gpurun_out/tr/est.*
+    RAYDP_TRACE=gpurun_out/tr/est timeout -k 10 300 python bench.py --gpus $N --gpu-share $(python -c "print(1/$N)") \
+      --topology estimator --steps 20 --warmup 5 --no-reference-config > gpurun_out/trace_est.jsonl \
+      2> gpurun_out/trace_est.err || exit 17
+    python scripts/trace_summary.py gpurun_out/tr/est > gpurun_out/trace_est_timeline.txt 2>&1
+    head -60 gpurun_out/trace_est_timeline.txt;;
+  xgmi)
+    for W in ${@:-4 8}; do
+      timeout -k 10 300 python benchmarks/xgmi_bench.py --world $W >> gpurun_out/xgmi.jsonl \
+        2>> gpurun_out/xgmi.err || exit 18
+    done
+    cat gpurun_out/xgmi.jsonl;;
+  warm)
+    timeout -k 10 300 python scripts/dev/warm_gap.py --warm ${1:-3,2} --runs ${2:-8} >> gpurun_out/warm_gap.jsonl \
+      2>> gpurun_out/warm_gap.err || exit 19
+    cut -c1-300 gpurun_out/warm_gap.jsonl;;
+  *) echo "usage: scripts/gpu.sh tests|bench|rehearse|prof|pmc|dlrm|e2e|trace|xgmi|warm ..."; exit 2;;
 esac
