@@ -288,9 +288,12 @@ def main():
     for p, ws in warm_csvs:
         run_pipeline(spark, p, ws, n_train, storage, **kw)
     # long-lived framework state (modules, plans, kernels) goes to the permanent GC generation:
-    # a full collection over it costs ~100 ms and would land at random inside the timed region
+    # a full collection over it costs ~100 ms and would land at random inside the timed region.
+    # Freeze only, no gc.collect() first: collecting the warm-up's garbage hands its memory back
+    # and the next pipeline pays to fault it in again -- measured on the box, the first pipeline
+    # after collect+freeze took 7.0-8.0 ms against 4.7 ms after a plain freeze, every phase of it
+    # slower (profiles/r3s4_warm_gap_variants.txt; scripts/dev/warm_gap.py --gc)
     import gc
-    gc.collect()
     gc.freeze()
     from raydp_amd.utils.devmon import DeviceMonitor
     # power / HBM / activity of the node's GPUs during the timed region, sampled by a child

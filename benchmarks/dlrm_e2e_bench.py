@@ -90,7 +90,6 @@ def main():
         # code-object loads, executor-side compiled ETL programs), as bench.py does for NYC
         pipeline(warm, 1)
         import gc
-        gc.collect()
         gc.freeze()
     prof = None
     if args.profile_timed:

@@ -138,9 +138,11 @@ class GraphedTrainLoop:
         g = torch.cuda.CUDAGraph()
         self.e.zero_grad()
         # no garbage collection while capturing: a collected object owning a graph (or any HIP
-        # resource whose release is not capture-safe) would be destroyed mid-capture
+        # resource whose release is not capture-safe) would be destroyed mid-capture. No
+        # gc.collect() first either: pending garbage is collected after the capture, outside it,
+        # and a full collection here costs a heap walk plus re-faulting the freed memory in the
+        # steps that follow (profiles/r3s4_warm_gap_variants.txt)
         gc_was = gc.isenabled()
-        gc.collect()
         gc.disable()
         try:
             with torch.cuda.graph(g, pool=self.pool), _CaptureSafeIndexing(self.index_cache):

@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--runs", type=int, default=6)
     ap.add_argument("--pin", type=int, default=0, help="confine the process tree to this many CPUs")
-    ap.add_argument("--no-gc", action="store_true", help="skip the gc.collect + gc.freeze after warm-up")
+    ap.add_argument("--gc", choices=["collect_freeze", "freeze", "none"], default="freeze",
+                    help="what runs between the warm-up and the measured runs")
     args = ap.parse_args()
     if args.pin:
         cpus = sorted(os.sched_getaffinity(0))[:args.pin]
@@ -50,8 +51,9 @@ def main():
     for p, s in paths[:len(warm)]:
         bench.run_pipeline(spark, p, s, 1, storage, fused=cuda)
     import gc
-    if not args.no_gc:
+    if args.gc == "collect_freeze":
         gc.collect()
+    if args.gc != "none":
         gc.freeze()
     for i, (p, s) in enumerate(paths[len(warm):]):
         if cuda:
@@ -63,7 +65,7 @@ def main():
             torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         ph = {k: round(v * 1e3, 2) for k, v in list(LAST_TIMINGS.items()) + list(bench.DRIVER_TIMINGS.items())}
-        print(json.dumps({"run": i, "warm": args.warm, "pin": args.pin, "gc": not args.no_gc, "wall_ms": round(wall * 1e3, 2), "phases_ms": ph}), flush=True)
+        print(json.dumps({"run": i, "warm": args.warm, "pin": args.pin, "gc": args.gc, "wall_ms": round(wall * 1e3, 2), "phases_ms": ph}), flush=True)
     context.stop_spark()
     runtime.shutdown()
 

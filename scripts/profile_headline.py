@@ -44,7 +44,6 @@ def main():
     for p in paths[:3]:
         bench.run_pipeline(spark, p, args.steps, 1, storage)
     import gc
-    gc.collect()
     gc.freeze()
     phases, walls = {}, []
     prof = cProfile.Profile()
