@@ -37,7 +37,9 @@ for ps in sys.argv[1:] or ["1", "0"]:
 
 # timeline of the middle step of a persistent epoch (wall clock ticks, 10 ns)
 os.environ["RAYDP_MLP_PERSISTENT"] = "1"
-st = torch.zeros(64, dtype=torch.int64, device=dev)
+# the kernel writes the middle step's phase stamps at [0, 32) AND every step's start time at
+# [32 + s] (csrc/hip/mlp_persist.h RX_PS_STEP_STAMPS), so the buffer holds 32 + nsteps + 1 words
+st = torch.zeros(32 + n // 64 + 1, dtype=torch.int64, device=dev)
 tr.bufs.stamps = st.data_ptr()
 tr.train_epoch(feats, Yd, n, perm)
 torch.cuda.synchronize()
