@@ -293,8 +293,8 @@ def main():
     # and the next pipeline pays to fault it in again -- measured on the box, the first pipeline
     # after collect+freeze took 7.0-8.0 ms against 4.7 ms after a plain freeze, every phase of it
     # slower (profiles/r3s4_warm_gap_variants.txt; scripts/dev/warm_gap.py --gc)
-    import gc
-    gc.freeze()
+    from raydp_amd.utils.gcmeter import GcMeter, freeze_long_lived
+    freeze_long_lived()
     from raydp_amd.utils.devmon import DeviceMonitor
     # power / HBM / activity of the node's GPUs during the timed region, sampled by a child
     # process (rank 0 only; it touches no HIP context and no Python state of the pipeline)
@@ -308,8 +308,9 @@ def main():
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    gcm = GcMeter()
     t0 = time.perf_counter()
-    with tracing.span("timed run", cat="bench"):
+    with tracing.span("timed run", cat="bench"), gcm:
         res = run_pipeline(spark, main_csv, args.steps, n_train, storage, **kw)
         barrier()
     dt = time.perf_counter() - t0
@@ -358,6 +359,7 @@ def main():
                        if res.metrics_history else None,
                        "step_time_us": res.metrics_history[0].get("step_time_us") if res.metrics_history else None,
                        "device_telemetry": mon.summary() if mon is not None else None,
+                       "python_gc_in_timed_region": gcm.summary(),
                        "hbm_peak_allocated_mib": round(torch.cuda.max_memory_allocated() / 2 ** 20, 1),
                        "rank0_breakdown_s": dict({k: round(v, 4) for k, v in LAST_TIMINGS.items()},
                                                  **{k: round(v, 4) for k, v in DRIVER_TIMINGS.items()},

@@ -32,6 +32,8 @@ def main():
                     help="TorchEstimator num_workers (the notebook uses 2); > GPUs rehearses on a share "
                          "of one GPU (gloo bootstrap)")
     ap.add_argument("--fused-sgd", action="store_true", help="embedding SGD applied inside backward")
+    ap.add_argument("--gc-freeze", type=int, default=1,
+                    help="move the warmed-up process state to the permanent GC generation before timing")
     ap.add_argument("--profile-timed", default=None, help="cProfile the timed region into this file")
     ap.add_argument("--warmup-rows", type=int, default=20_000,
                     help="rows of an untimed warm-up run of the same pipeline (0: none)")
@@ -89,17 +91,20 @@ def main():
         # torch._dynamo on the first optimizer, pandas on the first empty Arrow table, kernel
         # code-object loads, executor-side compiled ETL programs), as bench.py does for NYC
         pipeline(warm, 1)
-        import gc
-        gc.freeze()
+    from raydp_amd.utils.gcmeter import GcMeter, freeze_long_lived
+    if args.gc_freeze:
+        freeze_long_lived()
     prof = None
     if args.profile_timed:
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
     t_ns = time.time_ns()
+    gcm = GcMeter()
     t0 = time.perf_counter()
-    res, sizes, t_plan, t_est = pipeline(path, args.epochs)
-    torch.cuda.synchronize()
+    with gcm:
+        res, sizes, t_plan, t_est = pipeline(path, args.epochs)
+        torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     tracing.complete("timed run", t_ns, cat="bench")
     if prof is not None:
@@ -126,6 +131,7 @@ def main():
         "final_train_loss": hist[-1]["train_loss"] if hist else None,
         "phases_s": {"plan_build": round(t_plan - t0, 4), "model_and_estimator_init": round(t_est - t_plan, 4),
                      **{k: round(v, 4) for k, v in LAST_TIMINGS.items()}},
+        "python_gc_in_timed_region": gcm.summary(), "gc_freeze": bool(args.gc_freeze),
         "synthetic_generation_s (untimed)": round(gen_s, 2),
         "warmup_rows (untimed)": args.warmup_rows,
         "data": "synthetic Criteo-shaped TSV (dlrm_data.synthetic_criteo), random-init weights",

@@ -55,7 +55,13 @@ def main():
         gc.collect()
     if args.gc != "none":
         gc.freeze()
+    gcs = []   # (phase, generation, t) of every collection during the measured runs
+
+    def on_gc(phase, info):
+        gcs.append((phase, info["generation"], time.perf_counter()))
+    gc.callbacks.append(on_gc)
     for i, (p, s) in enumerate(paths[len(warm):]):
+        gcs.clear()
         if cuda:
             torch.cuda.synchronize()
         bench.DRIVER_TIMINGS.clear()
@@ -64,8 +70,15 @@ def main():
         if cuda:
             torch.cuda.synchronize()
         wall = time.perf_counter() - t0
+        gc_ms, gen_n, t_start = 0.0, [0, 0, 0], {}
+        for phase, g, t in gcs:
+            if phase == "start":
+                t_start[g] = t
+            elif g in t_start:
+                gc_ms += t - t_start.pop(g)
+                gen_n[g] += 1
         ph = {k: round(v * 1e3, 2) for k, v in list(LAST_TIMINGS.items()) + list(bench.DRIVER_TIMINGS.items())}
-        print(json.dumps({"run": i, "warm": args.warm, "pin": args.pin, "gc": args.gc, "wall_ms": round(wall * 1e3, 2), "phases_ms": ph}), flush=True)
+        print(json.dumps({"run": i, "warm": args.warm, "pin": args.pin, "gc": args.gc, "wall_ms": round(wall * 1e3, 2), "gc_ms": round(gc_ms * 1e3, 2), "gc_collections": gen_n, "phases_ms": ph}), flush=True)
     context.stop_spark()
     runtime.shutdown()
 
