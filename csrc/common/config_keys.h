@@ -27,6 +27,7 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.mlp_persistent", "RAYDP_MLP_PERSISTENT", "1"},
     {"spark.ray.mi355x.mlp_persistent.timeout_s", "RAYDP_MLP_PERSISTENT_TIMEOUT_S", "5"},
     {"spark.ray.mi355x.fused_linear", "RAYDP_FUSED_LINEAR", "1"},
+    {"spark.ray.mi355x.driver_gc_freeze", "RAYDP_DRIVER_GC_FREEZE", "1"},
     {"spark.ray.mi355x.ddp.bucket_mb", "RAYDP_DDP_BUCKET_MB", "32"},
     {"spark.ray.mi355x.object_store_bytes", "RAYDP_OBJECT_STORE_BYTES", "0"},
     {"spark.ray.mi355x.trace", "RAYDP_TRACE", ""},

@@ -118,7 +118,9 @@ def init_spark(app_name: str, num_executors: int, executor_cores: int,
                     app_name, num_executors, executor_cores, executor_memory, enable_hive,
                     fault_tolerant_mode, placement_group_strategy, placement_group,
                     placement_group_bundle_indexes, configs)
-                return _global_spark_context.get_or_create_session()
+                session = _global_spark_context.get_or_create_session()
+                _freeze_driver_heap()
+                return session
             except BaseException:
                 if _global_spark_context is not None:
                     _global_spark_context.stop()
@@ -126,6 +128,17 @@ def init_spark(app_name: str, num_executors: int, executor_cores: int,
                 raise
         else:
             raise Exception("The spark environment has inited.")
+
+
+def _freeze_driver_heap():
+    """Everything alive once the session is up -- imported modules, the runtime, the executors'
+    handles -- lives as long as the driver: out of the collector's reach it costs nothing in the
+    full collections that otherwise walk it at random points of the user's job
+    (``spark.ray.mi355x.driver_gc_freeze``)."""
+    from raydp_amd.utils.config import get as conf_get
+    if conf_get("spark.ray.mi355x.driver_gc_freeze"):
+        from raydp_amd.utils.gcmeter import freeze_long_lived
+        freeze_long_lived()
 
 
 def stop_spark(cleanup_data=True):

@@ -27,3 +27,17 @@ def test_freeze_moves_live_objects_out_of_collections():
     finally:
         gc.unfreeze()
     assert gc.get_freeze_count() == 0
+
+
+def test_init_spark_freezes_driver_heap(monkeypatch):
+    """spark.ray.mi355x.driver_gc_freeze: the objects alive once the session is up are out of
+    the collector's reach (a full collection afterwards walks only what the job creates)."""
+    import raydp_amd
+    gc.unfreeze()
+    spark = raydp_amd.init_spark("gc-freeze", 1, 1, "500M")
+    try:
+        assert gc.get_freeze_count() > 10000
+        assert spark.range(0, 10).count() == 10
+    finally:
+        raydp_amd.stop_spark()
+        gc.unfreeze()
