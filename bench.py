@@ -298,7 +298,8 @@ def main():
     from raydp_amd.utils.devmon import DeviceMonitor
     # power / HBM / activity of the node's GPUs during the timed region, sampled by a child
     # process (rank 0 only; it touches no HIP context and no Python state of the pipeline)
-    mon = DeviceMonitor(interval_s=0.005) if local == 0 else None
+    mon = DeviceMonitor(interval_s=0.005) if local == 0 and os.environ.get("RAYDP_BENCH_DEVMON", "1") != "0" \
+        else None
     if mon is not None:
         mon.__enter__()
     barrier()

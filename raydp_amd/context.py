@@ -135,10 +135,26 @@ def _freeze_driver_heap():
     handles -- lives as long as the driver: out of the collector's reach it costs nothing in the
     full collections that otherwise walk it at random points of the user's job
     (``spark.ray.mi355x.driver_gc_freeze``)."""
+    global _gc_frozen
     from raydp_amd.utils.config import get as conf_get
     if conf_get("spark.ray.mi355x.driver_gc_freeze"):
         from raydp_amd.utils.gcmeter import freeze_long_lived
         freeze_long_lived()
+        _gc_frozen = True
+
+
+_gc_frozen = False
+
+
+def _unfreeze_driver_heap():
+    """stop_spark: the frozen objects go back to the oldest generation, so whatever of them the
+    stopped session leaves unreachable is reclaimed (repeated init/stop in one process would
+    otherwise keep every session's garbage)."""
+    global _gc_frozen
+    if _gc_frozen:
+        import gc
+        gc.unfreeze()
+        _gc_frozen = False
 
 
 def stop_spark(cleanup_data=True):
@@ -150,6 +166,7 @@ def stop_spark(cleanup_data=True):
             finally:
                 if cleanup_data is True:
                     _global_spark_context = None
+                    _unfreeze_driver_heap()
 
 
 atexit.register(stop_spark)
