@@ -330,12 +330,18 @@ def main():
         mon = DeviceMonitor(interval_s=0.005) if local == 0 else None
         if mon is not None:
             mon.__enter__()
-        barrier()
-        run_pipeline(spark, main_csv, args.steps, n_train, storage, **kw)
-        barrier()
+        err = None
+        try:
+            barrier()
+            run_pipeline(spark, main_csv, args.steps, n_train, storage, **kw)
+            barrier()
+        except Exception as e:  # noqa: BLE001 - telemetry never costs the measurement
+            err = repr(e)[-300:]
         if mon is not None:
             mon.__exit__(None, None, None)
             telemetry = dict(mon.summary(), region="an untimed repeat of the timed pipeline")
+            if err:
+                telemetry["repeat_error"] = err
     t = torch.tensor([dt], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
