@@ -27,6 +27,7 @@ import ctypes
 import itertools
 import struct
 import threading
+import weakref
 from typing import Dict, List, Optional, Tuple
 
 import pyarrow as pa  # noqa: F401 - libarrow must be loaded (pyarrow's copy) before ours
@@ -274,7 +275,11 @@ def lower(fn) -> Optional[Lowered]:
 # ------------------------------------------------------------------------------------------
 # the UDF bridge (called from the C++ worker threads; ctypes takes the GIL)
 # ------------------------------------------------------------------------------------------
-_REGISTRY: "Dict[int, Lowered]" = {}
+# key -> Lowered, for the UDF bridge of a task in flight. Weak: a stage's Lowered lives as long
+# as its plan (the executor keeps the last 16 stage functions), and a task's caller holds it
+# until the task is waited for -- a strong registry kept every stage's plan tree and C++ stage
+# handle for the executor's whole life.
+_REGISTRY: "weakref.WeakValueDictionary[int, Lowered]" = weakref.WeakValueDictionary()
 
 
 def _tap_impl(user, seg, m, vals, valids, nulls) -> int:

@@ -226,3 +226,27 @@ def test_python_cache_fallback_has_the_same_interface(store):
     assert c.cache_list("r") == [0] and c.cached_rdds() == ["r"]
     assert c.cache_unpersist("r", store) == 1 and not store.contains(oid)
     assert not c.available and native_exec.NativeExecutor.available
+
+
+def test_lowered_stages_do_not_outlive_their_plans(spark, store):
+    """The UDF bridge's key -> stage registry is weak: an executor that runs stage after stage
+    keeps only the stages whose plans are still alive (it caches the last 16 stage functions),
+    not every plan tree and C++ stage handle it ever lowered."""
+    import gc
+
+    import pandas as pd
+    import raydp_amd.spark.functions as F
+    before = len(native_exec._REGISTRY)
+    keys = []
+    for k in range(6):
+        df = spark.createDataFrame(pd.DataFrame({"x": np.arange(100.0) + k}))
+        plan = df.withColumn("y", F.col("x") * 2.0)._src()
+        low = native_exec.lower(plan.compute)
+        assert low is not None
+        keys.append(low.key)
+        statuses, _ = _run_all(low, plan.compute, store, plan.num_partitions())
+        assert all(s == native_exec.OK for s in statuses)
+        del df, plan, low
+    gc.collect()
+    assert not any(k in native_exec._REGISTRY for k in keys)
+    assert len(native_exec._REGISTRY) <= before
