@@ -36,7 +36,7 @@ OK, FALLBACK, RETRY, ERROR = 0, 1, 2, -1
 _ERRLEN = 1024
 
 STATS = {"native_tasks": 0, "native_fallbacks": 0, "native_retries": 0, "native_errors": 0,
-         "lowered_stages": 0, "not_lowered": 0, "native_csv_reads": 0}
+         "lowered_stages": 0, "not_lowered": 0, "native_csv_reads": 0, "stage_reuse": 0}
 LAST_ERROR = [None]     # message of the last native task that failed (then run in Python)
 
 _TAPFN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
@@ -158,6 +158,19 @@ class Lowered:
         self.segs_ref = None
         self.key = next(Lowered._ids)
         self.handle = None
+        self._owner = None     # _StageHandle: the C++ stage, shared by lowerings of one chain
+
+    def _source_key(self):
+        """What of the source the C++ stage spec encodes (not the file or partition: those
+        come with each task)."""
+        src = self.csv
+        if src is None:
+            return None
+        return (bool(src.header), src.sep, src.null_value or "",
+                tuple((f.name, str(f.type)) for f in src.schema()))
+
+    def adopt(self, owner: "_StageHandle", segs) -> None:
+        self._owner, self.handle, self.segs_ref = owner, owner.h, segs
 
     def build(self, segs) -> bool:
         import numpy as np
@@ -228,14 +241,29 @@ class Lowered:
         h = lib.rx_stage_create(spec, len(spec), err, _ERRLEN)
         if not h:
             return False
-        self.handle = h
-        self.segs_ref = segs
+        self.adopt(_StageHandle(h), segs)
         return True
 
+
+class _StageHandle:
+    """Owner of one C++ stage (``rx_stage_create``): destroyed when the last lowering that
+    uses it and the stage cache have both let go of it."""
+
+    def __init__(self, h):
+        self.h = h
+
     def __del__(self):
-        h, self.handle = self.handle, None
+        h, self.h = self.h, None
         if h and _lib_handle is not None:
             _lib_handle.rx_stage_destroy(h)
+
+
+# (compiled chain, source spec) -> (segments, stage handle): each fit of the same pipeline
+# builds a new plan tree over new data, but its chain compiles to the same cached segments
+# (exprc.segments_for), so the executor reuses the C++ stage built for them instead of
+# re-encoding and re-creating it on the critical path of every conversion stage.
+_STAGES: "Dict[tuple, tuple]" = {}
+_STAGES_MAX = 32
 
 
 def lower(fn) -> Optional[Lowered]:
@@ -263,9 +291,22 @@ def lower(fn) -> Optional[Lowered]:
         return None
     csv = base.source if isinstance(base, SourcePlan) and isinstance(base.source, CsvSource) else None
     low = Lowered(top, base, [s[1] for s in segs], csv)
-    if not low.build(segs):
-        STATS["not_lowered"] += 1
-        return None
+    try:
+        skey = (id(segs), low._source_key())
+    except Exception:  # noqa: BLE001 - a source whose schema cannot be read here: no reuse
+        skey = None
+    hit = _STAGES.get(skey) if skey is not None else None
+    if hit is not None and hit[0] is segs:
+        low.adopt(hit[1], segs)
+        STATS["stage_reuse"] += 1
+    else:
+        if not low.build(segs):
+            STATS["not_lowered"] += 1
+            return None
+        if skey is not None and low.csv is csv:     # (build drops an unencodable CSV source)
+            if len(_STAGES) >= _STAGES_MAX:
+                _STAGES.pop(next(iter(_STAGES)))
+            _STAGES[skey] = (segs, low._owner)     # keeps segs alive: its id stays unique
     STATS["lowered_stages"] += 1
     top.__dict__["_native_lowered"] = low
     _REGISTRY[low.key] = low

@@ -250,3 +250,22 @@ def test_lowered_stages_do_not_outlive_their_plans(spark, store):
     gc.collect()
     assert not any(k in native_exec._REGISTRY for k in keys)
     assert len(native_exec._REGISTRY) <= before
+
+
+def test_refit_of_the_same_chain_reuses_the_native_stage(spark, tmp_path, store):
+    """A second pipeline of the same shape over new data compiles to the same cached segments:
+    its lowering adopts the C++ stage built for the first one (no re-encode / re-create on the
+    executor's critical path) and still produces exactly the Python path's result."""
+    lows = []
+    for seed in (3, 4):
+        spark.conf.set("spark.sql.files.maxPartitionBytes", str(80 << 10))
+        df = _etl(spark.read.csv(_csv(tmp_path, seed=seed), header=True, inferSchema=True))
+        plan = df._src()
+        before = native_exec.STATS["stage_reuse"]
+        low = native_exec.lower(plan.compute)
+        assert low is not None
+        statuses, _ = _run_all(low, plan.compute, store, plan.num_partitions())
+        assert all(s == native_exec.OK for s in statuses)
+        lows.append((low, native_exec.STATS["stage_reuse"] - before))
+    (a, _), (b, reused) = lows
+    assert reused == 1 and a is not b and a.handle == b.handle and a.key != b.key
