@@ -32,6 +32,7 @@ class RayDPExecutor:
         self.app_id = app_id
         self.cores = cores
         self.conf = dict(conf)
+        self._size_thread_pools(cores)
         # the session's spark.ray.mi355x.* settings (e.g. fused_etl) reach executor-side code
         # through the environment, as they reach trainer workers
         import os
@@ -61,6 +62,19 @@ class RayDPExecutor:
             shuffle.set_local_service(self.registration.shuffle_socket)
         else:
             self.spark_executor_id = executor_id
+
+    @staticmethod
+    def _size_thread_pools(cores) -> int:
+        """An executor computes with ``spark.executor.cores`` cores, as a Spark executor does:
+        Arrow's CPU pool would otherwise start one thread per CPU the host shows (256 on an
+        MI355X node) in every executor, and a node of executors oversubscribes the cores it
+        was given (on a CPU-quota'd host the whole job then stalls on throttling)."""
+        import pyarrow as pa
+        if os.environ.get("RAYDP_EXECUTOR_SIZE_POOLS", "1") == "0":     # escape hatch / A-B
+            return pa.cpu_count()
+        n = max(1, int(cores))
+        pa.set_cpu_count(n)
+        return n
 
     @staticmethod
     def _warm_up():

@@ -352,3 +352,16 @@ def test_colocated_stores_share_the_node_shm_budget(monkeypatch):
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
     one = S.default_capacity()
     assert one >= min(64 << 30, 4 * max(s.capacity for s in stores)), one
+
+
+def test_executor_sizes_arrow_pool_to_its_cores():
+    """An executor's Arrow CPU pool is its spark.executor.cores, not the host's CPU count."""
+    import pyarrow as pa
+
+    from raydp_amd.spark.executor import RayDPExecutor
+    before = pa.cpu_count()
+    try:
+        assert RayDPExecutor._size_thread_pools(2) == 2 and pa.cpu_count() == 2
+        assert RayDPExecutor._size_thread_pools(0) == 1 and pa.cpu_count() == 1
+    finally:
+        pa.set_cpu_count(before)
