@@ -37,16 +37,13 @@ def init(comm=None, process_sets=None):
         if not _pg_ready():
             world = int(os.environ.get("WORLD_SIZE", os.environ.get("HOROVOD_SIZE", "1")))
             rank = int(os.environ.get("RANK", os.environ.get("HOROVOD_RANK", "0")))
-            if world == 1:
-                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-                if "MASTER_PORT" not in os.environ:
-                    import socket
-                    s = socket.socket()
-                    s.bind(("127.0.0.1", 0))
-                    os.environ["MASTER_PORT"] = str(s.getsockname()[1])
-                    s.close()
             backend = "nccl" if torch.cuda.is_available() else "gloo"
-            dist.init_process_group(backend, rank=rank, world_size=world)
+            if world == 1:
+                # a single rank needs no rendezvous: an in-memory store (no port, nothing left
+                # in the environment for the next init); the collectives below short-circuit
+                dist.init_process_group(backend, store=dist.HashStore(), rank=0, world_size=1)
+            else:
+                dist.init_process_group(backend, rank=rank, world_size=world)
             _state["owned"] = True
         _state["init"] = True
 
@@ -126,11 +123,13 @@ def _resolve_op(average, op):
 class _Handle:
     def __init__(self, work, tensor, post=None):
         self.work, self.tensor, self.post = work, tensor, post
+        self.done = False
 
     def wait(self):
-        if self.work is not None:
-            self.work.wait()
-            self.work = None
+        if not self.done:
+            if self.work is not None:
+                self.work.wait()
+            self.work, self.done = None, True
             if self.post is not None:
                 self.post(self.tensor)
         return self.tensor
@@ -141,7 +140,8 @@ def allreduce_async_(tensor, average=None, name=None, op=None, prescale_factor=1
     op = _resolve_op(average, op)
     if prescale_factor != 1.0:
         tensor.mul_(prescale_factor)
-    work = dist.all_reduce(tensor, op=_reduce_op(op), async_op=True)
+    # one rank: every reduction is the identity (no communicator is ever built)
+    work = dist.all_reduce(tensor, op=_reduce_op(op), async_op=True) if size() > 1 else None
     scale = postscale_factor / size() if op in (Average, Adasum) else postscale_factor
 
     def post(t):
@@ -159,7 +159,7 @@ def synchronize(handle):
 
 
 def poll(handle) -> bool:
-    return handle.work is None or handle.work.is_completed()
+    return handle.done or handle.work is None or handle.work.is_completed()
 
 
 def allreduce_(tensor, average=None, name=None, op=None, prescale_factor=1.0, postscale_factor=1.0):
@@ -181,6 +181,8 @@ def grouped_allreduce(tensors, average=None, name=None, op=None):
 def allgather(tensor, name=None):
     """Concatenate every rank's tensor along dim 0 (first dimensions may differ)."""
     _check()
+    if size() == 1:
+        return tensor.detach().clone()
     n = torch.tensor([tensor.shape[0]], device=tensor.device)
     sizes = [torch.zeros_like(n) for _ in range(size())]
     dist.all_gather(sizes, n)
@@ -194,7 +196,8 @@ def allgather(tensor, name=None):
 
 def broadcast_(tensor, root_rank, name=None):
     _check()
-    dist.broadcast(tensor, root_rank)
+    if size() > 1:
+        dist.broadcast(tensor, root_rank)
     return tensor
 
 
@@ -204,6 +207,8 @@ def broadcast(tensor, root_rank, name=None):
 
 def broadcast_object(obj, root_rank=0, name=None):
     _check()
+    if size() == 1:
+        return obj
     box = [obj if rank() == root_rank else None]
     dist.broadcast_object_list(box, src=root_rank)
     return box[0]
@@ -211,6 +216,8 @@ def broadcast_object(obj, root_rank=0, name=None):
 
 def allgather_object(obj, name=None):
     _check()
+    if size() == 1:
+        return [obj]
     out = [None] * size()
     dist.all_gather_object(out, obj)
     return out
@@ -219,6 +226,8 @@ def allgather_object(obj, name=None):
 def alltoall(tensor, splits=None, name=None):
     _check()
     w = size()
+    if w == 1:
+        return tensor.detach().clone()
     if splits is None:
         assert tensor.shape[0] % w == 0
         splits = [tensor.shape[0] // w] * w
@@ -234,7 +243,8 @@ def alltoall(tensor, splits=None, name=None):
 
 def barrier():
     _check()
-    dist.barrier()
+    if size() > 1:
+        dist.barrier()
 
 
 def join(device=-1):
@@ -248,7 +258,7 @@ def broadcast_parameters(params, root_rank: int = 0):
     _check()
     items = params.items() if isinstance(params, dict) else params
     for _, p in sorted(items, key=lambda kv: kv[0]) if isinstance(params, dict) else items:
-        if torch.is_tensor(p):
+        if torch.is_tensor(p) and size() > 1:
             t = p.data if isinstance(p, torch.nn.Parameter) else p
             dist.broadcast(t, root_rank)
 
@@ -256,6 +266,8 @@ def broadcast_parameters(params, root_rank: int = 0):
 def broadcast_optimizer_state(optimizer, root_rank: int = 0):
     """Make every rank's optimizer state (hyper-parameters and buffers) equal to ``root_rank``'s."""
     _check()
+    if size() == 1:
+        return
     opt = getattr(optimizer, "_inner", optimizer)
     sd = opt.state_dict()
     moved = {}
