@@ -106,6 +106,69 @@ __global__ __launch_bounds__(kThreads) void xg_allreduce_kernel(XgDev x, float* 
   }
 }
 
+// Two-shot in-place all-reduce (all-pairs reduce-scatter, then all-gather) of n floats, n a
+// multiple of 4 and buf 16-B aligned. The bucket is cut into `world` chunks of chunk4 float4s;
+// rank r owns chunk r:
+//   1. every rank publishes its whole bucket in its slot; launch-wide rendezvous (seq s0)
+//   2. rank r reads chunk r of every peer's slot (S/N bytes over each link, all links at once),
+//      sums in rank order, scales, writes the result into buf AND over chunk r of its own slot
+//      (no peer reads that chunk of this slot: peer q reads chunk q); rendezvous (seq s0 + 1)
+//   3. rank r copies every peer's reduced chunk p out of peer p's slot into buf.
+// Per link 2S/N bytes against the one-shot kernel's S: the path for buckets large enough that
+// link bandwidth, not the extra flag round, sets the time. Every element
+// is reduced by one rank only, so all ranks hold bit-identical sums.
+// Sequencing: one call consumes THREE sequence numbers (s0, s0 + 1, and s0 + 2 unused), so the
+// next call's first number has the other parity and uses the other slot, exactly as after a
+// one-shot call (which consumes one): slot reuse stays two calls apart whatever the mix.
+__global__ __launch_bounds__(kThreads) void xg_allreduce2_kernel(XgDev x, float* __restrict__ buf, int n,
+                                                                 int chunk4, float scale) {
+  const unsigned s0 = __hip_atomic_load(x.ctl + kXgDevSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int par = (int)(s0 & 1u);
+  float4* mine = reinterpret_cast<float4*>(x.region[x.rank] + (size_t)par * x.nf);
+  float4* b4 = reinterpret_cast<float4*>(buf);
+  const int n4 = n >> 2;
+  const int stride = gridDim.x * kThreads;
+  const int t = blockIdx.x * kThreads + threadIdx.x;
+  for (int i = t; i < n4; i += stride) mine[i] = b4[i];
+  if (!rx_xg_grid_rendezvous(x, s0, gridDim.x)) return;
+  {
+    const int c0 = x.rank * chunk4;
+    const int c1 = min(n4, c0 + chunk4);
+    for (int i = c0 + t; i < c1; i += stride) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int p = 0; p < x.world; ++p) {   // rank order: the same sum whichever rank owns it
+        const float4 v = p == x.rank ? b4[i] : rx_xg_load4(x.region[p] + (size_t)par * x.nf, (size_t)i);
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+      }
+      s.x *= scale;
+      s.y *= scale;
+      s.z *= scale;
+      s.w *= scale;
+      mine[i] = s;
+      b4[i] = s;
+    }
+  }
+  if (!rx_xg_grid_rendezvous(x, s0 + 1u, gridDim.x)) return;
+  for (int p = 0; p < x.world; ++p) {
+    if (p == x.rank) continue;
+    const int c0 = p * chunk4;
+    const int c1 = min(n4, c0 + chunk4);
+    const float* from = x.region[p] + (size_t)par * x.nf;
+    for (int i = c0 + t; i < c1; i += stride) b4[i] = rx_xg_load4(from, (size_t)i);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(x.ctl + kXgDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(x.ctl + kXgDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(x.ctl + kXgDevSeq, s0 + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // All-gather of n floats (raw 4-byte words of any dtype) per rank: dst[p * n + i] = rank p's
 // src[i]. Device-sequenced like the all-reduce (capturable); VEC: src and dst 16-B aligned and
 // n a multiple of 4.
@@ -338,6 +401,29 @@ int rx_xg_allreduce_scaled(float* buf, int n, float scale, void* ctx, hipStream_
   else
     hipLaunchKernelGGL(xg_allreduce_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, buf,
                        n, hseq, scale);
+  return (int)hipGetLastError();
+}
+
+// Two-shot in-place all-reduce (device-sequenced communicators only; n % 4 == 0 and buf 16-B
+// aligned, else -4 and the caller takes the one-shot path). -2: n outside the slot; -3:
+// host-sequenced communicator.
+int rx_xg_allreduce2_scaled(float* buf, int n, float scale, void* ctx, hipStream_t stream) {
+  XgHost* h = (XgHost*)ctx;
+  if (h->host_seq) return -3;
+  if (n < 0 || n > h->dev.nf) return -2;
+  if (n == 0) return 0;
+  if ((n & 3) || (reinterpret_cast<uintptr_t>(buf) & 15u)) return -4;
+  const int world = h->dev.world;
+  const int n4 = n >> 2;
+  const int chunk4 = (n4 + world - 1) / world;
+  // the busiest phase moves (world - 1) chunks per rank: ~4 float4 per thread before the grid
+  // grows, at most kMaxBlocks
+  const long units = (long)chunk4 * (world > 1 ? world - 1 : 1);
+  long blocks = (units + (long)kThreads * 4 - 1) / ((long)kThreads * 4);
+  if (blocks < 1) blocks = 1;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  hipLaunchKernelGGL(xg_allreduce2_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, stream, h->dev, buf, n, chunk4,
+                     scale);
   return (int)hipGetLastError();
 }
 

@@ -337,6 +337,7 @@ class _Fusion:
         if cur:
             self.buckets.append(cur)
         self.where = {id(p): b for b, ps in enumerate(self.buckets) for p in ps}
+        self.steps = 0
         self.reset()
 
     def reset(self):
@@ -366,6 +367,9 @@ class _Fusion:
         self.pending.append((b, flat, ctx, work, scaled))
 
     def finish(self):
+        self.steps += 1
+        if self._sum is not None and self.steps % 256 == 0:
+            self._sum.check()   # a timed-out xGMI exchange raises instead of drifting silently
         for b in range(len(self.buckets)):   # buckets never completed (unused params)
             if self.ready[b] != len(self.buckets[b]) and not any(x[0] == b for x in self.pending):
                 self._launch(b)

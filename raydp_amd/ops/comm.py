@@ -136,6 +136,20 @@ class XgmiComm:
                                              ctypes.c_void_p(self.ctx), _hip.stream_ptr(t.device))
         _hip.check(rc, "rx_xg_allreduce")
 
+    def allreduce2_(self, t, scale: float = 1.0) -> bool:
+        """Two-shot in-place sum (times ``scale``): all-pairs reduce-scatter + all-gather, 2S/N
+        bytes per xGMI link instead of the one-shot kernel's S (device-sequenced, capturable).
+        Needs a 16-B aligned tensor of a multiple of 4 floats; returns False (nothing launched)
+        otherwise, so the caller can take :meth:`allreduce_`."""
+        if t.numel() > self.max_floats:
+            raise ValueError(f"xGMI two-shot all-reduce of {t.numel()} floats > {self.max_floats}")
+        rc = self.lib.rx_xg_allreduce2_scaled(ctypes.c_void_p(t.data_ptr()), t.numel(), ctypes.c_float(scale),
+                                              ctypes.c_void_p(self.ctx), _hip.stream_ptr(t.device))
+        if rc == -4:
+            return False
+        _hip.check(rc, "rx_xg_allreduce2")
+        return True
+
     def allgather_(self, src, dst) -> None:
         """``dst`` (``world * src`` bytes, contiguous, same dtype family of 4-byte words or
         int64) receives every rank's ``src`` in rank order: one device-sequenced launch
@@ -180,8 +194,13 @@ class XgmiComm:
         _hip.check(rc, "rx_xg_vote")
 
     def check(self):
+        """Raise ``CollectiveError`` (and retire this communicator in this process) when any
+        exchange on it timed out. A set error word makes every later launch skip its exchange,
+        so the callers read it at their sync points (epoch end) instead of letting replicas
+        drift apart silently."""
         if self.error():
             from raydp_amd.exceptions import CollectiveError
+            forget_xgmi(self)
             raise CollectiveError("xGMI all-reduce: a peer did not arrive within the timeout")
 
     def close(self):
@@ -191,7 +210,10 @@ class XgmiComm:
 
     @classmethod
     def create(cls, nfloats: int, group=None, timeout_s: float = 30.0,
-               host_seq: bool = False) -> Optional["XgmiComm"]:
+               host_seq: bool = False, tag: str = "") -> Optional["XgmiComm"]:
+        """Collective: every rank of ``group`` calls it at the same point. ``tag`` keeps users
+        that launch on different streams apart (a communicator's launches must be serialised:
+        its sequence number lives on the device), e.g. the DDP buckets on the comm stream."""
         import socket
 
         import torch
@@ -201,12 +223,23 @@ class XgmiComm:
         world, rank = dist.get_world_size(group), dist.get_rank(group)
         if world < 2 or world > 16:
             return None
-        if _XGMI_DISABLED:
-            return None
         # the two sequencing modes share the flag words, so they never share a communicator
-        key = ("xg", id(group) if group is not None else "world", int(nfloats), bool(host_seq))
-        if key in _cache:
-            return _cache[key]
+        key = ("xg", id(group) if group is not None else "world", int(nfloats), bool(host_seq), tag)
+        # Agree first, with one collective, whatever the local state: a rank that retired xGMI
+        # (a peer timed out on it) or lost its cached communicator must not leave its peers in a
+        # different collective than itself. Any disabled rank -> None everywhere; any miss -> every
+        # rank rebuilds.
+        disabled, cached = _XGMI_DISABLED, _cache.get(key)
+        state = _agree_flags([int(disabled), int(cached is None)], group)
+        if state[0] or state[1]:
+            if cached is not None:
+                _cache.pop(key, None)
+                torch.cuda.synchronize()
+                cached.close()
+            if state[0]:
+                return None
+        else:
+            return cached
         comm, err = None, None
         try:
             comm = cls(world, rank, torch.cuda.current_device(), nfloats, timeout_s, host_seq)
@@ -273,6 +306,16 @@ def forget_xgmi(comm, disable: bool = True) -> None:
         _XGMI_DISABLED = True
 
 
+def _agree_flags(flags, group=None):
+    """Element-wise max of small integer flags over the group (one collective)."""
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor(list(flags), dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return [int(x) for x in t.tolist()]
+
+
 def _agree(ok: bool, group=None) -> bool:
     """True on every rank iff ``ok`` on every rank."""
     import torch
@@ -283,16 +326,24 @@ def _agree(ok: bool, group=None) -> bool:
     return int(t.item()) == 0
 
 
-XG_BUCKET_MAX_BYTES = 16 << 20  # largest one-shot bucket the communicator is sized for
+XG_BUCKET_MAX_BYTES = 16 << 20  # largest bucket the xGMI kernels are sized for
 
 
 def oneshot_max_bytes() -> int:
-    """Buckets up to this many bytes take the one-shot kernel (``spark.ray.mi355x.allreduce.
-    oneshot_max_mb``, capped at the communicator's ``XG_BUCKET_MAX_BYTES``). One-shot: each rank
-    reads the N-1 peer buckets concurrently, one per xGMI link, so it moves S bytes per link
-    whatever N; a ring moves 2(N-1)/N x S through every hop and pays 2(N-1) hand-offs."""
+    """Buckets up to this many bytes take an xGMI kernel (``spark.ray.mi355x.allreduce.
+    oneshot_max_mb``, capped at the communicator's ``XG_BUCKET_MAX_BYTES``); larger ones RCCL."""
     from raydp_amd.utils.config import get as conf_get
     return int(min(float(conf_get("spark.ray.mi355x.allreduce.oneshot_max_mb")) * (1 << 20), XG_BUCKET_MAX_BYTES))
+
+
+def twoshot_min_bytes() -> int:
+    """Buckets from this size on take the two-shot kernel when world > 2
+    (``spark.ray.mi355x.allreduce.twoshot_min_mb``). One-shot: every rank pulls the whole bucket
+    from each peer, S bytes per xGMI link, one flag round. Two-shot: 2S/N per link, two flag
+    rounds. At N = 8 the two-shot kernel moves 4x fewer bytes per link, which outweighs its
+    second round from about a MiB on."""
+    from raydp_amd.utils.config import get as conf_get
+    return int(float(conf_get("spark.ray.mi355x.allreduce.twoshot_min_mb")) * (1 << 20))
 
 
 class _Done:
@@ -305,22 +356,46 @@ class _Done:
         return True
 
 
+class _Joined:
+    """Handle of a bucket reduced on the comm stream: ``wait()`` makes the current stream wait
+    for it (an event join, capturable: the comm stream forks from and joins the captured one)."""
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def wait(self):
+        import torch
+        torch.cuda.current_stream().wait_stream(self.stream)
+        return True
+
+    def is_completed(self):
+        return self.stream.query()
+
+
 class BucketAllreduce:
     """All-reduce of gradient buckets for the DDP and Horovod wrappers.
 
-    fp32 buckets up to :func:`oneshot_max_bytes` go through the one-shot xGMI kernel
-    (stream-ordered, device-sequenced: capturable into a HIP graph, and the 1/world average
-    folded into the same pass); larger ones, other dtypes and non-RCCL groups use
-    ``torch.distributed.all_reduce``. Construct it on every rank at the same point (it runs
-    the collective xGMI set-up)."""
+    fp32 buckets up to :func:`oneshot_max_bytes` go through the xGMI kernels -- one-shot for small
+    buckets (and always at world 2), two-shot (all-pairs reduce-scatter + all-gather) from
+    :func:`twoshot_min_bytes` on -- with the 1/world average folded into the sum pass; larger
+    buckets, other dtypes and non-xGMI groups use ``torch.distributed.all_reduce``.
 
-    def __init__(self, group=None):
+    The xGMI launches go on a dedicated comm stream: a bucket that is ready forks the comm stream
+    off the compute stream (event), its reduction runs while backward continues, and ``wait()``
+    joins the comm stream back. Fork and join are events, so a captured HIP graph keeps the
+    concurrency. The communicator is this object's own (``tag``), because its launches are
+    ordered on the comm stream while other xGMI users (sharded embeddings) launch on the compute
+    stream. Construct it on every rank at the same point (it runs the collective xGMI set-up)."""
+
+    def __init__(self, group=None, overlap: Optional[bool] = None):
         import torch
         import torch.distributed as dist
         from raydp_amd.utils.config import get as conf_get
         self.group = group
         self.xg = None
+        self.stream = None
         self.limit = oneshot_max_bytes()
+        self.twoshot_min = twoshot_min_bytes()
         try:
             # gloo groups qualify too when the tensors are on the GPU (a rehearsal with several
             # ranks per device): the peer regions are bootstrapped over whatever group is given
@@ -328,36 +403,75 @@ class BucketAllreduce:
                     and torch.cuda.is_initialized() and conf_get("spark.ray.mi355x.allreduce") != "rccl"
                     and self.limit > 0):
                 self.xg = XgmiComm.create(XG_BUCKET_MAX_BYTES // 4, group=group,
-                                          timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"))
+                                          timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"),
+                                          tag="buckets")
         except Exception:  # noqa: BLE001
             self.xg = None
+        if overlap is None:
+            overlap = bool(conf_get("spark.ray.mi355x.ddp.comm_stream"))
+        if self.xg is not None and overlap:
+            self.stream = torch.cuda.Stream()
+        self.launched = {"oneshot": 0, "twoshot": 0, "torch": 0}
 
     @property
     def kind(self) -> str:
-        """What the buckets ride on: the one-shot xGMI kernel for small buckets (when the peer
+        """What the buckets ride on: the xGMI kernels for buckets up to the limit (when the peer
         mapping is up) and torch.distributed (RCCL / gloo) for the rest."""
         import torch.distributed as dist
         base = f"torch.distributed:{dist.get_backend(self.group)}" if dist.is_initialized() else "none"
         if self.xg is None:
             return base
-        return f"xgmi_oneshot(<={self.limit / (1 << 20):g}MiB)+{base}"
+        two = f",twoshot>={self.twoshot_min / (1 << 20):g}MiB" if self.xg.world > 2 else ""
+        return f"xgmi_oneshot(<={self.limit / (1 << 20):g}MiB{two}{',comm_stream' if self.stream else ''})+{base}"
 
     def routes_to_xgmi(self, flat) -> bool:
         import torch
         return (self.xg is not None and flat.is_cuda and flat.dtype == torch.float32 and flat.is_contiguous()
                 and flat.numel() * 4 <= self.limit and flat.numel() <= self.xg.max_floats)
 
-    def __call__(self, flat, scale: float = 1.0):
+    def _xg_launch(self, flat, scale):
+        if self.xg.world > 2 and flat.numel() * 4 >= self.twoshot_min and self.xg.allreduce2_(flat, scale):
+            self.launched["twoshot"] += 1
+            return
+        self.xg.allreduce_(flat, scale)
+        self.launched["oneshot"] += 1
+
+    def __call__(self, flat, scale: float = 1.0, overlap: bool = True):
         """Sum ``flat`` over ranks in place, times ``scale``. Returns a handle whose ``wait()``
-        orders the result before later work on the current stream."""
+        orders the result before later work on the current stream. ``overlap=False`` keeps the
+        reduction on the current stream (the caller needs it at once)."""
+        import torch
         import torch.distributed as dist
         if self.routes_to_xgmi(flat):
-            self.xg.allreduce_(flat, scale)
+            if self.stream is not None and overlap:
+                self.stream.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self.stream):
+                    self._xg_launch(flat, scale)
+                return _Joined(self.stream)
+            if self.stream is not None:
+                # every launch of this communicator stays on one stream, in program order
+                self.stream.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self.stream):
+                    self._xg_launch(flat, scale)
+                torch.cuda.current_stream().wait_stream(self.stream)
+                return _Done()
+            self._xg_launch(flat, scale)
             return _Done()
+        self.launched["torch"] += 1
         work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         if scale == 1.0:
             return work
         return _Scaled(work, flat, scale)
+
+    def check(self):
+        """Raise ``CollectiveError`` when an xGMI exchange of these buckets timed out (host sync:
+        call it where the caller syncs anyway, e.g. with the epoch's metrics)."""
+        if self.xg is not None:
+            try:
+                self.xg.check()
+            finally:
+                if self.xg.ctx is None or _XGMI_DISABLED:
+                    self.xg = None
 
 
 class _Scaled:

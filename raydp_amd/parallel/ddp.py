@@ -9,8 +9,11 @@ MI355X over RCCL/xGMI:
   straight into the buffer that is all-reduced -- no per-step copy in, no copy back out. A
   bucket's all-reduce is launched the moment its last gradient is accumulated, so
   communication overlaps the rest of backward;
-* fp32 buckets up to ``spark.ray.mi355x.allreduce.oneshot_max_mb`` (16 MiB) ride the one-shot
-  xGMI kernel with the 1/world average folded into its sum pass; larger ones go to RCCL;
+* fp32 buckets up to ``spark.ray.mi355x.allreduce.oneshot_max_mb`` (16 MiB) ride the xGMI
+  kernels (one-shot below ``twoshot_min_mb``, all-pairs two-shot above it at world > 2) with the
+  1/world average folded into the sum pass, on a dedicated comm stream (``ddp.comm_stream``):
+  the reduction of a finished bucket runs beside the rest of backward and the compute stream
+  joins it at the end of backward; larger buckets go to RCCL;
 * bucket size defaults to 32 MiB (``RAYDP_DDP_BUCKET_MB``): xGMI links are per-link bound
   (~153 GB/s per link), so fewer, larger messages amortise the ~10-20 us collective latency;
   tiny models (NYC_Model: 194 KB) end up in one bucket = one collective per step;
@@ -237,6 +240,20 @@ class DistributedDataParallel(nn.Module):
                     p.grad = b.views[pi]
         for p in self.sparse_params:
             p.grad = None
+
+    def check_comm(self):
+        """Raise ``CollectiveError`` if any xGMI exchange of this model (gradient buckets,
+        sharded-table all-to-alls, replicated-table row gathers) timed out: a timed-out exchange
+        leaves the communicator's error word set and every later launch skips its exchange, so
+        replicas would drift apart silently. One small D2H read per communicator: call it at a
+        point that syncs anyway (the trainer does at every epoch end)."""
+        self._allreduce.check()
+        seen = set()
+        for m in self.module.modules():
+            for xg in (getattr(m, "_xg", None), (getattr(m, "sync", None) or (None,))[0]):
+                if xg is not None and hasattr(xg, "check") and id(xg) not in seen:
+                    seen.add(id(xg))
+                    xg.check()
 
     def capturable(self) -> bool:
         """True when one training step issues no host-synchronising collective: every

@@ -163,6 +163,8 @@ class Expr:
 
 
 class ColRef(Expr):
+    qualifier = None      # ``alias`` of an SQL ``alias.col`` reference (set by the SQL parser)
+
     def __init__(self, col_name: str):
         self.col_name = col_name
 

@@ -143,6 +143,11 @@ class CsvSource(Source):
         for f in self.files:
             size = os.path.getsize(f)
             nsplit = max(1, int(np.ceil(size / split_bytes)))
+            if nsplit > parallelism > 1:
+                # whole waves: 10 splits on 4 cores run as 4 + 4 + 2 (the last wave half idle,
+                # measured 2.09 s for 10 M NYC rows, profiles/r4_datascale_10M_e1_timeline.txt);
+                # 12 smaller ones run as 4 + 4 + 4. Same rows, same order, smaller splits.
+                nsplit = -(-nsplit // parallelism) * parallelism
             b = np.linspace(0, size, nsplit + 1).astype(np.int64)
             for j in range(nsplit):
                 self.splits.append((f, int(b[j]), int(b[j + 1])))

@@ -329,7 +329,7 @@ class _Stmt:
         return ("expr", text)
 
     def _from(self):
-        df, alias = self._source()
+        df, lquals = self._source()
         while True:
             how = None
             if self.accept_kw("join") or self.accept_kw("inner", "join"):
@@ -351,9 +351,10 @@ class _Stmt:
                 how = "cross"
             else:
                 break
-            rhs, _ = self._source()
+            rhs, rquals = self._source()
             if how == "cross":
                 df = df.crossJoin(rhs)
+                lquals |= rquals
                 continue
             if self.accept_kw("using"):
                 self.expect_op("(")
@@ -364,10 +365,12 @@ class _Stmt:
                         break
                 self.expect_op(")")
                 df = df.join(rhs, cols, how)
+                lquals |= rquals
                 continue
             self.expect_kw("on")
             cond = self._expr(self.span(_CLAUSE - {"as", "asc", "desc", "all", "by", "first", "last"}))
-            df = _join_on(df, rhs, cond, how)
+            df = _join_on(df, rhs, cond, how, lquals, rquals)
+            lquals |= rquals
         return df
 
     def _source(self):
@@ -384,11 +387,16 @@ class _Stmt:
         elif self.peek()[0] in ("id", "bq") and self.kw() not in _CLAUSE | {"join", "on", "using", "left", "right",
                                                                             "full", "inner", "cross", "where"}:
             alias = self.name()
-        # qualifier -> its columns, for ``alias.*`` in the select list
+        # qualifier -> its columns, for ``alias.*`` in the select list; the set of names that
+        # refer to this source, for ``alias.col`` in JOIN ... ON
+        quals = set()
         for q in (alias, tname, tname.split(".")[-1] if tname else None):
             if q:
                 self.qualifiers[q] = list(df.columns)
-        return df, alias
+                quals.add(q)
+        if alias:      # an alias hides the table's own name (Spark: t AS a -> only a.col)
+            quals = {alias}
+        return df, quals
 
     def _expr(self, text):
         from raydp_amd.spark.sqlexpr import parse
@@ -551,9 +559,30 @@ def lift_keys(e, keys, key_names):
     return map_children(e, lambda c: lift_keys(c, keys, key_names))
 
 
-def _join_on(left, right, cond, how):
+def _side(ref, lcols, rcols, lquals, rquals):
+    """Which join input a column reference of an ON condition reads: "L", "R" or None (neither).
+    A qualified ``alias.col`` goes by its qualifier; a bare name must exist on exactly one side
+    (Spark's analyzer rejects an ambiguous reference instead of guessing)."""
+    q, c = ref.qualifier, ref.col_name
+    if q is not None:
+        if q in rquals and c in rcols:
+            return "R"
+        if q in lquals and c in lcols:
+            return "L"
+        if q not in rquals and q not in lquals:
+            raise SqlError(f"unknown qualifier {q!r} in JOIN ... ON")
+        raise SqlError(f"cannot resolve column {q}.{c} in JOIN ... ON")
+    inl, inr = c in lcols, c in rcols
+    if inl and inr:
+        raise SqlError(f"reference {c!r} in JOIN ... ON is ambiguous (both sides have it); qualify it")
+    return "L" if inl else "R" if inr else None
+
+
+def _join_on(left, right, cond, how, lquals=frozenset(), rquals=frozenset()):
     """Equi-join on every ``a = b`` conjunct between a left and a right column; other conjuncts
-    filter the joined rows (inner joins only)."""
+    filter the joined rows (inner joins only). Each side of an equality is resolved by its
+    qualifier (``ON b.k = a.j`` joins a.j with b.k whatever the order of the operands)."""
+    from raydp_amd.spark import wide as W
     from raydp_amd.spark.column import BinOp, ColRef, Column
     conj, stack = [], [cond._expr]
     while stack:
@@ -566,12 +595,14 @@ def _join_on(left, right, cond, how):
     lcols, rcols = set(left.columns), set(right.columns)
     for e in conj:
         if isinstance(e, BinOp) and e.op == "==" and isinstance(e.left, ColRef) and isinstance(e.right, ColRef):
+            sa = _side(e.left, lcols, rcols, lquals, rquals)
+            sb = _side(e.right, lcols, rcols, lquals, rquals)
             a, b = e.left.col_name, e.right.col_name
-            if a in lcols and b in rcols:
+            if (sa, sb) == ("L", "R"):
                 lk.append(a)
                 rk.append(b)
                 continue
-            if b in lcols and a in rcols:
+            if (sa, sb) == ("R", "L"):
                 lk.append(b)
                 rk.append(a)
                 continue
@@ -580,8 +611,12 @@ def _join_on(left, right, cond, how):
         raise SqlError("JOIN ... ON needs at least one equality between a left and a right column")
     if residual and how != "inner":
         raise SqlError("non-equality JOIN conditions are supported on inner joins only")
-    conds = [Column(ColRef(a)) == Column(ColRef(b)) for a, b in zip(lk, rk)]
-    out = left.join(right, conds if any(a != b for a, b in zip(lk, rk)) else lk, how)
+    if any(a != b for a, b in zip(lk, rk)):
+        # the keys are resolved already: build the join on them directly (DataFrame.join would
+        # guess the sides again by name, which a self-join cannot disambiguate)
+        out = left._with(W.JoinPlan(left._src(), right._src(), lk, rk, how))
+    else:
+        out = left.join(right, lk, how)
     for e in residual:
         out = out.filter(Column(e))
     return out

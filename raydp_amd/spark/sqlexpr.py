@@ -212,11 +212,16 @@ class _Parser:
         if kind == "id":
             if self.accept("op", "("):
                 return self._call(v)
-            name = v
+            parts = [v]
             while self.peek() == ("op", "."):
                 self.next()
-                name = self.next()[1].strip("`")   # qualified names: keep the last part
-            return F.col(name)
+                parts.append(self.next()[1].strip("`"))
+            c = F.col(parts[-1])
+            if len(parts) > 1:
+                # ``t.c``: the column is ``c``; the qualifier names the relation it comes from
+                # (JOIN ... ON resolves each side by it)
+                c._expr.qualifier = parts[-2]
+            return c
         raise ValueError(f"unexpected token {v!r}")
 
     def _type_name(self):

@@ -51,9 +51,11 @@ class JoinPlan(WidePlan):
         # disambiguate non-key duplicate names like Spark (right side suffix is dropped by
         # select later; keep both columns)
         overlap = (set(lt.column_names) & set(rt.column_names)) - (set(self.lk) if same else set())
+        rk = self.rk
         if overlap:
             rt = rt.rename_columns([c + "#r" if c in overlap else c for c in rt.column_names])
-        out = lt.join(rt, keys=self.lk, right_keys=self.rk, join_type=self.how,
+            rk = [c + "#r" if c in overlap else c for c in rk]    # a right key may be renamed too
+        out = lt.join(rt, keys=self.lk, right_keys=rk, join_type=self.how,
                       use_threads=True, coalesce_keys=same)
         if overlap:
             out = out.rename_columns([c[:-2] if c.endswith("#r") else c for c in out.column_names])

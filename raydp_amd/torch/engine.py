@@ -504,8 +504,15 @@ class TorchLoopEngine:
             self.metrics.reset()
 
     def train_epoch(self):
-        if self.graphed is not None:
-            return self.graphed.train_epoch()
+        out = self.graphed.train_epoch() if self.graphed is not None else self._train_epoch_eager()
+        if self.world > 1 and hasattr(self.model, "check_comm"):
+            # the epoch's metrics readback synced the device already: a timed-out xGMI exchange
+            # surfaces here as CollectiveError (the trainer restarts the group) instead of
+            # replicas silently training on unsynchronised gradients
+            self.model.check_comm()
+        return out
+
+    def _train_epoch_eager(self):
         self.model.train()
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         nb = 0

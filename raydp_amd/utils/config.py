@@ -126,9 +126,15 @@ register("spark.ray.mi355x.allreduce.timeout_s", "float", 30.0,
          "bound on every xGMI flag wait before the kernel gives up and reports an error",
          env="RAYDP_ALLREDUCE_TIMEOUT_S")
 register("spark.ray.mi355x.allreduce.oneshot_max_mb", "float", 16.0,
-         "DDP / Horovod buckets up to this size take the one-shot xGMI kernel (every rank reads the "
-         "N-1 peer buckets at once, one per link: S / 153 GB/s whatever N); larger ones go to RCCL",
-         env="RAYDP_ALLREDUCE_ONESHOT_MAX_MB")
+         "DDP / Horovod buckets up to this size take the xGMI kernels (one-shot or two-shot, see "
+         "twoshot_min_mb); larger ones go to RCCL", env="RAYDP_ALLREDUCE_ONESHOT_MAX_MB")
+register("spark.ray.mi355x.allreduce.twoshot_min_mb", "float", 1.0,
+         "at world > 2, xGMI buckets from this size on take the two-shot kernel (all-pairs "
+         "reduce-scatter + all-gather: 2S/N bytes per link, two flag rounds) instead of the one-shot "
+         "kernel (S bytes per link, one flag round)", env="RAYDP_ALLREDUCE_TWOSHOT_MIN_MB")
+register("spark.ray.mi355x.ddp.comm_stream", "bool", True,
+         "reduce DDP / Horovod gradient buckets on a dedicated comm stream, concurrent with the rest "
+         "of backward (event fork/join: capturable)", env="RAYDP_DDP_COMM_STREAM")
 register("spark.ray.mi355x.fused", "str", "auto",
          "TorchEstimator engine: auto (fused HIP MLP when the model is an MLP), on (required), off",
          env="RAYDP_FUSED", choices=["auto", "on", "off"])

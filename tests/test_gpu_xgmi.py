@@ -480,3 +480,162 @@ def test_sharded_embeddings_exchange_over_xgmi(world):
         assert used_xg, "the GPU lookup should ride the xGMI all-to-all"
         assert fwd_err < 1e-6 and w_err < 1e-6, (rank, fwd_err, w_err)
         assert graph_err < 1e-6, f"rank {rank}: graph replay diverged from eager ({graph_err})"
+
+
+def _twoshot_main(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    _init(rank, world, port)
+    try:
+        from raydp_amd.ops.comm import XgmiComm
+        sizes = [48_516, 262_144, 2_177_188, 50_004]      # multiples of 4 (the two-shot contract)
+        comm = XgmiComm.create(max(sizes), timeout_s=20.0)
+        if comm is None:
+            q.put((rank, "create failed", 0.0, False))
+            return
+        worst, ran2, outs = 0.0, True, []
+        for it in range(10):
+            n = sizes[it % len(sizes)]
+            data = [torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + r)).cuda()
+                    for r in range(world)]
+            want = torch.zeros(n, device="cuda")
+            for r in range(world):
+                want = want + data[r]
+            scale = 1.0 / world if it % 2 else 1.0
+            t = data[rank].clone()
+            # interleave the kernels: one-shot calls consume one sequence number, two-shot three,
+            # and the slot parity must still alternate call to call
+            if it % 3 == 2:
+                comm.allreduce_(t, scale)
+            else:
+                ran2 = comm.allreduce2_(t, scale) and ran2
+            torch.cuda.synchronize()
+            worst = max(worst, float((t - want * scale).abs().max()))
+            outs.append(t.cpu())
+        # an unaligned buffer is refused (the caller falls back to the one-shot kernel)
+        buf = torch.zeros(1025, device="cuda")
+        refused = not comm.allreduce2_(buf[1:])
+        gathered = [None] * world
+        dist.all_gather_object(gathered, torch.cat(outs))
+        same = all(bool(torch.equal(gathered[0], x)) for x in gathered)
+        q.put((rank, "ok" if comm.error() == 0 else "error word set", worst, ran2 and refused and same))
+        torch.cuda.synchronize()
+        dist.barrier()
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_xgmi_twoshot_allreduce_interleaved_with_oneshot(world):
+    """The all-pairs two-shot kernel (reduce-scatter + all-gather over the same slots) gives the
+    rank-order sum, bit-identical on every rank, including when its calls alternate with one-shot
+    calls on the same communicator (slot parity and sequence numbers stay consistent)."""
+    res = _run(_twoshot_main, world)
+    assert len(res) == world
+    for rank, status, worst, ok in res:
+        assert status == "ok", (rank, status)
+        assert worst < 1e-5, (rank, worst)
+        assert ok, f"rank {rank}: two-shot not used, unaligned not refused, or replicas differ"
+
+
+def _ddp_overlap_main(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    import torch.nn as nn
+    _init(rank, world, port)
+    try:
+        from raydp_amd.ops import comm as C
+        from raydp_amd.parallel.ddp import DistributedDataParallel
+        dev = torch.device("cuda", 0)
+        g = torch.Generator().manual_seed(21 + rank)
+        xs = [torch.randn(128, 64, generator=g).to(dev) for _ in range(5)]
+        ys = [torch.randn(128, 1, generator=g).to(dev) for _ in range(5)]
+        outs, kinds, launched = {}, {}, {}
+        # comm stream + small buckets (several per step) + every xGMI bucket two-shot, against the
+        # plain one-bucket stream-ordered one-shot path and the torch.distributed fallback
+        cfgs = {"overlap": {"RAYDP_DDP_COMM_STREAM": "1", "RAYDP_ALLREDUCE_TWOSHOT_MIN_MB": "0"},
+                "serial": {"RAYDP_DDP_COMM_STREAM": "0", "RAYDP_ALLREDUCE_TWOSHOT_MIN_MB": "1024"},
+                "rccl": {"RAYDP_ALLREDUCE": "rccl"}}
+        for name, env in cfgs.items():
+            os.environ.update(env)
+            torch.manual_seed(0)
+            net = nn.Sequential(nn.Linear(64, 256), nn.ReLU(), nn.Linear(256, 256), nn.ReLU(),
+                                nn.Linear(256, 1)).to(dev)
+            ddp = DistributedDataParallel(net, bucket_cap_mb=0.1 if name == "overlap" else None)
+            opt = torch.optim.SGD(ddp.parameters(), lr=0.05)
+            for x, y in zip(xs, ys):
+                ddp.zero_grad()
+                nn.functional.mse_loss(ddp(x), y).backward()
+                opt.step()
+            torch.cuda.synchronize()
+            ddp.check_comm()
+            outs[name] = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).cpu()
+            kinds[name] = (len(ddp.buckets), ddp._allreduce.kind)
+            launched[name] = dict(ddp._allreduce.launched)
+            for k in env:
+                os.environ.pop(k, None)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, outs["overlap"])
+        same = all(bool(torch.equal(gathered[0], t)) for t in gathered)
+        q.put((rank, same, float((outs["overlap"] - outs["serial"]).abs().max()),
+               float((outs["overlap"] - outs["rccl"]).abs().max()), kinds, launched))
+        dist.barrier()
+        C.reset_cache()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ddp_buckets_on_comm_stream_twoshot_match_serial(world):
+    """Gradient buckets reduced on the comm stream while backward continues (several buckets per
+    step, every one two-shot at world > 2) train like the stream-ordered one-shot path and the
+    torch.distributed fallback; replicas stay identical."""
+    res = _run(_ddp_overlap_main, world)
+    for rank, same, d_serial, d_rccl, kinds, launched in res:
+        assert same, f"rank {rank}: replicas diverged"
+        assert d_serial < 1e-5 and d_rccl < 1e-5, (rank, d_serial, d_rccl)
+        assert kinds["overlap"][0] > 1 and "comm_stream" in kinds["overlap"][1], kinds
+        if world > 2:
+            assert launched["overlap"]["twoshot"] > 0 and launched["serial"]["twoshot"] == 0, launched
+        assert launched["rccl"]["oneshot"] == 0 and launched["rccl"]["twoshot"] == 0, launched
+
+
+def _ddp_error_main(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    import torch.nn as nn
+    _init(rank, world, port)
+    try:
+        from raydp_amd.exceptions import CollectiveError
+        from raydp_amd.ops import comm as C
+        from raydp_amd.parallel.ddp import DistributedDataParallel
+        dev = torch.device("cuda", 0)
+        net = nn.Sequential(nn.Linear(16, 32), nn.ReLU(), nn.Linear(32, 1)).to(dev)
+        ddp = DistributedDataParallel(net)
+        xg = ddp._allreduce.xg
+        if rank == 1:
+            xg._inject_error()                  # as if rank 1 had missed a peer
+        raised = False
+        try:
+            ddp.check_comm()
+        except CollectiveError:
+            raised = True
+        torch.cuda.synchronize()
+        # the rank that retired xGMI and its healthy peers agree on the next set-up: no hang,
+        # every rank falls back together
+        again = C.XgmiComm.create(1024, timeout_s=5.0, tag="after")
+        q.put((rank, raised, ddp._allreduce.xg is None, again is None))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_xgmi_error_word_raises_and_ranks_fall_back_together():
+    """A timed-out exchange on the DDP path is not silent: the epoch-end check raises
+    CollectiveError on the rank that saw it, and the next communicator set-up is refused on EVERY
+    rank through one agreement collective (no rank left waiting in a different collective)."""
+    res = _run(_ddp_error_main, 2)
+    assert res[0][1] is False and res[1][1] is True, res
+    assert res[1][2], res
+    assert all(r[3] for r in res), res

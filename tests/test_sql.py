@@ -143,3 +143,39 @@ def test_hive_style_tables_persist_in_the_warehouse(spark, tmp_path):
     assert [r[0] for r in desc] == ["store", "q"]
     spark.sql("DROP DATABASE db CASCADE")
     assert not (tmp_path / "warehouse" / "db.db").exists()
+
+
+def _pairs(spark):
+    rng = np.random.default_rng(3)
+    ta = pa.table({"k": pa.array(rng.integers(0, 6, 50)), "j": pa.array(rng.integers(0, 6, 50)),
+                   "va": pa.array(np.arange(50))})
+    tb = pa.table({"k": pa.array(rng.integers(0, 6, 40)), "j": pa.array(rng.integers(0, 6, 40)),
+                   "vb": pa.array(np.arange(100, 140))})
+    spark.createDataFrame(ta).createOrReplaceTempView("ta")
+    spark.createDataFrame(tb).createOrReplaceTempView("tb")
+    return ta.to_pandas(), tb.to_pandas()
+
+
+@pytest.mark.parametrize("on", ["b.k = a.j", "a.j = b.k"])
+def test_join_on_resolves_sides_by_qualifier(spark, on):
+    # both tables have k and j: a bare-name guess would join a.k = b.j instead of a.j = b.k
+    pa_, pb = _pairs(spark)
+    got = spark.sql(f"SELECT a.va, b.vb FROM ta a JOIN tb b ON {on}")
+    want = pa_.merge(pb, left_on="j", right_on="k")
+    assert sorted((int(r[0]), int(r[1])) for r in got.collect()) == \
+        sorted(zip(want["va"].tolist(), want["vb"].tolist()))
+
+
+def test_self_join_on_qualified_columns(spark):
+    pa_, _ = _pairs(spark)
+    got = spark.sql("SELECT count(*) AS n FROM ta x JOIN ta y ON x.j = y.k")
+    assert int(got.collect()[0][0]) == len(pa_.merge(pa_, left_on="j", right_on="k"))
+
+
+def test_join_on_ambiguous_bare_name_raises(spark):
+    from raydp_amd.spark.sql import SqlError
+    _pairs(spark)
+    with pytest.raises(SqlError, match="ambiguous"):
+        spark.sql("SELECT a.va FROM ta a JOIN tb b ON k = j").collect()
+    with pytest.raises(SqlError, match="unknown qualifier"):
+        spark.sql("SELECT a.va FROM ta a JOIN tb b ON c.k = a.j").collect()
