@@ -135,6 +135,99 @@ struct Tile {
   static constexpr int XS = BP + 8;          // stride (elements) of transposed matrices
 };
 
+// ------------------------------------------------------------------------------------------
+// Multi-workgroup step (batch > one workgroup's 16 * MT rows; TorchEstimator batch_size 129 ..
+// 16384, e.g. the reference's own test at batch 1000, python/raydp/tests/test_torch.py:70-80):
+// G workgroups of the same launch each run the single-workgroup step on rows [wg * BP, wg * BP +
+// BP) of the batch, activations in their own LDS. What couples the rows of a batch goes through
+// global memory:
+//   * BatchNorm batch statistics (forward) and the batch sums of its backward: each workgroup
+//     publishes per-column partials (count-weighted sums and centred second moments, combined in
+//     workgroup order: every workgroup computes bit-identical statistics), then a grid barrier;
+//   * bias gradients: per-workgroup partial column sums, reduced in workgroup order after the
+//     last barrier of the step into the gradient buffer (deterministic, no float atomics);
+//   * weight gradients: every workgroup exports its rows of X^T / G^T into the batch-wide
+//     activation area (row stride = the padded batch), and the optimizer kernel's dW = X^T G runs
+//     over the whole batch (K = G * BP) as before;
+//   * the loss mean and the BatchNorm averages divide by the batch's row count, not the tile's.
+// Hand-off form (MI355X_MICROARCH.md "inter-workgroup visibility", first table row): partials are
+// written with sc1 stores by every wave, each wave drains them (s_waitcnt vmcnt(0)), a workgroup
+// barrier, then ONE lane's agent-scope add to a monotonic counter; the consumer lane polls the
+// counter with sc1 loads, its workgroup joins a barrier and every wave reads the partials with
+// sc1 loads. All G workgroups must be co-resident (the host checks occupancy); every wait is
+// bounded and a timeout sets the error word, after which every barrier returns at once.
+struct NoMw {  // one workgroup per step (the fields only make MWT::on ? a : b well-formed)
+  static constexpr bool on = false;
+  int k, G, wg, n_total;
+  float* part;
+};
+
+struct MwCtx {
+  static constexpr bool on = true;
+  int k;                       // grid barriers passed so far in this step (uniform)
+  float* part;                 // [G][pr_total] partials (the per-column parameter-block layout)
+  unsigned* ctl;               // [0] barrier counter, [1] done counter, [2] error word
+  int G, wg;                   // workgroups of the step, this one's index
+  int n_total;                 // valid rows of the whole batch
+  unsigned long long ticks;    // wall-clock bound of one barrier wait
+};
+
+#define RX_MW_CTR 0
+#define RX_MW_DONE 1
+#define RX_MW_ERR 2
+
+__device__ __forceinline__ float rx_ld_sc1f(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void rx_st_sc1f(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Grid barrier number `k` (1-based, counted by the caller) of the step. Every thread of every
+// workgroup calls it. Returns false when any workgroup timed out (error word set).
+__device__ __forceinline__ bool mw_barrier(const MwCtx& mw, int k) {
+  __shared__ int mw_ok;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores have left
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    __hip_atomic_fetch_add(mw.ctl + RX_MW_CTR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (unsigned)(k * mw.G);
+    const unsigned long long t0 = wall_clock64();
+    for (int it = 1;; ++it) {
+      if (__hip_atomic_load(mw.ctl + RX_MW_CTR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      if ((it & 15) == 0) {
+        if (__hip_atomic_load(mw.ctl + RX_MW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+            wall_clock64() - t0 > mw.ticks) {
+          __hip_atomic_store(mw.ctl + RX_MW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    mw_ok = ok;
+  }
+  __syncthreads();
+  return mw_ok != 0;
+}
+
+// End of the step: the last workgroup through resets the barrier counter for the next launch
+// (every workgroup has passed every wait by then).
+__device__ __forceinline__ void mw_finish(const MwCtx& mw) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(mw.ctl + RX_MW_DONE, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned)mw.G - 1u) {
+      __hip_atomic_store(mw.ctl + RX_MW_CTR, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(mw.ctl + RX_MW_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Rows of workgroup w when the batch's n valid rows are dealt BP per workgroup.
+__device__ __forceinline__ int mw_rows(int n, int w, int bp) { return max(0, min(bp, n - w * bp)); }
+
 __device__ __forceinline__ float act_fwd(int act, float z) { return act == 1 ? fmaxf(z, 0.f) : z; }
 
 // C[Bpad x 16-col tile n] += A (LDS, row-major, K contiguous) x Bt (global bf16, [n][K]).
@@ -214,13 +307,15 @@ __device__ __forceinline__ void fwd_prefetch(const LY& ly, const u16* __restrict
 // `byte_base`: byte offset of the destination inside the gradient buffer Gr. Persistent (PS) with
 // `wt`: write-through sc1 stores (some optimizer workgroup of the launch sits on another XCD);
 // plain stores otherwise (every reader shares this XCD's L2 and reads it with sc1 loads).
+// Multi-workgroup step: `bp_total` (the exported rows' stride, the padded batch) and `col0` (this
+// workgroup's first batch row) place the workgroup's BP columns inside the batch-wide area.
 template <int MT, bool PS>
 __device__ __forceinline__ void export_rows(const u16* lds, int rows, float* __restrict__ Gr, int byte_base,
-                                            bool wt = true) {
+                                            bool wt = true, int bp_total = Tile<MT>::BP, int col0 = 0) {
   constexpr int BP = Tile<MT>::BP, XS = Tile<MT>::XS, CH = BP / 8;
   for (int idx = rx_tid<PS>(); idx < rows * CH; idx += RX_THREADS) {
     const int r = idx / CH, c = idx % CH;
-    const int boff = byte_base + (r * BP + c * 8) * 2;
+    const int boff = byte_base + (r * bp_total + col0 + c * 8) * 2;
     const u32x4 val = *reinterpret_cast<const u32x4*>(lds + r * XS + c * 8);
     if (PS && wt)
       rx_store16_sc1(Gr, boff, val);
@@ -254,14 +349,14 @@ __device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __res
 // act/BN) in R (row-major) and in XT_{l+1}; for the last layer computes loss, metrics and
 // writes dL/dy into R/GT as G_{L-1}.
 // ------------------------------------------------------------------------------------------
-template <int MT, bool TRAIN, bool PS, class D, class LY, class NX>
+template <int MT, bool TRAIN, bool PS, class D, class LY, class NX, class MWT = NoMw>
 __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX& nx, bool last, char* smem,
                                               const u16* __restrict__ img, const float* __restrict__ P,
                               float* __restrict__ Gr, const float* __restrict__ labels,
                               const int* __restrict__ rowidx, int nvalid, float* __restrict__ scratch,
                               double* __restrict__ metrics, bf16x8 (&wpre)[RX_PJ][RX_PK], bool ps_wt = true,
                               int l = 0, unsigned long long* __restrict__ stamps = nullptr,
-                              const float* lab_pre = nullptr) {
+                              const float* lab_pre = nullptr, MWT* mw = nullptr) {
   // optional intra-layer timeline (wave 0, s_memtime): [40 + 5 l ..] export, GEMM, epilogue,
   // first barrier, publish + second barrier
   auto fst = [&](int k) {
@@ -275,9 +370,14 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   u16* GT = reinterpret_cast<u16*>(smem + d.gt_lds_off);
   float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
   const int ntiles = ly.out_n >> 4;
-  if (TRAIN && d.wgrad_mode == 1)  // X^T_l (published by the previous layer / the input load)
-    export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
-                        ps_wt);
+  if (TRAIN && d.wgrad_mode == 1) {  // X^T_l (published by the previous layer / the input load)
+    if constexpr (MWT::on)
+      export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
+                          ps_wt, mw->G * T::BP, mw->wg * T::BP);
+    else
+      export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
+                          ps_wt);
+  }
   fst(0);
 
   f32x4 acc[T::NTW * MT];
@@ -302,167 +402,197 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   if (!last) fwd_prefetch<PS>(nx, img, wpre);
 
   // ---- epilogue in registers, in place on acc: bias, act, BN, loss ----
-#pragma unroll
-  for (int j = 0; j < T::NTW; ++j) {
+  // Phase A of a tile: bias, act, and the BatchNorm statistics of this workgroup's rows (its BN
+  // input saved for the backward). Phase B: the batch statistics (stats LDS, running averages),
+  // normalisation, padding, loss. One workgroup runs B right after A per tile; the
+  // multi-workgroup step publishes every tile's partials, meets the other workgroups and
+  // combines the batch statistics in between.
+  const int n_batch = MWT::on ? mw->n_total : nvalid;   // rows the batch statistics / loss cover
+  float bn_mean[T::NTW], bn_var[T::NTW];
+  auto epi_a = [&](int j) {
     const int n = wave + j * RX_NW;
-    if (n < ntiles) {
-      const int c = n * 16 + lr;
-      const bool colok = c < ly.out;
-      const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off) + ly.pr_off;
-      const float bias = pr[c];
-      const bool act_first = ly.bn != 2;
+    if (n >= ntiles) return;
+    const int c = n * 16 + lr;
+    const bool colok = c < ly.out;
+    const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off) + ly.pr_off;
+    const float bias = pr[c];
+    const bool act_first = ly.bn != 2;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float z = acc[j * MT + mt][r] + bias;
-          acc[j * MT + mt][r] = act_first ? act_fwd(ly.act, z) : z;
-        }
-      if (ly.bn != 0) {
-        float mean, invstd;
-        if (TRAIN) {
-          float s = 0.f;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              s += (mt * 16 + lg * 4 + r < nvalid) ? acc[j * MT + mt][r] : 0.f;
-          s = rx_colsum16(s);
-          mean = s / (float)nvalid;
-          float v = 0.f;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float dv = acc[j * MT + mt][r] - mean;
-              v = (mt * 16 + lg * 4 + r < nvalid) ? fmaf(dv, dv, v) : v;
-            }
-          v = rx_colsum16(v);
-          const float var = v / (float)nvalid;
-          invstd = rsqrtf(var + ly.eps);
-          if (colok && lg == 0) {
-            stats[ly.stat_off + 2 * c] = mean;
-            stats[ly.stat_off + 2 * c + 1] = invstd;
-            const float unb = nvalid > 1 ? var * (float)nvalid / (float)(nvalid - 1) : var;
-            float* prw = reinterpret_cast<float*>(smem + d.pr_lds_off) + ly.pr_off;
-            prw[3 * ly.out_n + c] = fmaf(1.f - ly.momentum, prw[3 * ly.out_n + c], ly.momentum * mean);
-            prw[4 * ly.out_n + c] = fmaf(1.f - ly.momentum, prw[4 * ly.out_n + c], ly.momentum * unb);
-          }
-          // save the BN input for the backward pass (fragment-major, see frag_off)
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) = acc[j * MT + mt];
-        } else {
-          mean = colok ? pr[3 * ly.out_n + c] : 0.f;
-          invstd = colok ? rsqrtf(pr[4 * ly.out_n + c] + ly.eps) : 0.f;
-        }
-        const float gam = pr[ly.out_n + c];
-        const float bet = pr[2 * ly.out_n + c];
-        const bool act_after = ly.bn == 2;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float t = fmaf((acc[j * MT + mt][r] - mean) * invstd, gam, bet);
-            acc[j * MT + mt][r] = act_after ? act_fwd(ly.act, t) : t;
-          }
-      } else if (TRAIN && !last) {
-        // ReLU mask source for the backward pass
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-          *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) =
-              colok ? acc[j * MT + mt] : z;
-        }
+      for (int r = 0; r < 4; ++r) {
+        const float z = acc[j * MT + mt][r] + bias;
+        acc[j * MT + mt][r] = act_first ? act_fwd(ly.act, z) : z;
       }
-      // padded rows / columns carry exact zeros through every GEMM
+    if (TRAIN && ly.bn != 0) {
+      float s = 0.f;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (!colok || mt * 16 + lg * 4 + r >= nvalid) acc[j * MT + mt][r] = 0.f;
-      if (last) {
-        // loss, metrics and dL/dy (mean reduction over nvalid * out_dim elements)
-        float lsum = 0.f, asum = 0.f, ssum = 0.f, gsum = 0.f, csum = 0.f;
-        const float inv_n = 1.f / (float)(nvalid * ly.out);
-        const int lcode = d.loss;
-        const float beta = d.beta;
-        // labels of all padded rows, loaded back to back (padded rows read row 0)
-        const int cl = colok ? c : 0;
-        float tl[MT * 4];
-        if (lab_pre != nullptr && ly.out_n == 16) {  // fetched at the start of the step
+          s += (mt * 16 + lg * 4 + r < nvalid) ? acc[j * MT + mt][r] : 0.f;
+      s = rx_colsum16(s);
+      // (a multi-workgroup step's trailing workgroups may hold no rows of a short last batch)
+      const float mean = nvalid > 0 ? s / (float)nvalid : 0.f;
+      float v = 0.f;
 #pragma unroll
-          for (int q = 0; q < MT * 4; ++q) tl[q] = lab_pre[q];
-        } else {
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
+        for (int r = 0; r < 4; ++r) {
+          const float dv = acc[j * MT + mt][r] - mean;
+          v = (mt * 16 + lg * 4 + r < nvalid) ? fmaf(dv, dv, v) : v;
         }
-        if (lcode == 4) {
-          // Cross entropy over the out <= 16 classes of one tile (a row's logits live in the 16
-          // lanes sharing lg). Labels arrive as a weighted one-hot row (t_c = w[y] at c = y,
-          // else 0; an ignored row is all zeros): with W = sum of the rows' weights,
-          //   loss = sum_rows (w_y * logsumexp(x) - w_y * x_y) / W
-          //   dL/dx_c = (w_y * softmax(x)_c - t_c) / W      (torch's weighted mean)
-          // and the row counts as correct when argmax_c x (first index on ties) is y.
-          float wsum = 0.f;
+      v = rx_colsum16(v);
+      if constexpr (MWT::on) {
+        // this workgroup's (sum, centred second moment) of column c
+        if (colok && lg == 0) {
+          float* pp = mw->part + (size_t)mw->wg * d.pr_total + ly.pr_off + 2 * c;
+          rx_st_sc1f(pp, s);
+          rx_st_sc1f(pp + 1, v);
+        }
+      } else {
+        bn_mean[j] = mean;
+        bn_var[j] = v / (float)nvalid;
+      }
+      // save the BN input for the backward pass (fragment-major, see frag_off)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
+        *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) = acc[j * MT + mt];
+    }
+  };
+  auto epi_b = [&](int j) {
+    const int n = wave + j * RX_NW;
+    if (n >= ntiles) return;
+    const int c = n * 16 + lr;
+    const bool colok = c < ly.out;
+    const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off) + ly.pr_off;
+    if (ly.bn != 0) {
+      float mean, invstd;
+      if (TRAIN) {
+        mean = bn_mean[j];
+        const float var = bn_var[j];
+        invstd = rsqrtf(var + ly.eps);
+        if (colok && lg == 0) {
+          stats[ly.stat_off + 2 * c] = mean;
+          stats[ly.stat_off + 2 * c + 1] = invstd;
+          const float unb = n_batch > 1 ? var * (float)n_batch / (float)(n_batch - 1) : var;
+          float* prw = reinterpret_cast<float*>(smem + d.pr_lds_off) + ly.pr_off;
+          prw[3 * ly.out_n + c] = fmaf(1.f - ly.momentum, prw[3 * ly.out_n + c], ly.momentum * mean);
+          prw[4 * ly.out_n + c] = fmaf(1.f - ly.momentum, prw[4 * ly.out_n + c], ly.momentum * unb);
+        }
+      } else {
+        mean = colok ? pr[3 * ly.out_n + c] : 0.f;
+        invstd = colok ? rsqrtf(pr[4 * ly.out_n + c] + ly.eps) : 0.f;
+      }
+      const float gam = pr[ly.out_n + c];
+      const float bet = pr[2 * ly.out_n + c];
+      const bool act_after = ly.bn == 2;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = mt * 16 + lg * 4 + r;
-              const float x = acc[j * MT + mt][r];
-              const float t = (colok && row < nvalid) ? tl[mt * 4 + r] : 0.f;
-              float mx = colok ? x : -INFINITY;
-              int bi = colok ? c : 1 << 20;
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-              for (int o = 1; o < 16; o <<= 1) {
-                const float om = __shfl_xor(mx, o);
-                const int oi = __shfl_xor(bi, o);
-                if (om > mx || (om == mx && oi < bi)) {
-                  mx = om;
-                  bi = oi;
-                }
+        for (int r = 0; r < 4; ++r) {
+          const float t = fmaf((acc[j * MT + mt][r] - mean) * invstd, gam, bet);
+          acc[j * MT + mt][r] = act_after ? act_fwd(ly.act, t) : t;
+        }
+    } else if (TRAIN && !last) {
+      // ReLU mask source for the backward pass
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) =
+            colok ? acc[j * MT + mt] : z;
+      }
+    }
+    // padded rows / columns carry exact zeros through every GEMM
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!colok || mt * 16 + lg * 4 + r >= nvalid) acc[j * MT + mt][r] = 0.f;
+    if (last) {
+      // loss, metrics and dL/dy (mean reduction over n_batch * out_dim elements)
+      float lsum = 0.f, asum = 0.f, ssum = 0.f, gsum = 0.f, csum = 0.f;
+      const float inv_n = 1.f / (float)(n_batch * ly.out);
+      const int lcode = d.loss;
+      const float beta = d.beta;
+      // labels of all padded rows, loaded back to back (padded rows read row 0)
+      const int cl = colok ? c : 0;
+      float tl[MT * 4];
+      if (lab_pre != nullptr && ly.out_n == 16) {  // fetched at the start of the step
+#pragma unroll
+        for (int q = 0; q < MT * 4; ++q) tl[q] = lab_pre[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
+      }
+      const bool head_wg = !MWT::on || mw->wg == 0;   // the batch is counted once
+      if (lcode == 4) {
+        // Cross entropy over the out <= 16 classes of one tile (a row's logits live in the 16
+        // lanes sharing lg). Labels arrive as a weighted one-hot row (t_c = w[y] at c = y,
+        // else 0; an ignored row is all zeros): with W = sum of the rows' weights,
+        //   loss = sum_rows (w_y * logsumexp(x) - w_y * x_y) / W
+        //   dL/dx_c = (w_y * softmax(x)_c - t_c) / W      (torch's weighted mean)
+        // and the row counts as correct when argmax_c x (first index on ties) is y.
+        // (single workgroup only: the host never runs it multi-workgroup)
+        float wsum = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = mt * 16 + lg * 4 + r;
+            const float x = acc[j * MT + mt][r];
+            const float t = (colok && row < nvalid) ? tl[mt * 4 + r] : 0.f;
+            float mx = colok ? x : -INFINITY;
+            int bi = colok ? c : 1 << 20;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+              const float om = __shfl_xor(mx, o);
+              const int oi = __shfl_xor(bi, o);
+              if (om > mx || (om == mx && oi < bi)) {
+                mx = om;
+                bi = oi;
               }
-              const float ex = colok ? __expf(x - mx) : 0.f;
-              float se = ex, wr = t, tx = t * (colok ? x : 0.f);
-#pragma unroll
-              for (int o = 1; o < 16; o <<= 1) {
-                se += __shfl_xor(se, o);
-                wr += __shfl_xor(wr, o);
-                tx += __shfl_xor(tx, o);
-              }
-              const bool head = lr == 0 && row < nvalid;   // one lane per row
-              if (head) {
-                lsum += wr * (mx + __logf(se)) - tx;
-                wsum += wr;
-              }
-              if (t > 0.f && c == bi) csum += 1.f;          // the label's lane of a correct row
-              acc[j * MT + mt][r] = (colok && row < nvalid) ? wr * (ex / se) - t : 0.f;
             }
-          const float wt = rx_wavesum(wsum);
-          const float invw = wt > 0.f ? 1.f / wt : 0.f;
+            const float ex = colok ? __expf(x - mx) : 0.f;
+            float se = ex, wr = t, tx = t * (colok ? x : 0.f);
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              acc[j * MT + mt][r] *= invw;
-              gsum += acc[j * MT + mt][r];
+            for (int o = 1; o < 16; o <<= 1) {
+              se += __shfl_xor(se, o);
+              wr += __shfl_xor(wr, o);
+              tx += __shfl_xor(tx, o);
             }
-          lsum = rx_wavesum(lsum) * invw;
-          csum = rx_wavesum(csum);
-          if (lane == 0) {
-            atomicAdd(&metrics[0], (double)lsum);
-            atomicAdd(&metrics[5], (double)csum);
-            if (n == 0) {
-              atomicAdd(&metrics[3], (double)nvalid);
-              atomicAdd(&metrics[4], 1.0);
+            const bool head = lr == 0 && row < nvalid;   // one lane per row
+            if (head) {
+              lsum += wr * (mx + __logf(se)) - tx;
+              wsum += wr;
             }
+            if (t > 0.f && c == bi) csum += 1.f;          // the label's lane of a correct row
+            acc[j * MT + mt][r] = (colok && row < nvalid) ? wr * (ex / se) - t : 0.f;
           }
-          if (TRAIN) {
-            gsum = rx_colsum16(gsum);
-            if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum;
+        const float wt = rx_wavesum(wsum);
+        const float invw = wt > 0.f ? 1.f / wt : 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc[j * MT + mt][r] *= invw;
+            gsum += acc[j * MT + mt][r];
           }
-        } else {
+        lsum = rx_wavesum(lsum) * invw;
+        csum = rx_wavesum(csum);
+        if (lane == 0) {
+          atomicAdd(&metrics[0], (double)lsum);
+          atomicAdd(&metrics[5], (double)csum);
+          if (n == 0) {
+            atomicAdd(&metrics[3], (double)nvalid);
+            atomicAdd(&metrics[4], 1.0);
+          }
+        }
+        if (TRAIN) {
+          gsum = rx_colsum16(gsum);
+          if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum;
+        }
+      } else {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -507,15 +637,59 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
           if (d.acc_mode == 1) atomicAdd(&metrics[5], (double)csum);
           if (n == 0) {
             atomicAdd(&metrics[3], (double)(nvalid * ly.out));
-            atomicAdd(&metrics[4], 1.0);
+            if (head_wg) atomicAdd(&metrics[4], 1.0);
           }
         }
         if (TRAIN) {
           gsum = rx_colsum16(gsum);
-          if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum;
+          if (colok && lg == 0 && ly.b_off >= 0) {
+            if constexpr (MWT::on)
+              rx_st_sc1f(mw->part + (size_t)mw->wg * d.pr_total + ly.pr_off + 4 * ly.out_n + c, gsum);
+            else
+              Gr[ly.b_off + c] = gsum;
+          }
         }
-        }  // regression / BCE losses
+      }  // regression / BCE losses
+    }
+  };
+  bool split = false;
+  if constexpr (MWT::on) split = TRAIN && ly.bn != 0;
+  if (split) {
+    if constexpr (MWT::on) {
+#pragma unroll
+      for (int j = 0; j < T::NTW; ++j) epi_a(j);
+      mw_barrier(*mw, ++mw->k);
+      // batch statistics from every workgroup's (sum, centred second moment), workgroup order
+#pragma unroll
+      for (int j = 0; j < T::NTW; ++j) {
+        const int n = wave + j * RX_NW;
+        if (n >= ntiles) continue;
+        const int c = n * 16 + lr;
+        const int cc = c < ly.out ? c : 0;
+        float S = 0.f;
+        for (int w = 0; w < mw->G; ++w) S += rx_ld_sc1f(mw->part + (size_t)w * d.pr_total + ly.pr_off + 2 * cc);
+        const float mean = S / (float)n_batch;
+        float M2 = 0.f;
+        for (int w = 0; w < mw->G; ++w) {
+          const float* pp = mw->part + (size_t)w * d.pr_total + ly.pr_off + 2 * cc;
+          const int nwi = mw_rows(n_batch, w, T::BP);
+          if (nwi == 0) continue;      // an empty workgroup published nothing meaningful
+          const float nw = (float)nwi;
+          const float dm = rx_ld_sc1f(pp) / nw - mean;
+          M2 += rx_ld_sc1f(pp + 1);
+          M2 = fmaf(nw * dm, dm, M2);
+        }
+        bn_mean[j] = mean;
+        bn_var[j] = M2 / (float)n_batch;
       }
+#pragma unroll
+      for (int j = 0; j < T::NTW; ++j) epi_b(j);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < T::NTW; ++j) {
+      epi_a(j);
+      epi_b(j);
     }
   }
   fst(2);
@@ -563,13 +737,13 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
 // PS (persistent epoch kernel): once this layer's dgrad has read its last weight byte and its
 // G^T export has drained, lane 0 publishes flag `sync[32 l] = step + 1` -- the optimizer
 // workgroups of layer l may then compute dW_l and rewrite W_l / Wt_l while the backward goes on.
-template <int MT, bool PS, class D, class LY, class PV>
+template <int MT, bool PS, class D, class LY, class PV, class MWT = NoMw>
 __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const PV& pv, int l, char* smem,
                                                const u16* __restrict__ img, const float* __restrict__ P,
                                                float* __restrict__ Gr, int nvalid, const float* __restrict__ scratch,
                                                unsigned long long* __restrict__ stamps,
                                                unsigned* __restrict__ sync = nullptr, int step = 0,
-                                               bool ps_wt = true) {
+                                               bool ps_wt = true, MWT* mw = nullptr) {
   using T = Tile<MT>;
   const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
   const int lr = lane & 15, lg = lane >> 4;
@@ -605,7 +779,10 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 
   if (d.wgrad_mode == 1) {
     // G^T_l leaves for the optimizer kernel's wgrad (GT is overwritten with G_{l-1} below)
-    export_rows<MT, PS>(GT, ly.out_n, Gr, d.act_off * 4 + ly.gg_off * 2, ps_wt);
+    if constexpr (MWT::on)
+      export_rows<MT, PS>(GT, ly.out_n, Gr, d.act_off * 4 + ly.gg_off * 2, ps_wt, mw->G * T::BP, mw->wg * T::BP);
+    else
+      export_rows<MT, PS>(GT, ly.out_n, Gr, d.act_off * 4 + ly.gg_off * 2, ps_wt);
   } else
   // ---- wgrad, computed transposed: dW^T[i][o] = sum_b X[b][i] G[b][o]  (A = XT, B = GT) ----
   // each lane then holds 4 consecutive i of one o = 16 contiguous bytes of dW[o][:] ->
@@ -721,10 +898,14 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[22 + 4 * l] = __builtin_amdgcn_s_memtime();
 
   // ---- post-op backward of layer l-1 (BN / act), producing G_{l-1} ----
-#pragma unroll
-  for (int j = 0; j < T::NTW; ++j) {
+  // mode 0: one workgroup, batch sums from its own rows. Multi-workgroup with BN: mode 1
+  // publishes this workgroup's partial sums of dL/dy and dL/dy * x_hat, a grid barrier, then
+  // mode 2 recomputes the (cheap) per-element terms and finishes with the batch sums.
+  const int n_batch = MWT::on ? mw->n_total : nvalid;
+  float bsg[T::NTW], bsgx[T::NTW];
+  auto post = [&](int j, int mode) {
     const int n = wave + j * RX_NW;
-    if (n >= ntiles) continue;
+    if (n >= ntiles) return;
     const int c = n * 16 + lr;
     const bool colok = c < pv.out;
     // The forward saved this layer's BN input / activation (fp32) for every padded row and
@@ -766,19 +947,38 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
         xh[q] = (sv[q] - mean) * invstd;
         g[q] = (relu_after && !(fmaf(xh[q], gam, bet) > 0.f)) ? 0.f : g[q];
       }
-      float sg = 0.f, sgx = 0.f;
+      float sg, sgx;
+      if (mode == 2) {
+        sg = bsg[j];
+        sgx = bsgx[j];
+      } else {
+        sg = 0.f;
+        sgx = 0.f;
 #pragma unroll
-      for (int q = 0; q < MT * 4; ++q) {
-        sg += g[q];
-        sgx = fmaf(g[q], xh[q], sgx);
+        for (int q = 0; q < MT * 4; ++q) {
+          sg += g[q];
+          sgx = fmaf(g[q], xh[q], sgx);
+        }
+        sg = rx_colsum16(sg);
+        sgx = rx_colsum16(sgx);
       }
-      sg = rx_colsum16(sg);
-      sgx = rx_colsum16(sgx);
-      if (colok && lg == 0) {
+      if (mode == 1) {
+        if (colok && lg == 0) {
+          if constexpr (MWT::on) {
+            float* pp = mw->part + (size_t)mw->wg * d.pr_total + pv.pr_off + 2 * pv.out_n + 2 * c;
+            rx_st_sc1f(pp, sg);
+            rx_st_sc1f(pp + 1, sgx);
+          }
+        }
+        return;
+      }
+      bool owner = true;   // gamma / beta gradients are batch sums: one workgroup writes them
+      if constexpr (MWT::on) owner = mw->wg == 0;
+      if (colok && lg == 0 && owner) {
         if (pv.g_off >= 0) Gr[pv.g_off + c] = sgx;
         if (pv.be_off >= 0) Gr[pv.be_off + c] = sg;
       }
-      const float inv_n = 1.f / (float)nvalid;
+      const float inv_n = 1.f / (float)n_batch;
       const float k1 = gam * invstd;
 #pragma unroll
       for (int q = 0; q < MT * 4; ++q) {
@@ -788,12 +988,17 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
         g[q] = (row < nvalid && colok) ? dz : 0.f;
       }
     }
-    // bias grad of layer l-1
+    // bias grad of layer l-1 (multi-workgroup: this workgroup's partial, reduced at step end)
     float bs = 0.f;
 #pragma unroll
     for (int q = 0; q < MT * 4; ++q) bs += g[q];
     bs = rx_colsum16(bs);
-    if (colok && lg == 0 && pv.b_off >= 0) Gr[pv.b_off + c] = bs;
+    if (colok && lg == 0 && pv.b_off >= 0) {
+      if constexpr (MWT::on)
+        rx_st_sc1f(mw->part + (size_t)mw->wg * d.pr_total + pv.pr_off + 4 * pv.out_n + c, bs);
+      else
+        Gr[pv.b_off + c] = bs;
+    }
     // publish G_{l-1}
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -806,6 +1011,35 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       R[(mt * 16 + lg * 4 + 3) * RS + c] = (u16)(pk.y >> 16);
       *reinterpret_cast<uint2*>(GT + c * XS + mt * 16 + lg * 4) = pk;
     }
+  };
+  bool split = false;
+  if constexpr (MWT::on) split = pv.bn != 0;
+  if (split) {
+    if constexpr (MWT::on) {
+#pragma unroll
+      for (int j = 0; j < T::NTW; ++j) post(j, 1);
+      mw_barrier(*mw, ++mw->k);
+#pragma unroll
+      for (int j = 0; j < T::NTW; ++j) {
+        const int n = wave + j * RX_NW;
+        if (n >= ntiles) continue;
+        const int c = n * 16 + lr;
+        const int cc = c < pv.out ? c : 0;
+        float sg = 0.f, sgx = 0.f;
+        for (int w = 0; w < mw->G; ++w) {
+          const float* pp = mw->part + (size_t)w * d.pr_total + pv.pr_off + 2 * pv.out_n + 2 * cc;
+          sg += rx_ld_sc1f(pp);
+          sgx += rx_ld_sc1f(pp + 1);
+        }
+        bsg[j] = sg;
+        bsgx[j] = sgx;
+      }
+#pragma unroll
+      for (int j = 0; j < T::NTW; ++j) post(j, 2);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < T::NTW; ++j) post(j, 0);
   }
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[23 + 4 * l] = __builtin_amdgcn_s_memtime();
   // zero the K tail [out_n, out_k) of G_{l-1} in R for the next dgrad
@@ -1043,21 +1277,99 @@ __device__ __forceinline__ void mlp_train_step_body(
 #undef RX_STAMP
 }
 
+// Multi-workgroup training step (see MwCtx): workgroup blockIdx.x of mw.G runs rows
+// perm[row0 + wg * BP .. ) of a batch of mw.n_total rows. `scratch` is the whole scratch
+// buffer; each workgroup saves its BN inputs / masks in its own `scratch_stride` floats. Needs
+// wgrad_mode 1 and no embedding front (the host checks).
+template <class C, int MT>
+__device__ __forceinline__ void mlp_train_step_mw_body(
+    const MlpDesc* __restrict__ dp, const u16* __restrict__ img, float* __restrict__ rstats,
+    const float* __restrict__ P, float* __restrict__ Gr, const u16* __restrict__ feats,
+    const float* __restrict__ labels, const int* __restrict__ perm, int row0, float* __restrict__ scratch,
+    long long scratch_stride, double* __restrict__ metrics, MwCtx mw, char* smem, int* rowidx) {
+  auto&& d = C::desc(dp);
+  constexpr int BP = Tile<MT>::BP;
+  mw.wg = (int)blockIdx.x;
+  mw.k = 0;
+  const int nvalid = mw_rows(mw.n_total, mw.wg, BP);
+  const int r0 = row0 + mw.wg * BP;
+  float* sc = scratch + (size_t)mw.wg * (size_t)scratch_stride;
+  bf16x8 wpre[RX_PJ][RX_PK];
+  fwd_prefetch<false>(C::first(d), img, wpre);
+  // padded rows (and every row of a workgroup past a short last batch) read the batch's first
+  // row: always inside the input, masked to zero on load
+  for (int i = rx_tid<false>(); i < BP; i += RX_THREADS)
+    rowidx[i] = i < nvalid ? (perm ? rx_g(perm)[r0 + i] : r0 + i) : (perm ? rx_g(perm)[row0] : row0);
+  load_params<C>(d, smem, P, rstats);
+  __syncthreads();
+  load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, true, dp, P, metrics);
+  float labp[MT * 4];
+  prefetch_labels<MT, false>(d, labels, rowidx, labp);
+  C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
+    layer_forward<MT, true, false>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, sc, metrics, wpre,
+                                   true, l, nullptr, labp, &mw);
+  });
+  // every workgroup computed the same batch statistics: one stores the running averages
+  if (mw.wg == 0) store_running_stats<C>(d, smem, rstats);
+  C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
+    layer_backward<MT, false>(d, ly, pv, l, smem, img, P, Gr, nvalid, sc, nullptr, nullptr, 0, true, &mw);
+  });
+  // bias gradients: the workgroups' partial column sums, added in workgroup order, each
+  // (layer, column) by one thread of the grid
+  mw_barrier(mw, ++mw.k);
+  C::each_layer(d, [&](const auto& ly, int) {
+    if (ly.b_off >= 0) {
+      for (int c = (int)blockIdx.x * RX_THREADS + rx_tid<false>(); c < ly.out; c += mw.G * RX_THREADS) {
+        float s = 0.f;
+        for (int w = 0; w < mw.G; ++w) s += rx_ld_sc1f(mw.part + (size_t)w * d.pr_total + ly.pr_off + 4 * ly.out_n + c);
+        Gr[ly.b_off + c] = s;
+      }
+    }
+  });
+  mw_finish(mw);
+}
+
 // Evaluation: forward + loss metrics only; one workgroup per batch.
+// chunked (a batch wider than one workgroup's BP rows): ceil(batch / BP) workgroups per batch,
+// each on BP rows of ONE batch, so the loss is still the mean of per-batch means (the host's
+// batch count comes from each batch's first chunk).
 template <class C, int MT>
 __device__ __forceinline__ void mlp_eval_body(const MlpDesc* __restrict__ dp, const u16* __restrict__ img,
                                               const float* __restrict__ rstats, const float* __restrict__ P,
                                               const u16* __restrict__ feats, const float* __restrict__ labels,
                                               int n_rows, int batch, double* __restrict__ metrics, char* smem,
-                                              int* rowidx) {
+                                              int* rowidx, int chunked = 0) {
   auto&& d = C::desc(dp);
+  constexpr int BP = Tile<MT>::BP;
+  bf16x8 wpre[RX_PJ][RX_PK];
+  if (chunked) {
+    const int cpb = (batch + BP - 1) / BP;
+    const int b = (int)blockIdx.x / cpb, q = (int)blockIdx.x % cpb;
+    const int nb = min(batch, n_rows - b * batch);
+    const int row0 = b * batch + q * BP;
+    const int nvalid = max(0, min(BP, nb - q * BP));
+    if (nvalid <= 0) return;
+    for (int i = rx_tid<false>(); i < BP; i += RX_THREADS) rowidx[i] = i < nvalid ? row0 + i : row0;
+    load_params<C>(d, smem, P, rstats);
+    __syncthreads();
+    load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, false, dp, P, metrics);
+    fwd_prefetch<false>(C::first(d), img, wpre);
+    MwCtx ev{};
+    ev.n_total = nb;   // the loss mean runs over the whole batch; chunk 0 counts the batch
+    ev.wg = q;
+    ev.G = cpb;
+    C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
+      layer_forward<MT, false, false>(d, ly, nx, last, smem, img, P, nullptr, labels, rowidx, nvalid, nullptr,
+                                      metrics, wpre, true, l, nullptr, nullptr, &ev);
+    });
+    return;
+  }
   const int row0 = blockIdx.x * batch;
   const int nvalid = min(batch, n_rows - row0);
-  for (int i = rx_tid<false>(); i < Tile<MT>::BP; i += RX_THREADS) rowidx[i] = i < nvalid ? row0 + i : row0;
+  for (int i = rx_tid<false>(); i < BP; i += RX_THREADS) rowidx[i] = i < nvalid ? row0 + i : row0;
   load_params<C>(d, smem, P, rstats);
   __syncthreads();
   load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, false, dp, P, metrics);
-  bf16x8 wpre[RX_PJ][RX_PK];
   fwd_prefetch<false>(C::first(d), img, wpre);
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
     layer_forward<MT, false, false>(d, ly, nx, last, smem, img, P, nullptr, labels, rowidx, nvalid, nullptr, metrics,

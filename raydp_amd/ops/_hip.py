@@ -57,7 +57,14 @@ class StepBufs(ctypes.Structure):
     """Device buffers of one fused model (csrc/hip/fused_mlp.hip StepBufs)."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("d_dev", "img", "rstats", "params", "grads", "scratch",
                                                "metrics", "stamps", "jit_step", "jit_eval",
-                                               "jit_persist")]
+                                               "jit_persist", "mw")]
+
+
+class MwArgs(ctypes.Structure):
+    """Multi-workgroup step of one fused model (csrc/hip/fused_mlp.hip MwArgs)."""
+    _fields_ = [("part", ctypes.c_void_p), ("ctl", ctypes.c_void_p), ("G", ctypes.c_int),
+                ("resident_ok", ctypes.c_int), ("scratch_stride", ctypes.c_longlong),
+                ("ticks", ctypes.c_ulonglong)]
 
 
 class OptSeg(ctypes.Structure):
@@ -148,6 +155,9 @@ def lib():
                                           ctypes.c_double, vp]
     L.rx_mlp_train_persistent.restype = i
     L.rx_ps_sync_words.restype = i
+    L.rx_mw_args_size.restype = i
+    L.rx_mw_resident.argtypes = [i, i, i]
+    L.rx_mw_resident.restype = i
     L.rx_ps_err_index.restype = i
     L.rx_ps_grid_blocks.argtypes = [vp]
     L.rx_ps_grid_blocks.restype = i
@@ -176,7 +186,8 @@ def lib():
                "rx_comm_allreduce", "rx_comm_broadcast", "rx_comm_destroy"):
         getattr(L, fn).restype = i
     for name, cls in (("rx_mlp_desc_size", MlpDesc), ("rx_opt_desc_size", OptDesc),
-                      ("rx_ingest_args_size", IngestArgs), ("rx_step_bufs_size", StepBufs)):
+                      ("rx_ingest_args_size", IngestArgs), ("rx_step_bufs_size", StepBufs),
+                      ("rx_mw_args_size", MwArgs)):
         got = getattr(L, name)()
         if got != ctypes.sizeof(cls):
             raise RuntimeError(f"ABI mismatch for {cls.__name__}: C {got} vs ctypes {ctypes.sizeof(cls)}")

@@ -114,10 +114,35 @@ _ATTR = {"weight": "weight", "bias": "bias", "gamma": "weight", "beta": "bias", 
 
 
 def pick_mt(batch: int) -> Optional[int]:
+    """Row tiles of a single-workgroup step (batch <= 128), else None."""
     for mt in (2, 4, 8):
         if batch <= mt * 16:
             return mt
     return None
+
+
+# Largest batch of the multi-workgroup step: every one of its ceil(batch / 16 mt) workgroups
+# must be resident at once (one per CU at the step kernel's LDS size; the host also checks the
+# occupancy on the device).
+MAX_FUSED_BATCH = 16384
+
+
+def fused_batch_ok(batch: int) -> bool:
+    return 1 <= int(batch) <= MAX_FUSED_BATCH
+
+
+def layout_candidates(batch: int):
+    """(row tiles per workgroup, workgroups per step) to try, best first: one workgroup for a
+    batch that fits its tile, else the multi-workgroup step with the widest tile whose LDS
+    image fits (csrc/hip/mlp_core.h MwCtx)."""
+    out = []
+    single = pick_mt(batch)
+    if single is not None:
+        out.append((single, 1))
+    for mt in (8, 4, 2):
+        if batch > 16 * mt:
+            out.append((mt, -(-batch // (16 * mt))))
+    return out
 
 
 class FusedMLPTrainer:
@@ -129,21 +154,36 @@ class FusedMLPTrainer:
         self.layout_only = layout_only
         self.spec, self.cfg, self.device = spec, opt_cfg, torch.device("cpu" if layout_only else device)
         self.batch = int(batch_size)
-        self.mt = pick_mt(self.batch)
-        if self.mt is None:
-            raise ValueError("batch too large for the fused trainer")
-        self.bp = self.mt * 16
+        if not fused_batch_ok(self.batch):
+            raise ValueError(f"batch {self.batch} outside the fused trainer's range (1..{MAX_FUSED_BATCH})")
         self.loss_code, self.beta = loss
         self.lr_schedule = lr_schedule
         self.acc_thr = acc_thr           # binary accuracy threshold (None: not counted)
         self.record_steps = False        # per-step device times of persistent epochs
         self.step_count = 0
         self.lib = _hip.lib()
-        self._build()
+        err = None
+        for mt, G in layout_candidates(self.batch):
+            self.mt, self.G, self.bp = mt, G, mt * 16
+            try:
+                self._build()
+                err = None
+                break
+            except ValueError as e:      # LDS / width limits of this tile: try the next layout
+                err = e
+        if err is not None:
+            raise err
 
     # ----------------------------------------------------------------------- layout -------
     def _build(self):
         spec, dev, bp, mt = self.spec, self.device, self.bp, self.mt
+        G = self.G
+        bp_all = G * bp      # exported X^T / G^T columns: the whole (padded) batch
+        if G > 1:
+            if spec.front:
+                raise ValueError("the multi-workgroup step has no embedding front")
+            if self.loss_code == 4:
+                raise ValueError("cross entropy's weight sum is per workgroup: one-workgroup batches only")
         L = len(spec.layers)
         ntw = 16 // mt
         flat: List[torch.Tensor] = []
@@ -184,7 +224,7 @@ class FusedMLPTrainer:
         nseg = 0
         seg_images = []
         act = 0           # bf16 elements of the exported X^T_l / G^T_l area (wgrad_mode 1)
-        wmode = wgrad_mode()
+        wmode = wgrad_mode() if G == 1 else 1   # multi-workgroup: dW over the whole batch
 
         def vseg(start, n):
             # bias / BN gamma+beta vectors: plain element-wise optimizer segments
@@ -216,9 +256,9 @@ class FusedMLPTrainer:
             seg.start, seg.len, seg.kind = off, oo * i, 1
             seg.out, seg.in_, seg.in_k, seg.out_k = oo, i, in_k, out_k
             x.xg_off = seg.xg_off = act
-            act += in_n * bp
+            act += in_n * bp_all
             x.gg_off = seg.gg_off = act
-            act += out_n * bp
+            act += out_n * bp_all
             seg.in_n, seg.out_n = in_n, out_n
             seg_images.append((nseg, x.w_img, x.wt_img))
             nseg += 1
@@ -323,8 +363,12 @@ class FusedMLPTrainer:
         self._arena_plan = {"params": (params_h.numel(), torch.float32), "rstats": (rs_h.numel(), torch.float32)}
         self._arena_host = {"params": params_h, "rstats": rs_h}
         self._arena_zero = [("grads", act_off + act_floats, torch.float32), ("m", params_h.numel(), torch.float32),
-                            ("v", params_h.numel(), torch.float32), ("scratch", max(1, scratch_off), torch.float32),
-                            ("metrics", 8, torch.float64), ("img", max(8, img_off), torch.bfloat16)]
+                            ("v", params_h.numel(), torch.float32),
+                            ("scratch", max(1, scratch_off) * G, torch.float32),
+                            ("metrics", 8, torch.float64), ("img", max(8, img_off), torch.bfloat16),
+                            ("mw_part", max(1, pr_total) * G if G > 1 else 1, torch.float32),
+                            ("mw_ctl", 4, torch.int32)]
+        self._scratch_stride = max(1, scratch_off)
         self._arena_dev = dev
         self._seg_images = seg_images
         cfg = self.cfg
@@ -332,7 +376,7 @@ class FusedMLPTrainer:
         o.b1, o.b2, o.eps = cfg.get("b1", 0.9), cfg.get("b2", 0.999), cfg.get("eps", 1e-8)
         o.wd, o.momentum, o.dampening = cfg.get("wd", 0.0), cfg.get("momentum", 0.0), cfg.get("dampening", 0.0)
         o.nesterov, o.maximize = int(cfg.get("nesterov", False)), int(cfg.get("maximize", False))
-        o.act_off, o.act_floats, o.bp, o.wgrad_mode = act_off, act_floats, bp, wmode
+        o.act_off, o.act_floats, o.bp, o.wgrad_mode = act_off, act_floats, bp_all, wmode
         self.opt = o
         self.lds_bytes = lds
         # descriptors live in device memory: the kernels index them with runtime layer ids
@@ -345,9 +389,24 @@ class FusedMLPTrainer:
         b.scratch, b.metrics = self.scratch.data_ptr(), self.metrics.data_ptr()
         self.bufs = b
         self.jit = None
+        self._mw_args = None
+        if G > 1:
+            a = _hip.MwArgs()
+            a.part, a.ctl, a.G = self.mw_part.data_ptr(), self.mw_ctl.data_ptr(), G
+            a.scratch_stride = self._scratch_stride
+            from raydp_amd.utils.config import get as conf_get
+            khz = 100000
+            a.ticks = int(float(conf_get("spark.ray.mi355x.mlp_persistent.timeout_s")) * khz * 1000)
+            a.resident_ok = 0
+            if not self.layout_only:
+                if int(self.lib.rx_mw_resident(mt, lds, G)) != 0:
+                    raise ValueError(f"{G} step workgroups of {lds} B LDS cannot be resident at once")
+                a.resident_ok = 1
+            self._mw_args = a
+            b.mw = ctypes.addressof(a)
         if self.layout_only:
             return
-        if jit_enabled():
+        if jit_enabled() and G == 1:
             from raydp_amd.ops import mlp_jit
             self.jit = mlp_jit.load_specialized(self)
         self.refresh_images()
@@ -382,6 +441,7 @@ class FusedMLPTrainer:
         self.params, self.rstats = view("params"), view("rstats")
         self.grads, self.m, self.v = view("grads"), view("m"), view("v")
         self.scratch, self.metrics, self.img = view("scratch"), view("metrics"), view("img")
+        self.mw_part, self.mw_ctl = view("mw_part"), view("mw_ctl")
         self._desc_buf = arena[desc_off:desc_off + len(desc_bytes)]
         base = self.img.data_ptr()
         o = self.opt
@@ -540,6 +600,13 @@ class FusedMLPTrainer:
             # epoch-end agreement over xGMI, read with the metrics (one D2H copy)
             xg.vote(self.metrics[7:8])
         pre, self._metrics_np = getattr(self, "_metrics_np", None), None
+        if self.G > 1 and pre is None:
+            # the multi-workgroup barriers' timeout word comes back with the metrics (one sync)
+            back = self._readback([self.mw_ctl[2:3], self.metrics])
+            if int(back[0][0]) != 0:
+                raise RuntimeError("fused MLP multi-workgroup step: a grid barrier wait timed out "
+                                   "(a step workgroup was not resident)")
+            pre = back[1].copy()
         out = self._read_metrics(pre)
         if xg is not None and out["xg_vote"] != 0.0:
             from raydp_amd.exceptions import CollectiveError
@@ -572,7 +639,7 @@ class FusedMLPTrainer:
     def _run_persistent(self, feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream) -> bool:
         """The whole epoch as one persistent launch (csrc/hip/mlp_persist.h); False when this
         model / configuration cannot use it (the caller then runs the launch-per-step loop)."""
-        if self.desc.wgrad_mode != 1 or not persistent_enabled() or self.desc.front_n:
+        if self.desc.wgrad_mode != 1 or not persistent_enabled() or self.desc.front_n or self.G > 1:
             # (an embedding front's tables are updated between steps by the optimizer kernel,
             # which the persistent epoch does not run)
             return False

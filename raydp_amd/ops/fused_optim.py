@@ -78,6 +78,10 @@ def sgd_supported(opt) -> Optional[str]:
         if isinstance(g["lr"], torch.Tensor) or g.get("differentiable", False):
             return "tensor / differentiable learning rate"
         for p in g["params"]:
+            if p.grad is not None and p.grad.is_sparse and float(g["momentum"]) != 0.0:
+                # torch.optim.SGD keeps a momentum buffer for sparse gradients too (it densifies
+                # the buffer): torch's own step reproduces that, this one does not
+                return "sparse gradient with momentum"
             if p.grad is not None and not p.grad.is_sparse and (
                     not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous()
                     or not p.grad.is_contiguous() or p.grad.dtype != torch.float32):
@@ -97,7 +101,9 @@ def sgd_step(opt) -> None:
             if p.grad is None:
                 continue
             if p.grad.is_sparse:
-                # embedding rows: torch's sparse path (momentum is not defined for sparse grads)
+                # embedding rows, plain SGD (sgd_supported sends sparse + momentum to torch)
+                if mom != 0.0:
+                    raise RuntimeError("sgd_step: sparse gradient with momentum (use opt.step())")
                 g = p.grad if not maxim else -p.grad
                 if wd:
                     raise RuntimeError("weight decay with sparse gradients is not supported by SGD")

@@ -355,6 +355,18 @@ class ClusterBackend:
             pg = pgroup.get_placement_group_by_id(self.conf["spark.ray.placement_group"])
             bundles = [int(x) for x in self.conf.get("spark.ray.bundle_indexes", "").split(",") if x != ""] \
                 or list(range(pg.bundle_count))
+        if not bundles:
+            # fail fast (with the node table in the message) when no node can ever host one
+            # executor of this shape; a shortfall of capacity only warns: the app master's
+            # orders queue until resources free up, as executors do under Ray
+            from raydp_amd.ray_cluster_resources import plan_executors
+            req = {"CPU": float(cpu) if cpu else float(self.cores), **custom}
+            if mem:
+                req["memory"] = float(parse_memory_size(mem))
+            plan = plan_executors(self._initial_executors(), req)
+            if plan.nodes and plan.capacity_total < plan.wanted:
+                logger.warning("the cluster can host %d of the %d requested executors %s (%s)",
+                               plan.capacity_total, plan.wanted, plan.request, plan.describe())
         dyn = self.conf.get("spark.dynamicAllocation.enabled", "false").lower() == "true"
         max_n = self.conf.get("spark.dynamicAllocation.maxExecutors")
         orders = self.appmaster.register_app(

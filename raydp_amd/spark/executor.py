@@ -153,7 +153,6 @@ class RayDPExecutor:
     def persist_partitions(self, payload: bytes, rdd_id: str, indices: List[int]):
         """Compute ``indices`` and seal them in this node's store; returns
         ``[(index, object_id, node_id, store_path, num_rows)]``."""
-        from raydp_amd.spark import native_exec
         from raydp_amd.utils import tracing
         with tracing.span("stage unpickle", cat="executor"):
             fn = self._fn(payload)
@@ -171,23 +170,21 @@ class RayDPExecutor:
             # every partition of this call goes onto the native worker pool at once
             with tracing.span("native tasks", cat="executor", tasks=len(indices), persist=rdd_id):
                 sub = []
-                for i in indices:
-                    tid, keep = self._native.submit(low, i, st, oids[i])
-                    sub.append((i, tid, keep))
-                for i, tid, keep in sub:
-                    if tid < 0:
-                        continue
-                    status, n, _, err = self._native.wait(tid)
-                    if status == native_exec.OK:
-                        rows[i] = n
-                        native_exec.STATS["native_tasks"] += 1
-                        continue
-                    # FALLBACK / RETRY (a UDF was retired) / ERROR (e.g. the store is full):
-                    # the Python path computes the partition and raises its own error if any
-                    kind = {native_exec.RETRY: "native_retries", native_exec.ERROR: "native_errors"}
-                    native_exec.STATS[kind.get(status, "native_fallbacks")] += 1
-                    if status == native_exec.ERROR:
-                        native_exec.LAST_ERROR[0] = err
+                waited = set()
+                try:
+                    for i in indices:
+                        tid, keep = self._native.submit(low, i, st, oids[i])
+                        sub.append((i, tid, keep))
+                    self._wait_native(sub, waited, rows)
+                finally:
+                    # never leave a submitted task running behind a failed submit / wait: it would
+                    # keep writing the same object ids the retried partition is about to create
+                    for _i, tid, _keep in sub:
+                        if tid >= 0 and tid not in waited:
+                            try:
+                                self._native.wait(tid)
+                            except Exception:  # noqa: BLE001 - draining only; the first error propagates
+                                pass
         out = []
         for i in indices:
             oid = oids[i]
@@ -199,6 +196,24 @@ class RayDPExecutor:
             out.append((i, oid, st.node_id, st.path, rows[i]))
             self.tasks_run += 1
         return out
+
+    def _wait_native(self, sub, waited, rows):
+        from raydp_amd.spark import native_exec
+        for i, tid, keep in sub:
+            if tid < 0:
+                continue
+            status, n, _, err = self._native.wait(tid)
+            waited.add(tid)
+            if status == native_exec.OK:
+                rows[i] = n
+                native_exec.STATS["native_tasks"] += 1
+                continue
+            # FALLBACK / RETRY (a UDF was retired) / ERROR (e.g. the store is full):
+            # the Python path computes the partition and raises its own error if any
+            kind = {native_exec.RETRY: "native_retries", native_exec.ERROR: "native_errors"}
+            native_exec.STATS[kind.get(status, "native_fallbacks")] += 1
+            if status == native_exec.ERROR:
+                native_exec.LAST_ERROR[0] = err
 
     def _persist_python(self, fn, i, st, oid, rdd_id) -> int:
         import pyarrow as pa

@@ -130,8 +130,8 @@ class FusedMLPEngine:
         if device.type != "cuda":
             return None
         from raydp_amd.models.mlp_spec import extract_mlp_spec
-        from raydp_amd.ops.fused_mlp import loss_code, optimizer_config, pick_mt
-        if pick_mt(batch_size) is None:
+        from raydp_amd.ops.fused_mlp import fused_batch_ok, loss_code, optimizer_config, pick_mt
+        if not fused_batch_ok(batch_size):
             return None
         if feature_columns and isinstance(feature_columns[0], (list, tuple)):
             return None
@@ -144,6 +144,8 @@ class FusedMLPEngine:
             return None
         if (spec.raw_features or spec.in_features) != len(feature_columns):
             return None
+        if pick_mt(batch_size) is None and (spec.front or lc[0] == 4):
+            return None     # the multi-workgroup step (batch > 128) has neither
         if lc[0] == 4:
             # cross entropy: the classes of one 16-wide output tile; accuracy is the argmax,
             # counted by the kernel (regression metrics do not apply)

@@ -244,9 +244,14 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             lr_fn = None
             if config["lr_scheduler_creator"]:
                 lr_fn = _make_lr_schedule(optimizer, config["lr_scheduler_creator"], config)
-            engine = FusedMLPEngine(model, optimizer, spec, lc, oc, acc_thr, metrics, device, config, lr_fn,
-                                    loss=loss)
-        else:
+            try:
+                engine = FusedMLPEngine(model, optimizer, spec, lc, oc, acc_thr, metrics, device, config, lr_fn,
+                                        loss=loss)
+            except ValueError:
+                if fused_mode == "on":
+                    raise
+                fused = None   # a layout limit of the fused kernels (LDS, residency): torch loop
+        if fused is None:
             model = model.to(device)       # in place: the optimizer keeps its parameter objects
             sched = config["lr_scheduler_creator"](optimizer, config) if config["lr_scheduler_creator"] else None
             if resume_dir:
@@ -285,8 +290,13 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         if fused is None:
             return None
         spec, lc, oc, acc_thr = fused
-        return FusedMLPEngine(model, opt, spec, lc, oc, acc_thr, metrics, device, config, None,
-                              detached=True, loss=loss)
+        try:
+            return FusedMLPEngine(model, opt, spec, lc, oc, acc_thr, metrics, device, config, None,
+                                  detached=True, loss=loss)
+        except ValueError:
+            if fused_mode == "on":
+                raise
+            return None     # a layout limit of the fused kernels (LDS, residency): torch loop
 
     @staticmethod
     def _train_loop(config, engine, start_epoch, device):
