@@ -108,11 +108,13 @@ def make_csv(path: str, n: int, seed: int, chunk: int = 1 << 20):
             writer.close()
 
 
-def nyc_model(cols):
+def _nyc_class():
     import torch.nn as nn
     import torch.nn.functional as F
 
     class NYC_Model(nn.Module):
+        """examples/pytorch_nyctaxi.py NYC_Model (defined once, at module level, as there)."""
+
         def __init__(self, cols):
             super().__init__()
             self.fc1 = nn.Linear(cols, 256)
@@ -135,7 +137,17 @@ def nyc_model(cols):
             x = F.relu(self.fc4(x))
             x = self.bn4(x)
             return self.fc5(x)
-    return NYC_Model(cols)
+    return NYC_Model
+
+
+_NYC_MODEL = None
+
+
+def nyc_model(cols):
+    global _NYC_MODEL
+    if _NYC_MODEL is None:
+        _NYC_MODEL = _nyc_class()
+    return _NYC_MODEL(cols)
 
 
 def _read_nyc(spark, csv_path):

@@ -126,7 +126,10 @@ def main():
                           "mlp": "eager torch" if args.eager_mlp else "fused MFMA towers (csrc/hip/linear_act.hip)",
                           "tables": 26, "rows_per_table": args.rows_per_table, "scaling": "weak",
                           "hip_graph": graph is not None, "graph_error": graph_err,
-                          "mp_capturable": bool(mp_capturable)}), flush=True)
+                          "mp_capturable": bool(mp_capturable),
+                          "ddp": {"buckets": len(net.buckets), "bucket_mb": os.environ.get("RAYDP_DDP_BUCKET_MB"),
+                                  "allreduce": net._allreduce.kind,
+                                  "launched": dict(net._allreduce.launched)} if mp else None}), flush=True)
     if mp:
         dist.destroy_process_group()
 

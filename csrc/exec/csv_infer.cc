@@ -190,6 +190,9 @@ int rx_csv_infer(const char* data, int64_t len, char delim, void* out) {
       if (static_cast<unsigned char>(h.p[j]) >= 0x80) return 0;
     bool any_real = false, any_text = false, any_value = false;
     for (size_t r = 0; r < nrow; ++r) {
+      // one surely-text value decides the column (Arrow's ladder ends on string whatever the
+      // other values are; "" stays the only null): the rest need no classification
+      if (any_text) break;
       const Kind k = classify(cells[(r + 1) * ncol + c], &ivals[r], &dvals[r]);
       if (k == kAmbiguous) return 0;
       kinds[r] = k;

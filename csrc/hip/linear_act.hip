@@ -113,18 +113,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t lin_rsrc(const LinOperand& o, 
 
 // The T/32 chunks a thread stages for one operand tile of T rows: tile rows r0..r0+T-1,
 // reduction k0..k0+63 (memory orientation: ROW -> (i, j) = (row, k); RED -> (i, j) = (k, row)).
+// Index math is 32-bit unsigned: the host bounds every operand extent below 2^31 bytes (the
+// buffer resource's num_records), so no element offset needs 64 bits -- 64-bit multiplies per
+// chunk per stage were most of the kernel's VALU work (profiles/pmc/SUMMARY.md: VALU/MFMA 12.3).
 template <int MODE, int LAY, int T>
 __device__ __forceinline__ void lin_fetch(__amdgpu_buffer_rsrc_t rs, long long ld, long long r0, long long k0,
                                           long long R, long long Kd, int tid, LinStage<MODE, T / 32>& st) {
   constexpr int CPR = LAY == LIN_ROW ? LIN_BK / 8 : T / 8;  // chunks per memory row of the tile
-  const long long I = LAY == LIN_ROW ? R : Kd, J = LAY == LIN_ROW ? Kd : R;
+  const unsigned I = (unsigned)(LAY == LIN_ROW ? R : Kd), J = (unsigned)(LAY == LIN_ROW ? Kd : R);
+  const unsigned ldu = (unsigned)ld, r0u = (unsigned)r0, k0u = (unsigned)k0;
 #pragma unroll
   for (int t = 0; t < T / 32; ++t) {
     const int c = tid + 256 * t;
-    const int ci = c / CPR, cj = (c % CPR) * 8;
-    const long long i = LAY == LIN_ROW ? r0 + ci : k0 + ci;
-    const long long j = LAY == LIN_ROW ? k0 + cj : r0 + cj;
-    const long long e0 = i * ld + j;  // element offset of the chunk
+    const unsigned ci = (unsigned)(c / CPR), cj = (unsigned)((c % CPR) * 8);
+    const unsigned i = LAY == LIN_ROW ? r0u + ci : k0u + ci;
+    const unsigned j = LAY == LIN_ROW ? k0u + cj : r0u + cj;
+    const unsigned e0 = i * ldu + j;  // element offset of the chunk
     if constexpr (MODE == LIN_V16) {
       const unsigned off = (i < I && j < J) ? (unsigned)(e0 * 2) : LIN_OOB;
       st.v[t] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);

@@ -64,7 +64,7 @@ struct MlpLayer {
   int bn;            // 0 none, 1 act->bn, 2 bn->act
   int g_off, be_off; // BN affine params (-1: not affine)
   int rs_off;        // float offset of [running_mean | running_var] in the stats buffer (-1: none)
-  int pad_;
+  int mw_off;        // multi-workgroup step: float offset of this layer's partial block (MwCtx)
   float eps, momentum;
   int xt_off;        // LDS byte offset of XT_l
   int stat_off;      // float offset of (mean, invstd) pairs for this layer's outputs in LDS
@@ -158,19 +158,38 @@ struct Tile {
 // bounded and a timeout sets the error word, after which every barrier returns at once.
 struct NoMw {  // one workgroup per step (the fields only make MWT::on ? a : b well-formed)
   static constexpr bool on = false;
-  int k, G, wg, n_total;
+  int k, G, wg, n_total, stride;
   float* part;
 };
 
 struct MwCtx {
   static constexpr bool on = true;
   int k;                       // grid barriers passed so far in this step (uniform)
-  float* part;                 // [G][pr_total] partials (the per-column parameter-block layout)
+  float* part;                 // [G][stride] partials; layer l's block at mw_off_l: [fwd | bwd | bias]
+  int stride;                  // floats per workgroup (a multiple of 32: 128-B lines)
   unsigned* ctl;               // [0] barrier counter, [1] done counter, [2] error word
   int G, wg;                   // workgroups of the step, this one's index
   int n_total;                 // valid rows of the whole batch
   unsigned long long ticks;    // wall-clock bound of one barrier wait
 };
+
+// Partial blocks: every (layer, phase) region of every workgroup starts on its own 128-B line. A
+// consumer's XCD must not hold a line of a region before that region's last write of the step
+// (its L2 would then serve the stale copy to the sc1 loads): with regions sharing lines, reading
+// layer l's forward statistics pulled in bytes of a region written only later in the backward.
+__host__ __device__ __forceinline__ int rx_ru32(int x) { return (x + 31) & ~31; }
+template <class LY>
+__device__ __forceinline__ float* mw_fwd(float* part, int stride, const LY& ly, int w) {
+  return part + (size_t)w * stride + ly.mw_off;
+}
+template <class LY>
+__device__ __forceinline__ float* mw_bwd(float* part, int stride, const LY& ly, int w) {
+  return part + (size_t)w * stride + ly.mw_off + rx_ru32(2 * ly.out_n);
+}
+template <class LY>
+__device__ __forceinline__ float* mw_bias(float* part, int stride, const LY& ly, int w) {
+  return part + (size_t)w * stride + ly.mw_off + 2 * rx_ru32(2 * ly.out_n);
+}
 
 #define RX_MW_CTR 0
 #define RX_MW_DONE 1
@@ -446,7 +465,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       if constexpr (MWT::on) {
         // this workgroup's (sum, centred second moment) of column c
         if (colok && lg == 0) {
-          float* pp = mw->part + (size_t)mw->wg * d.pr_total + ly.pr_off + 2 * c;
+          float* pp = mw_fwd(mw->part, mw->stride, ly, mw->wg) + 2 * c;
           rx_st_sc1f(pp, s);
           rx_st_sc1f(pp + 1, v);
         }
@@ -644,7 +663,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
           gsum = rx_colsum16(gsum);
           if (colok && lg == 0 && ly.b_off >= 0) {
             if constexpr (MWT::on)
-              rx_st_sc1f(mw->part + (size_t)mw->wg * d.pr_total + ly.pr_off + 4 * ly.out_n + c, gsum);
+              rx_st_sc1f(mw_bias(mw->part, mw->stride, ly, mw->wg) + c, gsum);
             else
               Gr[ly.b_off + c] = gsum;
           }
@@ -667,11 +686,11 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         const int c = n * 16 + lr;
         const int cc = c < ly.out ? c : 0;
         float S = 0.f;
-        for (int w = 0; w < mw->G; ++w) S += rx_ld_sc1f(mw->part + (size_t)w * d.pr_total + ly.pr_off + 2 * cc);
+        for (int w = 0; w < mw->G; ++w) S += rx_ld_sc1f(mw_fwd(mw->part, mw->stride, ly, w) + 2 * cc);
         const float mean = S / (float)n_batch;
         float M2 = 0.f;
         for (int w = 0; w < mw->G; ++w) {
-          const float* pp = mw->part + (size_t)w * d.pr_total + ly.pr_off + 2 * cc;
+          const float* pp = mw_fwd(mw->part, mw->stride, ly, w) + 2 * cc;
           const int nwi = mw_rows(n_batch, w, T::BP);
           if (nwi == 0) continue;      // an empty workgroup published nothing meaningful
           const float nw = (float)nwi;
@@ -965,7 +984,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       if (mode == 1) {
         if (colok && lg == 0) {
           if constexpr (MWT::on) {
-            float* pp = mw->part + (size_t)mw->wg * d.pr_total + pv.pr_off + 2 * pv.out_n + 2 * c;
+            float* pp = mw_bwd(mw->part, mw->stride, pv, mw->wg) + 2 * c;
             rx_st_sc1f(pp, sg);
             rx_st_sc1f(pp + 1, sgx);
           }
@@ -995,7 +1014,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     bs = rx_colsum16(bs);
     if (colok && lg == 0 && pv.b_off >= 0) {
       if constexpr (MWT::on)
-        rx_st_sc1f(mw->part + (size_t)mw->wg * d.pr_total + pv.pr_off + 4 * pv.out_n + c, bs);
+        rx_st_sc1f(mw_bias(mw->part, mw->stride, pv, mw->wg) + c, bs);
       else
         Gr[pv.b_off + c] = bs;
     }
@@ -1027,7 +1046,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
         const int cc = c < pv.out ? c : 0;
         float sg = 0.f, sgx = 0.f;
         for (int w = 0; w < mw->G; ++w) {
-          const float* pp = mw->part + (size_t)w * d.pr_total + pv.pr_off + 2 * pv.out_n + 2 * cc;
+          const float* pp = mw_bwd(mw->part, mw->stride, pv, w) + 2 * cc;
           sg += rx_ld_sc1f(pp);
           sgx += rx_ld_sc1f(pp + 1);
         }
@@ -1321,7 +1340,7 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
     if (ly.b_off >= 0) {
       for (int c = (int)blockIdx.x * RX_THREADS + rx_tid<false>(); c < ly.out; c += mw.G * RX_THREADS) {
         float s = 0.f;
-        for (int w = 0; w < mw.G; ++w) s += rx_ld_sc1f(mw.part + (size_t)w * d.pr_total + ly.pr_off + 4 * ly.out_n + c);
+        for (int w = 0; w < mw.G; ++w) s += rx_ld_sc1f(mw_bias(mw.part, mw.stride, ly, w) + c);
         Gr[ly.b_off + c] = s;
       }
     }

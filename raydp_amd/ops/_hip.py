@@ -22,7 +22,7 @@ class MlpLayer(ctypes.Structure):
         ("w_off", ctypes.c_int), ("b_off", ctypes.c_int),
         ("act", ctypes.c_int), ("bn", ctypes.c_int),
         ("g_off", ctypes.c_int), ("be_off", ctypes.c_int),
-        ("rs_off", ctypes.c_int), ("pad_", ctypes.c_int),
+        ("rs_off", ctypes.c_int), ("mw_off", ctypes.c_int),
         ("eps", ctypes.c_float), ("momentum", ctypes.c_float),
         ("xt_off", ctypes.c_int), ("stat_off", ctypes.c_int), ("r_off", ctypes.c_int),
         ("pr_off", ctypes.c_int), ("xg_off", ctypes.c_int), ("gg_off", ctypes.c_int),
@@ -63,8 +63,8 @@ class StepBufs(ctypes.Structure):
 class MwArgs(ctypes.Structure):
     """Multi-workgroup step of one fused model (csrc/hip/fused_mlp.hip MwArgs)."""
     _fields_ = [("part", ctypes.c_void_p), ("ctl", ctypes.c_void_p), ("G", ctypes.c_int),
-                ("resident_ok", ctypes.c_int), ("scratch_stride", ctypes.c_longlong),
-                ("ticks", ctypes.c_ulonglong)]
+                ("resident_ok", ctypes.c_int), ("stride", ctypes.c_int), ("pad_", ctypes.c_int),
+                ("scratch_stride", ctypes.c_longlong), ("ticks", ctypes.c_ulonglong)]
 
 
 class OptSeg(ctypes.Structure):

@@ -221,6 +221,7 @@ class FusedMLPTrainer:
         scratch_off = 0
         stat_off = 0
         pr_total = 0
+        mw_total = 0
         nseg = 0
         seg_images = []
         act = 0           # bf16 elements of the exported X^T_l / G^T_l area (wgrad_mode 1)
@@ -300,6 +301,10 @@ class FusedMLPTrainer:
             scratch_off += bp * out_n
             x.pr_off = pr_total
             pr_total += 5 * out_n
+            # multi-workgroup partials: [fwd 2 out_n | bwd 2 out_n | bias out_n], each region on
+            # its own 128-B lines (csrc/hip/mlp_core.h mw_fwd)
+            x.mw_off = mw_total
+            mw_total += 2 * _ru(2 * out_n, 32) + _ru(out_n, 32)
         # embedding front: every table is one contiguous run of the flat vector (element-wise
         # optimizer segment); front column k reads element [id][j] at poff + id * stride
         front = spec.front or []
@@ -366,9 +371,10 @@ class FusedMLPTrainer:
                             ("v", params_h.numel(), torch.float32),
                             ("scratch", max(1, scratch_off) * G, torch.float32),
                             ("metrics", 8, torch.float64), ("img", max(8, img_off), torch.bfloat16),
-                            ("mw_part", max(1, pr_total) * G if G > 1 else 1, torch.float32),
+                            ("mw_part", mw_total * G if G > 1 else 1, torch.float32),
                             ("mw_ctl", 4, torch.int32)]
         self._scratch_stride = max(1, scratch_off)
+        self._mw_stride = mw_total
         self._arena_dev = dev
         self._seg_images = seg_images
         cfg = self.cfg
@@ -393,6 +399,7 @@ class FusedMLPTrainer:
         if G > 1:
             a = _hip.MwArgs()
             a.part, a.ctl, a.G = self.mw_part.data_ptr(), self.mw_ctl.data_ptr(), G
+            a.stride = self._mw_stride
             a.scratch_stride = self._scratch_stride
             from raydp_amd.utils.config import get as conf_get
             khz = 100000

@@ -1,6 +1,11 @@
-"""Copy/kernel overlap summary of a rocprofv3 ``--kernel-trace --memory-copy-trace`` CSV run.
+"""Copy/kernel or kernel/kernel overlap summary of a rocprofv3 CSV run.
 
     python scripts/trace_overlap.py gpurun_out/prof/ingest [--kernel arrow_ingest]
+    python scripts/trace_overlap.py gpurun_out/prof/ddp_overlap --kernel lin_ --with xg_allreduce
+
+The second form (``--with``) reports, per process, how much of the ``--with`` kernels' time
+runs concurrently with ``--kernel`` kernels on another stream: the DDP gradient buckets on the
+comm stream under the backward GEMMs.
 
 For every kernel whose name contains ``--kernel``, reports how much of its execution overlaps
 an in-flight host->device copy (and on which copy stream), plus per-stream busy time. Used to
@@ -41,11 +46,38 @@ def _overlap(a, b):
     return tot
 
 
+def kernel_pair(prefix, kernel, other):
+    rows = _rows(prefix + "_kernel_trace.csv")
+    out = {}
+    pids = sorted({r.get("Process_Id", "0") for r in rows})
+    for pid in pids:
+        mine = [r for r in rows if r.get("Process_Id", "0") == pid]
+        a = [r for r in mine if kernel in r["Kernel_Name"]]
+        b = [r for r in mine if other in r["Kernel_Name"]]
+        if not a or not b:
+            continue
+        aiv = _merge([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in a])
+        biv = _merge([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in b])
+        b_busy = sum(e - s for s, e in biv)
+        ov = _overlap(aiv, biv)
+        out[pid] = {"kernel": kernel, "kernel_streams": sorted({r["Stream_Id"] for r in a}),
+                    "with": other, "with_streams": sorted({r["Stream_Id"] for r in b}),
+                    "with_launches": len(b), "with_busy_us": round(b_busy / 1e3, 1),
+                    "with_time_under_kernel_us": round(ov / 1e3, 1),
+                    "with_time_under_kernel_frac": round(ov / b_busy, 3) if b_busy else None}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prefix", help="rocprofv3 output prefix, e.g. gpurun_out/prof/ingest")
     ap.add_argument("--kernel", default="")
+    ap.add_argument("--with", dest="other", default=None,
+                    help="kernel/kernel mode: overlap of these kernels with --kernel ones")
     a = ap.parse_args()
+    if a.other:
+        print(json.dumps(kernel_pair(a.prefix, a.kernel, a.other), indent=1))
+        return
     ks = [r for r in _rows(a.prefix + "_kernel_trace.csv") if a.kernel in r["Kernel_Name"]]
     cs = [r for r in _rows(a.prefix + "_memory_copy_trace.csv") if "HOST_TO_DEVICE" in r["Direction"]]
     kiv = _merge([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in ks])

@@ -203,3 +203,27 @@ def test_batch_100_nyc_no_longer_falls_off_the_fused_engine():
 
 
 _ = os
+
+
+def test_multi_workgroup_consecutive_steps_read_fresh_partials():
+    """The partial and counter lines are rewritten every launch: a step must see this step's
+    partials, never a previous launch's copy in some XCD's L2. Two different batches through the
+    same trainer (no optimizer step between them): the second matches its own reference."""
+    loss = nn.MSELoss()
+    model = NYC()
+    tr, ref, ropt, feats, Y, X = _setup(model, loss, torch.optim.Adam, 2048, 4096, 20, 1, lr=1e-3)
+    assert tr.G > 1
+    for half in (0, 1):
+        rows = slice(half * 2048, half * 2048 + 2048)
+        f = feats[rows].contiguous()
+        y = Y[rows].contiguous()
+        g = tr.forward_backward(f, y, 2048).clone()
+        emu = copy.deepcopy(ref)
+        emu.train()
+        loss(emulate(emu, X[rows].to(torch.bfloat16).float()), y).backward()
+        gmap = tr.unflatten(g)
+        emods = dict(emu.named_modules())
+        for name, mod in model.named_modules():
+            if (id(mod), "weight") in gmap:
+                e = _relerr(gmap[(id(mod), "weight")], emods[name].weight.grad)
+                assert e < 2e-2, (half, name, e)
