@@ -280,6 +280,42 @@ def run_dlrm(spark, tsv_path, world, storage, gpu_share=1.0, batch=DLRM_BATCH, e
     return est.fit_on_spark(train_df, test_df)
 
 
+def make_text(path, lines, seed):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    vocab = np.array([f"w{i}" for i in range(5000)])
+    with open(path, "w") as f:
+        for s in range(0, lines, 10000):
+            n = min(10000, lines - s)
+            k = rng.integers(3, 12, n)
+            z = np.minimum(rng.zipf(1.2, int(k.sum())), len(vocab)) - 1
+            words = vocab[z]
+            o = 0
+            out = []
+            for c in k:
+                out.append(" ".join(words[o:o + c]))
+                o += c
+            f.write("\n".join(out) + "\n")
+
+
+class _WordCountResult:
+    """fit-result-shaped record of the word-count run (BASELINE.json config 1)."""
+
+    def __init__(self, lines, words):
+        self.metrics_history = [{"train_rows": lines, "distinct_words": words, "loss": None}]
+
+
+def run_wordcount(spark, path):
+    """BASELINE.json config 1: ``init_spark`` + word count + ``from_spark`` on the CPU: read the
+    text, split / explode, group-by count, convert to a dataset through the object store."""
+    from raydp_amd.spark import functions as F
+    from raydp_amd.spark.dataset import spark_dataframe_to_ray_dataset
+    df = spark.read.text(path)
+    counts = df.select(F.explode(F.split(F.col("value"), " ")).alias("word")).groupBy("word").count()
+    ds = spark_dataframe_to_ray_dataset(counts)
+    return _WordCountResult(None, ds.count())
+
+
 def run_reference_config(spark, storage, epochs=30):
     """The reference example's own configuration (examples/pytorch_nyctaxi.py:50-105 of the
     reference): the 500-row fake_nyctaxi.csv, full ETL, 90/10 random_split, NYC_Model, batch 64,
@@ -427,7 +463,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--workload", choices=["nyc", "horovod", "dlrm"], default="nyc",
                     help="the workload measured as the line's value")
-    ap.add_argument("--extra-workloads", default="horovod,dlrm",
+    ap.add_argument("--extra-workloads", default="horovod,dlrm,wordcount",
                     help="with the nyc headline: other workloads measured afterwards at the same "
                          "N/K/W, reported under config.other_workloads ('none' to skip)")
     ap.add_argument("--extra-timeout", type=float, default=300.0,
@@ -541,6 +577,9 @@ def main():
             if wl == "dlrm":
                 p = os.path.join(tmp, f"{wl}{i}.tsv")
                 make_dlrm_tsv(p, _dlrm_rows(rows // (b * rows_mult), b, rows_mult), seed)
+            elif wl == "wordcount":
+                p = os.path.join(tmp, f"{wl}{i}.txt")
+                make_text(p, rows * 10, seed)
             else:
                 p = os.path.join(tmp, f"{wl}{i}.csv")
                 make_csv(p, rows, seed)
@@ -569,6 +608,8 @@ def main():
         if wl == "horovod":
             return run_horovod(spark, path, n_train, storage, topology=args.topology, gpu_share=share,
                                batch=b or BATCH, epochs=epochs)
+        if wl == "wordcount":
+            return run_wordcount(spark, path)
         return run_dlrm(spark, path, n_train, storage, gpu_share=share, batch=b or DLRM_BATCH, epochs=epochs)
 
     def measure(wl, b, epochs, sampler=None, profile=None):
@@ -720,6 +761,14 @@ def main():
             b = DLRM_BATCH if wl == "dlrm" else BATCH
             try:
                 edt, eres, eph, edrv, _ = measure(wl, b, 1)
+                if wl == "wordcount":
+                    m0 = eres.metrics_history[0]
+                    lines = args.steps * BATCH * rows_mult * 10      # make_text's line count
+                    out_extra[wl] = {
+                        "metric": "word count + from_spark lines/s on the CPU (BASELINE.json config 1)",
+                        "value": round(lines / edt, 1), "unit": "lines/s", "wall_s": round(edt, 4),
+                        "lines": lines, "distinct_words": m0["distinct_words"], "executors": cpus}
+                    continue
                 eh = _train_hist(eres)
                 rows = (eh[0].get("train_rows") if eh else None) or args.steps * b
                 out_extra[wl] = {

@@ -13,7 +13,7 @@ import pyarrow.csv as pacsv
 import pyarrow.parquet as pq
 
 from raydp_amd.spark import plan as P
-from raydp_amd.spark.sources import CsvSource, JsonSource, ParquetSource
+from raydp_amd.spark.sources import CsvSource, JsonSource, ParquetSource, TextSource
 
 
 def _local(path: str) -> str:
@@ -62,6 +62,8 @@ class DataFrameReader:
             return self.parquet(path)
         if fmt == "json":
             return self.json(path)
+        if fmt == "text":
+            return self.text(path)
         raise ValueError(f"unsupported format {fmt}")
 
     def csv(self, path, schema=None, sep=None, header=None, inferSchema=None, **kw):
@@ -82,6 +84,17 @@ class DataFrameReader:
                         parallelism=self._session._default_parallelism(),
                         open_cost_bytes=int(self._session.conf.get(
                             "spark.sql.files.openCostInBytes", str(4 << 20))))
+        return DataFrame(P.SourcePlan(src), self._session)
+
+    def text(self, paths, wholetext: bool = False, lineSep=None):
+        """``spark.read.text``: a DataFrame with one string column ``value``, one row per line
+        (``wholetext=True``: one row per file)."""
+        from raydp_amd.spark.dataframe import DataFrame
+        if lineSep not in (None, "\n"):
+            raise ValueError("text: only newline-separated lines are supported")
+        mpb = int(self._session.conf.get("spark.sql.files.maxPartitionBytes", str(128 << 20)))
+        src = TextSource(paths if isinstance(paths, (str, list, tuple)) else str(paths), max_partition_bytes=mpb,
+                         parallelism=self._session._default_parallelism(), wholetext=wholetext)
         return DataFrame(P.SourcePlan(src), self._session)
 
     def parquet(self, *paths):

@@ -249,6 +249,61 @@ class CsvSource(Source):
         return t
 
 
+class TextSource(Source):
+    """``spark.read.text``: one string column ``value``, one row per line (without the line
+    terminator; a trailing ``\r`` is dropped too, as Hadoop's LineRecordReader does). Files are cut
+    into line-aligned byte splits like CSV files (``CsvSource``), in whole waves of the cores."""
+
+    def __init__(self, path, max_partition_bytes=128 * 1024 * 1024, parallelism=1, wholetext=False):
+        self.files = _expand_paths(path)
+        self.wholetext = wholetext
+        self.splits = []
+        total = sum(os.path.getsize(f) for f in self.files)
+        split_bytes = max(1, min(max_partition_bytes, max(4 << 20, total // max(1, parallelism))))
+        for f in self.files:
+            size = os.path.getsize(f)
+            if wholetext:
+                self.splits.append((f, 0, size))
+                continue
+            nsplit = max(1, int(np.ceil(size / split_bytes)))
+            if nsplit > parallelism > 1:
+                nsplit = -(-nsplit // parallelism) * parallelism
+            b = np.linspace(0, size, nsplit + 1).astype(np.int64)
+            for j in range(nsplit):
+                self.splits.append((f, int(b[j]), int(b[j + 1])))
+        self._schema = pa.schema([pa.field("value", pa.string())])
+
+    def num_partitions(self):
+        return len(self.splits)
+
+    def schema(self):
+        return self._schema
+
+    def load(self, i):
+        f, lo, hi = self.splits[i]
+        with open(f, "rb") as fh:
+            if self.wholetext:
+                return pa.table({"value": pa.array([fh.read().decode("utf-8")], pa.string())})
+            if lo > 0:
+                fh.seek(lo - 1)
+                if fh.read(1) != b"\n":
+                    fh.readline()            # the line belongs to the previous split
+            start = fh.tell() if lo > 0 else 0
+            if start >= hi and lo > 0:
+                return self._schema.empty_table()
+            fh.seek(start)
+            data = fh.read(max(0, hi - start))
+            if data and not data.endswith(b"\n"):
+                data += fh.readline()
+        if not data:
+            return self._schema.empty_table()
+        lines = data.split(b"\n")
+        if lines and lines[-1] == b"":
+            lines.pop()
+        arr = pa.array([ln[:-1] if ln.endswith(b"\r") else ln for ln in lines], pa.binary())
+        return pa.table({"value": arr.cast(pa.string())})
+
+
 class ParquetSource(Source):
     def __init__(self, path):
         self.files = [f for f in _expand_paths(path) if not os.path.basename(f).startswith(("_", "."))]
