@@ -24,6 +24,7 @@
 // compile-time constants and the compiler schedules each layer with full knowledge.
 #pragma once
 #include "rx_common.h"
+#include "rx_grid.h"
 
 // No implicit multiply-add contraction in the training kernels: whether the compiler fuses an
 // a * b + c depends on the inlining context (and on what the SLP vectorizer pairs into v_pk_*
@@ -189,17 +190,6 @@ __device__ __forceinline__ float* mw_bwd(float* part, int stride, const LY& ly, 
 template <class LY>
 __device__ __forceinline__ float* mw_bias(float* part, int stride, const LY& ly, int w) {
   return part + (size_t)w * stride + ly.mw_off + 2 * rx_ru32(2 * ly.out_n);
-}
-
-#define RX_MW_CTR 0
-#define RX_MW_DONE 1
-#define RX_MW_ERR 2
-
-__device__ __forceinline__ float rx_ld_sc1f(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void rx_st_sc1f(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Grid barrier number `k` (1-based, counted by the caller) of the step. Every thread of every

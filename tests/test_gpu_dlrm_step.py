@@ -1,0 +1,190 @@
+"""The persistent DLRM step (csrc/hip/dlrm_step.hip) against an fp32 torch step of the same model.
+
+Reference configuration: examples/pytorch_dlrm.ipynb cells 9 and 14 (Dlrm 13 dense, 26 tables x
+32, bottom 512-128-32, top 1024-1024-512-256-1, SGD, BCEWithLogitsLoss); smaller tables here.
+The kernel runs bf16 MFMA operands with fp32 accumulation, so parity is on the loss and on the
+parameter UPDATES (new - old) relative to the fp32 reference's.
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+
+def _model(rows=2000, seed=0):
+    from raydp_amd.models.dlrm import Dlrm
+    torch.manual_seed(seed)
+    return Dlrm(13, [rows] * 26, [512, 128, 32], [1024, 1024, 512, 256, 1], 32)
+
+
+def _data(n, rows=2000, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    dense = torch.randn(n, 13, generator=g)
+    cats = torch.randint(0, rows, (n, 26), generator=g)
+    # a few duplicate ids inside each batch (the atomics must accumulate them)
+    cats[1::7, 3] = cats[0, 3]
+    y = torch.randint(0, 2, (n,), generator=g).float()
+    return dense, cats, y
+
+
+def _ref_steps(model, dense, cats, y, perm, B, nsteps, lr, nvalid_last=None):
+    """fp32 torch steps on the CPU (eager nn.Linear, sparse embedding gradients, torch SGD)."""
+    opt = torch.optim.SGD(model.parameters(), lr=lr)
+    lossf = torch.nn.BCEWithLogitsLoss()
+    losses = []
+    for j in range(nsteps):
+        nv = B if (nvalid_last is None or j + 1 < nsteps) else nvalid_last
+        idx = perm[j * B: j * B + nv]
+        out = model(dense[idx], cats[idx])
+        loss = lossf(out.view(-1), y[idx])
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    return losses
+
+
+def _params(model):
+    return {k: v.detach().float().cpu().clone() for k, v in model.named_parameters()}
+
+
+def _compare_updates(before, ours, ref, tol):
+    worst = {}
+    for k in before:
+        du, dr = ours[k] - before[k], ref[k] - before[k]
+        n = float(dr.norm())
+        if n == 0.0:
+            assert float(du.norm()) < 1e-6, k
+            continue
+        worst[k] = float((du - dr).norm()) / n
+    bad = {k: v for k, v in worst.items() if v > tol}
+    assert not bad, f"update mismatch: {bad}"
+    return worst
+
+
+@pytest.mark.parametrize("B,nsteps,nvalid_last", [(128, 1, None), (128, 3, None), (64, 2, 40), (256, 1, None)])
+def test_persistent_step_matches_fp32_torch(B, nsteps, nvalid_last):
+    from raydp_amd.ops.dlrm_step import DlrmStep
+    dev = torch.device("cuda", 0)
+    lr = 0.05
+    ref = _model()
+    gpu = copy.deepcopy(ref).to(dev)
+    before = _params(ref)
+    n = B * nsteps + 7
+    dense, cats, y = _data(n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(3))
+    st = DlrmStep(gpu, lr, B, dev)
+    st.bind_data(dense.to(dev), cats.to(dev), y.to(dev))
+    st.steps(perm.to(dev), 0, nsteps, nvalid_last)
+    torch.cuda.synchronize()
+    st.check()
+    ours_loss = float(st.loss_acc.item())
+    ref_losses = _ref_steps(ref, dense, cats, y, perm, B, nsteps, lr, nvalid_last)
+    assert abs(ours_loss - sum(ref_losses)) <= 2e-2 * max(1.0, abs(sum(ref_losses))), (ours_loss, ref_losses)
+    worst = _compare_updates(before, _params(gpu), _params(ref), tol=0.08)
+    assert st.sync_parity() == nsteps % 2
+    print(B, nsteps, {k: round(v, 4) for k, v in sorted(worst.items(), key=lambda kv: -kv[1])[:5]})
+
+
+def test_persistent_step_trains_like_torch_over_many_steps():
+    from raydp_amd.ops.dlrm_step import DlrmStep
+    dev = torch.device("cuda", 0)
+    lr, B, nsteps = 0.1, 128, 40
+    ref = _model(rows=500)
+    gpu = copy.deepcopy(ref).to(dev)
+    n = B * nsteps
+    dense, cats, y = _data(n, rows=500)
+    # learnable labels: a fixed function of the inputs
+    y = ((dense[:, 0] + 0.5 * dense[:, 1] - (cats[:, 0] % 2).float()) > 0).float()
+    perm = torch.arange(n)
+    st = DlrmStep(gpu, lr, B, dev)
+    st.bind_data(dense.to(dev), cats.to(dev), y.to(dev))
+    losses = []
+    for j in range(nsteps):
+        st.steps(perm.to(dev), j * B, 1)
+        losses.append(float(st.step_loss.item()))
+    st.check()
+    ref_losses = _ref_steps(ref, dense, cats, y, perm, B, nsteps, lr)
+    first = sum(losses[:5]) / 5
+    last = sum(losses[-5:]) / 5
+    assert last < first * 0.9, losses
+    rlast = sum(ref_losses[-5:]) / 5
+    assert abs(last - rlast) < 0.05 + 0.1 * rlast, (losses[-5:], ref_losses[-5:])
+
+
+def test_after_training_the_model_forward_sees_the_new_weights():
+    """The model's own fused towers (eval path) must not keep serving pre-training images."""
+    from raydp_amd.ops.dlrm_step import DlrmStep
+    dev = torch.device("cuda", 0)
+    B = 64
+    m = _model().to(dev)
+    dense, cats, y = _data(4 * B)
+    d, c = dense.to(dev), cats.to(dev)
+    with torch.no_grad():
+        before = m(d[:B], c[:B]).clone()    # builds and caches the towers' images
+    st = DlrmStep(m, 0.5, B, dev)
+    st.bind_data(d, c, y.to(dev))
+    st.steps(torch.arange(4 * B, device=dev), 0, 4)
+    torch.cuda.synchronize()
+    st.after_training()
+    with torch.no_grad():
+        after = m(d[:B], c[:B])
+    # reference forward of the trained weights on the CPU (eager fp32)
+    cpu = copy.deepcopy(m).cpu()
+    with torch.no_grad():
+        want = cpu(dense[:B], cats[:B]).to(dev)
+    assert float((after - before).abs().max()) > 1e-3
+    assert float((after - want).abs().max()) < 5e-2 * (1 + float(want.abs().max()))
+
+
+def test_estimator_trains_dlrm_on_the_persistent_step(tmp_path):
+    """The notebook pipeline shape (examples/pytorch_dlrm.ipynb cell 14): Dlrm + SGD +
+    BCEWithLogitsLoss through TorchEstimator.fit_on_spark at batch 128 on one worker runs on the
+    persistent step engine, trains, and its saved model evaluates like the trained weights."""
+    import numpy as np
+    import pyarrow as pa
+    import raydp_amd
+    from raydp_amd import runtime
+    from raydp_amd.torch import TorchEstimator
+    runtime.shutdown()
+    runtime.init(num_cpus=4)
+    try:
+        spark = raydp_amd.init_spark("dlrm-step", 1, 2, "500M")
+        rng = np.random.default_rng(0)
+        n = 128 * 24
+        dense = rng.standard_normal((n, 13)).astype(np.float32)
+        cats = rng.integers(0, 300, (n, 26))
+        y = ((dense[:, 0] + 0.5 * dense[:, 1] - (cats[:, 0] % 2)) > 0).astype(np.float32)
+        cols = {"_c0": y}
+        for i in range(13):
+            cols[f"_c{i + 1}"] = dense[:, i]
+        for i in range(26):
+            cols[f"_c{i + 14}"] = cats[:, i]
+        df = spark.createDataFrame(pa.table(cols))
+
+        def make(config):
+            from raydp_amd.models.dlrm import Dlrm
+            torch.manual_seed(0)
+            return Dlrm(13, [300] * 26, [512, 128, 32], [1024, 1024, 512, 256, 1], 32)
+        est = TorchEstimator(num_workers=1, model=make,
+                             optimizer=lambda m, c: torch.optim.SGD(m.parameters(), lr=0.1),
+                             loss=torch.nn.BCEWithLogitsLoss(), feature_columns=[f"_c{i}" for i in range(1, 40)],
+                             feature_types=[torch.float32] * 13 + [torch.long] * 26, label_column="_c0",
+                             label_type=torch.float, batch_size=128, num_epochs=4, drop_last=True,
+                             storage_path=str(tmp_path), resources_per_worker={"CPU": 1, "GPU": 1})
+        est.fit_on_spark(df)
+        hist = [m for m in est.results.metrics_history if "train_loss" in m]
+        assert hist and all(m["engine"] == "dlrm_step_hip" for m in hist), hist
+        assert hist[-1]["train_loss"] < hist[0]["train_loss"], hist
+        model = est.get_model()
+        with torch.no_grad():
+            out = model(torch.from_numpy(dense[:64]), torch.from_numpy(cats[:64]))
+        assert out.shape == (64, 1) and torch.isfinite(out).all()
+    finally:
+        raydp_amd.stop_spark()
+        runtime.shutdown()
