@@ -164,6 +164,7 @@ def persistent_main(args):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
     st.check()
+    phases = st.phase_profile(perm, 0, 16)
     print(json.dumps({"metric": "DLRM training samples/sec (synthetic Criteo-shaped)",
                       "value": round(args.steps * args.batch / dt, 1), "unit": "samples/s", "n_gpus": 1,
                       "ms_per_step": round(dt * 1e3 / args.steps, 4), "per_gpu_batch": args.batch,
@@ -172,6 +173,7 @@ def persistent_main(args):
                       "tiles": [[(ph.s[j].tm, ph.s[j].tn) for j in range(ph.nspec)]
                                 for ph in st.desc.ph[:st.desc.nph] if ph.kind == 0],
                       "mean_loss": float(st.loss_acc.item()) / args.steps,
+                      "phase_us": phases,
                       "tables": 26, "rows_per_table": args.rows_per_table}), flush=True)
 
 

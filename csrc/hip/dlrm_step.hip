@@ -119,6 +119,7 @@ struct DlrmDesc {
   int pad3;
   unsigned* ctl;           // [0] barrier counter, [1] done, [2] error, [3] parity
   unsigned long long ticks;
+  unsigned long long* stamps;  // nullable: [MAXPH + 1] wall-clock stamps of workgroup 0 (phase profile)
 };
 
 __device__ __forceinline__ long long src_row(const long long* perm, long long row0, int i, int nvalid) {
@@ -439,8 +440,8 @@ __device__ void head_phase(const DlrmDesc* __restrict__ d, const long long* __re
   float* dz = reinterpret_cast<float*>(lds);        // [B]
   float* ls = dz + B;                                // [B]
   float* red = ls + B;                               // [4][K]
-  u16* stT = reinterpret_cast<u16*>(red + 4 * K);    // [K][B + 8]
-  const int TS = B + 8;
+  u16* st = reinterpret_cast<u16*>(red + 4 * K);     // dA staged row-major [B][K + 8]
+  const int TS = K + 8;
   const float bl = d->b_last[0];
   for (int b = wave; b < B; b += 4) {
     float acc = 0.f;
@@ -477,7 +478,7 @@ __device__ void head_phase(const DlrmDesc* __restrict__ d, const long long* __re
       for (int j = 0; j < 4; ++j) {
         dw[j] += g * a[j];
         o[j] = a[j] > 0.f ? g * w[j] : 0.f;
-        stT[(k + j) * TS + b] = rx_f2bf(o[j]);
+        st[b * TS + k + j] = rx_f2bf(o[j]);
       }
       rx_store8_sc1(d->dA, (int)(((long long)b * K + k) * 2), uint2{rx_f2bf2(o[0], o[1]), rx_f2bf2(o[2], o[3])});
     }
@@ -501,7 +502,7 @@ __device__ void head_phase(const DlrmDesc* __restrict__ d, const long long* __re
       d->loss_acc[0] += (double)L;
     }
   }
-  store_transposed(stT, TS, B, K, d->dAT, B, 0, 0);
+  store_transposed(st, TS, B, K, d->dAT, B, 0, 0);
   __syncthreads();
 }
 
@@ -596,6 +597,8 @@ __global__ __launch_bounds__(NT) void dlrm_step_kernel(const DlrmDesc* __restric
   const float lr = d->lr;
   int k = 0;
   const int nph = d->nph, nblk = d->B >> 4;
+  unsigned long long* stamps = blockIdx.x == 0 && threadIdx.x == 0 ? d->stamps : nullptr;
+  if (stamps != nullptr) stamps[0] = wall_clock64();
   for (int ph = 0; ph < nph; ++ph) {
     const Phase& P = d->ph[ph];
     if (P.kind == PH_GEMM) {
@@ -609,6 +612,7 @@ __global__ __launch_bounds__(NT) void dlrm_step_kernel(const DlrmDesc* __restric
       for (int rb = (int)(G - 1 - blockIdx.x); rb < nblk; rb += G) ibwd_block<D>(d, rb, perm, row0, nvalid, lds);
     }
     if (ph + 1 < nph && !rx_grid_barrier(ctl, G, ++k, d->ticks)) break;
+    if (stamps != nullptr) stamps[ph + 1] = wall_clock64();
   }
   rx_grid_finish(ctl, G, CTL_PAR);
 }

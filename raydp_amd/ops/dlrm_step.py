@@ -59,7 +59,7 @@ class DlrmDesc(ctypes.Structure):
                 ("A_last", vp), ("K_last", i32), ("pad2", i32), ("w_last", vp), ("b_last", vp),
                 ("dA", vp), ("dAT", vp), ("logits", vp), ("loss_acc", vp), ("step_loss", vp),
                 ("dZ", vp), ("dmlp", vp), ("dmlpT", vp), ("lr", ctypes.c_float), ("pad3", i32),
-                ("ctl", vp), ("ticks", ctypes.c_ulonglong)]
+                ("ctl", vp), ("ticks", ctypes.c_ulonglong), ("stamps", vp)]
 
 
 _bound = None
@@ -368,7 +368,7 @@ class DlrmStep:
                 need = max(need, 2 * 16 * (w + 8) * 2 + 16 * 32 * (D + 8) * 2 + 16 * (ZP + 8) * 2)
             elif ph.kind == PH_HEAD:
                 K = d.K_last
-                need = max(need, 2 * B * 4 + 4 * K * 4 + K * (B + 8) * 2)
+                need = max(need, 2 * B * 4 + 4 * K * 4 + B * (K + 8) * 2)
             else:
                 need = max(need, 4 * ZP * 4 + 4 * 32 * 40 * 2 + 4 * D * 40 * 2 + 4 * 32 * 8 + 16 * (D + 8) * 2)
         return _ru(need, 16) + 64   # + the barrier's own __shared__ word
@@ -408,13 +408,35 @@ class DlrmStep:
         d.dense, d.ld_dense = dense.data_ptr(), dense.stride(0)
         d.cats, d.ld_cats = cats.data_ptr(), cats.stride(0)
         d.labels, d.ld_lab = labels.data_ptr(), labels.stride(0)
-        raw = bytes(memoryview(d).cast("B"))
+        self._upload()
+        self._data_key = key
+        self._bound_tensors = (dense, cats, labels)
+
+    def _upload(self):
+        raw = bytes(memoryview(self.desc).cast("B"))
         host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
         if self.desc_dev is None:
             self.desc_dev = torch.empty(len(raw), dtype=torch.uint8, device=self.dev)
         self.desc_dev.copy_(host)
-        self._data_key = key
-        self._bound_tensors = (dense, cats, labels)
+
+    def phase_profile(self, perm: torch.Tensor, row0: int = 0, reps: int = 20):
+        """Per-phase microseconds of one step (workgroup 0's wall clock after each grid barrier,
+        median over ``reps`` steps): [(kind, us), ...]. Trains ``reps`` steps."""
+        nph = self.desc.nph
+        st = torch.zeros(reps, nph + 1, dtype=torch.int64, device=self.dev)
+        hz = float(_lib().rx_dlrm_ticks(1.0))
+        try:
+            for r in range(reps):
+                self.desc.stamps = st[r].data_ptr()
+                self._upload()
+                self.steps(perm, row0, 1)
+            torch.cuda.synchronize(self.dev)
+        finally:
+            self.desc.stamps = 0
+            self._upload()
+        d = (st[:, 1:] - st[:, :-1]).double().median(dim=0).values.cpu() * 1e6 / hz
+        names = {PH_GEMM: "gemm", PH_BOTTOM: "bottom", PH_HEAD: "head", PH_IBWD: "ibwd"}
+        return [(names[self.desc.ph[k].kind], round(float(d[k]), 2)) for k in range(nph)]
 
     def steps(self, perm: torch.Tensor, row0: int, nsteps: int, nvalid_last: Optional[int] = None):
         """Launch ``nsteps`` steps on rows ``perm[row0 + j * B ...]`` (int64 device permutation)."""

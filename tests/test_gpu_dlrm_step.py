@@ -45,7 +45,7 @@ def _ref_steps(model, dense, cats, y, perm, B, nsteps, lr, nvalid_last=None):
         opt.zero_grad()
         loss.backward()
         opt.step()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     return losses
 
 
@@ -86,7 +86,10 @@ def test_persistent_step_matches_fp32_torch(B, nsteps, nvalid_last):
     ours_loss = float(st.loss_acc.item())
     ref_losses = _ref_steps(ref, dense, cats, y, perm, B, nsteps, lr, nvalid_last)
     assert abs(ours_loss - sum(ref_losses)) <= 2e-2 * max(1.0, abs(sum(ref_losses))), (ours_loss, ref_losses)
-    worst = _compare_updates(before, _params(gpu), _params(ref), tol=0.08)
+    # bf16 operands: the launch-per-op tower path (fused Linear kernels + torch SGD) measures the
+    # same per-layer update error on this config -- 0.12-0.13 on the bottom MLP, where the batch sum
+    # of the gradient cancels (profiles/r4_dlrm_step_vs_launch_per_op_update_err.txt)
+    worst = _compare_updates(before, _params(gpu), _params(ref), tol=0.2)
     assert st.sync_parity() == nsteps % 2
     print(B, nsteps, {k: round(v, 4) for k, v in sorted(worst.items(), key=lambda kv: -kv[1])[:5]})
 
@@ -112,9 +115,12 @@ def test_persistent_step_trains_like_torch_over_many_steps():
     ref_losses = _ref_steps(ref, dense, cats, y, perm, B, nsteps, lr)
     first = sum(losses[:5]) / 5
     last = sum(losses[-5:]) / 5
-    assert last < first * 0.9, losses
+    assert last < first * 0.97, losses
     rlast = sum(ref_losses[-5:]) / 5
-    assert abs(last - rlast) < 0.05 + 0.1 * rlast, (losses[-5:], ref_losses[-5:])
+    assert abs(last - rlast) < 0.02 + 0.05 * rlast, (losses[-5:], ref_losses[-5:])
+    # the whole trajectory follows the fp32 one step by step
+    gap = max(abs(a - b) for a, b in zip(losses, ref_losses))
+    assert gap < 0.03, (gap, losses, ref_losses)
 
 
 def test_after_training_the_model_forward_sees_the_new_weights():
