@@ -14,7 +14,8 @@
 //           in LDS (MFMA 16x16x32 bf16) -> interaction input X = [bottom out; 26 table rows] ->
 //           Z = [x0 | strict lower triangle of X X^T | 0]; stores H_l, H_l^T, X, Z, Z^T
 //   GEMM    top forward layers: tiles of Y = relu(A W^T + b), stored row-major and transposed
-//   HEAD    one workgroup: last layer (N = 1) + BCE + its backward and SGD -> dA of layer L-1
+//   HEAD    per 16-row block: last layer (N = 1) + BCE + its backward -> dA of layer L-1 and the
+//           block's partial of the last layer's gradient (its SGD: one workgroup, next phase)
 //   GEMM    per top layer, backward: dgrad tiles (dX = dY W, ReLU mask of X) AND wgrad tiles
 //           (dW = dY^T X with the SGD update of the fp32 master in the epilogue) in ONE phase
 //   IBWD    per 16 samples: dX = S X (S = symmetric dZ), bottom-MLP gradient (ReLU-masked),
@@ -120,6 +121,8 @@ struct DlrmDesc {
   unsigned* ctl;           // [0] barrier counter, [1] done, [2] error, [3] parity
   unsigned long long ticks;
   unsigned long long* stamps;  // nullable: [MAXPH + 1] wall-clock stamps of workgroup 0 (phase profile)
+  float* head_part;        // [B / 16][head_ld]: per 16-row block sum dz A (K_last), sum dz, sum loss
+  int head_ld, pad4;
 };
 
 __device__ __forceinline__ long long src_row(const long long* perm, long long row0, int i, int nvalid) {
@@ -157,12 +160,18 @@ __device__ __forceinline__ void store_transposed(const u16* st, int ss, int TM, 
 }
 
 // ------------------------------------------------------------------------------------- GEMM --
+// Every global operand of a job is requested before the job waits for any: the K loop's A / B
+// fragments in bursts, and ahead of them the epilogue's own operands that do not depend on the
+// product (fp32 master weights of a WGRAD tile, the FWD bias, the DGRAD ReLU mask), so their
+// latency hides under the K loop instead of following it.
 template <int MS, int NS>
 __device__ void gemm_job(const GSpec& s, int p, int mt, int nt, float lr, char* lds) {
   constexpr int TM = MS * 16, TN = NS * 16;
   constexpr int KC = (32 / (MS + NS)) > 8 ? 8 : (32 / (MS + NS));
   constexpr int PS = TN + 4;             // fp32 partial row stride
   constexpr int SS = TN + 8;             // bf16 staging row stride
+  constexpr int CC = TN / 8;             // 8-column chunks per row
+  constexpr int IT = (TM * CC + NT - 1) / NT;   // epilogue chunks per thread
   float* part = reinterpret_cast<float*>(lds);                       // [4][TM][PS]
   u16* st = reinterpret_cast<u16*>(lds + 4 * TM * PS * 4);          // [TM][SS]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr_ = lane & 15, lg = lane >> 4;
@@ -172,6 +181,30 @@ __device__ void gemm_job(const GSpec& s, int p, int mt, int nt, float lr, char* 
   const int nks = s.K >> 5;
   const int per = (nks + 3) >> 2;
   const int k0s = wave * per, k1s = min(nks, k0s + per);
+  float pre[IT][8];
+  u32x4 mk[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = tid + it * NT;
+    const int r = idx / CC, c = (idx % CC) * 8, m = m0 + r, n = n0 + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pre[it][j] = 0.f;
+    mk[it] = u32x4{0u, 0u, 0u, 0u};
+    if (idx < TM * CC) {
+      if (s.epi == EPI_WGRAD) {
+        const RX_GLOBAL float* w = rx_g(s.W) + (long long)m * s.kvalid;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (n + j < s.kvalid) pre[it][j] = w[n + j];
+      } else if (s.epi == EPI_FWD) {
+        const RX_GLOBAL float* bias = rx_g(s.bias);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pre[it][j] = bias[n + j];
+      } else if (s.mask != nullptr) {
+        mk[it] = rx_load16_sc1(s.mask, (int)(((long long)m * s.ldmask + n) * 2));
+      }
+    }
+  }
   f32x4 acc[MS][NS];
 #pragma unroll
   for (int i = 0; i < MS; ++i)
@@ -203,8 +236,10 @@ __device__ void gemm_job(const GSpec& s, int p, int mt, int nt, float lr, char* 
 #pragma unroll
       for (int r = 0; r < 4; ++r) part[(wave * TM + 16 * i + 4 * lg + r) * PS + 16 * j + lr_] = acc[i][j][r];
   __syncthreads();
-  constexpr int CC = TN / 8;
-  for (int idx = tid; idx < TM * CC; idx += NT) {
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = tid + it * NT;
+    if (idx >= TM * CC) break;
     const int r = idx / CC, c = (idx % CC) * 8;
     float v[8];
 #pragma unroll
@@ -215,11 +250,11 @@ __device__ void gemm_job(const GSpec& s, int p, int mt, int nt, float lr, char* 
     const int m = m0 + r, n = n0 + c;
     if (s.epi == EPI_WGRAD) {
       // SGD on the fp32 master (columns past kvalid are the image's zero padding)
-      float* w = s.W + (long long)m * s.kvalid;
+      RX_GLOBAL float* w = rx_g(s.W) + (long long)m * s.kvalid;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         if (n + j < s.kvalid) {
-          const float nw = w[n + j] - lr * v[j];
+          const float nw = pre[it][j] - lr * v[j];
           w[n + j] = nw;
           v[j] = nw;
         } else {
@@ -231,14 +266,14 @@ __device__ void gemm_job(const GSpec& s, int p, int mt, int nt, float lr, char* 
       if (s.epi == EPI_FWD) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          v[j] += s.bias[n + j];
+          v[j] += pre[it][j];
           if (s.relu) v[j] = fmaxf(v[j], 0.f);
         }
       } else if (s.mask != nullptr) {
-        float mk[8];
-        unpack8(rx_load16_sc1(s.mask, (int)(((long long)m * s.ldmask + n) * 2)), mk);
+        float mf[8];
+        unpack8(mk[it], mf);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = mk[j] > 0.f ? v[j] : 0.f;
+        for (int j = 0; j < 8; ++j) v[j] = mf[j] > 0.f ? v[j] : 0.f;
       }
       if (s.Yf != nullptr) {
         const int bo = (int)(((long long)m * s.ldyf + n) * 4);
@@ -247,25 +282,29 @@ __device__ void gemm_job(const GSpec& s, int p, int mt, int nt, float lr, char* 
       }
       if (s.Y != nullptr) rx_store16_sc1(s.Y, (int)(((long long)m * s.ldy + n) * 2), pack8(v));
     }
-    const u32x4 pk = pack8(v);
-    *reinterpret_cast<u32x4*>(st + r * SS + c) = pk;
+    *reinterpret_cast<u32x4*>(st + r * SS + c) = pack8(v);
   }
   __syncthreads();
   if (s.epi == EPI_WGRAD) {
     if (s.imgT[1 - p] != nullptr) store_transposed(st, SS, TM, TN, s.imgT[1 - p], s.ldimgT, m0, n0);
     if (s.b != nullptr && nt == 0) {
-      // bias gradient = row sums of dY^T over the batch; SGD on the fp32 bias
-      for (int r = wave; r < TM; r += 4) {
-        const int m = m0 + r;
-        float acc1 = 0.f;
-        for (int c = lane * 4; c < s.brows; c += 256) {
-          const uint2 q = rx_load8_sc1(s.dyT, (int)(((long long)m * s.lddyT + c) * 2));
-          acc1 += __uint_as_float(q.x << 16) + __uint_as_float(q.x & 0xffff0000u) + __uint_as_float(q.y << 16) +
-                  __uint_as_float(q.y & 0xffff0000u);
+      // bias gradient = row sums of dY^T over the batch (brows <= 256: at most 32 chunks of 8
+      // per row, dealt over the TPR adjacent lanes of the row); SGD on the fp32 bias
+      constexpr int TPR = NT / TM;
+      const int r = tid / TPR, q = tid % TPR;
+      float a1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 32 / TPR + (32 % TPR != 0); ++i) {
+        const int c = (q + i * TPR) * 8;
+        if (c < s.brows) {
+          float f[8];
+          unpack8(rx_load16_sc1(s.dyT, (int)(((long long)(m0 + r) * s.lddyT + c) * 2)), f);
+          a1 += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
         }
-        acc1 = rx_wavesum(acc1);
-        if (lane == 0) s.b[m] -= lr * acc1;
       }
+#pragma unroll
+      for (int o = TPR / 2; o > 0; o >>= 1) a1 += __shfl_xor(a1, o);
+      if (q == 0) rx_g(s.b)[m0 + r] -= lr * a1;
     }
   } else if (s.YT != nullptr) {
     store_transposed(st, SS, TM, TN, s.YT, s.ldyt, m0, n0);
@@ -305,59 +344,116 @@ __device__ void gemm_phase(const Phase& P, int p, float lr, int G, char* lds) {
 }
 
 // ----------------------------------------------------------------------------------- BOTTOM --
-// One 16-row block: bottom MLP in LDS, then gather + interaction for its 16 samples.
+// One 16-row block: bottom MLP in LDS, then gather + interaction for its 16 samples. The
+// dependent index chain (permutation -> source row -> table-local id) runs once for the whole
+// block; the embedding rows are requested before the MLP and land while it computes.
 template <int D>
 __device__ void bottom_block(const DlrmDesc* __restrict__ d, int p, int rb, const long long* __restrict__ perm,
                              long long row0, int nvalid, char* lds) {
   constexpr int XR = D + 8;            // interaction image row stride (bf16)
+  constexpr int CH = D / 8;            // 16-B bf16 chunks per interaction row
+  constexpr int GI = 16 * MAXF * CH / NT;   // gathered chunks per thread
+  static_assert(16 * MAXF * CH % NT == 0, "gather split");
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr_ = lane & 15, lg = lane >> 4;
   const int r0 = rb * 16;
   const int B = d->B, F = d->F, ZP = d->ZP, nbot = d->nbot;
-  // LDS: two activation buffers [16][HS], the interaction images [16][32][XR], Z staging [16][ZS]
+  // LDS: embedding row ids [16][MAXF], two activation buffers [16][HS], the interaction images
+  // [16][MAXF][XR], Z staging [16][ZS]
   int maxw = 32;
   for (int l = 0; l < nbot; ++l) maxw = max(maxw, max(d->bot[l].Kp, d->bot[l].N));
   const int HS = maxw + 8;
-  u16* h0 = reinterpret_cast<u16*>(lds);
+  long long* erow = reinterpret_cast<long long*>(lds);
+  u16* h0 = reinterpret_cast<u16*>(erow + 16 * MAXF);
   u16* h1 = h0 + 16 * HS;
-  u16* xs = h1 + 16 * HS;              // [16][32][XR]
+  u16* xs = h1 + 16 * HS;              // [16][MAXF][XR]
   const int ZS = ZP + 8;
-  u16* zs = xs + 16 * 32 * XR;         // [16][ZS]
-  // dense rows -> h0 (bf16, zero-padded to Kp0)
-  const int Kp0 = d->bot[0].Kp;
-  for (int e = tid; e < 16 * Kp0; e += NT) {
-    const int i = e / Kp0, c = e % Kp0;
+  u16* zs = xs + 16 * MAXF * XR;       // [16][ZS]
+  const int Kp0 = d->bot[0].Kp;        // <= 32 (host-checked)
+  const RX_GLOBAL float* dense = rx_g(d->dense);
+  const RX_GLOBAL long long* cats = rx_g(d->cats);
+  const RX_GLOBAL long long* offs = rx_g(d->offs);
+  // (sample, column) pairs: dense features -> h0, table ids -> erow (-1: no table row)
+#pragma unroll
+  for (int i = 0; i < 16 * MAXF / NT; ++i) {
+    const int t = tid + i * NT, sm = t / MAXF, c = t % MAXF;
+    const long long src = src_row(perm, row0, r0 + sm, nvalid);
     float v = 0.f;
-    if (c < d->ndense) v = d->dense[src_row(perm, row0, r0 + i, nvalid) * d->ld_dense + c];
-    h0[i * HS + c] = rx_f2bf(v);
+    if (c < d->ndense) v = dense[src * d->ld_dense + c];
+    long long row = -1;
+    if (c >= 1 && c < F) {
+      row = offs[c - 1] + cats[src * d->ld_cats + c - 1];
+      row = row < 0 ? 0 : (row >= d->emb_rows ? d->emb_rows - 1 : row);
+    }
+    erow[sm * MAXF + c] = row;
+    if (c < Kp0) h0[sm * HS + c] = rx_f2bf(v);
   }
   __syncthreads();
+  f32x4 ga[GI], gb[GI];
+  {
+    const RX_GLOBAL float* emb = rx_g(d->emb);
+#pragma unroll
+    for (int i = 0; i < GI; ++i) {
+      const int e = tid + i * NT, sm = e / (MAXF * CH), rem = e % (MAXF * CH), r = rem / CH, c = (rem % CH) * 8;
+      const long long row = erow[sm * MAXF + r];
+      ga[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      gb[i] = ga[i];
+      if (row >= 0) {
+        ga[i] = *reinterpret_cast<const RX_GLOBAL f32x4*>(emb + row * D + c);
+        gb[i] = *reinterpret_cast<const RX_GLOBAL f32x4*>(emb + row * D + c + 4);
+      }
+    }
+  }
   store_transposed(h0, HS, 16, Kp0, d->XdT, B, r0, 0);
   u16* hin = h0;
   u16* hout = h1;
   for (int l = 0; l < nbot; ++l) {
     const BotLayer& L = d->bot[l];
     const u16* img = L.img[p];
+    const RX_GLOBAL float* bias = rx_g(L.bias);
     const int ntile = L.N >> 4, nks = L.Kp >> 5;
-    for (int t = wave; t < ntile; t += 4) {
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int kc = 0; kc < nks; kc += 8) {
+    if (nks == 1) {
+      // K <= 32: up to 8 of this wave's tiles per burst of weight loads
+      for (int t0 = wave; t0 < ntile; t0 += 32) {
         bf16x8 bfr[8];
+        float bv[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int ks = min(kc + q, nks - 1);
-          bfr[q] = ld16(img, (long long)(t * 16 + lr_) * L.Kp + ks * 32 + 8 * lg);
+        for (int j = 0; j < 8; ++j) {
+          const int t = min(t0 + 4 * j, ntile - 1);
+          bfr[j] = ld16(img, (long long)(t * 16 + lr_) * L.Kp + 8 * lg);
+          bv[j] = bias[t * 16 + lr_];
+        }
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(hin + lr_ * HS + 8 * lg);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int t = t0 + 4 * j;
+          if (t < ntile) {
+            const f32x4 acc = rx_mfma16(a, bfr[j], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hout[(4 * lg + r) * HS + t * 16 + lr_] = rx_f2bf(fmaxf(acc[r] + bv[j], 0.f));
+          }
+        }
+      }
+    } else {
+      for (int t = wave; t < ntile; t += 4) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float bv = bias[t * 16 + lr_];
+        for (int kc = 0; kc < nks; kc += 16) {
+          bf16x8 bfr[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int ks = min(kc + q, nks - 1);
+            bfr[q] = ld16(img, (long long)(t * 16 + lr_) * L.Kp + ks * 32 + 8 * lg);
+          }
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            if (kc + q < nks) {
+              const bf16x8 a = *reinterpret_cast<const bf16x8*>(hin + lr_ * HS + (kc + q) * 32 + 8 * lg);
+              acc = rx_mfma16(a, bfr[q], acc);
+            }
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (kc + q < nks) {
-            const bf16x8 a = *reinterpret_cast<const bf16x8*>(hin + lr_ * HS + (kc + q) * 32 + 8 * lg);
-            acc = rx_mfma16(a, bfr[q], acc);
-          }
+        for (int r = 0; r < 4; ++r) hout[(4 * lg + r) * HS + t * 16 + lr_] = rx_f2bf(fmaxf(acc[r] + bv, 0.f));
       }
-      const int col = t * 16 + lr_;
-      const float bv = L.bias[col];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) hout[(4 * lg + r) * HS + col] = rx_f2bf(fmaxf(acc[r] + bv, 0.f));
     }
     __syncthreads();
     if (L.H != nullptr) {
@@ -374,33 +470,28 @@ __device__ void bottom_block(const DlrmDesc* __restrict__ d, int p, int rb, cons
     hout = t_;
     __syncthreads();
   }
-  // hin: the bottom output [16][D] (ReLU'd), row 0 of every sample's interaction input
-  const int T = F - 1;
-  constexpr int CH = D / 8;  // 16-B chunks per row
-  for (int e = tid; e < 16 * MAXF * CH; e += NT) {
-    const int s = e / (MAXF * CH), rem = e % (MAXF * CH), r = rem / CH, c = (rem % CH) * 8;
-    u32x4 v = u32x4{0u, 0u, 0u, 0u};
-    if (r == 0) {
-      v = *reinterpret_cast<const u32x4*>(hin + s * HS + c);
-    } else if (r < F) {
-      const long long src = src_row(perm, row0, r0 + s, nvalid);
-      long long row = d->offs[r - 1] + d->cats[src * d->ld_cats + r - 1];
-      row = row < 0 ? 0 : (row >= d->emb_rows ? d->emb_rows - 1 : row);
-      const f32x4 a = *reinterpret_cast<const f32x4*>(d->emb + row * D + c);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(d->emb + row * D + c + 4);
-      v = u32x4{rx_f2bf2(a[0], a[1]), rx_f2bf2(a[2], a[3]), rx_f2bf2(b[0], b[1]), rx_f2bf2(b[2], b[3])};
-    }
-    *reinterpret_cast<u32x4*>(xs + (s * MAXF + r) * XR + c) = v;
-    rx_store16_sc1(d->ximg, (int)((((long long)(r0 + s) * MAXF + r) * D + c) * 2), v);
+  // hin: the bottom output [16][D] (ReLU'd), row 0 of every sample's interaction input; rows
+  // 1..T the gathered table rows
+#pragma unroll
+  for (int i = 0; i < GI; ++i) {
+    const int e = tid + i * NT, sm = e / (MAXF * CH), rem = e % (MAXF * CH), r = rem / CH, c = (rem % CH) * 8;
+    u32x4 v;
+    if (r == 0)
+      v = *reinterpret_cast<const u32x4*>(hin + sm * HS + c);
+    else
+      v = u32x4{rx_f2bf2(ga[i][0], ga[i][1]), rx_f2bf2(ga[i][2], ga[i][3]), rx_f2bf2(gb[i][0], gb[i][1]),
+                rx_f2bf2(gb[i][2], gb[i][3])};
+    *reinterpret_cast<u32x4*>(xs + (sm * MAXF + r) * XR + c) = v;
+    rx_store16_sc1(d->ximg, (int)((((long long)(r0 + sm) * MAXF + r) * D + c) * 2), v);
   }
   // Z staging: x0 in front, zeros everywhere else (the triangle is scattered in below)
   for (int e = tid; e < 16 * ZP; e += NT) {
-    const int s = e / ZP, c = e % ZP;
-    zs[s * ZS + c] = c < D ? hin[s * HS + c] : (u16)0;
+    const int sm = e / ZP, c = e % ZP;
+    zs[sm * ZS + c] = c < D ? hin[sm * HS + c] : (u16)0;
   }
   __syncthreads();
-  for (int s = wave; s < 16; s += 4) {
-    const u16* X = xs + s * MAXF * XR;
+  for (int sm = wave; sm < 16; sm += 4) {
+    const u16* X = xs + sm * MAXF * XR;
     f32x4 acc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int k0 = 0; k0 < D; k0 += 32) {
@@ -416,7 +507,7 @@ __device__ void bottom_block(const DlrmDesc* __restrict__ d, int p, int rb, cons
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = I * 16 + 4 * lg + r, j = J * 16 + lr_;
-        if (i < F && j < i) zs[s * ZS + D + i * (i - 1) / 2 + j] = rx_f2bf(acc[blk][r]);
+        if (i < F && j < i) zs[sm * ZS + D + i * (i - 1) / 2 + j] = rx_f2bf(acc[blk][r]);
       }
     }
   }
@@ -431,121 +522,203 @@ __device__ void bottom_block(const DlrmDesc* __restrict__ d, int p, int rb, cons
 }
 
 // ------------------------------------------------------------------------------------- HEAD --
-// Last layer (N = 1), BCE with logits (mean over the valid rows), its backward and SGD.
-__device__ void head_phase(const DlrmDesc* __restrict__ d, const long long* __restrict__ perm, long long row0,
+// Last layer (N = 1) and BCE with logits over one 16-row block: logits, the mean-loss gradient
+// dz, dA = dz w (x) relu'(A) (row-major and transposed, for the next layer's dgrad / wgrad), and
+// this block's partial of the last layer's own gradient (sum dz A, sum dz, sum loss), which ONE
+// workgroup reduces and applies in the next phase (head_finish). K_last <= 512, multiple of 32.
+__device__ void head_block(const DlrmDesc* __restrict__ d, int rb, const long long* __restrict__ perm, long long row0,
                            int nvalid, char* lds) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int B = d->B, K = d->K_last;
-  const float lr = d->lr;
-  float* dz = reinterpret_cast<float*>(lds);        // [B]
-  float* ls = dz + B;                                // [B]
-  float* red = ls + B;                               // [4][K]
-  u16* st = reinterpret_cast<u16*>(red + 4 * K);     // dA staged row-major [B][K + 8]
-  const int TS = K + 8;
-  const float bl = d->b_last[0];
-  for (int b = wave; b < B; b += 4) {
-    float acc = 0.f;
-    for (int k = lane * 4; k < K; k += 256) {
-      const uint2 q = rx_load8_sc1(d->A_last, (int)(((long long)b * K + k) * 2));
-      const f32x4 w = *reinterpret_cast<const f32x4*>(d->w_last + k);
-      acc += __uint_as_float(q.x << 16) * w[0] + __uint_as_float(q.x & 0xffff0000u) * w[1] +
-             __uint_as_float(q.y << 16) * w[2] + __uint_as_float(q.y & 0xffff0000u) * w[3];
-    }
-    acc = rx_wavesum(acc);
-    if (lane == 0) {
-      const float z = acc + bl;
-      const bool valid = b < nvalid;
-      const float y = valid ? d->labels[src_row(perm, row0, b, nvalid) * d->ld_lab] : 0.f;
-      const float l = fmaxf(z, 0.f) - z * y + log1pf(expf(-fabsf(z)));
-      const float sg = 1.f / (1.f + expf(-z));
-      dz[b] = valid ? (sg - y) / (float)nvalid : 0.f;
-      ls[b] = valid ? l : 0.f;
-      if (d->logits != nullptr) d->logits[b] = z;
-    }
+  const int B = d->B, K = d->K_last, r0 = rb * 16;
+  const int AS = K + 8, ch = K >> 3;
+  u16* a = reinterpret_cast<u16*>(lds);                  // [16][AS]: A rows, then dA rows
+  float* red = reinterpret_cast<float*>(a + 16 * AS);    // [4][K] per-wave partial dw
+  float* rowv = red + 4 * K;                             // [16] dz, [16] loss, [16] labels
+  u32x4 av[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + i * NT;
+    av[i] = u32x4{0u, 0u, 0u, 0u};
+    if (idx < 16 * ch) av[i] = rx_load16_sc1(d->A_last, (int)(((long long)(r0 + idx / ch) * K + (idx % ch) * 8) * 2));
+  }
+  if (tid < 16) {
+    const int b = r0 + tid;
+    rowv[32 + tid] = b < nvalid ? rx_g(d->labels)[src_row(perm, row0, b, nvalid) * d->ld_lab] : 0.f;
+  }
+  float w[8];
+  {
+    const RX_GLOBAL float* wl = rx_g(d->w_last);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = h * 256 + lane * 4 + j;
+        w[h * 4 + j] = k < K ? wl[k] : 0.f;
+      }
+  }
+  const float bl = rx_g(d->b_last)[0];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + i * NT;
+    if (idx < 16 * ch) *reinterpret_cast<u32x4*>(a + (idx / ch) * AS + (idx % ch) * 8) = av[i];
   }
   __syncthreads();
-  // dA = dz w (x) relu'(A); dw partial sums
-  for (int k = (tid & 63) * 4; k < K; k += 256) {
-    const f32x4 w = *reinterpret_cast<const f32x4*>(d->w_last + k);
-    float dw[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int b = wave; b < B; b += 4) {
-      const uint2 q = rx_load8_sc1(d->A_last, (int)(((long long)b * K + k) * 2));
-      const float a[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u), __uint_as_float(q.y << 16),
-                          __uint_as_float(q.y & 0xffff0000u)};
-      const float g = dz[b];
+  float dw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int rr = 0; rr < 4; ++rr) {
+    const int r = wave * 4 + rr, b = r0 + r;
+    float x[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = h * 256 + lane * 4;
+      uint2 q = uint2{0u, 0u};
+      if (k < K) q = *reinterpret_cast<const uint2*>(a + r * AS + k);
+      x[h * 4 + 0] = __uint_as_float(q.x << 16);
+      x[h * 4 + 1] = __uint_as_float(q.x & 0xffff0000u);
+      x[h * 4 + 2] = __uint_as_float(q.y << 16);
+      x[h * 4 + 3] = __uint_as_float(q.y & 0xffff0000u);
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += x[j] * w[j];
+    acc = rx_wavesum(acc);
+    const float z = acc + bl;
+    const bool valid = b < nvalid;
+    const float y = rowv[32 + r];
+    const float g = valid ? (1.f / (1.f + expf(-z)) - y) / (float)nvalid : 0.f;
+    if (lane == 0) {
+      rowv[r] = g;
+      rowv[16 + r] = valid ? fmaxf(z, 0.f) - z * y + log1pf(expf(-fabsf(z))) : 0.f;
+      if (d->logits != nullptr) rx_g(d->logits)[b] = z;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = h * 256 + lane * 4;
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        dw[j] += g * a[j];
-        o[j] = a[j] > 0.f ? g * w[j] : 0.f;
-        st[b * TS + k + j] = rx_f2bf(o[j]);
+        dw[h * 4 + j] += g * x[h * 4 + j];
+        o[j] = x[h * 4 + j] > 0.f ? g * w[h * 4 + j] : 0.f;
       }
-      rx_store8_sc1(d->dA, (int)(((long long)b * K + k) * 2), uint2{rx_f2bf2(o[0], o[1]), rx_f2bf2(o[2], o[3])});
+      if (k < K) *reinterpret_cast<uint2*>(a + r * AS + k) = uint2{rx_f2bf2(o[0], o[1]), rx_f2bf2(o[2], o[3])};
     }
+  }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) red[wave * K + k + j] = dw[j];
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = h * 256 + lane * 4 + j;
+      if (k < K) red[wave * K + k] = dw[h * 4 + j];
+    }
+  __syncthreads();
+  for (int idx = tid; idx < 16 * ch; idx += NT) {
+    const int r = idx / ch, c = (idx % ch) * 8;
+    rx_store16_sc1(d->dA, (int)(((long long)(r0 + r) * K + c) * 2), *reinterpret_cast<const u32x4*>(a + r * AS + c));
+  }
+  store_transposed(a, AS, 16, K, d->dAT, B, r0, 0);
+  float* hp = d->head_part + (long long)rb * d->head_ld;
+  for (int k = tid * 4; k < K + 4; k += NT * 4) {
+    f32x4 v;
+    if (k < K) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = red[k + j] + red[K + k + j] + red[2 * K + k + j] + red[3 * K + k + j];
+    } else {
+      float sd = 0.f, sl = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        sd += rowv[r];
+        sl += rowv[16 + r];
+      }
+      v = f32x4{sd, sl, 0.f, 0.f};
+    }
+    rx_store16_sc1(hp, k * 4, __builtin_bit_cast(u32x4, v));
   }
   __syncthreads();
-  for (int k = tid; k < K; k += NT) d->w_last[k] -= lr * (red[k] + red[K + k] + red[2 * K + k] + red[3 * K + k]);
-  if (wave == 0) {
-    float sd = 0.f, sl = 0.f;
-    for (int b = lane; b < B; b += 64) {
-      sd += dz[b];
-      sl += ls[b];
-    }
-    sd = rx_wavesum(sd);
-    sl = rx_wavesum(sl);
-    if (lane == 0) {
-      d->b_last[0] = bl - lr * sd;
-      const float L = sl / (float)nvalid;
-      d->step_loss[0] = L;
-      d->loss_acc[0] += (double)L;
+}
+
+// The last layer's SGD from the blocks' partials (one workgroup, the phase after HEAD).
+__device__ void head_finish(const DlrmDesc* __restrict__ d, int nvalid) {
+  const int K = d->K_last, nblk = d->B >> 4;
+  const float lr = d->lr;
+  for (int k = (int)threadIdx.x * 4; k < K + 4; k += NT * 4) {
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x4 v[16];
+#pragma unroll
+    for (int rb = 0; rb < 16; ++rb)
+      v[rb] = rb < nblk ? rx_load16_sc1(d->head_part, (int)(((long long)rb * d->head_ld + k) * 4)) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int rb = 0; rb < 16; ++rb) s += __builtin_bit_cast(f32x4, v[rb]);
+    if (k < K) {
+      RX_GLOBAL float* w = rx_g(d->w_last);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[k + j] -= lr * s[j];
+    } else {
+      rx_g(d->b_last)[0] -= lr * s[0];
+      const float L = s[1] / (float)nvalid;
+      rx_g(d->step_loss)[0] = L;
+      rx_g(d->loss_acc)[0] += (double)L;
     }
   }
-  store_transposed(st, TS, B, K, d->dAT, B, 0, 0);
-  __syncthreads();
 }
 
 // ------------------------------------------------------------------------------------- IBWD --
 // 16 samples: dX = S X per sample; row 0 -> the bottom-MLP gradient (masked by x0 > 0), rows
-// 1..T -> W_emb[row] -= lr * dX[t] (fp32 atomics: duplicate ids accumulate).
+// 1..T -> W_emb[row] -= lr * dX[t] (fp32 atomics: duplicate ids accumulate). Every load of the
+// block (table ids, dZ rows, interaction inputs) is in flight before any is waited for.
 template <int D>
 __device__ void ibwd_block(const DlrmDesc* __restrict__ d, int rb, const long long* __restrict__ perm, long long row0,
                            int nvalid, char* lds) {
   constexpr int XS = MAXF + 8;
+  constexpr int DS = D + 8;
+  constexpr int CH = D / 8;
+  constexpr int XI = 16 * MAXF * CH / NT;   // interaction-input chunks per thread
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr_ = lane & 15, lg = lane >> 4;
   const int r0 = rb * 16, F = d->F, ZP = d->ZP, B = d->B;
   const float lr = d->lr;
-  float* dzr = reinterpret_cast<float*>(lds);                  // [4][ZP]
-  u16* S = reinterpret_cast<u16*>(dzr + 4 * ZP);               // [4][MAXF][XS]
-  u16* XT = S + 4 * MAXF * XS;                                 // [4][D][XS]
-  long long* rows = reinterpret_cast<long long*>(XT + 4 * D * XS);   // [4][MAXF]
-  u16* dm = reinterpret_cast<u16*>(rows + 4 * MAXF);           // [16][D + 8]
-  constexpr int DS = D + 8;
-  for (int round = 0; round < 4; ++round) {
-    const int sl = round * 4 + wave, b = r0 + sl;
-    const long long src = src_row(perm, row0, b, nvalid);
-    float* zr = dzr + wave * ZP;
-    u16* Sw = S + wave * MAXF * XS;
-    u16* Xw = XT + wave * D * XS;
-    for (int c = lane * 4; c < ZP; c += 256)
-      *reinterpret_cast<u32x4*>(zr + c) = rx_load16_sc1(d->dZ, (int)(((long long)b * ZP + c) * 4));
-    for (int e = lane; e < MAXF * (D / 8); e += 64) {
-      const int r = e / (D / 8), c = (e % (D / 8)) * 8;
-      float f[8];
-      unpack8(rx_load16_sc1(d->ximg, (int)((((long long)b * MAXF + r) * D + c) * 2)), f);
+  float* dzr = reinterpret_cast<float*>(lds);                  // [16][ZP]
+  u16* XT = reinterpret_cast<u16*>(dzr + 16 * ZP);             // [16][D][XS]
+  u16* S = XT + 16 * D * XS;                                   // [4][MAXF][XS] (one per wave)
+  long long* rows = reinterpret_cast<long long*>(S + 4 * MAXF * XS);   // [16][MAXF]
+  u16* dm = reinterpret_cast<u16*>(rows + 16 * MAXF);          // [16][DS]
+  u32x4 xv[XI];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Xw[(c + j) * XS + r] = rx_f2bf(f[j]);
-    }
-    if (lane < MAXF) {
+  for (int i = 0; i < XI; ++i) {
+    const int e = tid + i * NT, sm = e / (MAXF * CH), rem = e % (MAXF * CH);
+    xv[i] = rx_load16_sc1(d->ximg, (int)((((long long)(r0 + sm) * MAXF + rem / CH) * D + (rem % CH) * 8) * 2));
+  }
+  {
+    const RX_GLOBAL long long* cats = rx_g(d->cats);
+    const RX_GLOBAL long long* offs = rx_g(d->offs);
+#pragma unroll
+    for (int i = 0; i < 16 * MAXF / NT; ++i) {
+      const int t = tid + i * NT, sm = t / MAXF, c = t % MAXF, b = r0 + sm;
       long long row = -1;
-      if (lane >= 1 && lane < F && b < nvalid) {
-        row = d->offs[lane - 1] + d->cats[src * d->ld_cats + lane - 1];
+      if (c >= 1 && c < F && b < nvalid) {
+        row = offs[c - 1] + cats[src_row(perm, row0, b, nvalid) * d->ld_cats + c - 1];
         if (row < 0 || row >= d->emb_rows) row = -1;
       }
-      rows[wave * MAXF + lane] = row;
+      rows[sm * MAXF + c] = row;
     }
-    __syncthreads();
+  }
+  const int zq = ZP >> 2;
+#pragma unroll 4
+  for (int e = tid; e < 16 * zq; e += NT) {
+    const int sm = e / zq, c = (e % zq) * 4;
+    *reinterpret_cast<u32x4*>(dzr + sm * ZP + c) = rx_load16_sc1(d->dZ, (int)(((long long)(r0 + sm) * ZP + c) * 4));
+  }
+#pragma unroll
+  for (int i = 0; i < XI; ++i) {
+    const int e = tid + i * NT, sm = e / (MAXF * CH), rem = e % (MAXF * CH), r = rem / CH, c = (rem % CH) * 8;
+    u16* Xw = XT + sm * D * XS;
+    float f[8];
+    unpack8(xv[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Xw[(c + j) * XS + r] = rx_f2bf(f[j]);
+  }
+  __syncthreads();
+  u16* Sw = S + wave * MAXF * XS;
+  for (int k = 0; k < 4; ++k) {
+    const int sl = wave * 4 + k;
+    const float* zr = dzr + sl * ZP;
+    const u16* Xw = XT + sl * D * XS;
     for (int e = lane; e < MAXF * MAXF; e += 64) {
       const int i = e / MAXF, j = e % MAXF;
       float v = 0.f;
@@ -570,8 +743,9 @@ __device__ void ibwd_block(const DlrmDesc* __restrict__ d, int rb, const long lo
             const float x0 = rx_bf2f(Xw[dd * XS]);
             dm[sl * DS + dd] = rx_f2bf(x0 > 0.f ? c[r] + zr[dd] : 0.f);
           } else if (i < F) {
-            const long long row = rows[wave * MAXF + i];
-            if (row >= 0) atomicAdd(d->emb + row * D + dd, -lr * c[r]);
+            const long long row = rows[sl * MAXF + i];
+            if (row >= 0)
+              __hip_atomic_fetch_add(rx_g(d->emb) + row * D + dd, -lr * c[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
       }
@@ -599,16 +773,23 @@ __global__ __launch_bounds__(NT) void dlrm_step_kernel(const DlrmDesc* __restric
   const int nph = d->nph, nblk = d->B >> 4;
   unsigned long long* stamps = blockIdx.x == 0 && threadIdx.x == 0 ? d->stamps : nullptr;
   if (stamps != nullptr) stamps[0] = wall_clock64();
+  bool head_done = false;
   for (int ph = 0; ph < nph; ++ph) {
     const Phase& P = d->ph[ph];
+    if (head_done) {
+      // the phase after HEAD: the last workgroup applies the last layer's SGD
+      if (blockIdx.x == G - 1) head_finish(d, nvalid);
+      head_done = false;
+    }
     if (P.kind == PH_GEMM) {
       gemm_phase(P, p, lr, G, lds);
     } else if (P.kind == PH_BOTTOM) {
       for (int rb = blockIdx.x; rb < nblk; rb += G) bottom_block<D>(d, p, rb, perm, row0, nvalid, lds);
     } else if (P.kind == PH_HEAD) {
-      if (blockIdx.x == 0) head_phase(d, perm, row0, nvalid, lds);
+      for (int rb = blockIdx.x; rb < nblk; rb += G) head_block(d, rb, perm, row0, nvalid, lds);
+      head_done = true;
     } else {
-      // IBWD: blocks dealt from the top of the grid down (block 0 ran the head)
+      // IBWD: blocks dealt from the top of the grid down
       for (int rb = (int)(G - 1 - blockIdx.x); rb < nblk; rb += G) ibwd_block<D>(d, rb, perm, row0, nvalid, lds);
     }
     if (ph + 1 < nph && !rx_grid_barrier(ctl, G, ++k, d->ticks)) break;

@@ -59,7 +59,8 @@ class DlrmDesc(ctypes.Structure):
                 ("A_last", vp), ("K_last", i32), ("pad2", i32), ("w_last", vp), ("b_last", vp),
                 ("dA", vp), ("dAT", vp), ("logits", vp), ("loss_acc", vp), ("step_loss", vp),
                 ("dZ", vp), ("dmlp", vp), ("dmlpT", vp), ("lr", ctypes.c_float), ("pad3", i32),
-                ("ctl", vp), ("ticks", ctypes.c_ulonglong), ("stamps", vp)]
+                ("ctl", vp), ("ticks", ctypes.c_ulonglong), ("stamps", vp), ("head_part", vp),
+                ("head_ld", i32), ("pad4", i32)]
 
 
 _bound = None
@@ -145,7 +146,8 @@ def supported(model, optimizer, loss, batch: int) -> Optional[str]:
     top = model.top_mlp.linears + [model.out]
     if len(bot) > MAXBOT or bot[0].in_features > 32 or any(l.out_features % 32 for l in bot):
         return "bottom MLP shape"
-    if top[-1].out_features != 1 or any(l.out_features % 32 for l in top[:-1]) or top[-1].in_features % 32:
+    if top[-1].out_features != 1 or any(l.out_features % 32 for l in top[:-1]) or top[-1].in_features % 32 \
+            or top[-1].in_features > 512:
         return "top MLP shape"
     if any(l.bias is None for l in bot + top):
         return "Linear without bias"
@@ -217,6 +219,8 @@ class DlrmStep:
         self.logits = buf(B, dtype=torch.float32)
         self.loss_acc = buf(1, dtype=torch.float64)
         self.step_loss = buf(1, dtype=torch.float32)
+        self.head_ld = _ru(self.top[-1].in_features + 4, 4)
+        self.head_part = buf(B // 16, self.head_ld, dtype=torch.float32)
         self.ctl = buf(int(L.rx_dlrm_ctl_words()), dtype=torch.int32)
         self._err, self._par = int(L.rx_dlrm_err_index()), int(L.rx_dlrm_parity_index())
         self.ticks = int(L.rx_dlrm_ticks(float(timeout_s)))
@@ -352,6 +356,7 @@ class DlrmStep:
         d.logits, d.loss_acc, d.step_loss = _p(self.logits), _p(self.loss_acc), _p(self.step_loss)
         d.dZ, d.dmlp, d.dmlpT = _p(self.dZ), _p(self.dmlp), _p(self.dmlpT)
         d.lr, d.ctl, d.ticks = self.lr, _p(self.ctl), self.ticks
+        d.head_part, d.head_ld = _p(self.head_part), self.head_ld
 
     def _lds_bytes(self):
         B, D, ZP = self.B, self.D, self.ZP
@@ -365,12 +370,12 @@ class DlrmStep:
                     need = max(need, 4 * s.tm * (s.tn + 4) * 4 + s.tm * (s.tn + 8) * 2)
             elif ph.kind == PH_BOTTOM:
                 w = max([32] + [max(l.Kp, l.N) for l in d.bot[:d.nbot]])
-                need = max(need, 2 * 16 * (w + 8) * 2 + 16 * 32 * (D + 8) * 2 + 16 * (ZP + 8) * 2)
+                need = max(need, 16 * 32 * 8 + 2 * 16 * (w + 8) * 2 + 16 * 32 * (D + 8) * 2 + 16 * (ZP + 8) * 2)
             elif ph.kind == PH_HEAD:
                 K = d.K_last
-                need = max(need, 2 * B * 4 + 4 * K * 4 + B * (K + 8) * 2)
+                need = max(need, 16 * (K + 8) * 2 + 4 * K * 4 + 48 * 4)
             else:
-                need = max(need, 4 * ZP * 4 + 4 * 32 * 40 * 2 + 4 * D * 40 * 2 + 4 * 32 * 8 + 16 * (D + 8) * 2)
+                need = max(need, 16 * ZP * 4 + 16 * D * 40 * 2 + 4 * 32 * 40 * 2 + 16 * 32 * 8 + 16 * (D + 8) * 2)
         return _ru(need, 16) + 64   # + the barrier's own __shared__ word
 
     # ------------------------------------------------------------------ state

@@ -135,9 +135,11 @@ register("spark.ray.mi355x.allreduce.twoshot_min_mb", "float", 1.0,
 register("spark.ray.mi355x.ddp.comm_stream", "bool", True,
          "reduce DDP / Horovod gradient buckets on a dedicated comm stream, concurrent with the rest "
          "of backward (event fork/join: capturable)", env="RAYDP_DDP_COMM_STREAM")
-register("spark.ray.mi355x.dlrm_step", "bool", True,
+register("spark.ray.mi355x.dlrm_step", "bool", False,
          "train a single-GPU Dlrm (replicated tables, plain SGD, BCEWithLogitsLoss) with the whole "
-         "step as one persistent HIP launch (csrc/hip/dlrm_step.hip)", env="RAYDP_DLRM_STEP")
+         "step as one persistent HIP launch (csrc/hip/dlrm_step.hip); off by default while the "
+         "HIP-graph replay of the launch-per-op step is faster (profiles/r4_dlrm_step_phases.jsonl)",
+         env="RAYDP_DLRM_STEP")
 register("spark.ray.mi355x.fused", "str", "auto",
          "TorchEstimator engine: auto (fused HIP MLP when the model is an MLP), on (required), off",
          env="RAYDP_FUSED", choices=["auto", "on", "off"])

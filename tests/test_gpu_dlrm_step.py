@@ -148,7 +148,7 @@ def test_after_training_the_model_forward_sees_the_new_weights():
     assert float((after - want).abs().max()) < 5e-2 * (1 + float(want.abs().max()))
 
 
-def test_estimator_trains_dlrm_on_the_persistent_step(tmp_path):
+def test_estimator_trains_dlrm_on_the_persistent_step(tmp_path, monkeypatch):
     """The notebook pipeline shape (examples/pytorch_dlrm.ipynb cell 14): Dlrm + SGD +
     BCEWithLogitsLoss through TorchEstimator.fit_on_spark at batch 128 on one worker runs on the
     persistent step engine, trains, and its saved model evaluates like the trained weights."""
@@ -157,6 +157,7 @@ def test_estimator_trains_dlrm_on_the_persistent_step(tmp_path):
     import raydp_amd
     from raydp_amd import runtime
     from raydp_amd.torch import TorchEstimator
+    monkeypatch.setenv("RAYDP_DLRM_STEP", "1")
     runtime.shutdown()
     runtime.init(num_cpus=4)
     try:
