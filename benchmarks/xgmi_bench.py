@@ -18,7 +18,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _rank(rank, world, port, sizes, reps, q):
+def _rank(rank, world, port, sizes, reps, q, kernel="oneshot"):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -31,14 +31,15 @@ def _rank(rank, world, port, sizes, reps, q):
         for nbytes in sizes:
             n = nbytes // 4
             t = torch.randn(n, device="cuda")
+            op = comm.allreduce2_ if kernel == "twoshot" else comm.allreduce_
             for _ in range(10):
-                comm.allreduce_(t, 1.0 / world)
+                op(t, 1.0 / world)
             torch.cuda.synchronize()
             dist.barrier()
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             ev[0].record()
             for _ in range(reps):
-                comm.allreduce_(t, 1.0 / world)
+                op(t, 1.0 / world)
             ev[1].record()
             ev[1].synchronize()
             out[nbytes] = ev[0].elapsed_time(ev[1]) * 1000.0 / reps
@@ -54,6 +55,9 @@ def main():
     ap.add_argument("--world", type=int, default=4)
     ap.add_argument("--sizes", default="194052,1048576,8708740")
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--kernel", choices=["oneshot", "twoshot"], default="oneshot",
+                    help="oneshot: every rank pulls the whole bucket from every peer; twoshot: all-pairs "
+                         "reduce-scatter + all-gather (2S/N bytes per link)")
     args = ap.parse_args()
     sizes = [int(x) for x in args.sizes.split(",")]
     sys.path.insert(0, ROOT)
@@ -61,15 +65,15 @@ def main():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_rank, args=(r, args.world, port, sizes, args.reps, q)) for r in range(args.world)]
+    ps = [ctx.Process(target=_rank, args=(r, args.world, port, sizes, args.reps, q, args.kernel)) for r in range(args.world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=300) for _ in ps)
     for p in ps:
         p.join(timeout=60)
     per = {s: statistics.median(r[1][s] for r in res) for s in sizes}
-    print(json.dumps({"metric": "xGMI one-shot all-reduce device time per call (us), ranks sharing one GPU",
-                      "world": args.world, "reps": args.reps,
+    print(json.dumps({"metric": f"xGMI {args.kernel} all-reduce device time per call (us), ranks sharing one GPU",
+                      "kernel": args.kernel, "world": args.world, "reps": args.reps,
                       "us_per_call": {str(s): round(v, 2) for s, v in per.items()},
                       "errors": [r[2] for r in res]}), flush=True)
 

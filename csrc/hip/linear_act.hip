@@ -331,7 +331,7 @@ __device__ __forceinline__ void lin_gemm_body(const LinArgs& a, u16* lds, int bx
       for (int x = 0; x < FM; ++x) {
         const float sx = rx_colsum16(asum[x]);
         if (lane < 16)
-          __hip_atomic_store(mine + TM * TN + wm * (TM / 2) + 16 * x + lane, sx, __ATOMIC_RELAXED,
+          __hip_atomic_store(rx_g(mine) + TM * TN + wm * (TM / 2) + 16 * x + lane, sx, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -341,7 +341,7 @@ __device__ __forceinline__ void lin_gemm_body(const LinArgs& a, u16* lds, int bx
     // second LDS object (and push the 64x64 block past 40 KiB: one resident workgroup less per CU)
     unsigned* last_flag = reinterpret_cast<unsigned*>(&lds[0]);
     if (tid == 0) {
-      const unsigned done = __hip_atomic_fetch_add(a.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned done = __hip_atomic_fetch_add(rx_g(a.counters) + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *last_flag = done + 1 == (unsigned)a.splits;
     }
     __syncthreads();
@@ -364,11 +364,11 @@ __device__ __forceinline__ void lin_gemm_body(const LinArgs& a, u16* lds, int bx
       if (want_db && lane < 16) {
 #pragma unroll
         for (int x = 0; x < FM; ++x)
-          dsum[x] += __hip_atomic_load(ps + TM * TN + wm * (TM / 2) + 16 * x + lane, __ATOMIC_RELAXED,
+          dsum[x] += __hip_atomic_load(rx_g(ps) + TM * TN + wm * (TM / 2) + 16 * x + lane, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    if (tid == 0) __hip_atomic_store(a.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(rx_g(a.counters) + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (want_db) {
 #pragma unroll
       for (int x = 0; x < FM; ++x) {

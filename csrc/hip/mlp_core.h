@@ -200,15 +200,15 @@ __device__ __forceinline__ bool mw_barrier(const MwCtx& mw, int k) {
   __syncthreads();
   if (threadIdx.x == 0) {
     int ok = 1;
-    __hip_atomic_fetch_add(mw.ctl + RX_MW_CTR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(rx_g(mw.ctl) + RX_MW_CTR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned target = (unsigned)(k * mw.G);
     const unsigned long long t0 = wall_clock64();
     for (int it = 1;; ++it) {
-      if (__hip_atomic_load(mw.ctl + RX_MW_CTR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      if (__hip_atomic_load(rx_g(mw.ctl) + RX_MW_CTR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
       if ((it & 15) == 0) {
-        if (__hip_atomic_load(mw.ctl + RX_MW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+        if (__hip_atomic_load(rx_g(mw.ctl) + RX_MW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
             wall_clock64() - t0 > mw.ticks) {
-          __hip_atomic_store(mw.ctl + RX_MW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(rx_g(mw.ctl) + RX_MW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           ok = 0;
           break;
         }
@@ -226,10 +226,10 @@ __device__ __forceinline__ bool mw_barrier(const MwCtx& mw, int k) {
 __device__ __forceinline__ void mw_finish(const MwCtx& mw) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(mw.ctl + RX_MW_DONE, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add(rx_g(mw.ctl) + RX_MW_DONE, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (old == (unsigned)mw.G - 1u) {
-      __hip_atomic_store(mw.ctl + RX_MW_CTR, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(mw.ctl + RX_MW_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rx_g(mw.ctl) + RX_MW_CTR, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rx_g(mw.ctl) + RX_MW_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -902,7 +902,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
   if constexpr (PS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's G^T export drained
   __syncthreads();  // all reads of G_l (R, GT) are done; they are overwritten with G_{l-1}
   if constexpr (PS) {
-    if (rx_tid<PS>() == 0) __hip_atomic_store(sync + 32 * l, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (rx_tid<PS>() == 0) __hip_atomic_store(rx_g(sync) + 32 * l, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[22 + 4 * l] = __builtin_amdgcn_s_memtime();
 

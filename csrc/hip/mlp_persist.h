@@ -42,7 +42,7 @@
 #define RX_PS_OPT_LDS (2 * 32 * 33 * 4 + 2 * 32 * 40 * 2)  // dynamic LDS an optimizer workgroup uses
 
 __device__ __forceinline__ unsigned rx_ps_load(const unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load sc1
+  return __hip_atomic_load(rx_g(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load sc1
 }
 
 // One lane: wait until *p >= target. False (error word set) on timeout, or at once when another
@@ -55,7 +55,7 @@ __device__ __forceinline__ bool rx_ps_wait(unsigned* sync, const unsigned* p, un
     if ((++k & 15) == 0) {
       if (rx_ps_load(sync + RX_PS_ERR) != 0u) return false;
       if (wall_clock64() - t0 > ticks) {
-        __hip_atomic_store(sync + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rx_g(sync) + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return false;
       }
     }
@@ -172,7 +172,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
   // XCD's L2, write-through (sc1) ones otherwise
   if (rx_tid() == 0) {
     const unsigned me = rx_xcc_id() + 1u;
-    __hip_atomic_store(sync + RX_PS_XCC, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(rx_g(sync) + RX_PS_XCC, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int nw = ps_grid_blocks(o);
     bool ok = true, same = true;
     for (int w = 1; w < nw && ok; ++w) {
@@ -222,7 +222,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
           if ((k & 15) == 0) {
             const bool bad = rx_ps_load(sync + RX_PS_ERR) != 0u || wall_clock64() - t0 > ticks;
             if (__builtin_amdgcn_readfirstlane(bad ? 1 : 0)) {
-              if (lane == 0) __hip_atomic_store(sync + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (lane == 0) __hip_atomic_store(rx_g(sync) + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               ok = false;
               break;
             }
@@ -250,7 +250,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (rx_tid() == 0)
-      __hip_atomic_store(sync + RX_PS_FLAG(0), (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rx_g(sync) + RX_PS_FLAG(0), (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     stamp(s, 4);
     ps_vector_update<C>(d, o, smem, Gr, m, v, rx_g(sched)[s], rx_g(sched)[nsteps + s], rx_g(sched)[2 * nsteps + s],
                         (opt_first && s == 0) ? 1 : 0);
@@ -326,7 +326,7 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, int b, float* __rest
   // write-through (sc1) ones otherwise; the step workgroup reads them with sc1 loads either way
   if (rx_tid() == 0) {
     const unsigned me = rx_xcc_id() + 1u;
-    __hip_atomic_store(sync + RX_PS_XCC + 1 + bw, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(rx_g(sync) + RX_PS_XCC + 1 + bw, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool ok = rx_ps_wait(sync, sync + RX_PS_XCC, 1u, ticks);
     flag_lds[0] = ok ? 0 : 1;
     flag_lds[1] = (ok && rx_ps_load(sync + RX_PS_XCC) == me) ? 0 : 1;
@@ -386,7 +386,7 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, int b, float* __rest
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (rx_tid() == 0) __hip_atomic_fetch_add(sync + RX_PS_CNT(l), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (rx_tid() == 0) __hip_atomic_fetch_add(rx_g(sync) + RX_PS_CNT(l), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (st) rx_g(stamps)[17 + 2 * l] = wall_clock64();
   }
 #pragma unroll

@@ -118,7 +118,7 @@ def _key(src: str) -> str:
     global _headers_digest
     if _headers_digest is None:      # the kernel headers a process compiles against: read once
         h = hashlib.sha256()
-        for f in ("mlp_core.h", "mlp_opt.h", "mlp_persist.h", "rx_common.h"):
+        for f in ("mlp_core.h", "mlp_opt.h", "mlp_persist.h", "rx_common.h", "rx_grid.h"):
             with open(os.path.join(CSRC_HIP, f), "rb") as fh:
                 h.update(fh.read())
         h.update(ARCH.encode())

@@ -14,6 +14,7 @@ from test_gpu_kernels import NYC, _relerr, _setup, emulate  # noqa: E402
 
 def one(batch, nvalid, seed):
     loss = nn.SmoothL1Loss()
+    torch.manual_seed(seed)
     model = NYC()
     tr, ref, ropt, feats, Y, X = _setup(model, loss, torch.optim.Adam, batch, nvalid, 20, 1, seed=seed, lr=1e-3)
     g = tr.forward_backward(feats, Y, nvalid).clone()
