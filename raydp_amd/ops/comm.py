@@ -7,6 +7,7 @@ all-reduce is enqueued on the compute stream from C++ (kernel -> all-reduce -> A
 between steps).
 """
 import ctypes
+import os
 from typing import Optional
 
 from raydp_amd.ops import _hip
@@ -372,6 +373,34 @@ class _Joined:
         return self.stream.query()
 
 
+def _device_key():
+    """(host, PCI location or uuid) of the current GPU: equal on two ranks iff they share it."""
+    import socket
+    import torch
+    p = torch.cuda.get_device_properties(torch.cuda.current_device())
+    loc = tuple(getattr(p, a, None) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if all(v is None for v in loc):
+        loc = (str(getattr(p, "uuid", "")), os.environ.get("HIP_VISIBLE_DEVICES", ""), torch.cuda.current_device())
+    return (socket.gethostname(),) + tuple(loc)
+
+
+def comm_stream_wanted(group=None) -> bool:
+    """``spark.ray.mi355x.ddp.comm_stream``: on / off, or auto = on only when no two ranks of
+    ``group`` share a GPU (collective: every rank calls it at the same point)."""
+    import torch.distributed as dist
+    from raydp_amd.utils.config import get as conf_get
+    v = str(conf_get("spark.ray.mi355x.ddp.comm_stream")).lower()
+    if v in ("on", "true", "1"):
+        return True
+    if v in ("off", "false", "0"):
+        return False
+    if not dist.is_initialized():
+        return True
+    keys = [None] * dist.get_world_size(group)
+    dist.all_gather_object(keys, _device_key(), group=group)
+    return len(set(keys)) == len(keys)
+
+
 class BucketAllreduce:
     """All-reduce of gradient buckets for the DDP and Horovod wrappers.
 
@@ -407,8 +436,8 @@ class BucketAllreduce:
                                           tag="buckets")
         except Exception:  # noqa: BLE001
             self.xg = None
-        if overlap is None:
-            overlap = bool(conf_get("spark.ray.mi355x.ddp.comm_stream"))
+        if overlap is None and self.xg is not None:
+            overlap = comm_stream_wanted(group)
         if self.xg is not None and overlap:
             self.stream = torch.cuda.Stream()
         self.launched = {"oneshot": 0, "twoshot": 0, "torch": 0}

@@ -11,12 +11,17 @@ MI355X over RCCL/xGMI:
   communication overlaps the rest of backward;
 * fp32 buckets up to ``spark.ray.mi355x.allreduce.oneshot_max_mb`` (16 MiB) ride the xGMI
   kernels (one-shot below ``twoshot_min_mb``, all-pairs two-shot above it at world > 2) with the
-  1/world average folded into the sum pass, on a dedicated comm stream (``ddp.comm_stream``):
-  the reduction of a finished bucket runs beside the rest of backward and the compute stream
-  joins it at the end of backward; larger buckets go to RCCL;
+  1/world average folded into the sum pass, on a dedicated comm stream (``ddp.comm_stream``,
+  ``auto``: when every rank has a GPU of its own): the reduction of a finished bucket runs
+  beside the rest of backward and the compute stream joins it at the end of backward; larger
+  buckets go to RCCL. Ranks that share a GPU keep the buckets stream-ordered: there the early
+  comm kernel spins for its peer on the CUs that peer's backward needs (5-8x slower steps,
+  profiles/r4_ddp_bucket_sweep.txt);
 * bucket size defaults to 32 MiB (``RAYDP_DDP_BUCKET_MB``): xGMI links are per-link bound
-  (~153 GB/s per link), so fewer, larger messages amortise the ~10-20 us collective latency;
-  tiny models (NYC_Model: 194 KB) end up in one bucket = one collective per step;
+  (~153 GB/s per link), so fewer, larger messages amortise the collective's flag rendezvous;
+  the measured sweep on DLRM's 8.7 MB of dense gradients (1 / 2 / 4 / 8 / 32 MiB buckets, 2 and
+  4 ranks) is fastest with one bucket; tiny models (NYC_Model: 194 KB) end up in one bucket =
+  one collective per step;
 * parameters are broadcast from rank 0 at wrap time (one collective per bucket); replicated
   floating-point buffers (BatchNorm running statistics) are re-pointed into one flat tensor
   and re-broadcast before each forward with ONE collective (torch's ``broadcast_buffers``);

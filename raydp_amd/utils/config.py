@@ -132,9 +132,13 @@ register("spark.ray.mi355x.allreduce.twoshot_min_mb", "float", 1.0,
          "at world > 2, xGMI buckets from this size on take the two-shot kernel (all-pairs "
          "reduce-scatter + all-gather: 2S/N bytes per link, two flag rounds) instead of the one-shot "
          "kernel (S bytes per link, one flag round)", env="RAYDP_ALLREDUCE_TWOSHOT_MIN_MB")
-register("spark.ray.mi355x.ddp.comm_stream", "bool", True,
+register("spark.ray.mi355x.ddp.comm_stream", "str", "auto",
          "reduce DDP / Horovod gradient buckets on a dedicated comm stream, concurrent with the rest "
-         "of backward (event fork/join: capturable)", env="RAYDP_DDP_COMM_STREAM")
+         "of backward (event fork/join: capturable): on, off, or auto = on when every rank of the "
+         "group has a GPU of its own. Ranks sharing a GPU measured 5-8x slower with it (the early "
+         "comm kernel spins for its peer on the CUs the peer's backward needs; "
+         "profiles/r4_ddp_bucket_sweep.txt)", env="RAYDP_DDP_COMM_STREAM",
+         choices=["auto", "on", "off", "true", "false", "1", "0"])
 register("spark.ray.mi355x.dlrm_step", "bool", False,
          "train a single-GPU Dlrm (replicated tables, plain SGD, BCEWithLogitsLoss) with the whole "
          "step as one persistent HIP launch (csrc/hip/dlrm_step.hip); off by default while the "
