@@ -23,8 +23,8 @@ for prog in ("bench", "lin"):
             disp[key].add(did)
             dur[key][did] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e9
     print(f"## {prog}")
-    print("| kernel | grid | dispatches | time/dispatch us | bf16 TFLOP/s | MFMA busy / (active CUs x cycles) | LDS conflict cycles / LDS inst | HBM read KiB | HBM write KiB | L2 hit % |")
-    print("|---|---|---|---|---|---|---|---|---|---|")
+    print("| kernel | grid | dispatches | time/dispatch us | bf16 TFLOP/s | MFMA busy / (active CUs x cycles) | LDS conflict cycles / LDS inst | HBM read KiB | HBM write KiB | L2 hit % | VALU / MFMA | SALU / MFMA |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     for key in sorted(agg, key=lambda k: -sum(dur[k].values())):
         c = agg[key]
         n_pass = len({f for f, _ in disp[key]})
@@ -42,6 +42,9 @@ for prog in ("bench", "lin"):
         conf = c.get("SQ_LDS_BANK_CONFLICT", 0) / lds if lds else 0
         hit, miss = c.get("TCC_HIT_sum", 0), c.get("TCC_MISS_sum", 0)
         l2 = 100 * hit / (hit + miss) if hit + miss else 0
+        nm = c.get("SQ_INSTS_MFMA", 0)
+        valu = f"{c['SQ_INSTS_VALU'] / nm:.1f}" if nm and "SQ_INSTS_VALU" in c else "-"
+        salu = f"{c['SQ_INSTS_SALU'] / nm:.1f}" if nm and "SQ_INSTS_SALU" in c else "-"
         print(f"| {key[0]} | {key[1]} | {ndisp:.0f} | {t * 1e6:.1f} | {tf:.2f} | {util:.1f}% | {conf:.2f} | "
-              f"{c.get('FETCH_SIZE', 0) / ndisp:.0f} | {c.get('WRITE_SIZE', 0) / ndisp:.0f} | {l2:.1f} |")
+              f"{c.get('FETCH_SIZE', 0) / ndisp:.0f} | {c.get('WRITE_SIZE', 0) / ndisp:.0f} | {l2:.1f} | {valu} | {salu} |")
     print()
