@@ -51,6 +51,32 @@ class DeferredDatasetError(RuntimeError):
         self.original = original
 
 
+class _Then:
+    """Future-like: ``fn(parent)`` of a deferred parent Dataset, computed once, on the first
+    ``result()`` (a failure of the parent's own computation is re-raised as itself)."""
+
+    def __init__(self, parent, fn):
+        import threading
+        self.parent, self.fn = parent, fn
+        self._lock = threading.Lock()
+        self._done, self._val, self._exc = False, None, None
+
+    def result(self):
+        with self._lock:
+            if not self._done:
+                try:
+                    _ = self.parent._blocks          # resolve the parent first
+                    self._val = self.fn(self.parent)
+                except DeferredDatasetError as e:
+                    self._exc = e.original
+                except BaseException as e:  # noqa: BLE001
+                    self._exc = e
+                self._done = True
+        if self._exc is not None:
+            raise self._exc
+        return self._val
+
+
 class Dataset:
     def __init__(self, blocks: List[Union[ObjectRef, pa.Table]], schema: Optional[pa.Schema] = None):
         self._pending = None
@@ -224,6 +250,9 @@ class Dataset:
 
     # ---------------------------------------------------------------- transforms ---------
     def random_shuffle(self, seed: Optional[int] = None, num_blocks: Optional[int] = None):
+        if self._pending is not None:
+            # still being produced: the shuffle waits with it (lazy, like Ray Data's)
+            return Dataset.deferred(_Then(self, lambda d: d.random_shuffle(seed=seed, num_blocks=num_blocks)))
         t = self.to_arrow()
         rng = np.random.default_rng(seed)
         perm = rng.permutation(t.num_rows)

@@ -291,6 +291,11 @@ class DataParallelTrainer:
                 import torch.distributed as dist
                 dist.destroy_process_group()
 
+    def _deferred_datasets(self, world) -> bool:
+        """Datasets still being produced (``Dataset.deferred``) that the ranks get split."""
+        return world > 1 and not self.local_shards and bool(self.datasets) and any(
+            getattr(ds, "_pending", None) is not None for ds in self.datasets.values())
+
     def _run_spawned(self, world, use_gpu, storage, reporter):
         """Worker group of ``world`` process actors (one per rank, GPUs assigned by the
         runtime), joined into one ``torch.distributed`` group (RCCL when they own GPUs).
@@ -341,9 +346,30 @@ class DataParallelTrainer:
                     common = S.dumps((self.fn, self.config, self.resume, storage), transfer=False)
                 except ValueError:
                     common = cloudpickle.dumps((self.fn, self.config, self.resume, storage))
-            for r, w in enumerate(workers):
-                shards = _shard(self.datasets, r, world)
-                refs.append(w.run.remote(common, cloudpickle.dumps(shards)))
+            conv_error = None
+            if self._deferred_datasets(world):
+                # fit_on_spark's conversion stage is still running on the executors: start every
+                # rank now (payload unpickle, engine build, kernel load, parameter upload) and send
+                # each its shard the moment the stage is done -- the same overlap the in-process
+                # N = 1 path gets from a deferred Dataset
+                chan = uuid.uuid4().hex
+                names = list(self.datasets)
+                for w in workers:
+                    refs.append(w.run.remote(common, None, chan, names))
+                try:
+                    with tracing.span("shard split", cat="train", world=world):
+                        payloads = [cloudpickle.dumps(_shard(self.datasets, r, world)) for r in range(world)]
+                    for r, w in enumerate(workers):
+                        w.deliver_shards.remote(chan, payloads[r])
+                except Exception as e:  # noqa: BLE001 - the conversion failed: stop every rank
+                    conv_error = e
+                    blob = cloudpickle.dumps(RuntimeError(f"dataset conversion failed: {e!r}"))
+                    for w in workers:
+                        w.deliver_shards.remote(chan, None, blob)
+            else:
+                for r, w in enumerate(workers):
+                    shards = _shard(self.datasets, r, world)
+                    refs.append(w.run.remote(common, cloudpickle.dumps(shards)))
             # wait on all ranks at once: when one dies, its peers are blocked in a collective
             # that will never complete -- fail the attempt at the first error (the group is
             # killed below) instead of waiting on rank 0 forever
@@ -357,6 +383,15 @@ class DataParallelTrainer:
                     except Exception:  # noqa: BLE001 - a rank failed (user error or lost process)
                         error = traceback.format_exc()
                         break
+            if conv_error is not None:
+                # the input failed, not the workers: no group restart can fix it (the ranks have
+                # all returned by now: their shards resolved to the same failure)
+                for ref in pending:
+                    try:
+                        runtime.get(ref)
+                    except Exception:  # noqa: BLE001
+                        pass
+                raise conv_error
             if error is not None:
                 raise _WorkerFailure(error)
             for r, reports in enumerate(outs):
@@ -504,8 +539,27 @@ class _TrainWorker:
     its group is warm; its process group is torn down with the process."""
 
     def __init__(self, rank: int, world: int, storage: str, use_gpu: bool):
+        import threading
         self.rank, self.world, self.storage, self.use_gpu = rank, world, storage, use_gpu
         self.local_rank, self.local_world, self.node_rank = 0, 1, rank
+        self._chans: Dict[str, Any] = {}          # shard deliveries of deferred fits, by channel
+        self._chan_lock = threading.Lock()
+
+    def _chan(self, chan: str):
+        import concurrent.futures as cf
+        with self._chan_lock:
+            return self._chans.setdefault(chan, cf.Future())
+
+    def deliver_shards(self, chan: str, payload: Optional[bytes], error: Optional[bytes] = None) -> bool:
+        """The shards of a fit started with deferred datasets (runs beside ``run`` on the
+        actor's second thread): ``{name: Dataset}`` pickled, or the conversion's failure."""
+        import cloudpickle
+        fut = self._chan(chan)
+        if error is not None:
+            fut.set_exception(cloudpickle.loads(error))
+        else:
+            fut.set_result(cloudpickle.loads(payload))
+        return True
 
     def setup(self, addr: str, port: int, visible=None, local_rank: int = 0, local_world: int = 1,
               node_rank: int = 0, device_index: Optional[int] = None, backend: Optional[str] = None,
@@ -537,12 +591,27 @@ class _TrainWorker:
             _init_dist(backend, self.rank, self.world, addr, port, timeout_s)
         return True
 
-    def run(self, common: bytes, shard_payload: bytes):
+    def run(self, common: bytes, shard_payload: Optional[bytes], chan: Optional[str] = None,
+            names: Optional[List[str]] = None):
         import cloudpickle
         from raydp_amd.utils import tracing
         with tracing.span("unpickle fit payload", cat="train", rank=self.rank):
             fn, config, resume, storage = cloudpickle.loads(common)
-            shards = cloudpickle.loads(shard_payload)
+            if shard_payload is None and chan is not None:
+                # deferred: the shards arrive through deliver_shards while the loop builds its engine
+                from raydp_amd.data.dataset import Dataset
+                fut = self._chan(chan)
+                shards = {n: Dataset.deferred(_ShardOf(fut, n)) for n in names or []}
+            else:
+                shards = cloudpickle.loads(shard_payload)
+        try:
+            return self._run_loop(fn, config, resume, storage, shards)
+        finally:
+            if chan is not None:
+                with self._chan_lock:
+                    self._chans.pop(chan, None)
+
+    def _run_loop(self, fn, config, resume, storage, shards):
         self.storage = storage
         reports = []
 
@@ -556,6 +625,16 @@ class _TrainWorker:
         finally:
             S._set_session(None)
         return reports
+
+
+class _ShardOf:
+    """Future-like view of one named shard of a delivery future's ``{name: Dataset}``."""
+
+    def __init__(self, fut, name):
+        self.fut, self.name = fut, name
+
+    def result(self):
+        return self.fut.result()[self.name]
 
 
 class _WorkerFailure(Exception):

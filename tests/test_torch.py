@@ -162,3 +162,57 @@ def test_deferred_conversion_failure_is_raised_once(spark_on_ray_small, monkeypa
         with pytest.raises(DeferredDatasetError) as e2:
             ds.count()
         assert isinstance(e2.value.original, KeyError)
+
+
+def test_spawned_workers_build_their_engines_before_their_shards_exist(spark_on_ray_small, monkeypatch):
+    """num_workers=2 (spawned ranks, gloo): with the conversion overlapped, every rank starts its
+    loop at once and receives its shard when the stage is done (deliver_shards) -- same model as
+    the conversion finished first."""
+    from raydp_amd.train import trainer as T
+    seen = []
+    orig = T.DataParallelTrainer._deferred_datasets
+
+    def spy(self, world):
+        v = orig(self, world)
+        seen.append(v)
+        return v
+    monkeypatch.setattr(T.DataParallelTrainer, "_deferred_datasets", spy)
+    df = _tiny_df(spark_on_ray_small)
+    outs = []
+    for ov in ("0", "1"):
+        monkeypatch.setenv("RAYDP_OVERLAP_CONVERSION", ov)
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(2, 8), torch.nn.ReLU(), torch.nn.Linear(8, 1))
+        est = TorchEstimator(num_workers=2, model=model, optimizer=torch.optim.Adam(model.parameters(), lr=1e-2),
+                             loss=torch.nn.MSELoss(), feature_columns=["x", "y"], feature_types=torch.float,
+                             label_column="z", label_type=torch.float, batch_size=32, num_epochs=2,
+                             use_gpu=False, shuffle_seed=7, drop_last=True)
+        est.fit_on_spark(df)
+        outs.append(est)
+    assert seen == [False, True], seen
+    sa, sb = outs[0].get_model().state_dict(), outs[1].get_model().state_dict()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+
+
+def test_spawned_deferred_conversion_failure_is_raised_once(spark_on_ray_small, monkeypatch):
+    """The deferred-shard path at num_workers=2: a failing conversion reaches the caller as its
+    own error, not as a worker-group failure with restarts."""
+    from pyspark.sql.functions import col, udf
+    from raydp_amd.data.dataset import DeferredDatasetError
+    from raydp_amd.train.trainer import TrainingFailedError
+    monkeypatch.setenv("RAYDP_OVERLAP_CONVERSION", "1")
+
+    @udf("double")
+    def boom(v):
+        raise ValueError("bad row")
+    df = _tiny_df(spark_on_ray_small, 64).withColumn("x", boom(col("x")))
+    est = TorchEstimator(num_workers=2, model=lambda c: torch.nn.Linear(2, 1),
+                         optimizer=lambda m, c: torch.optim.SGD(m.parameters(), lr=0.1),
+                         loss=torch.nn.MSELoss(), feature_columns=["x", "y"], feature_types=torch.float,
+                         label_column="z", label_type=torch.float, batch_size=16, num_epochs=1,
+                         use_gpu=False)
+    with pytest.raises(Exception) as ei:
+        est.fit_on_spark(df, max_retries=3)
+    assert not isinstance(ei.value, (TrainingFailedError, DeferredDatasetError)), repr(ei.value)
+    assert "bad row" in str(ei.value)
