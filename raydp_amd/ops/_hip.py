@@ -57,7 +57,7 @@ class StepBufs(ctypes.Structure):
     """Device buffers of one fused model (csrc/hip/fused_mlp.hip StepBufs)."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("d_dev", "img", "rstats", "params", "grads", "scratch",
                                                "metrics", "stamps", "jit_step", "jit_eval",
-                                               "jit_persist", "mw")]
+                                               "jit_persist", "mw", "jit_step_mw")]
 
 
 class MwArgs(ctypes.Structure):
@@ -148,7 +148,8 @@ def lib():
     L.rx_opt_step.argtypes = [vp, vp, vp, vp, vp, vp, f, f, f, f, i, vp]
     L.rx_mlp_wgrad.argtypes = [vp, vp, vp, vp]
     L.rx_mlp_eval.argtypes = [vp, vp, i, vp, vp, i, i, vp]
-    L.rx_jit_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), i]
+    L.rx_jit_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                              ctypes.POINTER(vp), i]
     # (desc, bufs, opt, opt_dev, mt, m, v, feats, labels, perm, n_rows, batch, nsteps, sched, opt_first,
     #  sync, timeout_s, stream)
     L.rx_mlp_train_persistent.argtypes = [vp, vp, vp, vp, i, vp, vp, vp, vp, vp, i, i, i, vp, i, vp,

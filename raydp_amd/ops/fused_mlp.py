@@ -413,7 +413,7 @@ class FusedMLPTrainer:
             b.mw = ctypes.addressof(a)
         if self.layout_only:
             return
-        if jit_enabled() and G == 1:
+        if jit_enabled():
             from raydp_amd.ops import mlp_jit
             self.jit = mlp_jit.load_specialized(self)
         self.refresh_images()

@@ -81,6 +81,16 @@ def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
         "  mlp_train_step_body<JitCfg, RX_MT>(dp, img, rstats, P, Gr, feats, labels, perm, row0, nvalid, scratch,",
         "                                     metrics, stamps, smem, rowidx);",
         "}",
+        'extern "C" __global__ __launch_bounds__(RX_THREADS) void rx_jit_step_mw(',
+        "    const MlpDesc* __restrict__ dp, const u16* __restrict__ img, float* __restrict__ rstats,",
+        "    const float* __restrict__ P, float* __restrict__ Gr, const u16* __restrict__ feats,",
+        "    const float* __restrict__ labels, const int* __restrict__ perm, int row0, float* __restrict__ scratch,",
+        "    long long scratch_stride, double* __restrict__ metrics, MwCtx mw) {",
+        "  extern __shared__ __attribute__((aligned(16))) char smem[];",
+        "  __shared__ int rowidx[Tile<RX_MT>::BP];",
+        "  mlp_train_step_mw_body<JitCfg, RX_MT>(dp, img, rstats, P, Gr, feats, labels, perm, row0, scratch,",
+        "                                        scratch_stride, metrics, mw, smem, rowidx);",
+        "}",
         'extern "C" __global__ __launch_bounds__(RX_THREADS) void rx_jit_eval(',
         "    const MlpDesc* __restrict__ dp, const u16* __restrict__ img, const float* __restrict__ rstats,",
         "    const float* __restrict__ P, const u16* __restrict__ feats, const float* __restrict__ labels,",
@@ -167,15 +177,15 @@ def load_specialized(trainer) -> Optional[str]:
     with _lock:
         fns = _loaded.get(path)
         if fns is None:
-            step, ev, ps = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+            step, ev, ps, mw = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
             _hip.check(_hip.lib().rx_jit_load(path.encode(), ctypes.byref(step), ctypes.byref(ev), ctypes.byref(ps),
-                                              int(trainer.desc.lds_bytes)), "rx_jit_load")
-            fns = (step.value, ev.value, ps.value)
+                                              ctypes.byref(mw), int(trainer.desc.lds_bytes)), "rx_jit_load")
+            fns = (step.value, ev.value, ps.value, mw.value)
             if not _loaded:
                 import atexit
                 atexit.register(_unload_all)
             _loaded[path] = fns
-    trainer.bufs.jit_step, trainer.bufs.jit_eval, trainer.bufs.jit_persist = fns
+    trainer.bufs.jit_step, trainer.bufs.jit_eval, trainer.bufs.jit_persist, trainer.bufs.jit_step_mw = fns
     return path
 
 
