@@ -543,6 +543,7 @@ class _TrainWorker:
         self.rank, self.world, self.storage, self.use_gpu = rank, world, storage, use_gpu
         self.local_rank, self.local_world, self.node_rank = 0, 1, rank
         self._chans: Dict[str, Any] = {}          # shard deliveries of deferred fits, by channel
+        self._closed: List[str] = []              # channels whose fit already returned
         self._chan_lock = threading.Lock()
 
     def _chan(self, chan: str):
@@ -554,6 +555,9 @@ class _TrainWorker:
         """The shards of a fit started with deferred datasets (runs beside ``run`` on the
         actor's second thread): ``{name: Dataset}`` pickled, or the conversion's failure."""
         import cloudpickle
+        with self._chan_lock:
+            if chan in self._closed:     # the fit failed before its shards came: nothing waits
+                return False
         fut = self._chan(chan)
         if error is not None:
             fut.set_exception(cloudpickle.loads(error))
@@ -610,6 +614,7 @@ class _TrainWorker:
             if chan is not None:
                 with self._chan_lock:
                     self._chans.pop(chan, None)
+                    self._closed = (self._closed + [chan])[-32:]
 
     def _run_loop(self, fn, config, resume, storage, shards):
         self.storage = storage
