@@ -3,7 +3,8 @@
   RAYDP_TRACE=gpurun_out/tr/nyc python bench.py --steps 20 --warmup 5 --no-reference-config
   python scripts/trace_summary.py gpurun_out/tr/nyc > profiles/<name>.txt
 
-Prints one line per span that starts inside the last ``timed run`` span: start offset and
+Prints one line per span that starts inside the last ``timed run`` span (of the workload named
+by the optional second argument): start offset and
 duration in ms, the process, and the span name, indented by nesting within its process.
 """
 import glob
@@ -11,7 +12,7 @@ import json
 import sys
 
 
-def main(prefix):
+def main(prefix, workload=None):
     events = []
     for fn in sorted(glob.glob(f"{glob.escape(prefix)}.*.jsonl")):
         with open(fn) as f:
@@ -24,7 +25,8 @@ def main(prefix):
                     events.append(e)
                 elif e.get("ph") == "i":
                     events.append(dict(e, dur=0.0))
-    runs = [e for e in events if e["name"] == "timed run"]
+    runs = [e for e in events if e["name"] == "timed run"
+            and (workload is None or (e.get("args") or {}).get("workload") == workload)]
     if not runs:
         raise SystemExit("no 'timed run' span")
     run = runs[-1]
@@ -47,4 +49,5 @@ def main(prefix):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    # optional second argument: the workload whose timed run to show (default: the last one)
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
