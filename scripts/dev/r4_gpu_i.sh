@@ -3,4 +3,5 @@
 cd "$GRAFT_REPO_ROOT"; export HSA_ENABLE_IPC_MODE_LEGACY=0; mkdir -p gpurun_out/pmc
 for p in 1 3; do bash scripts/gpu.sh pmc $p lin || exit 1; done
 for p in 1 3; do bash scripts/gpu.sh pmc $p bench || exit 2; done
+for p in 1 2 3; do bash scripts/gpu.sh pmc $p mw || exit 3; done
 python scripts/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.md 2>&1; head -40 gpurun_out/pmc_summary.md

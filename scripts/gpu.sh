@@ -56,9 +56,11 @@ case $cmd in
       3) P="WRITE_SIZE TCC_MISS_sum SQ_INSTS_VALU SQ_INSTS_SALU";;
       *) echo "pass 1..3"; exit 2;;
     esac
-    REGEX="rx_jit_persist|mlp_persist|lin_gemm|arrow_ingest|xg_allreduce|mt_sgd"
+    REGEX="rx_jit_persist|rx_jit_step_mw|opt_tiled|mlp_persist|lin_gemm|arrow_ingest|xg_allreduce|mt_sgd"
     if [ "$2" = bench ]; then
-      CMD="python3 $R/bench.py --steps 200 --warmup 5 --no-reference-config"
+      CMD="python3 $R/bench.py --steps 200 --warmup 5 --no-reference-config --extra-workloads none"
+    elif [ "$2" = mw ]; then
+      CMD="python3 $R/bench.py --rows 400000 --epochs 1 --batch 4096 --steps 20 --warmup 5 --extra-workloads none"
     else
       CMD="python3 $R/benchmarks/linear_gemm_bench.py --reps 3"
     fi

@@ -10,7 +10,7 @@ import os
 import sys
 
 d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc")
-for prog in ("bench", "lin"):
+for prog in ("bench", "lin", "mw"):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     dur = collections.defaultdict(dict)
