@@ -210,3 +210,17 @@ def precompile(model, optimizer, loss, batch_size: int, acc_thr=None) -> str:
     tr = FusedMLPTrainer(extract_mlp_spec(model), optimizer_config(optimizer), loss_code(loss), batch_size,
                          None, layout_only=True, acc_thr=acc_thr)
     return compile_for(tr)
+
+
+def precompile_many(jobs, workers: Optional[int] = None):
+    """``precompile`` over ``[(model, optimizer, loss, batch_size, acc_thr), ...]``: the layouts
+    are derived one after the other (spec extraction runs the model), the hipcc builds in
+    parallel. Returns the code-object paths."""
+    from concurrent.futures import ThreadPoolExecutor
+    from raydp_amd.models.mlp_spec import extract_mlp_spec
+    from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+    trs = [FusedMLPTrainer(extract_mlp_spec(m), optimizer_config(o), loss_code(l), b, None, layout_only=True,
+                           acc_thr=a) for m, o, l, b, a in jobs]
+    n = workers or max(1, min(8, os.cpu_count() or 1))
+    with ThreadPoolExecutor(n) as ex:
+        return list(ex.map(compile_for, trs))
