@@ -79,6 +79,8 @@ class _Then:
 
 class Dataset:
     def __init__(self, blocks: List[Union[ObjectRef, pa.Table]], schema: Optional[pa.Schema] = None):
+        import threading
+        self._lock = threading.Lock()     # resolves a deferred dataset once, whoever asks first
         self._pending = None
         self._blocks_ = list(blocks)
         self._schema_ = schema
@@ -95,13 +97,16 @@ class Dataset:
         return ds
 
     def _wait(self):
-        fut, self._pending = self._pending, None
-        try:
-            done = fut.result()
-        except BaseException as e:  # noqa: BLE001
-            self._pending = fut           # every later access reports the same failure
-            raise DeferredDatasetError(e) from e
-        self._blocks_, self._schema_ = done._blocks, done._schema
+        with self._lock:
+            fut = self._pending
+            if fut is None:               # another thread resolved it meanwhile
+                return
+            try:
+                done = fut.result()
+            except BaseException as e:  # noqa: BLE001 - every later access reports the same failure
+                raise DeferredDatasetError(e) from e
+            self._blocks_, self._schema_ = done._blocks, done._schema
+            self._pending = None
 
     @property
     def _blocks(self):
@@ -128,7 +133,13 @@ class Dataset:
         _ = self._blocks
         d = dict(self.__dict__)
         d["_pending"] = None
+        d.pop("_lock", None)
         return d
+
+    def __setstate__(self, d):
+        import threading
+        self.__dict__.update(d)
+        self._lock = threading.Lock()
 
     # ---------------------------------------------------------------- internals ----------
     def _get_tables(self) -> List[pa.Table]:

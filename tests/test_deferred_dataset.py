@@ -1,0 +1,58 @@
+"""``Dataset.deferred`` (raydp_amd/data/dataset.py): a dataset whose blocks are still being
+produced. Operations that only need the blocks later stay lazy (``random_shuffle`` -- what the
+estimator applies before splitting shards for spawned workers), a failure surfaces as the
+original error on every access, and the lazy result equals the eager one."""
+import concurrent.futures as cf
+import threading
+
+import pyarrow as pa
+import pytest
+
+from raydp_amd.data.dataset import Dataset, DeferredDatasetError
+
+
+def _ds(n=100, blocks=4):
+    t = pa.table({"x": list(range(n)), "y": [float(i) * 0.5 for i in range(n)]})
+    per = n // blocks
+    return Dataset([t.slice(i * per, per) for i in range(blocks)], t.schema)
+
+
+def test_random_shuffle_of_a_deferred_dataset_is_lazy_and_equal_to_eager():
+    fut = cf.Future()
+    lazy = Dataset.deferred(fut).random_shuffle(seed=7)
+    assert lazy._pending is not None          # nothing resolved yet
+    fut.set_result(_ds())
+    eager = _ds().random_shuffle(seed=7)
+    assert lazy.to_arrow().equals(eager.to_arrow())
+    assert lazy.num_blocks() == eager.num_blocks()
+
+
+def test_lazy_shuffle_resolves_once_across_threads():
+    fut = cf.Future()
+    calls = []
+    src = _ds()
+
+    class Counting:
+        def result(self):
+            calls.append(1)
+            return fut.result()
+    lazy = Dataset.deferred(Counting()).random_shuffle(seed=1)
+    out = []
+    ts = [threading.Thread(target=lambda: out.append(lazy.count())) for _ in range(4)]
+    for t in ts:
+        t.start()
+    fut.set_result(src)
+    for t in ts:
+        t.join()
+    assert out == [100] * 4 and len(calls) == 1
+
+
+def test_failed_source_raises_its_own_error_through_the_lazy_shuffle():
+    fut = cf.Future()
+    fut.set_exception(KeyError("source failed"))
+    lazy = Dataset.deferred(fut).random_shuffle(seed=3)
+    for _ in range(2):
+        with pytest.raises(DeferredDatasetError) as ei:
+            lazy.count()
+        # the parent's failure, not a DeferredDatasetError wrapped in another
+        assert isinstance(ei.value.original, KeyError)
