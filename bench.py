@@ -519,7 +519,10 @@ def main():
             raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
         n_train = world
         driver_gpu = True
-    cpus = int(os.environ.get("RAYDP_BENCH_CPUS", "4"))
+    # executors (one single-core executor per CPU): 4 for the driver-config pipelines (one CSV
+    # split each); 8 for data-scale runs, whose 1 GB+ CSVs split into whole waves of 8 tasks
+    # (the one-GPU box gives a process 16 CPUs)
+    cpus = int(os.environ.get("RAYDP_BENCH_CPUS", "8" if args.rows is not None else "4"))
     if args.topology == "estimator" and n_train > cpus:
         # one driver feeds N workers: one single-core executor per worker, within the host
         cpus = min(n_train, max(cpus, (os.cpu_count() or 8) // 4))

@@ -237,6 +237,61 @@ __device__ __forceinline__ void mw_finish(const MwCtx& mw) {
 // Rows of workgroup w when the batch's n valid rows are dealt BP per workgroup.
 __device__ __forceinline__ int mw_rows(int n, int w, int bp) { return max(0, min(bp, n - w * bp)); }
 
+// Sums over the G workgroups' partial pairs at p0 + w * stride + {0, 1}. The four lanes that
+// share (lane & 15) split the workgroups (lane group q takes w = q, q + 4, ...), each issuing its
+// loads 8 workgroups at a time, and rx_colsum16 adds the four lane sums -- every lane gets the
+// bit-identical total, in a fixed order (deterministic). A loop of G dependent sc1 loads per
+// column, the form this replaces, was most of the multi-workgroup step's time.
+__device__ __forceinline__ void mw_pair_sum(const float* p0, int stride, int G, int q, float& a, float& b) {
+  float sa = 0.f, sb = 0.f;
+  for (int w0 = q; w0 < G; w0 += 32) {
+    float va[8], vb[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int w = w0 + 4 * i;
+      const float* pp = p0 + (size_t)(w < G ? w : q) * (size_t)stride;
+      va[i] = rx_ld_sc1f(pp);
+      vb[i] = rx_ld_sc1f(pp + 1);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (w0 + 4 * i < G) {
+        sa += va[i];
+        sb += vb[i];
+      }
+  }
+  a = rx_colsum16(sa);
+  b = rx_colsum16(sb);
+}
+
+// Count-weighted centred second moment of the batch from every workgroup's (sum, M2) pair of
+// p0 + w * stride (Chan et al.'s parallel combination), split over lanes as mw_pair_sum.
+__device__ __forceinline__ float mw_m2_sum(const float* p0, int stride, int G, int q, float mean, int n_batch,
+                                           int bp) {
+  float m2 = 0.f;
+  for (int w0 = q; w0 < G; w0 += 32) {
+    float vs[8], vm[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int w = w0 + 4 * i;
+      const float* pp = p0 + (size_t)(w < G ? w : q) * (size_t)stride;
+      vs[i] = rx_ld_sc1f(pp);
+      vm[i] = rx_ld_sc1f(pp + 1);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int w = w0 + 4 * i;
+      const int nwi = w < G ? mw_rows(n_batch, w, bp) : 0;
+      if (nwi == 0) continue;      // an empty workgroup published nothing meaningful
+      const float nw = (float)nwi;
+      const float dm = vs[i] / nw - mean;
+      m2 += vm[i];
+      m2 = fmaf(nw * dm, dm, m2);
+    }
+  }
+  return rx_colsum16(m2);
+}
+
 __device__ __forceinline__ float act_fwd(int act, float z) { return act == 1 ? fmaxf(z, 0.f) : z; }
 
 // C[Bpad x 16-col tile n] += A (LDS, row-major, K contiguous) x Bt (global bf16, [n][K]).
@@ -675,19 +730,11 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         if (n >= ntiles) continue;
         const int c = n * 16 + lr;
         const int cc = c < ly.out ? c : 0;
-        float S = 0.f;
-        for (int w = 0; w < mw->G; ++w) S += rx_ld_sc1f(mw_fwd(mw->part, mw->stride, ly, w) + 2 * cc);
+        const float* p0 = mw_fwd(mw->part, mw->stride, ly, 0) + 2 * cc;
+        float S, unused;
+        mw_pair_sum(p0, mw->stride, mw->G, lg, S, unused);
         const float mean = S / (float)n_batch;
-        float M2 = 0.f;
-        for (int w = 0; w < mw->G; ++w) {
-          const float* pp = mw_fwd(mw->part, mw->stride, ly, w) + 2 * cc;
-          const int nwi = mw_rows(n_batch, w, T::BP);
-          if (nwi == 0) continue;      // an empty workgroup published nothing meaningful
-          const float nw = (float)nwi;
-          const float dm = rx_ld_sc1f(pp) / nw - mean;
-          M2 += rx_ld_sc1f(pp + 1);
-          M2 = fmaf(nw * dm, dm, M2);
-        }
+        const float M2 = mw_m2_sum(p0, mw->stride, mw->G, lg, mean, n_batch, T::BP);
         bn_mean[j] = mean;
         bn_var[j] = M2 / (float)n_batch;
       }
@@ -1034,12 +1081,8 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
         if (n >= ntiles) continue;
         const int c = n * 16 + lr;
         const int cc = c < pv.out ? c : 0;
-        float sg = 0.f, sgx = 0.f;
-        for (int w = 0; w < mw->G; ++w) {
-          const float* pp = mw_bwd(mw->part, mw->stride, pv, w) + 2 * cc;
-          sg += rx_ld_sc1f(pp);
-          sgx += rx_ld_sc1f(pp + 1);
-        }
+        float sg, sgx;
+        mw_pair_sum(mw_bwd(mw->part, mw->stride, pv, 0) + 2 * cc, mw->stride, mw->G, lg, sg, sgx);
         bsg[j] = sg;
         bsgx[j] = sgx;
       }
@@ -1329,8 +1372,17 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
   C::each_layer(d, [&](const auto& ly, int) {
     if (ly.b_off >= 0) {
       for (int c = (int)blockIdx.x * RX_THREADS + rx_tid<false>(); c < ly.out; c += mw.G * RX_THREADS) {
+        // G loads in flight 8 at a time, added in workgroup order
+        const float* p0 = mw_bias(mw.part, mw.stride, ly, 0) + c;
         float s = 0.f;
-        for (int w = 0; w < mw.G; ++w) s += rx_ld_sc1f(mw_bias(mw.part, mw.stride, ly, w) + c);
+        for (int w0 = 0; w0 < mw.G; w0 += 8) {
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = rx_ld_sc1f(p0 + (size_t)min(w0 + i, mw.G - 1) * (size_t)mw.stride);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (w0 + i < mw.G) s += v[i];
+        }
         Gr[ly.b_off + c] = s;
       }
     }
