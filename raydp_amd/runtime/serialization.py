@@ -150,19 +150,48 @@ def _load_shared(node_id: str, path: str, oid: str):
     return v
 
 
+_FLAT_DISPATCH = [None, -1]
+
+
+def _flat_dispatch():
+    """cloudpickle's dispatch table is a ChainMap over copyreg's: the C pickler then looks every
+    object's type up through Python-level ``ChainMap.__getitem__`` / ``__missing__`` (~2 us
+    each, 40 % of a model payload's pickling). The same mapping as one dict, rebuilt when
+    copyreg gains entries."""
+    import copyreg
+    n = len(copyreg.dispatch_table)
+    if _FLAT_DISPATCH[0] is None or _FLAT_DISPATCH[1] != n:
+        _FLAT_DISPATCH[0] = dict(cloudpickle.CloudPickler.dispatch_table)
+        _FLAT_DISPATCH[1] = n
+    return _FLAT_DISPATCH[0]
+
+
 class _Pickler(cloudpickle.CloudPickler):
     def __init__(self, f, transfer: bool):
+        # the C pickler reads dispatch_table once, in __init__: set it on the class first
+        _Pickler.dispatch_table = _flat_dispatch()
         super().__init__(f, protocol=5)
         self.transfer = transfer
         self.oids: List[str] = []
         self.store = _store()
 
     def reducer_override(self, obj):
-        t = _torch_tensor_type()
-        if t is not None and type(obj) is t:
+        # every object of the stream passes through here (a model + optimizer payload: ~300
+        # modules, dicts and tensors): decide by type once per type, not by a chain of checks
+        kind = _KIND.get(type(obj))
+        if kind is None:
+            kind = _classify(type(obj))
+        if kind == _PLAIN:
+            # an instance of an ordinary class: cloudpickle's reducer_override returns
+            # NotImplemented for those too (it rewrites classes and functions only)
+            return NotImplemented
+        if kind == _CLOUD:
+            return super().reducer_override(obj)
+        if kind == _TENSOR:
             red = _reduce_cpu_tensor(self, obj)
             if red is not None:
                 return red
+            return super().reducer_override(obj)
         if isinstance(obj, pa.Schema):
             # one IPC message instead of pyarrow's field-by-field reduction (plans cache their
             # output schema on every node: ~25 fields x 20 nodes per stage closure)
@@ -189,6 +218,28 @@ class _Pickler(cloudpickle.CloudPickler):
             self.oids.append(oid)
             return _load_shared, key
         return super().reducer_override(obj)
+
+
+_PLAIN, _TENSOR, _CHECK, _CLOUD = 0, 1, 2, 3
+_KIND = {}      # type -> how reducer_override treats its instances
+
+
+def _classify(tp) -> int:
+    """_TENSOR for torch.Tensor itself, _CHECK for the Arrow / plan types reducer_override
+    rewrites (and their subclasses), _PLAIN for everything else (cloudpickle's own rules)."""
+    t = _torch_tensor_type()
+    if t is not None and tp is t:
+        kind = _TENSOR
+    elif issubclass(tp, (pa.Schema, pa.Table, pa.RecordBatch)) or tp.__name__ == "MapPlan":
+        kind = _CHECK
+    elif issubclass(tp, type) or issubclass(tp, types.FunctionType):
+        kind = _CLOUD          # classes and functions: cloudpickle decides by value / reference
+    else:
+        kind = _PLAIN
+    if t is not None or kind != _PLAIN:
+        # before torch is imported, a plain verdict might be torch.Tensor's own later: not cached
+        _KIND[tp] = kind
+    return kind
 
 
 def _torch_tensor_type():
