@@ -133,7 +133,19 @@ template <int MT>
 struct Tile {
   static constexpr int BP = MT * 16;         // padded batch rows
   static constexpr int NTW = 16 / MT;        // max output n-tiles per wave (64 acc regs)
-  static constexpr int XS = BP + 8;          // stride (elements) of transposed matrices
+  // transposed matrices (XT_l, GT): rows of BP bf16, no padding; the 16-B chunks of row r are
+  // XOR-permuted by swz(r). Every access keeps to whole chunks -- the publish step's 8-B stores
+  // (16 rows per lane group), the wgrad fragments' and the export's 16-B reads -- so a chunk
+  // permutation is free, and swz spreads each lane group over the banks: LDS cycles per
+  // wave-instruction (ds_read_b128 ideal 4) export 8 -> 4, wgrad fragments 8 -> 4 at MT 4 / 8
+  // (12 -> 4 export at MT 2); the 8-B stores stay at 8 (2 dwords per lane over 32 banks: 2-way is
+  // the floor for a 16-B permutation). The padded stride BP + 8 this replaces gave 8 / 8 / 8.
+  static constexpr int XS = BP;
+  __host__ __device__ static constexpr int swz(int r) {
+    return MT == 1 ? (r >> 2) & 1 : MT == 8 ? r & 15 : (r >> 1) & (2 * MT - 1);
+  }
+  // element index of (row r, batch column e) in a transposed matrix
+  __host__ __device__ static constexpr int tix(int r, int e) { return r * XS + (((e >> 3) ^ swz(r)) << 3) + (e & 7); }
 };
 
 // ------------------------------------------------------------------------------------------
@@ -380,7 +392,7 @@ __device__ __forceinline__ void export_rows(const u16* lds, int rows, float* __r
   for (int idx = rx_tid<PS>(); idx < rows * CH; idx += RX_THREADS) {
     const int r = idx / CH, c = idx % CH;
     const int boff = byte_base + (r * bp_total + col0 + c * 8) * 2;
-    const u32x4 val = *reinterpret_cast<const u32x4*>(lds + r * XS + c * 8);
+    const u32x4 val = *reinterpret_cast<const u32x4*>(lds + r * XS + ((c ^ Tile<MT>::swz(r)) << 3));
     if (PS && wt)
       rx_store16_sc1(Gr, boff, val);
     else
@@ -756,7 +768,6 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   // ---- publish y (or G_{L-1}) as bf16: row-major into R, transposed into XT_{l+1} / GT ----
   const int XS = T::XS;
   u16* dstT = last ? GT : reinterpret_cast<u16*>(smem + nx.xt_off);
-  const int tstride = last ? (T::BP + 8) : XS;
 #pragma unroll
   for (int j = 0; j < T::NTW; ++j) {
     const int n = wave + j * RX_NW;
@@ -771,7 +782,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         R[(mt * 16 + lg * 4 + 1) * RS + c] = (u16)(pk.x >> 16);
         R[(mt * 16 + lg * 4 + 2) * RS + c] = (u16)pk.y;
         R[(mt * 16 + lg * 4 + 3) * RS + c] = (u16)(pk.y >> 16);
-        if (TRAIN || !last) *reinterpret_cast<uint2*>(dstT + c * tstride + mt * 16 + lg * 4) = pk;
+        if (TRAIN || !last) *reinterpret_cast<uint2*>(dstT + T::tix(c, mt * 16 + lg * 4)) = pk;
       }
     }
   }
@@ -873,13 +884,13 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
           const int ni = min(nb0 + q * RX_NW, ni_tiles - 1);
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks)
-            xa[q][ks] = *reinterpret_cast<const bf16x8*>(XT + (ni * 16 + lr) * XS + ks * 32 + 8 * lg);
+            xa[q][ks] = *reinterpret_cast<const bf16x8*>(XT + T::tix(ni * 16 + lr, ks * 32 + 8 * lg));
         }
         for (int mo = 0; mo < mo_tiles; ++mo) {
           bf16x8 gb[KS];
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks)
-            gb[ks] = *reinterpret_cast<const bf16x8*>(GT + (mo * 16 + lr) * XS + ks * 32 + 8 * lg);
+            gb[ks] = *reinterpret_cast<const bf16x8*>(GT + T::tix(mo * 16 + lr, ks * 32 + 8 * lg));
 #pragma unroll
           for (int q = 0; q < NB; ++q) {
             const int ni = nb0 + q * RX_NW;
@@ -901,13 +912,13 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
           const int mo = min(mb0 + q * RX_NW, mo_tiles - 1);
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks)
-            gb[q][ks] = *reinterpret_cast<const bf16x8*>(GT + (mo * 16 + lr) * XS + ks * 32 + 8 * lg);
+            gb[q][ks] = *reinterpret_cast<const bf16x8*>(GT + T::tix(mo * 16 + lr, ks * 32 + 8 * lg));
         }
         for (int ni = 0; ni < ni_tiles; ++ni) {
           bf16x8 xa[KS];
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks)
-            xa[ks] = *reinterpret_cast<const bf16x8*>(XT + (ni * 16 + lr) * XS + ks * 32 + 8 * lg);
+            xa[ks] = *reinterpret_cast<const bf16x8*>(XT + T::tix(ni * 16 + lr, ks * 32 + 8 * lg));
 #pragma unroll
           for (int q = 0; q < NB; ++q) {
             const int mo = mb0 + q * RX_NW;
@@ -1065,7 +1076,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       R[(mt * 16 + lg * 4 + 1) * RS + c] = (u16)(pk.x >> 16);
       R[(mt * 16 + lg * 4 + 2) * RS + c] = (u16)pk.y;
       R[(mt * 16 + lg * 4 + 3) * RS + c] = (u16)(pk.y >> 16);
-      *reinterpret_cast<uint2*>(GT + c * XS + mt * 16 + lg * 4) = pk;
+      *reinterpret_cast<uint2*>(GT + T::tix(c, mt * 16 + lg * 4)) = pk;
     }
   };
   bool split = false;
@@ -1195,7 +1206,7 @@ __device__ __forceinline__ void load_front(const D& d, const MlpDesc* __restrict
       }
     }
     R[row * RS + k] = v;
-    if (need_t && k < l0.in_n) XT[k * T::XS + row] = v;
+    if (need_t && k < l0.in_n) XT[T::tix(k, row)] = v;
   }
   if (bad && metrics != nullptr) atomicAdd(&metrics[6], 1.0);
   __syncthreads();
@@ -1280,7 +1291,7 @@ __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int k = ch * 8 + e;
-        if (k < in_n) XT[k * T::XS + row] = h[e];
+        if (k < in_n) XT[T::tix(k, row)] = h[e];
       }
     }
   }

@@ -205,7 +205,7 @@ class FusedMLPTrainer:
         img_off = 0       # bf16 elements: W_l [out_n][in_k] then Wt_l [in_n][out_k], per layer
         rs_total = 0      # fp32 running statistics [mean | var] per BN layer
         rs_init = []
-        xs = bp + 8
+        xs = bp          # transposed-image stride: Tile<MT>::XS (csrc/hip/mlp_core.h)
         lds = 0
 
         def alloc(nbytes):
