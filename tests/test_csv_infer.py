@@ -129,3 +129,30 @@ def test_sources_use_the_native_reader(tmp_path):
     assert src._schema.field("k").type == pa.int32() and src._schema.field("x").type == pa.float64()
     assert src.load(0).column("x").to_pylist() == [2.5, None, 1000.0]
     assert native_exec.STATS["native_csv_reads"] >= 1
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_short_mantissa_reals_are_bit_exact(seed):
+    """Reals the exact fast path decides (mantissa < 2^53, |decimal exponent| <= 22) and the
+    ones just outside it (17-digit mantissas, 2^53 +- 1, exponents 22 / 23) -- bit for bit
+    against Arrow's parser, on a file wide enough for the threaded column pass."""
+    rng = random.Random(seed)
+    pool = ["9007199254740992", "9007199254740993", "9007199254740991.5", "1e22", "1e23", "1.5e-22",
+            "4.9e-23", "123456789012345678.5", "0.000000000000000000001", "-0.0", "0.30000000000000004"]
+
+    def val():
+        r = rng.random()
+        if r < 0.25:
+            return rng.choice(pool)
+        if r < 0.6:
+            return f"{rng.uniform(-1e4, 1e4):.{rng.randint(1, 9)}f}"
+        if r < 0.8:
+            return f"{rng.randint(1, 99999)}e{rng.choice(['-', ''])}{rng.randint(0, 25)}"
+        return repr(rng.uniform(-180, 180))
+    ncol, nrow = 8, 1500
+    lines = [",".join(f"c{i}" for i in range(ncol))]
+    lines += [",".join(val() for _ in range(ncol)) for _ in range(nrow)]
+    data = ("\n".join(lines) + "\n").encode()
+    got = native_exec.read_csv_infer(data)
+    assert got is not None
+    _same(got, _arrow(data))
