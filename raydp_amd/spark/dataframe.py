@@ -818,10 +818,20 @@ def _hoist_windows(e):
 
 
 def _has_window(x) -> bool:
-    if isinstance(x, WindowExpr):
-        return True
-    if isinstance(x, Expr):
-        return any(_has_window(v) for v in vars(x).values() if isinstance(v, (Expr, list, tuple)))
-    if isinstance(x, (list, tuple)):
-        return any(_has_window(v) for v in x if isinstance(v, (Expr, list, tuple)))
+    # explicit stack: every withColumn of a plan build asks this (the recursive generator form
+    # was ~a tenth of the NYC plan build)
+    stack = [x]
+    while stack:
+        y = stack.pop()
+        if isinstance(y, WindowExpr):
+            return True
+        if isinstance(y, Expr):
+            vals = y.__dict__.values()
+        elif isinstance(y, (list, tuple)):
+            vals = y
+        else:
+            continue
+        for v in vals:
+            if isinstance(v, (Expr, list, tuple)):
+                stack.append(v)
     return False
