@@ -50,7 +50,35 @@ def send_frame(conn, lock, data: bytes):
             conn.sendall(rest)
 
 
+_SPIN = []
+
+
+def _spin_cfg():
+    """(window ns, native poll) of the busy-poll before a blocking frame read (``RAYDP_ACTOR_SPIN_US``, default 0 = sleep
+    in recv at once); see csrc/runtime/spin.cc."""
+    if not _SPIN:
+        try:
+            us = float(os.environ.get("RAYDP_ACTOR_SPIN_US", "0") or 0)
+        except ValueError:
+            us = 0.0
+        fn = None
+        if us > 0:
+            try:
+                from raydp_amd.runtime.store import _lib
+                lib = _lib()
+                fn = lib.rt_spin_readable
+                import ctypes
+                fn.argtypes, fn.restype = [ctypes.c_int, ctypes.c_int64], ctypes.c_int
+            except Exception:  # noqa: BLE001 - no native runtime: plain blocking reads
+                fn = None
+        _SPIN.append((int(us * 1000), fn))
+    return _SPIN[0]
+
+
 def recv_frame(conn) -> bytearray:
+    ns, spin = _spin_cfg()
+    if spin is not None:
+        spin(conn.fileno(), ns)     # GIL released while it polls
     (n,) = struct.unpack("<Q", _recv_exact(conn, 8))
     return _recv_exact(conn, n)
 

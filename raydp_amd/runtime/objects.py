@@ -100,6 +100,29 @@ def contains(ref: ObjectRef) -> bool:
         return ref.id in _local
 
 
+_GET_SPIN = []
+
+
+def _spin_until_done(fut):
+    """Poll a pending call's future for up to ``RAYDP_ACTOR_SPIN_US`` before blocking on it: the
+    reply is set by the connection's reader thread, and a getter asleep on the future's
+    condition pays a second wake-up (csrc/runtime/spin.cc). ``time.sleep(0)`` hands the GIL
+    over on every turn, so the reader thread is never kept from setting the result."""
+    if not _GET_SPIN:
+        import os
+        try:
+            _GET_SPIN.append(float(os.environ.get("RAYDP_ACTOR_SPIN_US", "0") or 0) * 1e-6)
+        except ValueError:
+            _GET_SPIN.append(0.0)
+    window = _GET_SPIN[0]
+    if window <= 0:
+        return
+    import time
+    end = time.perf_counter() + window
+    while not fut.done() and time.perf_counter() < end:
+        time.sleep(0)
+
+
 def get(ref, timeout: Optional[float] = None):
     if isinstance(ref, (list, tuple)):
         return [get(r, timeout) for r in ref]
@@ -108,6 +131,8 @@ def get(ref, timeout: Optional[float] = None):
     from raydp_amd.runtime import core
     pending = core.pending_result(ref)
     if pending is not None:
+        if not pending.done():
+            _spin_until_done(pending)
         return pending.result(timeout)
     from raydp_amd.runtime.core import store_for
     store = store_for(ref.node_id) if ref.node_id is not None else _store()
