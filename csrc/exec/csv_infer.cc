@@ -28,7 +28,6 @@
 #include <cstring>
 #include <memory>
 #include <string>
-#include <thread>
 #include <vector>
 
 namespace {
@@ -292,21 +291,13 @@ int rx_csv_infer(const char* data, int64_t len, char delim, void* out) {
   if (len <= 0 || !tokenize(data, len, delim, &cells, &ncol)) return 0;
   const size_t nrow = cells.size() / ncol - 1;
   if (nrow == 0) return 0;
-  // columns are independent: a file of more than a few thousand fields types them on up to 4
-  // threads (the 17-significant-digit doubles of a NYC file take ~45 ns each to parse exactly)
+  // one column after the other on the calling thread (typing them on 4 threads measured slower
+  // on the GPU box: thread start-up on a shared 256-core host outweighed ~60 us of parsing)
   std::vector<std::shared_ptr<arrow::Array>> cols(ncol);
   std::vector<int> rc(ncol, 1);
-  const size_t nthr = nrow * ncol >= 8192 ? std::min<size_t>(4, ncol) : 1;
-  auto work = [&](size_t t) {
-    for (size_t c = t; c < ncol; c += nthr) rc[c] = build_column(cells, ncol, nrow, c, &cols[c]);
-  };
-  if (nthr > 1) {
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < nthr; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
-  } else {
-    work(0);
+  for (size_t c = 0; c < ncol; ++c) {
+    rc[c] = build_column(cells, ncol, nrow, c, &cols[c]);
+    if (rc[c] != 1) return rc[c];
   }
   std::vector<std::shared_ptr<arrow::Field>> fields;
   for (size_t c = 0; c < ncol; ++c) {
