@@ -148,6 +148,19 @@ struct Tile {
   __host__ __device__ static constexpr int tix(int r, int e) { return r * XS + (((e >> 3) ^ swz(r)) << 3) + (e & 7); }
 };
 
+// R, the row-major activation / gradient image (stride RS = max_k + RX_RPAD, b128-friendly):
+// the 16-B chunks of row r are XOR-permuted by rx_rsw(r) in {0, 2}. The publish step writes R
+// with 2-byte stores, rows 4 apart in the two 16-lane halves of a lane group, and at this
+// stride those rows share banks (2-way); flipping chunk bit 1 between them separates them, and
+// the GEMM A-fragment reads (rows lr of a 16-row tile, k-chunks s*4 + lg) stay conflict-free
+// (bank model: publish 4 -> 2 LDS cycles per wave-instruction, A reads 4 -> 4, for max_k 64 ..
+// 512). The permutation only touches chunk bit 1, so offsets of whole 4-chunk (64-B) steps --
+// the GEMM's k-steps -- commute with it.
+__host__ __device__ constexpr int rx_rsw(int r) { return (((r >> 2) ^ (r >> 3)) & 1) << 1; }
+__host__ __device__ constexpr int rx_rix(int r, int k, int RS) {
+  return r * RS + (((k >> 3) ^ rx_rsw(r)) << 3) + (k & 7);
+}
+
 // ------------------------------------------------------------------------------------------
 // Multi-workgroup step (batch > one workgroup's 16 * MT rows; TorchEstimator batch_size 129 ..
 // 16384, e.g. the reference's own test at batch 1000, python/raydp/tests/test_torch.py:70-80):
@@ -323,7 +336,7 @@ __device__ __forceinline__ bf16x8 ld_w(const u16* __restrict__ img, int off) {
 
 template <int MT, bool PS>
 __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
-                                          const u16* __restrict__ img, int boff, int K, int lg) {
+                                          const u16* __restrict__ img, int boff, int K, int lg, int alg) {
   constexpr int KC = 8;
   const int nks = K >> 5;
   for (int kc = 0; kc < nks; kc += KC) {
@@ -336,7 +349,7 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restric
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
       if (kc + s < nks) {
-        const int k0 = (kc + s) * 32 + 8 * lg;
+        const int k0 = (kc + s) * 32 + 8 * alg;   // alg = lg ^ rx_rsw(row): R's chunk swizzle
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const bf16x8 a = *reinterpret_cast<const bf16x8*>(Arow + mt * 16 * RS + k0);
@@ -402,13 +415,13 @@ __device__ __forceinline__ void export_rows(const u16* lds, int rows, float* __r
 
 template <int MT, bool PS>
 __device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
-                                              const u16* __restrict__ img, int boff, int K, int lg,
+                                              const u16* __restrict__ img, int boff, int K, int lg, int alg,
                                               const bf16x8 (&pre)[RX_PK]) {
   const int nks = K >> 5;
 #pragma unroll
   for (int s = 0; s < RX_PK; ++s) {
     if (s < nks) {
-      const int k0 = s * 32 + 8 * lg;
+      const int k0 = s * 32 + 8 * alg;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(Arow + mt * 16 * RS + k0);
@@ -417,7 +430,7 @@ __device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __res
     }
   }
   if (nks > RX_PK)
-    gemm_tile<MT, PS>(acc, Arow + RX_PK * 32, RS, img, boff + RX_PK * 32, K - RX_PK * 32, lg);
+    gemm_tile<MT, PS>(acc, Arow + RX_PK * 32, RS, img, boff + RX_PK * 32, K - RX_PK * 32, lg, alg);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -466,9 +479,9 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     if (n < ntiles) {
       const int boff = ly.w_img + (n * 16 + lr) * ly.in_k;
       if (j < RX_PJ)
-        gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg, wpre[j < RX_PJ ? j : 0]);
+        gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg, lg ^ rx_rsw(lr), wpre[j < RX_PJ ? j : 0]);
       else
-        gemm_tile<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg);
+        gemm_tile<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg, lg ^ rx_rsw(lr));
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
@@ -778,10 +791,10 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         uint2 pk;
         pk.x = rx_f2bf2(acc[j * MT + mt][0], acc[j * MT + mt][1]);
         pk.y = rx_f2bf2(acc[j * MT + mt][2], acc[j * MT + mt][3]);
-        R[(mt * 16 + lg * 4 + 0) * RS + c] = (u16)pk.x;
-        R[(mt * 16 + lg * 4 + 1) * RS + c] = (u16)(pk.x >> 16);
-        R[(mt * 16 + lg * 4 + 2) * RS + c] = (u16)pk.y;
-        R[(mt * 16 + lg * 4 + 3) * RS + c] = (u16)(pk.y >> 16);
+        R[rx_rix(mt * 16 + lg * 4 + 0, c, RS)] = (u16)pk.x;
+        R[rx_rix(mt * 16 + lg * 4 + 1, c, RS)] = (u16)(pk.x >> 16);
+        R[rx_rix(mt * 16 + lg * 4 + 2, c, RS)] = (u16)pk.y;
+        R[rx_rix(mt * 16 + lg * 4 + 3, c, RS)] = (u16)(pk.y >> 16);
         if (TRAIN || !last) *reinterpret_cast<uint2*>(dstT + T::tix(c, mt * 16 + lg * 4)) = pk;
       }
     }
@@ -791,7 +804,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   if (kpad > 0) {
     for (int idx = rx_tid<PS>(); idx < T::BP * kpad; idx += RX_THREADS) {
       const int row = idx / kpad, cc = ly.out_n + idx % kpad;
-      R[row * RS + cc] = 0;
+      R[rx_rix(row, cc, RS)] = 0;
     }
   }
   fst(4);
@@ -949,9 +962,9 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     if (n < ntiles) {
       const int boff = ly.wt_img + (n * 16 + lr) * ly.out_k;
       if (j < RX_PJ)
-        gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg, wpre[j < RX_PJ ? j : 0]);
+        gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg, lg ^ rx_rsw(lr), wpre[j < RX_PJ ? j : 0]);
       else
-        gemm_tile<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg);
+        gemm_tile<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg, lg ^ rx_rsw(lr));
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
@@ -1072,10 +1085,10 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       uint2 pk;
       pk.x = rx_f2bf2(g[mt * 4 + 0], g[mt * 4 + 1]);
       pk.y = rx_f2bf2(g[mt * 4 + 2], g[mt * 4 + 3]);
-      R[(mt * 16 + lg * 4 + 0) * RS + c] = (u16)pk.x;
-      R[(mt * 16 + lg * 4 + 1) * RS + c] = (u16)(pk.x >> 16);
-      R[(mt * 16 + lg * 4 + 2) * RS + c] = (u16)pk.y;
-      R[(mt * 16 + lg * 4 + 3) * RS + c] = (u16)(pk.y >> 16);
+      R[rx_rix(mt * 16 + lg * 4 + 0, c, RS)] = (u16)pk.x;
+      R[rx_rix(mt * 16 + lg * 4 + 1, c, RS)] = (u16)(pk.x >> 16);
+      R[rx_rix(mt * 16 + lg * 4 + 2, c, RS)] = (u16)pk.y;
+      R[rx_rix(mt * 16 + lg * 4 + 3, c, RS)] = (u16)(pk.y >> 16);
       *reinterpret_cast<uint2*>(GT + T::tix(c, mt * 16 + lg * 4)) = pk;
     }
   };
@@ -1110,7 +1123,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
   if (kpad > 0) {
     for (int idx = rx_tid<PS>(); idx < T::BP * kpad; idx += RX_THREADS) {
       const int row = idx / kpad, cc = pv.out_n + idx % kpad;
-      R[row * RS + cc] = 0;
+      R[rx_rix(row, cc, RS)] = 0;
     }
   }
   __syncthreads();
@@ -1205,7 +1218,7 @@ __device__ __forceinline__ void load_front(const D& d, const MlpDesc* __restrict
         v = rx_f2bf(rx_g(P)[fc.poff + id * fc.stride]);
       }
     }
-    R[row * RS + k] = v;
+    R[rx_rix(row, k, RS)] = v;
     if (need_t && k < l0.in_n) XT[T::tix(k, row)] = v;
   }
   if (bad && metrics != nullptr) atomicAdd(&metrics[6], 1.0);
@@ -1235,7 +1248,8 @@ __device__ __forceinline__ void front_backward(const D& d, const MlpDesc* __rest
     f32x4 part[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_tile<MT, false>(part, R + lr * RS, RS, img, l0.wt_img + (n * 16 + lr) * l0.out_k, l0.out_k, lg);
+    gemm_tile<MT, false>(part, R + lr * RS, RS, img, l0.wt_img + (n * 16 + lr) * l0.out_k, l0.out_k, lg,
+                         lg ^ rx_rsw(lr));
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -1285,7 +1299,7 @@ __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem
     const int row = idx / chunks, ch = idx % chunks;
     u32x4 v = *reinterpret_cast<const RX_GLOBAL u32x4*>(rx_g(feats) + (size_t)rowidx[row] * d.feat_k + ch * 8);
     if (row >= nvalid) v = u32x4{0u, 0u, 0u, 0u};
-    *reinterpret_cast<u32x4*>(R + row * RS + ch * 8) = v;
+    *reinterpret_cast<u32x4*>(R + row * RS + ((ch ^ rx_rsw(row)) << 3)) = v;
     if (need_t) {
       const u16* h = reinterpret_cast<const u16*>(&v);
 #pragma unroll
