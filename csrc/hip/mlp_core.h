@@ -786,16 +786,21 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     const int n = wave + j * RX_NW;
     if (n < ntiles) {
       const int c = n * 16 + lr;
+      // rows mt * 16 + lg * 4 + q all take rx_rsw(lg * 4): one swizzled column per tile, and the
+      // row offsets stay immediates of the stores
+      u16* Rc = R + lg * 4 * RS + ((((c >> 3) ^ rx_rsw(lg * 4)) << 3) | (c & 7));
+      const int tsw = T::swz(c);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         uint2 pk;
         pk.x = rx_f2bf2(acc[j * MT + mt][0], acc[j * MT + mt][1]);
         pk.y = rx_f2bf2(acc[j * MT + mt][2], acc[j * MT + mt][3]);
-        R[rx_rix(mt * 16 + lg * 4 + 0, c, RS)] = (u16)pk.x;
-        R[rx_rix(mt * 16 + lg * 4 + 1, c, RS)] = (u16)(pk.x >> 16);
-        R[rx_rix(mt * 16 + lg * 4 + 2, c, RS)] = (u16)pk.y;
-        R[rx_rix(mt * 16 + lg * 4 + 3, c, RS)] = (u16)(pk.y >> 16);
-        if (TRAIN || !last) *reinterpret_cast<uint2*>(dstT + T::tix(c, mt * 16 + lg * 4)) = pk;
+        Rc[(mt * 16 + 0) * RS] = (u16)pk.x;
+        Rc[(mt * 16 + 1) * RS] = (u16)(pk.x >> 16);
+        Rc[(mt * 16 + 2) * RS] = (u16)pk.y;
+        Rc[(mt * 16 + 3) * RS] = (u16)(pk.y >> 16);
+        if (TRAIN || !last)
+          *reinterpret_cast<uint2*>(dstT + c * XS + ((((mt * 16 + lg * 4) >> 3) ^ tsw) << 3) + ((lg & 1) << 2)) = pk;
       }
     }
   }
@@ -1079,16 +1084,17 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       else
         Gr[pv.b_off + c] = bs;
     }
-    // publish G_{l-1}
+    // publish G_{l-1} (same hoisted swizzle as the forward publish)
+    u16* Rc = R + lg * 4 * RS + ((((c >> 3) ^ rx_rsw(lg * 4)) << 3) | (c & 7));
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       uint2 pk;
       pk.x = rx_f2bf2(g[mt * 4 + 0], g[mt * 4 + 1]);
       pk.y = rx_f2bf2(g[mt * 4 + 2], g[mt * 4 + 3]);
-      R[rx_rix(mt * 16 + lg * 4 + 0, c, RS)] = (u16)pk.x;
-      R[rx_rix(mt * 16 + lg * 4 + 1, c, RS)] = (u16)(pk.x >> 16);
-      R[rx_rix(mt * 16 + lg * 4 + 2, c, RS)] = (u16)pk.y;
-      R[rx_rix(mt * 16 + lg * 4 + 3, c, RS)] = (u16)(pk.y >> 16);
+      Rc[(mt * 16 + 0) * RS] = (u16)pk.x;
+      Rc[(mt * 16 + 1) * RS] = (u16)(pk.x >> 16);
+      Rc[(mt * 16 + 2) * RS] = (u16)pk.y;
+      Rc[(mt * 16 + 3) * RS] = (u16)(pk.y >> 16);
       *reinterpret_cast<uint2*>(GT + T::tix(c, mt * 16 + lg * 4)) = pk;
     }
   };
