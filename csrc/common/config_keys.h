@@ -31,7 +31,11 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.mlp_persistent.timeout_s", "RAYDP_MLP_PERSISTENT_TIMEOUT_S", "5"},
     {"spark.ray.mi355x.fused_linear", "RAYDP_FUSED_LINEAR", "1"},
     {"spark.ray.mi355x.driver_gc_freeze", "RAYDP_DRIVER_GC_FREEZE", "1"},
-    {"spark.ray.mi355x.ddp.bucket_mb", "RAYDP_DDP_BUCKET_MB", "32"},
+    {"spark.ray.mi355x.ddp.bucket_mb", "RAYDP_DDP_BUCKET_MB", "0"},
+    {"spark.ray.mi355x.ddp.first_bucket_mb", "RAYDP_DDP_FIRST_BUCKET_MB", "1"},
+    {"spark.ray.mi355x.ddp.overlap_bucket_mb", "RAYDP_DDP_OVERLAP_BUCKET_MB", "4"},
+    {"spark.ray.mi355x.runtime.port", "RAYDP_RUNTIME_PORT", "-1"},
+    {"spark.ray.mi355x.runtime.host", "RAYDP_RUNTIME_HOST", "127.0.0.1"},
     {"spark.ray.mi355x.object_store_bytes", "RAYDP_OBJECT_STORE_BYTES", "0"},
     {"spark.ray.mi355x.trace", "RAYDP_TRACE", ""},
     {"spark.ray.mi355x.roctx", "RAYDP_ROCTX", "0"},

@@ -740,8 +740,12 @@ int rx_exec_wait(void* exp, int64_t id, int64_t* rows, int64_t* bytes, int64_t* 
       p->done = true;
     }
     ex->cv_done.wait(g, [p] { return p->done; });
-    t = std::move(it->second);
-    ex->tasks.erase(it);
+    // `mu` was released above (inline run, cv wait): a concurrent rx_exec_submit may have
+    // inserted into `tasks` and rehashed it, so the iterator from before is stale -- look the
+    // task up again by its id.
+    auto it2 = ex->tasks.find(id);
+    t = std::move(it2->second);
+    ex->tasks.erase(it2);
   }
   *rows = t->rows;
   *bytes = t->bytes;

@@ -149,8 +149,11 @@ __device__ __forceinline__ void ps_store_vectors(const D& d, const char* smem, f
 }
 
 // stamps[0..31]: phase stamps of the middle step (diagnostics); stamps[32 + s]: start of step s,
-// stamps[32 + nsteps]: end of the last step
+// stamps[32 + nsteps]: end of the last step; stamps[33 + nsteps + k], k < RX_PS_LAYER_STAMPS:
+// the middle step's intra-layer shader-clock stamps (s_memtime; layer_forward [40 + 5 l + k],
+// layer_backward [20 + 4 l + k]) -- a stamps buffer holds 33 + nsteps + RX_PS_LAYER_STAMPS words
 #define RX_PS_STEP_STAMPS 32
+#define RX_PS_LAYER_STAMPS 96
 
 template <class C, int MT>
 __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const OptDesc& o, const u16* __restrict__ img,
@@ -235,15 +238,17 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       if (flag_lds[0]) return;
     }
     stamp(s, 2);
+    unsigned long long* lst =
+        (stamps != nullptr && s == sstep) ? stamps + RX_PS_STEP_STAMPS + nsteps + 1 : nullptr;
     bf16x8 wpre[RX_PJ][RX_PK];
     fwd_prefetch<true>(C::first(d), img, wpre);
     C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
       layer_forward<MT, true, true>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre,
-                                    ps_wt, l, nullptr, labp);
+                                    ps_wt, l, lst, labp);
     });
     stamp(s, 3);
     C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
-      layer_backward<MT, true>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, nullptr, sync, s, ps_wt);
+      layer_backward<MT, true>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, lst, sync, s, ps_wt);
       stamp(s, 8 + l);
     });
     // layer 0's backward ends with its G^T export (no dgrad)

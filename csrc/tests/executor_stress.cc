@@ -149,6 +149,25 @@ int main(int argc, char** argv) {
       }
     });
   }
+  // a burst submitter: hundreds of queued tasks (failing fast on a missing file) inserted while
+  // the threads above wait on theirs -- the task map rehashes under a waiter that released the
+  // executor lock for an inline run or a condition wait (the waiter must not keep an iterator)
+  std::thread burst([&] {
+    for (int round = 0; round < per; ++round) {
+      std::vector<int64_t> ids;
+      for (int k = 0; k < 256; ++k) {
+        char oid[33], e[256];
+        snprintf(oid, sizeof(oid), "burst%03d%04d%020d", round, k, 0);
+        ids.push_back(rx_exec_submit(ex, stage, "/nonexistent/rx_burst.csv", 0, 1, nullptr, store, oid, nullptr, nullptr,
+                                     e, sizeof(e)));
+      }
+      for (int64_t id : ids) {
+        int64_t n = 0, b = 0, tm[3];
+        char e[256];
+        if (rx_exec_wait(ex, id, &n, &b, tm, e, sizeof(e)) != -1) failures++;
+      }
+    }
+  });
   // concurrent cache readers and the CSV inference reader
   std::atomic<bool> stop{false};
   std::thread reader([&] {
@@ -167,6 +186,7 @@ int main(int argc, char** argv) {
     }
   });
   for (auto& t : ts) t.join();
+  burst.join();
   stop = true;
   reader.join();
   char oid[33];

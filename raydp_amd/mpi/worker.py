@@ -105,13 +105,28 @@ class MPIWorker:
         rep = self.driver.RegisterWorkerService(network.RegisterWorkerServiceRequest(
             world_rank=self.world_rank, worker_ip=self.node_ip, worker_port=port), timeout=wait_timeout)
         if rep.ray_address:
+            # join the job driver's runtime node before any function runs (the reference's rank
+            # calls ray.init(address=reply.ray_address), python/raydp/mpi/mpi_worker.py:159-160):
+            # rank functions reach its object store and (named) actors
             os.environ.setdefault("RAYDP_RUNTIME_ADDRESS", rep.ray_address)
+            try:
+                from raydp_amd import runtime
+                runtime.init(address=rep.ray_address)
+            except (ConnectionError, OSError, ValueError) as e:
+                print(f"MPI worker {self.world_rank}: cannot attach to the runtime at "
+                      f"{rep.ray_address!r}: {e}", file=sys.stderr)
         ctx = WorkerContext(self.job_id, self.world_rank, self.local_rank, self.node_ip)
         t = threading.Thread(target=self._task_loop, args=(ctx,), name="mpi-task-runner", daemon=True)
         t.start()
         self.stop_event.wait()
         self.server.stop(0.5)
         self.driver.close()
+        try:
+            from raydp_amd.runtime import core
+            if core.is_initialized():
+                core.shutdown()
+        except Exception:  # noqa: BLE001 - best effort at exit
+            pass
         if self.failed is not None:
             print(f"MPI worker failed: {self.failed}", file=sys.stderr)
             return 1

@@ -443,6 +443,16 @@ class BucketAllreduce:
         self.launched = {"oneshot": 0, "twoshot": 0, "torch": 0}
 
     @property
+    def overlaps(self) -> bool:
+        """True when a bucket reduction launched during backward runs BESIDE the rest of
+        backward: the xGMI kernels on the comm stream, or torch.distributed's asynchronous
+        collectives (RCCL's own stream / gloo's worker thread) when no xGMI communicator is up.
+        False when the xGMI kernels are stream-ordered behind backward (ranks sharing a GPU)."""
+        if self.xg is not None:
+            return self.stream is not None
+        return True
+
+    @property
     def kind(self) -> str:
         """What the buckets ride on: the xGMI kernels for buckets up to the limit (when the peer
         mapping is up) and torch.distributed (RCCL / gloo) for the rest."""

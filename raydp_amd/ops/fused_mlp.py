@@ -22,6 +22,10 @@ from raydp_amd.ops import _hip
 _LOSSES = {nn.MSELoss: 0, nn.SmoothL1Loss: 1, nn.L1Loss: 2}
 
 
+# words after the per-step stamps of a persistent epoch's stamp buffer: the middle step's
+# intra-layer shader-clock stamps (csrc/hip/mlp_persist.h RX_PS_LAYER_STAMPS)
+_PS_LAYER_STAMPS = 96
+
 def _ru(x, m):
     return (x + m - 1) // m * m
 
@@ -628,7 +632,7 @@ class FusedMLPTrainer:
         if st is None:
             return None
         self._step_stamps = None
-        t = np.asarray(st)[32:].astype(np.float64)
+        t = np.asarray(st)[32:-_PS_LAYER_STAMPS].astype(np.float64)
         return np.diff(t) * 0.01 if t.size > 1 else None
 
     def snapshot(self):
@@ -678,7 +682,7 @@ class FusedMLPTrainer:
         stamps = None
         if self.record_steps:
             # device wall clock at every step start (csrc/hip/mlp_persist.h RX_PS_STEP_STAMPS)
-            stamps = self._dev_buf("stamps", 32 + nsteps + 1, torch.int64)
+            stamps = self._dev_buf("stamps", 32 + nsteps + 1 + _PS_LAYER_STAMPS, torch.int64)
             stamps.zero_()
             self.bufs.stamps = stamps.data_ptr()
         rc = self.lib.rx_mlp_train_persistent(

@@ -17,11 +17,14 @@ MI355X over RCCL/xGMI:
   buckets go to RCCL. Ranks that share a GPU keep the buckets stream-ordered: there the early
   comm kernel spins for its peer on the CUs that peer's backward needs (5-8x slower steps,
   profiles/r4_ddp_bucket_sweep.txt);
-* bucket size defaults to 32 MiB (``RAYDP_DDP_BUCKET_MB``): xGMI links are per-link bound
-  (~153 GB/s per link), so fewer, larger messages amortise the collective's flag rendezvous;
-  the measured sweep on DLRM's 8.7 MB of dense gradients (1 / 2 / 4 / 8 / 32 MiB buckets, 2 and
-  4 ranks) is fastest with one bucket; tiny models (NYC_Model: 194 KB) end up in one bucket =
-  one collective per step;
+* bucket sizes follow whether a reduction can overlap backward (:func:`bucket_caps`): with
+  the comm stream (or RCCL's asynchronous collectives) on GPUs of their own, a 1 MiB first
+  bucket and 4 MiB after it -- DLRM's 8.7 MB of dense gradients become 3 buckets, 2 of them
+  reduced while backward still runs (torch DDP likewise starts with a small first bucket);
+  stream-ordered (ranks sharing a GPU: nothing overlaps) 32 MiB, which the one-GPU sweep
+  measured fastest (1 / 2 / 4 / 8 / 32 MiB, 2 and 4 ranks, profiles/r4_ddp_bucket_sweep.txt).
+  The overlap itself is unmeasured until an 8-GPU run. Tiny models (NYC_Model:
+  194 KB) end up in one bucket = one collective per step;
 * parameters are broadcast from rank 0 at wrap time (one collective per bucket); replicated
   floating-point buffers (BatchNorm running statistics) are re-pointed into one flat tensor
   and re-broadcast before each forward with ONE collective (torch's ``broadcast_buffers``);
@@ -61,6 +64,24 @@ class _Bucket:
         self.work = None
 
 
+def bucket_caps(bucket_cap_mb=None, overlaps: bool = True) -> List[int]:
+    """Byte caps of the buckets in gradient-production order (the last entry repeats).
+
+    An explicit ``bucket_cap_mb`` (or ``spark.ray.mi355x.ddp.bucket_mb`` > 0) is one uniform
+    cap. Auto (0): when the reductions overlap backward, a small first bucket
+    (``ddp.first_bucket_mb``) and ``ddp.overlap_bucket_mb`` after it, so the reduction of every
+    bucket but the last runs beside the rest of backward; when they cannot overlap (stream-ordered
+    xGMI kernels on a GPU shared by ranks) few large buckets: 32 MiB."""
+    from raydp_amd.utils.config import get as conf_get
+    mb = float(bucket_cap_mb or conf_get("spark.ray.mi355x.ddp.bucket_mb") or 0.0)
+    if mb > 0:
+        return [int(mb * (1 << 20))]
+    if not overlaps:
+        return [32 << 20]
+    return [int(float(conf_get("spark.ray.mi355x.ddp.first_bucket_mb")) * (1 << 20)),
+            int(float(conf_get("spark.ray.mi355x.ddp.overlap_bucket_mb")) * (1 << 20))]
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, bucket_cap_mb: float = None, broadcast_buffers: bool = True,
                  process_group=None):
@@ -71,7 +92,9 @@ class DistributedDataParallel(nn.Module):
         self.rank = dist.get_rank(process_group)
         self.broadcast_buffers = broadcast_buffers
         from raydp_amd.utils.config import get as conf_get
-        cap = float(bucket_cap_mb or conf_get("spark.ray.mi355x.ddp.bucket_mb")) * (1 << 20)
+        from raydp_amd.ops.comm import BucketAllreduce
+        self._allreduce = BucketAllreduce(process_group)
+        self.bucket_caps = bucket_caps(bucket_cap_mb, self._allreduce.overlaps)
         sparse_ids = set()
         for m in module.modules():
             if isinstance(m, (nn.Embedding, nn.EmbeddingBag)) and m.sparse:
@@ -95,13 +118,12 @@ class DistributedDataParallel(nn.Module):
             if getattr(m, "_raydp_model_parallel", False):
                 local_ids.update(id(t) for t in list(m.parameters()) + list(m.buffers()))
         self._local_ids = local_ids
-        from raydp_amd.ops.comm import BucketAllreduce
-        self._allreduce = BucketAllreduce(process_group)
         # reverse order ~= gradient production order
         self.buckets: List[_Bucket] = []
         cur, size = [], 0
         for p in reversed(params):
             nbytes = p.numel() * p.element_size()
+            cap = self.bucket_caps[min(len(self.buckets), len(self.bucket_caps) - 1)]
             if cur and (size + nbytes > cap or p.dtype != cur[0].dtype):
                 self.buckets.append(_Bucket(cur))
                 cur, size = [], 0
@@ -120,6 +142,9 @@ class DistributedDataParallel(nn.Module):
             p.register_post_accumulate_grad_hook(self._sparse_hook)
         self._finalize_queued = False
         self.require_backward_grad_sync = True
+        # (kind, bucket) in launch order, with ("backward_end", -1) when autograd's end-of-backward
+        # callback runs: set to a list to record (tests/test_ddp_buckets.py)
+        self.launch_log = None
         # sharded embedding tables (raydp_amd.parallel.embedding_mp) set up their xGMI exchange
         # here, at a point every rank reaches together, so capturable() can count on it
         self._sharded = [m for m in module.modules() if hasattr(m, "_xg_plan")]
@@ -218,10 +243,14 @@ class DistributedDataParallel(nn.Module):
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
             if b.pending == 0:
                 b.work = self._allreduce(b.flat, 1.0 / self.world)
+                if self.launch_log is not None:
+                    self.launch_log.append(("bucket", bi))
         return hook
 
     def _finalize(self):
         self._finalize_queued = False
+        if self.launch_log is not None:
+            self.launch_log.append(("backward_end", -1))
         for p in self.sparse_params:
             self._reduce_sparse(p)
         for b in self.buckets:

@@ -254,7 +254,8 @@ class ActorManager:
                 from raydp_amd.runtime.supervisor import SupervisorClient
                 os.makedirs(os.path.join(self.node.session_dir, "actors"), exist_ok=True)
                 if getattr(self.node, "attached", False):
-                    self._sup = SupervisorClient(os.environ["RAYDP_SUPERVISOR_SOCK"])
+                    self._sup = SupervisorClient(getattr(self.node, "supervisor_sock", None)
+                                                 or os.environ["RAYDP_SUPERVISOR_SOCK"])
                 else:
                     self._sup = SupervisorClient.launch(self.node.session_dir)
                 self._sup.subscribe(self._on_event)
@@ -273,14 +274,32 @@ class ActorManager:
     def create(self, cls, args, kwargs, opts, name, namespace) -> ProcessActor:
         from raydp_amd.runtime.api import _resolve_args
         sup = self.supervisor
-        vnode, res, pg, bundle = self._place(opts)
+        gcs = getattr(self.node, "gcs", None)
+        remote = None
+        if gcs is not None:
+            # an attached driver: the head places the actor in its cluster table
+            strat = opts.get("scheduling_strategy")
+            pg = opts.get("placement_group") or getattr(strat, "placement_group", None)
+            bidx = opts.get("placement_group_bundle_index", getattr(strat, "placement_group_bundle_index", -1))
+            req = {k: opts[k] for k in ("num_cpus", "num_gpus", "memory", "resources") if opts.get(k) is not None}
+            if getattr(strat, "node_id", None):
+                req["node_id"] = strat.node_id
+            remote = gcs.call("place", req, pg.id.hex() if pg is not None else None, bidx)
+            from raydp_amd.runtime.node import VirtualNode
+            from raydp_amd.runtime.store import attach_store
+            st = self.node.store if remote["store_path"] == self.node.store.path else \
+                attach_store(remote["store_path"], remote["node_id"])
+            vnode, res, pg, bundle = VirtualNode(remote["node_id"], {}, st, ip=remote["node_ip"] or None), {}, None, None
+        else:
+            vnode, res, pg, bundle = self._place(opts)
         aid = uuid.uuid4().hex[:16]
         a = ProcessActor(self, aid, name, namespace, opts, vnode, res, pg, bundle)
+        a.gcs_token = remote["token"] if remote is not None else None
         ra, rk = _resolve_args(args, kwargs)
         clean = {k: v for k, v in opts.items() if k not in ("scheduling_strategy", "placement_group")}
         a.opts = dict(opts, _class_name=getattr(cls, "__name__", str(cls)))
-        a.gpu_take = self._take_gpus(vnode, res.get("GPU", 0.0))
-        a.gpu_ids = [g for g, _ in a.gpu_take]
+        a.gpu_take = [] if remote is not None else self._take_gpus(vnode, res.get("GPU", 0.0))
+        a.gpu_ids = list(remote["gpu_ids"]) if remote is not None else [g for g, _ in a.gpu_take]
         if a.gpu_ids:
             a.opts["_gpu_ids"] = a.gpu_ids
         with open(a.spec_path + ".tmp", "wb") as f:
@@ -352,6 +371,13 @@ class ActorManager:
             if getattr(a, "_released", False):
                 return
             a._released = True
+        token = getattr(a, "gcs_token", None)
+        if token is not None:
+            try:
+                self.node.gcs.call("release", token)
+            except (OSError, RuntimeError):
+                pass            # head gone: its table went with it
+            return
         if getattr(a, "gpu_take", None) and a.vnode is not None and hasattr(a.vnode, "gpu_cap"):
             for g, share in a.gpu_take:
                 a.vnode.gpu_cap[g] = min(1.0, a.vnode.gpu_cap[g] + share)
@@ -401,6 +427,24 @@ class ActorManager:
     def list(self):
         with self._lock:
             return list(self.actors.values())
+
+    def kill_owned(self):
+        """Kill the actors this process created (owned, not ``lifetime="detached"``)."""
+        with self._lock:
+            mine = [a for a in self.actors.values()
+                    if a.owned and not a.dead and (a.opts or {}).get("lifetime") != "detached"]
+        for a in mine:
+            try:
+                a.kill(no_restart=True)
+            except Exception:  # noqa: BLE001 - best effort at shutdown
+                pass
+            if a.name:
+                # (the process's current node is already unset at shutdown: use this node's dir)
+                safe = "".join(c if c.isalnum() or c in "-_." else "_" for c in f"{a.namespace}__{a.name}")
+                try:
+                    os.unlink(os.path.join(self.node.session_dir, "named", safe))
+                except OSError:
+                    pass
 
     def shutdown(self):
         with self._lock:

@@ -363,6 +363,8 @@ def nodes():
     n = core.current_node()
     if n is None:
         return []
+    if getattr(n, "gcs", None) is not None:
+        return n.gcs.call("nodes")
     return [{"NodeID": v.node_id, "Alive": v.alive, "NodeManagerAddress": v.ip,
              "Resources": dict(v.total)} for v in n.cluster.nodes.values()]
 
@@ -370,6 +372,8 @@ def nodes():
 def cluster_resources():
     out: Dict[str, float] = {}
     n = core.current_node()
+    if getattr(n, "gcs", None) is not None:
+        return n.gcs.call("resources")[0]
     if n is not None:
         for v in n.cluster.alive_nodes():
             for k, x in v.total.items():
@@ -380,6 +384,8 @@ def cluster_resources():
 def available_resources():
     out: Dict[str, float] = {}
     n = core.current_node()
+    if getattr(n, "gcs", None) is not None:
+        return n.gcs.call("resources")[1]
     if n is not None:
         for v in n.cluster.alive_nodes():
             for k, x in v.available.items():

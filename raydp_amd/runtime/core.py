@@ -129,6 +129,12 @@ def init(address=None, num_cpus=None, num_gpus=None, resources=None, object_stor
             _node = Node.attach(os.environ["RAYDP_SESSION_DIR"], os.environ["RAYDP_STORE_PATH"],
                                 os.environ["RAYDP_NODE_ID"], os.environ.get("RAYDP_NAMESPACE"))
             return _node.info()
+        if address is None:
+            address = os.environ.get("RAYDP_ADDRESS") or None
+        if address not in (None, "", "local"):
+            # another process's running node (raydp_amd/runtime/gcs.py): attach to it
+            _node = Node.connect(address, namespace=namespace)
+            return _node.info()
         _node = Node.create(address=address, num_cpus=num_cpus, num_gpus=num_gpus,
                             resources=resources, object_store_memory=object_store_memory,
                             namespace=namespace)

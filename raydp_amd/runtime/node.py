@@ -135,6 +135,9 @@ class Node:
         self.supervisor = None
         self.actors = None
         self.attached = False
+        self.gcs = None            # driver attached through the head's control endpoint
+        self.gcs_service = None    # head: the control endpoint it serves (raydp_amd/runtime/gcs.py)
+        self.supervisor_sock = None
 
     @classmethod
     def attach(cls, session_dir: str, store_path: str, node_id: str, namespace=None) -> "Node":
@@ -174,6 +177,49 @@ class Node:
             json.dump(head.total, f)
         from raydp_amd.runtime.actors import ActorManager
         n.actors = ActorManager(n)
+        n._serve_control()
+        return n
+
+    def _serve_control(self):
+        """Start the control endpoint other processes attach through (runtime.init(address=...))
+        and record this head as the host's current node (address='auto')."""
+        from raydp_amd.runtime import gcs
+        from raydp_amd.utils.config import get as conf_get
+        self.gcs_service = gcs.HeadService(self, int(conf_get("spark.ray.mi355x.runtime.port")),
+                                           str(conf_get("spark.ray.mi355x.runtime.host")))
+        self.address = self.gcs_service.address
+        gcs.record_current(self.address)
+
+    def attach_info(self) -> dict:
+        """What a process attaching to this head needs (the control endpoint's ``info``)."""
+        head = self.cluster.nodes.get(self.node_id)
+        return {"node_id": self.node_id, "session_dir": self.session_dir, "store_path": self.store.path,
+                "supervisor_sock": self.actors.supervisor.sock_path, "namespace": self.namespace,
+                "job_id": self.job_id, "address": self.address, "ip": head.ip if head is not None else "",
+                "resources": dict(head.total) if head is not None else {},
+                "tcp_address": self.gcs_service.tcp_address if self.gcs_service is not None else None}
+
+    @classmethod
+    def connect(cls, address: str, namespace=None) -> "Node":
+        """A driver process attached to a running head (``ray.init(address=...)``): the head's
+        object store, supervisor, named actors and cluster table, reached through its control
+        endpoint. Actors this process creates are placed by the head and die with this process
+        unless created with ``lifetime="detached"``."""
+        from raydp_amd.runtime import gcs
+        from raydp_amd.runtime.actors import ActorManager
+        from raydp_amd.runtime.store import attach_store
+        client = gcs.GcsClient(address)
+        info = client.call("info")
+        n = cls(namespace or info.get("namespace"))
+        n.attached = True
+        n.gcs = client
+        n.node_id = info["node_id"]
+        n.session_dir = info["session_dir"]
+        n.address = info["address"]
+        n.supervisor_sock = info["supervisor_sock"]
+        n.store = attach_store(info["store_path"], info["node_id"])
+        n.cluster.add(VirtualNode(info["node_id"], info.get("resources") or {}, n.store, ip=info.get("ip") or None))
+        n.actors = ActorManager(n)
         return n
 
     def add_virtual_node(self, num_cpus=1, num_gpus=0, resources=None, object_store_memory=None,
@@ -209,11 +255,20 @@ class Node:
                 "namespace": self.namespace}
 
     def shutdown(self):
+        if self.gcs is not None and self.actors is not None:
+            # an attached driver's actors die with it (Ray's non-detached actors die with their job)
+            self.actors.kill_owned()
         if self.actors is not None:
             self.actors.shutdown()
         if self.attached:
             self.store.close()
+            if self.gcs is not None:
+                self.gcs.close()
             return
+        if self.gcs_service is not None:
+            from raydp_amd.runtime import gcs
+            gcs.clear_current(self.address)
+            self.gcs_service.close()
         for vn in list(self.cluster.nodes.values()):
             if vn.store is not None:
                 vn.store.destroy()

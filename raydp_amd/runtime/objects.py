@@ -143,6 +143,12 @@ def get(ref, timeout: Optional[float] = None):
     with _local_lock:
         if ref.id in _local:
             return _local[ref.id]
+    if ref._lineage is None and store is not None and getattr(core.current_node(), "gcs", None) is not None:
+        # an attached driver holds refs other processes produce: the object may still be in
+        # flight (Ray's get blocks until it is sealed) -- poll the arena for a bounded time
+        value = _poll_store(store, ref.id, timeout)
+        if value is not _MISSING:
+            return value
     if ref._lineage is not None:
         # reconstruct from lineage (re-run the producing task) and re-seal under the same id
         value = ref._lineage()
@@ -151,6 +157,24 @@ def get(ref, timeout: Optional[float] = None):
         ref.node_id = st.node_id if st is not None else None
         return value
     raise ObjectLostError(f"object {ref.id} is lost and has no lineage to reconstruct it")
+
+
+_MISSING = object()
+
+
+def _poll_store(store, oid: str, timeout: Optional[float]):
+    import os
+    import time
+    limit = float(timeout if timeout is not None else os.environ.get("RAYDP_GET_TIMEOUT_S", "60"))
+    end = time.monotonic() + limit
+    delay = 0.0005
+    while time.monotonic() < end:
+        time.sleep(delay)
+        delay = min(delay * 2, 0.05)
+        found, value = store.get(oid)
+        if found:
+            return value
+    return _MISSING
 
 
 def free(refs):

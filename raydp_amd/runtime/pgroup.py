@@ -59,7 +59,16 @@ def placement_group(bundles: List[Dict[str, float]], strategy: str = "PACK", nam
     if not core.is_initialized():
         core.init()
     pg = PlacementGroup(bundles, strategy, name)
-    core.current_node().cluster.place_group(pg)
+    node = core.current_node()
+    if getattr(node, "gcs", None) is not None:
+        # an attached driver: the group lives in the head's table; this is its local mirror
+        pid, nodes = node.gcs.call("pg_create", [dict(b) for b in bundles], strategy, name)
+        pg.id = PlacementGroupID(pid)
+        pg.bundle_nodes = list(nodes)
+        pg.bundle_free = [dict(b) for b in pg.bundle_specs]
+        pg.remote = True
+    else:
+        node.cluster.place_group(pg)
     pg.state = "CREATED"
     with _lock:
         _groups[pg.id.hex()] = pg
@@ -73,7 +82,10 @@ def remove_placement_group(pg: PlacementGroup):
     if g is None or g.state == "REMOVED":
         return
     node = core.current_node()
-    if node is not None:
+    if getattr(g, "remote", False):
+        if node is not None and node.gcs is not None:
+            node.gcs.call("pg_remove", g.id.hex())
+    elif node is not None:
         node.cluster.release_group(g)
     g.state = "REMOVED"
 

@@ -13,8 +13,10 @@ options (``--jars``, ``--packages``, ``--driver-class-path``, ``--class``) are a
 ignored with a warning where they have no meaning without a JVM; a ``--class`` application
 (a jar) cannot run and is an error.
 
-``--ray-conf`` is the JSON file the reference writes (``{"ray": {"address": ..., ...}}``);
-``num-cpus`` / ``object-store-memory`` / ``namespace`` in it size the local runtime.
+``--ray-conf`` is the JSON file the reference writes (``{"ray": {"address": ..., ...}}``): an
+``address`` (``raydp://<session dir>``, ``auto``, or ``host:port?token=...``) runs the application
+against that running node (``raydp_amd/runtime/gcs.py``); without one, ``num-cpus`` /
+``object-store-memory`` / ``namespace`` size a fresh local runtime.
 
 The application runs in this process (as ``__main__``); its ``SparkSession.builder
 .getOrCreate()`` sees ``spark.master=ray`` and starts executor processes with the submitted
@@ -119,6 +121,9 @@ def _runtime_kwargs(ray_conf_path) -> dict:
     with open(ray_conf_path) as f:
         conf = json.load(f).get("ray", {})
     kw = {}
+    if conf.get("address"):
+        # run against the caller's running node (doc/spark_on_ray.md:116-144 of the reference)
+        kw["address"] = str(conf["address"])
     if "num-cpus" in conf:
         kw["num_cpus"] = int(conf["num-cpus"])
     if "object-store-memory" in conf:

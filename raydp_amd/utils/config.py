@@ -168,8 +168,26 @@ register("spark.ray.mi355x.driver_gc_freeze", "bool", True,
          "init_spark moves the driver's long-lived state (imported torch / pyarrow / engine modules, "
          "~180k objects) to the permanent GC generation, so a full collection no longer walks it "
          "(53-89 ms each, measured; raydp_amd/utils/gcmeter.py)", env="RAYDP_DRIVER_GC_FREEZE")
-register("spark.ray.mi355x.ddp.bucket_mb", "float", 32.0,
-         "DDP gradient bucket size (xGMI rings are per-link bound: few large buckets)", env="RAYDP_DDP_BUCKET_MB")
+register("spark.ray.mi355x.ddp.bucket_mb", "float", 0.0,
+         "DDP gradient bucket size in MiB; 0 = auto: when a bucket's all-reduce can run beside the rest "
+         "of backward (comm stream on, or RCCL/gloo async on GPUs of their own) the first bucket is "
+         "ddp.first_bucket_mb and the rest ddp.overlap_bucket_mb, so k buckets give k - 1 reductions "
+         "that overlap backward; with the reduction stream-ordered (ranks sharing a GPU) nothing can "
+         "overlap and 32 MiB buckets (few collectives) measured fastest (profiles/r4_ddp_bucket_sweep.txt)",
+         env="RAYDP_DDP_BUCKET_MB")
+register("spark.ray.mi355x.ddp.first_bucket_mb", "float", 1.0,
+         "auto bucketing with overlap: size of the first bucket (the last layers' gradients, produced "
+         "first by backward; small so its reduction starts early, as torch DDP's first bucket)",
+         env="RAYDP_DDP_FIRST_BUCKET_MB")
+register("spark.ray.mi355x.ddp.overlap_bucket_mb", "float", 4.0,
+         "auto bucketing with overlap: size of every later bucket (large enough that one xGMI bucket's "
+         "flag rendezvous is amortised over ~4 MiB of link traffic)", env="RAYDP_DDP_OVERLAP_BUCKET_MB")
+register("spark.ray.mi355x.runtime.port", "int", -1,
+         "TCP port of the head node's control endpoint (raydp_amd/runtime/gcs.py; 0 = any free port, "
+         "-1 = Unix socket in the session directory only); a TCP client presents the session token",
+         env="RAYDP_RUNTIME_PORT")
+register("spark.ray.mi355x.runtime.host", "str", "127.0.0.1",
+         "interface the control endpoint's TCP port binds to (loopback by default)", env="RAYDP_RUNTIME_HOST")
 register("spark.ray.mi355x.object_store_bytes", "bytes", "0",
          "shared-memory object-store arena per node (0: automatic)", env="RAYDP_OBJECT_STORE_BYTES")
 register("spark.ray.mi355x.trace", "str", None,
