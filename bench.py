@@ -520,9 +520,10 @@ def main():
         n_train = world
         driver_gpu = True
     # executors (one single-core executor per CPU): 4 for the driver-config pipelines (one CSV
-    # split each); 8 for data-scale runs, whose 1 GB+ CSVs split into whole waves of 8 tasks
-    # (the one-GPU box gives a process 16 CPUs)
-    cpus = int(os.environ.get("RAYDP_BENCH_CPUS", "8" if args.rows is not None else "4"))
+    # split each); for data-scale runs one per CPU the box gives a process (16 on the one-GPU
+    # box): the 1 GB+ CSVs split into whole waves of that many tasks, and the ETL is CPU-bound
+    # on CSV parsing (Arrow's reader, ~1.2 M rows/s per core)
+    cpus = int(os.environ.get("RAYDP_BENCH_CPUS", "16" if args.rows is not None else "4"))
     if args.topology == "estimator" and n_train > cpus:
         # one driver feeds N workers: one single-core executor per worker, within the host
         cpus = min(n_train, max(cpus, (os.cpu_count() or 8) // 4))

@@ -39,11 +39,7 @@ def main():
                          "backward: raydp_amd/ops/fused_optim.py)")
     ap.add_argument("--eager-mlp", action="store_true",
                     help="run the MLP towers as eager nn.Linear/ReLU instead of the fused MFMA kernels")
-    ap.add_argument("--persistent", action="store_true",
-                    help="one GPU: the whole step as ONE persistent launch (csrc/hip/dlrm_step.hip)")
     args = ap.parse_args()
-    if args.persistent:
-        return persistent_main(args)
     if args.eager_mlp:
         os.environ["RAYDP_FUSED_LINEAR"] = "0"
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,45 +132,6 @@ def main():
                                   "launched": dict(net._allreduce.launched)} if mp else None}), flush=True)
     if mp:
         dist.destroy_process_group()
-
-
-def persistent_main(args):
-    """The notebook's step (SGD, BCE) as one persistent launch per step over an 8-batch cycle."""
-    from raydp_amd.ops.dlrm_step import DlrmStep
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    torch.manual_seed(0)
-    model = Dlrm(13, [args.rows_per_table] * 26, [512, 128, 32], [1024, 1024, 512, 256, 1], 32).to(dev)
-    n = args.batch * 8
-    g = torch.Generator(device=dev).manual_seed(1000)
-    dense = torch.randn(n, 13, device=dev, generator=g)
-    cats = torch.randint(0, args.rows_per_table, (n, 26), device=dev, generator=g)
-    y = torch.randint(0, 2, (n,), device=dev, generator=g).float()
-    st = DlrmStep(model, 0.01, args.batch, dev)
-    st.bind_data(dense, cats, y)
-    perm = torch.arange(n, device=dev)
-    assert args.steps % 8 == 0 and args.warmup % 8 == 0, "whole 8-step data cycles"
-    for _ in range(args.warmup // 8):
-        st.steps(perm, 0, 8)
-    torch.cuda.synchronize()
-    st.loss_acc.zero_()
-    t = time.perf_counter()
-    for _ in range(args.steps // 8):
-        st.steps(perm, 0, 8)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t
-    st.check()
-    phases = st.phase_profile(perm, 0, 16)
-    print(json.dumps({"metric": "DLRM training samples/sec (synthetic Criteo-shaped)",
-                      "value": round(args.steps * args.batch / dt, 1), "unit": "samples/s", "n_gpus": 1,
-                      "ms_per_step": round(dt * 1e3 / args.steps, 4), "per_gpu_batch": args.batch,
-                      "steps": args.steps, "warmup": args.warmup, "engine": "persistent step (dlrm_step.hip)",
-                      "workgroups": st.G, "lds_bytes": st.lds,
-                      "tiles": [[(ph.s[j].tm, ph.s[j].tn) for j in range(ph.nspec)]
-                                for ph in st.desc.ph[:st.desc.nph] if ph.kind == 0],
-                      "mean_loss": float(st.loss_acc.item()) / args.steps,
-                      "phase_us": phases,
-                      "tables": 26, "rows_per_table": args.rows_per_table}), flush=True)
 
 
 def _graph_step(net, lossf, opt, dense, cats, y, args):

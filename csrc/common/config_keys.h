@@ -22,7 +22,6 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.allreduce.oneshot_max_mb", "RAYDP_ALLREDUCE_ONESHOT_MAX_MB", "16"},
     {"spark.ray.mi355x.allreduce.twoshot_min_mb", "RAYDP_ALLREDUCE_TWOSHOT_MIN_MB", "1"},
     {"spark.ray.mi355x.ddp.comm_stream", "RAYDP_DDP_COMM_STREAM", "auto"},
-    {"spark.ray.mi355x.dlrm_step", "RAYDP_DLRM_STEP", "0"},
     {"spark.ray.mi355x.fused", "RAYDP_FUSED", "auto"},
     {"spark.ray.mi355x.hip_graphs", "RAYDP_TORCH_GRAPHS", "1"},
     {"spark.ray.mi355x.mlp_jit", "RAYDP_MLP_JIT", "1"},

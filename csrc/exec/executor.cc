@@ -51,6 +51,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 extern "C" {
@@ -149,6 +150,7 @@ struct Segment {
 
 struct Stage {
   std::shared_ptr<arrow::Schema> src_schema;   // CSV column names + types
+  std::vector<bool> src_needed;                // source columns the first segment reads or passes
   bool header = true;
   char delim = ',';
   std::string null_token;
@@ -217,6 +219,16 @@ Stage* parse_stage(const uint8_t* data, int64_t len, std::string* err) {
     st->segs.push_back(std::move(g));
   }
   if (!r.ok || r.p != r.end) { *err = "truncated or oversized stage spec"; return nullptr; }
+  // projection: a CSV column no VM input reads and no output passes through (the NYC chain's
+  // "key", dropped unread) is not converted at all
+  const int nsrc = st->src_schema->num_fields();
+  st->src_needed.assign(static_cast<size_t>(nsrc), st->segs.empty());
+  if (!st->segs.empty()) {
+    for (const auto& in : st->segs[0].inputs)
+      if (in.col >= 0 && in.col < nsrc) st->src_needed[static_cast<size_t>(in.col)] = true;
+    for (const auto& c : st->segs[0].cols)
+      if (c.kind != 0 && c.idx >= 0 && c.idx < nsrc) st->src_needed[static_cast<size_t>(c.idx)] = true;
+  }
   return st.release();
 }
 
@@ -225,44 +237,62 @@ Stage* parse_stage(const uint8_t* data, int64_t len, std::string* err) {
 // that STARTS inside it (the line straddling `lo` belongs to the previous split).
 arrow::Result<std::shared_ptr<arrow::Table>> read_csv_split(const Stage& st, const std::string& path,
                                                            int64_t lo, int64_t hi) {
+  // Only this split's bytes are read (plus the line straddling `hi`, and the header line when
+  // the split starts the file): a 1 GB file cut into 16 splits costs 16 x 1/16 of it, not 16 x
+  // the whole file.
   int fd = ::open(path.c_str(), O_RDONLY);
   if (fd < 0) return arrow::Status::IOError("cannot open ", path);
   struct stat sb;
   if (fstat(fd, &sb) != 0) { ::close(fd); return arrow::Status::IOError("cannot stat ", path); }
   const int64_t size = sb.st_size;
-  std::string all(static_cast<size_t>(size), '\0');
+  // position just past the '\n' ending the line that contains byte `pos` (size at EOF)
+  auto line_end = [&](int64_t pos) -> int64_t {
+    char chunk[4096];
+    while (pos < size) {
+      const ssize_t k = ::pread(fd, chunk, sizeof(chunk), pos);
+      if (k <= 0) return size;
+      const void* nl = memchr(chunk, '\n', static_cast<size_t>(k));
+      if (nl != nullptr) return pos + (static_cast<const char*>(nl) - chunk) + 1;
+      pos += k;
+    }
+    return size;
+  };
+  auto byte_at = [&](int64_t pos) -> char {
+    char c = 0;
+    return ::pread(fd, &c, 1, pos) == 1 ? c : '\n';
+  };
+  const int64_t header_len = st.header ? line_end(0) : 0;
+  int64_t pos = header_len;
+  if (lo > 0) {
+    pos = lo;
+    if (byte_at(lo - 1) != '\n') pos = line_end(lo);
+  }
+  const int64_t start = std::max(pos, header_len);
+  if (start >= hi && lo > 0) { ::close(fd); return arrow::Table::MakeEmpty(st.src_schema); }
+  int64_t stop = std::min<int64_t>(std::max<int64_t>(hi, start), size);
+  if (stop > start && byte_at(stop - 1) != '\n') stop = line_end(stop);
+  const int64_t n = stop - start;
+  ARROW_ASSIGN_OR_RAISE(std::shared_ptr<arrow::ResizableBuffer> bufr, arrow::AllocateResizableBuffer(std::max<int64_t>(n, 1)));
+  char* all_p = reinterpret_cast<char*>(bufr->mutable_data());
   int64_t got = 0;
-  while (got < size) {
-    ssize_t k = ::pread(fd, &all[static_cast<size_t>(got)], static_cast<size_t>(size - got), got);
+  while (got < n) {
+    const ssize_t k = ::pread(fd, all_p + got, static_cast<size_t>(n - got), start + got);
     if (k <= 0) break;
     got += k;
   }
   ::close(fd);
-  if (got != size) return arrow::Status::IOError("short read of ", path);
-  auto line_end = [&](int64_t pos) {   // position just past the '\n' ending the line at pos
-    while (pos < size && all[static_cast<size_t>(pos)] != '\n') ++pos;
-    return pos < size ? pos + 1 : size;
-  };
-  int64_t header_len = st.header ? line_end(0) : 0;
-  int64_t pos = st.header ? header_len : 0;
-  if (lo > 0) {
-    pos = lo;
-    if (all[static_cast<size_t>(lo - 1)] != '\n') pos = line_end(lo);
-  }
-  const int64_t start = std::max(pos, header_len);
-  if (start >= hi && lo > 0) return arrow::Table::MakeEmpty(st.src_schema);
-  int64_t stop = std::min<int64_t>(std::max<int64_t>(hi, start), size);
-  if (stop > start && all[static_cast<size_t>(stop - 1)] != '\n') stop = line_end(stop);
+  if (got != n) return arrow::Status::IOError("short read of ", path);
+  ARROW_RETURN_NOT_OK(bufr->Resize(n, false));
   bool blank = true;
-  for (int64_t i = start; i < stop && blank; ++i) {
-    const char c = all[static_cast<size_t>(i)];
+  for (int64_t i = 0; i < n && blank; ++i) {
+    const char c = all_p[i];
     blank = c == ' ' || c == '\n' || c == '\r' || c == '\t' || c == '\v' || c == '\f';
   }
   if (blank) return arrow::Table::MakeEmpty(st.src_schema);
-  auto buf = arrow::Buffer::FromString(all.substr(static_cast<size_t>(start), static_cast<size_t>(stop - start)));
+  std::shared_ptr<arrow::Buffer> buf = std::move(bufr);
   auto ro = arrow::csv::ReadOptions::Defaults();
-  ro.use_threads = (stop - start) > (4 << 20);
-  ro.block_size = static_cast<int32_t>(std::max<int64_t>(1 << 20, std::min<int64_t>(stop - start + 1, INT32_MAX)));
+  ro.use_threads = n > (4 << 20);
+  ro.block_size = static_cast<int32_t>(std::max<int64_t>(1 << 20, std::min<int64_t>(n + 1, INT32_MAX)));
   for (const auto& f : st.src_schema->fields()) ro.column_names.push_back(f->name());
   auto po = arrow::csv::ParseOptions::Defaults();
   po.delimiter = st.delim;
@@ -270,9 +300,32 @@ arrow::Result<std::shared_ptr<arrow::Table>> read_csv_split(const Stage& st, con
   for (const auto& f : st.src_schema->fields()) co.column_types[f->name()] = f->type();
   co.strings_can_be_null = true;
   co.null_values = {st.null_token};
+  bool all_needed = true;
+  for (size_t i = 0; i < st.src_needed.size(); ++i) all_needed = all_needed && st.src_needed[i];
+  if (!all_needed) {   // include_columns selects by name: only with unique column names
+    std::unordered_set<std::string> names;
+    for (const auto& f : st.src_schema->fields()) all_needed = all_needed || !names.insert(f->name()).second;
+  }
+  if (!all_needed) {
+    for (size_t i = 0; i < st.src_needed.size(); ++i)
+      if (st.src_needed[i]) co.include_columns.push_back(st.src_schema->field(static_cast<int>(i))->name());
+  }
   auto in = std::make_shared<arrow::io::BufferReader>(buf);
   ARROW_ASSIGN_OR_RAISE(auto rd, arrow::csv::TableReader::Make(arrow::io::default_io_context(), in, ro, po, co));
-  return rd->Read();
+  ARROW_ASSIGN_OR_RAISE(auto t, rd->Read());
+  if (all_needed) return t;
+  // back to the source layout (column indices of the stage program): skipped columns all-null
+  std::vector<std::shared_ptr<arrow::ChunkedArray>> cols;
+  int k = 0;
+  for (int i = 0; i < st.src_schema->num_fields(); ++i) {
+    if (st.src_needed[static_cast<size_t>(i)]) {
+      cols.push_back(t->column(k++));
+    } else {
+      ARROW_ASSIGN_OR_RAISE(auto nul, arrow::MakeArrayOfNull(st.src_schema->field(i)->type(), t->num_rows()));
+      cols.push_back(std::make_shared<arrow::ChunkedArray>(nul));
+    }
+  }
+  return arrow::Table::Make(st.src_schema, cols, t->num_rows());
 }
 
 // ------------------------------------------------------------------ inputs ----------------

@@ -184,13 +184,15 @@ __host__ __device__ constexpr int rx_rix(int r, int k, int RS) {
 // bounded and a timeout sets the error word, after which every barrier returns at once.
 struct NoMw {  // one workgroup per step (the fields only make MWT::on ? a : b well-formed)
   static constexpr bool on = false;
-  int k, G, wg, n_total, stride;
+  int k, ok, G, wg, n_total, stride;
   float* part;
 };
 
 struct MwCtx {
   static constexpr bool on = true;
   int k;                       // grid barriers passed so far in this step (uniform)
+  int ok;                      // 0 once a barrier of this step timed out (uniform): no gradient,
+                               // running statistic or bias partial is stored from then on
   float* part;                 // [G][stride] partials; layer l's block at mw_off_l: [fwd | bwd | bias]
   int stride;                  // floats per workgroup (a multiple of 32: 128-B lines)
   unsigned* ctl;               // [0] barrier counter, [1] done counter, [2] error word
@@ -319,6 +321,67 @@ __device__ __forceinline__ float mw_m2_sum(const float* p0, int stride, int G, i
 
 __device__ __forceinline__ float act_fwd(int act, float z) { return act == 1 ? fmaxf(z, 0.f) : z; }
 
+// Element (mt, r) of an accumulator tile is batch row mt * 16 + 4 lg + r. FULL (the batch fills
+// the workgroup's BP rows -- every step of an epoch but a ragged last one) makes every row valid
+// at compile time: no per-element compare / select in the epilogues.
+template <bool FULL>
+__device__ __forceinline__ f32x4 rx_rowmask(f32x4 v, int mt, int lg, int nvalid) {
+  if constexpr (!FULL) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (mt * 16 + lg * 4 + r >= nvalid) v[r] = 0.f;
+  }
+  return v;
+}
+
+// Sum of the MT x 4 (row-masked) values of one lane: a tree over packed-fp32 adds (depth
+// log2(MT) + 2) instead of a serial chain of MT * 4 dependent adds.
+template <int MT, bool FULL>
+__device__ __forceinline__ float rx_lane_sum(const f32x4* a, int lg, int nvalid) {
+  f32x4 s4 = rx_rowmask<FULL>(a[0], 0, lg, nvalid);
+  if constexpr (MT >= 2) {
+    f32x4 t4 = rx_rowmask<FULL>(a[1], 1, lg, nvalid);
+#pragma unroll
+    for (int mt = 2; mt < MT; mt += 2) {
+      s4 += rx_rowmask<FULL>(a[mt], mt, lg, nvalid);
+      t4 += rx_rowmask<FULL>(a[mt + 1], mt + 1, lg, nvalid);
+    }
+    s4 += t4;
+  }
+  return (s4[0] + s4[1]) + (s4[2] + s4[3]);
+}
+
+// Sum of the (row-masked) squared deviations from `mean`, same tree.
+template <int MT, bool FULL>
+__device__ __forceinline__ float rx_lane_sqdev(const f32x4* a, float mean, int lg, int nvalid) {
+  const f32x4 m4 = f32x4{mean, mean, mean, mean};
+  f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f}, t4 = s4;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const f32x4 dv = rx_rowmask<FULL>(a[mt] - m4, mt, lg, nvalid);
+    if (mt & 1)
+      t4 = __builtin_elementwise_fma(dv, dv, t4);
+    else
+      s4 = __builtin_elementwise_fma(dv, dv, s4);
+  }
+  s4 += t4;
+  return (s4[0] + s4[1]) + (s4[2] + s4[3]);
+}
+
+// Publish one accumulator tile's bf16 image into R (row-major [row][k]): the 4 lanes of a quad
+// transpose their 4 x 4 block (rx_quad_transpose), so each lane stores 8 contiguous bytes of one
+// row -- 4 ds_write_b64 per tile instead of 16 ds_write_b16. `pk[mt]` are the tile's packed rows.
+template <int MT>
+__device__ __forceinline__ void rx_publish_rows(u16* R, int RS, int c, int lane, const uint2 (&pk)[MT]) {
+  const int lg = lane >> 4, q = lane & 3;
+  const int c0 = c & ~3;                         // this quad's first column
+  const int rin = lg * 4 + q;                    // the row (inside a 16-row tile) this lane writes
+  u16* Rq = R + rin * RS + ((((c0 >> 3) ^ rx_rsw(rin)) << 3) | (c0 & 7));
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+    *reinterpret_cast<uint2*>(Rq + mt * 16 * RS) = rx_quad_transpose(pk[mt], q);
+}
+
 // C[Bpad x 16-col tile n] += A (LDS, row-major, K contiguous) x Bt (global bf16, [n][K]).
 // The weight fragments of up to KC k-steps are fetched in ONE burst of unconditional
 // (address-clamped) 16-B loads before any MFMA consumes them, so a layer costs one global
@@ -360,33 +423,34 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restric
   }
 }
 
-// The first PK k-steps of a tile's weight fragments, fetched ahead of time (before the work
-// that precedes the GEMM) so their global round trip overlaps that work.
-constexpr int RX_PJ = 2;  // tiles per wave prefetched
-constexpr int RX_PK = 4;  // k-steps per tile prefetched (8 measured no faster: 27.95 vs 27.80 us/step)
+// Weight fragments fetched ahead of time (before the work that precedes the GEMM) so their global
+// round trip overlaps that work. The buffer holds RX_PF fragments, dealt flat over this wave's
+// (tile j, k-step s) pairs: fragment f = j * nks + s. At the NYC shapes that is every fragment of
+// every GEMM (layer 1 forward: 1 tile x 8 k-steps; layer 1 dgrad: 2 tiles x 4), so no GEMM issues
+// a load of its own: a load issued after the layer's stores would be waited for behind them
+// (vmcnt retires in issue order).
+constexpr int RX_PJ = 2;
+constexpr int RX_PK = 4;
+constexpr int RX_PF = RX_PJ * RX_PK;
 template <bool PS>
-__device__ __forceinline__ void gemm_prefetch(bf16x8 (&pre)[RX_PK], const u16* __restrict__ img, int boff, int K,
-                                              int lg) {
+__device__ __forceinline__ void gemm_prefetch_flat(bf16x8 (&pre)[RX_PJ][RX_PK], const u16* __restrict__ img,
+                                                   int img_off, int ntiles, int K, int wave, int lr, int lg) {
   const int nks = K >> 5;
 #pragma unroll
-  for (int s = 0; s < RX_PK; ++s) {
-    const int ks = min(s, nks - 1);
-    pre[s] = ld_w<PS>(img, boff + ks * 32 + 8 * lg);
+  for (int f = 0; f < RX_PF; ++f) {
+    const int j = f / nks, s = f - (f / nks) * nks;
+    if (j * RX_NW < ntiles) {   // some wave has a j-th tile (address-clamped for the others)
+      const int n = min(wave + j * RX_NW, ntiles - 1);
+      pre[f >> 2][f & 3] = ld_w<PS>(img, img_off + (n * 16 + lr) * K + s * 32 + 8 * lg);
+    }
   }
 }
 
-// Head of this wave's forward weight tiles of layer `ly` (W_l rows, K = in_k).
+// This wave's forward weight fragments of layer `ly` (W_l rows, K = in_k).
 template <bool PS, class LY>
 __device__ __forceinline__ void fwd_prefetch(const LY& ly, const u16* __restrict__ img, bf16x8 (&wpre)[RX_PJ][RX_PK]) {
   const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
-  const int lr = lane & 15, lg = lane >> 4;
-  const int ntiles = ly.out_n >> 4;
-#pragma unroll
-  for (int j = 0; j < RX_PJ; ++j)
-    if (j * RX_NW < ntiles) {
-      const int n = min(wave + j * RX_NW, ntiles - 1);
-      gemm_prefetch<PS>(wpre[j], img, ly.w_img + (n * 16 + lr) * ly.in_k, ly.in_k, lg);
-    }
+  gemm_prefetch_flat<PS>(wpre, img, ly.w_img, ly.out_n >> 4, ly.in_k, wave, lane & 15, lane >> 4);
 }
 
 // Copy `rows` rows of a transposed bf16 LDS matrix (row stride XS) to global memory packed
@@ -402,35 +466,51 @@ template <int MT, bool PS>
 __device__ __forceinline__ void export_rows(const u16* lds, int rows, float* __restrict__ Gr, int byte_base,
                                             bool wt = true, int bp_total = Tile<MT>::BP, int col0 = 0) {
   constexpr int BP = Tile<MT>::BP, XS = Tile<MT>::XS, CH = BP / 8;
+  if constexpr (PS) {
+    // persistent epoch: straight-line, every thread the same number of 16-B write-through
+    // stores (threads past the end repeat an earlier chunk's identical bytes), so the compiler
+    // can count them when it waits for the loads issued before them
+    const int total = rows * CH;
+    const int iters = (total + RX_THREADS - 1) / RX_THREADS;
+    for (int it = 0; it < iters; ++it) {
+      int idx = rx_tid<PS>() + it * RX_THREADS;
+      idx = idx < total ? idx : idx % total;
+      const int r = idx / CH, c = idx % CH;
+      const int boff = byte_base + (r * bp_total + col0 + c * 8) * 2;
+      rx_store16_sc1(Gr, boff, *reinterpret_cast<const u32x4*>(lds + r * XS + ((c ^ Tile<MT>::swz(r)) << 3)));
+    }
+    (void)wt;
+    return;
+  }
   for (int idx = rx_tid<PS>(); idx < rows * CH; idx += RX_THREADS) {
     const int r = idx / CH, c = idx % CH;
     const int boff = byte_base + (r * bp_total + col0 + c * 8) * 2;
     const u32x4 val = *reinterpret_cast<const u32x4*>(lds + r * XS + ((c ^ Tile<MT>::swz(r)) << 3));
-    if (PS && wt)
-      rx_store16_sc1(Gr, boff, val);
-    else
-      *reinterpret_cast<RX_GLOBAL u32x4*>(rx_g(reinterpret_cast<char*>(Gr)) + boff) = val;
+    *reinterpret_cast<RX_GLOBAL u32x4*>(rx_g(reinterpret_cast<char*>(Gr)) + boff) = val;
   }
 }
 
+// Tile j of this wave: the k-steps held in the flat prefetch buffer first (fragment f = j * nks +
+// s, statically indexed), the rest loaded here in one burst.
 template <int MT, bool PS>
 __device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
                                               const u16* __restrict__ img, int boff, int K, int lg, int alg,
-                                              const bf16x8 (&pre)[RX_PK]) {
+                                              const bf16x8 (&pre)[RX_PJ][RX_PK], int j) {
   const int nks = K >> 5;
 #pragma unroll
-  for (int s = 0; s < RX_PK; ++s) {
-    if (s < nks) {
+  for (int f = 0; f < RX_PF; ++f) {
+    const int s = f - j * nks;
+    if (s >= 0 && s < nks) {
       const int k0 = s * 32 + 8 * alg;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(Arow + mt * 16 * RS + k0);
-        acc[mt] = rx_mfma16(a, pre[s], acc[mt]);
+        acc[mt] = rx_mfma16(a, pre[f >> 2][f & 3], acc[mt]);
       }
     }
   }
-  if (nks > RX_PK)
-    gemm_tile<MT, PS>(acc, Arow + RX_PK * 32, RS, img, boff + RX_PK * 32, K - RX_PK * 32, lg, alg);
+  const int done = max(0, min(nks, RX_PF - j * nks));
+  if (nks > done) gemm_tile<MT, PS>(acc, Arow + done * 32, RS, img, boff + done * 32, K - done * 32, lg, alg);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -438,7 +518,7 @@ __device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __res
 // act/BN) in R (row-major) and in XT_{l+1}; for the last layer computes loss, metrics and
 // writes dL/dy into R/GT as G_{L-1}.
 // ------------------------------------------------------------------------------------------
-template <int MT, bool TRAIN, bool PS, class D, class LY, class NX, class MWT = NoMw>
+template <int MT, bool TRAIN, bool PS, bool FULL = false, class D, class LY, class NX, class MWT = NoMw>
 __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX& nx, bool last, char* smem,
                                               const u16* __restrict__ img, const float* __restrict__ P,
                               float* __restrict__ Gr, const float* __restrict__ labels,
@@ -449,7 +529,9 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   // optional intra-layer timeline (wave 0, s_memtime): [40 + 5 l ..] export, GEMM, epilogue,
   // first barrier, publish + second barrier
   auto fst = [&](int k) {
+#ifdef RX_LAYER_STAMPS
     if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[40 + 5 * l + k] = __builtin_amdgcn_s_memtime();
+#endif
   };
   using T = Tile<MT>;
   const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
@@ -459,14 +541,6 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   u16* GT = reinterpret_cast<u16*>(smem + d.gt_lds_off);
   float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
   const int ntiles = ly.out_n >> 4;
-  if (TRAIN && d.wgrad_mode == 1) {  // X^T_l (published by the previous layer / the input load)
-    if constexpr (MWT::on)
-      export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
-                          ps_wt, mw->G * T::BP, mw->wg * T::BP);
-    else
-      export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
-                          ps_wt);
-  }
   fst(0);
 
   f32x4 acc[T::NTW * MT];
@@ -478,17 +552,24 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     const int n = wave + j * RX_NW;
     if (n < ntiles) {
       const int boff = ly.w_img + (n * 16 + lr) * ly.in_k;
-      if (j < RX_PJ)
-        gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg, lg ^ rx_rsw(lr), wpre[j < RX_PJ ? j : 0]);
-      else
-        gemm_tile<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg, lg ^ rx_rsw(lr));
+      gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg, lg ^ rx_rsw(lr), wpre, j);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
   fst(1);
-  // the next layer's weight head travels while this layer's epilogue runs
+  // the next layer's weights travel while this layer's epilogue runs -- issued before this
+  // layer's stores (the X^T export, the saved BN inputs), so the next GEMM's wait for them does
+  // not also wait for those stores
   if (!last) fwd_prefetch<PS>(nx, img, wpre);
+  if (TRAIN && d.wgrad_mode == 1) {  // X^T_l (published by the previous layer / the input load)
+    if constexpr (MWT::on)
+      export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
+                          ps_wt, mw->G * T::BP, mw->wg * T::BP);
+    else
+      export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
+                          ps_wt);
+  }
 
   // ---- epilogue in registers, in place on acc: bias, act, BN, loss ----
   // Phase A of a tile: bias, act, and the BatchNorm statistics of this workgroup's rows (its BN
@@ -496,42 +577,35 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   // normalisation, padding, loss. One workgroup runs B right after A per tile; the
   // multi-workgroup step publishes every tile's partials, meets the other workgroups and
   // combines the batch statistics in between.
-  const int n_batch = MWT::on ? mw->n_total : nvalid;   // rows the batch statistics / loss cover
+  const int n_batch = MWT::on ? mw->n_total : (FULL ? T::BP : nvalid);   // rows the statistics / loss cover
+  // (a multi-workgroup step's trailing workgroups may hold no rows of a short last batch)
+  const float inv_nv = FULL ? 1.f / (float)T::BP : (nvalid > 0 ? 1.f / (float)nvalid : 0.f);
+  const float inv_nb = 1.f / (float)n_batch;
+  // every column of the tile grid is a real one when the layer's width is a multiple of 16
+  const bool cols_full = ly.out == ly.out_n;
   float bn_mean[T::NTW], bn_var[T::NTW];
   auto epi_a = [&](int j) {
     const int n = wave + j * RX_NW;
     if (n >= ntiles) return;
     const int c = n * 16 + lr;
-    const bool colok = c < ly.out;
+    const bool colok = cols_full || c < ly.out;
     const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off) + ly.pr_off;
     const float bias = pr[c];
+    const f32x4 b4 = f32x4{bias, bias, bias, bias};
     const bool act_first = ly.bn != 2;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt) {
+      f32x4 z = acc[j * MT + mt] + b4;
+      if (act_first && ly.act == 1) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = acc[j * MT + mt][r] + bias;
-        acc[j * MT + mt][r] = act_first ? act_fwd(ly.act, z) : z;
+        for (int r = 0; r < 4; ++r) z[r] = fmaxf(z[r], 0.f);
       }
+      acc[j * MT + mt] = z;
+    }
     if (TRAIN && ly.bn != 0) {
-      float s = 0.f;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          s += (mt * 16 + lg * 4 + r < nvalid) ? acc[j * MT + mt][r] : 0.f;
-      s = rx_colsum16(s);
-      // (a multi-workgroup step's trailing workgroups may hold no rows of a short last batch)
-      const float mean = nvalid > 0 ? s / (float)nvalid : 0.f;
-      float v = 0.f;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float dv = acc[j * MT + mt][r] - mean;
-          v = (mt * 16 + lg * 4 + r < nvalid) ? fmaf(dv, dv, v) : v;
-        }
-      v = rx_colsum16(v);
+      const float s = rx_colsum16(rx_lane_sum<MT, FULL>(&acc[j * MT], lg, nvalid));
+      const float mean = s * inv_nv;
+      const float v = rx_colsum16(rx_lane_sqdev<MT, FULL>(&acc[j * MT], mean, lg, nvalid));
       if constexpr (MWT::on) {
         // this workgroup's (sum, centred second moment) of column c
         if (colok && lg == 0) {
@@ -541,7 +615,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         }
       } else {
         bn_mean[j] = mean;
-        bn_var[j] = v / (float)nvalid;
+        bn_var[j] = v * inv_nv;
       }
       // save the BN input for the backward pass (fragment-major, see frag_off)
 #pragma unroll
@@ -553,7 +627,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     const int n = wave + j * RX_NW;
     if (n >= ntiles) return;
     const int c = n * 16 + lr;
-    const bool colok = c < ly.out;
+    const bool colok = cols_full || c < ly.out;
     const float* pr = reinterpret_cast<const float*>(smem + d.pr_lds_off) + ly.pr_off;
     if (ly.bn != 0) {
       float mean, invstd;
@@ -576,13 +650,18 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       const float gam = pr[ly.out_n + c];
       const float bet = pr[2 * ly.out_n + c];
       const bool act_after = ly.bn == 2;
+      // gamma * (x - mean) * invstd + beta as one fma per element: x * k1 + k0
+      const float k1 = invstd * gam, k0 = fmaf(-mean, k1, bet);
+      const f32x4 k14 = f32x4{k1, k1, k1, k1}, k04 = f32x4{k0, k0, k0, k0};
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt) {
+        f32x4 t = __builtin_elementwise_fma(acc[j * MT + mt], k14, k04);
+        if (act_after && ly.act == 1) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float t = fmaf((acc[j * MT + mt][r] - mean) * invstd, gam, bet);
-          acc[j * MT + mt][r] = act_after ? act_fwd(ly.act, t) : t;
+          for (int r = 0; r < 4; ++r) t[r] = fmaxf(t[r], 0.f);
         }
+        acc[j * MT + mt] = t;
+      }
     } else if (TRAIN && !last) {
       // ReLU mask source for the backward pass
 #pragma unroll
@@ -593,15 +672,15 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       }
     }
     // padded rows / columns carry exact zeros through every GEMM
+    if (!(FULL && cols_full)) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (!colok || mt * 16 + lg * 4 + r >= nvalid) acc[j * MT + mt][r] = 0.f;
+      for (int mt = 0; mt < MT; ++mt)
+        acc[j * MT + mt] = colok ? rx_rowmask<FULL>(acc[j * MT + mt], mt, lg, nvalid) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     if (last) {
       // loss, metrics and dL/dy (mean reduction over n_batch * out_dim elements)
       float lsum = 0.f, asum = 0.f, ssum = 0.f, gsum = 0.f, csum = 0.f;
-      const float inv_n = 1.f / (float)(n_batch * ly.out);
+      const float inv_n = inv_nb * (1.f / (float)ly.out);
       const int lcode = d.loss;
       const float beta = d.beta;
       // labels of all padded rows, loaded back to back (padded rows read row 0)
@@ -682,37 +761,49 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
           if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum;
         }
       } else {
+        // branch-free: every element computes its terms, invalid ones (padded rows / columns)
+        // are selected out; per-lane sums in packed-fp32 vectors
+        const float hb = 0.5f * beta, inv_beta = 1.f / beta, h_inv_beta = 0.5f * inv_beta;
+        f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f}, a4 = l4, s4 = l4, c4 = l4, g4s = l4;
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
+        for (int mt = 0; mt < MT; ++mt) {
+          const f32x4 x4 = acc[j * MT + mt];
+          f32x4 gv;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = mt * 16 + lg * 4 + r;
-            float g = 0.f;
-            if (colok && row < nvalid) {
-              const float t = tl[mt * 4 + r];
-              const float e = acc[j * MT + mt][r] - t;
-              const float ae = fabsf(e);
-              asum += ae;
-              ssum = fmaf(e, e, ssum);
-              if (d.acc_mode == 1)  // torch: (pred > thr).long() == target.long()
-                csum += ((acc[j * MT + mt][r] > d.acc_thr ? 1 : 0) == (int)t) ? 1.f : 0.f;
-              const float sgn = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+            const bool ok = colok && (FULL || row < nvalid);
+            const float t = tl[mt * 4 + r];
+            const float x = x4[r];
+            const float e = x - t;
+            const float ae = fabsf(e);
+            float li, gi;
+            if (lcode == 3) {
+              // BCE with logits, softplus form (stable for either sign):
+              //   l = max(x, 0) - x t + log1p(exp(-|x|)),  dl/dx = sigmoid(x) - t
+              li = fmaxf(x, 0.f) - x * t + log1pf(__expf(-fabsf(x)));
+              gi = 1.f / (1.f + __expf(-x)) - t;
+            } else {
               const bool quad = ae < beta;
-              if (lcode == 3) {
-                // BCE with logits, softplus form (stable for either sign):
-                //   l = max(x, 0) - x t + log1p(exp(-|x|)),  dl/dx = sigmoid(x) - t
-                const float x = acc[j * MT + mt][r];
-                lsum += fmaxf(x, 0.f) - x * t + log1pf(__expf(-fabsf(x)));
-                g = 1.f / (1.f + __expf(-x)) - t;
-              } else {
-                lsum += quad ? 0.5f * e * e / beta : ae - 0.5f * beta;  // smooth-L1 term
-                g = lcode == 0 ? 2.f * e : (lcode == 1 && quad ? e / beta : sgn);
-              }
-              g *= inv_n;
+              li = quad ? e * e * h_inv_beta : ae - hb;   // smooth-L1 term
+              const float sgn = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+              gi = lcode == 0 ? 2.f * e : (lcode == 1 && quad ? e * inv_beta : sgn);
             }
-            acc[j * MT + mt][r] = g;  // acc now holds G_{L-1}
-            gsum += g;
+            l4[r] += ok ? li : 0.f;
+            a4[r] += ok ? ae : 0.f;
+            s4[r] = ok ? fmaf(e, e, s4[r]) : s4[r];
+            if (d.acc_mode == 1)  // torch: (pred > thr).long() == target.long()
+              c4[r] += (ok && (x > d.acc_thr ? 1 : 0) == (int)t) ? 1.f : 0.f;
+            gv[r] = ok ? gi * inv_n : 0.f;
           }
+          acc[j * MT + mt] = gv;  // acc now holds G_{L-1}
+          g4s += gv;
+        }
+        lsum = (l4[0] + l4[1]) + (l4[2] + l4[3]);
+        asum = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        ssum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        csum = (c4[0] + c4[1]) + (c4[2] + c4[3]);
+        gsum = (g4s[0] + g4s[1]) + (g4s[2] + g4s[3]);
         lsum = rx_wavesum(lsum);
         asum = rx_wavesum(asum);
         ssum = rx_wavesum(ssum);
@@ -747,7 +838,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     if constexpr (MWT::on) {
 #pragma unroll
       for (int j = 0; j < T::NTW; ++j) epi_a(j);
-      mw_barrier(*mw, ++mw->k);
+      mw->ok = mw_barrier(*mw, ++mw->k) && mw->ok;
       // batch statistics from every workgroup's (sum, centred second moment), workgroup order
 #pragma unroll
       for (int j = 0; j < T::NTW; ++j) {
@@ -786,22 +877,16 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     const int n = wave + j * RX_NW;
     if (n < ntiles) {
       const int c = n * 16 + lr;
-      // rows mt * 16 + lg * 4 + q all take rx_rsw(lg * 4): one swizzled column per tile, and the
-      // row offsets stay immediates of the stores
-      u16* Rc = R + lg * 4 * RS + ((((c >> 3) ^ rx_rsw(lg * 4)) << 3) | (c & 7));
       const int tsw = T::swz(c);
+      uint2 pk[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        uint2 pk;
-        pk.x = rx_f2bf2(acc[j * MT + mt][0], acc[j * MT + mt][1]);
-        pk.y = rx_f2bf2(acc[j * MT + mt][2], acc[j * MT + mt][3]);
-        Rc[(mt * 16 + 0) * RS] = (u16)pk.x;
-        Rc[(mt * 16 + 1) * RS] = (u16)(pk.x >> 16);
-        Rc[(mt * 16 + 2) * RS] = (u16)pk.y;
-        Rc[(mt * 16 + 3) * RS] = (u16)(pk.y >> 16);
+        pk[mt].x = rx_f2bf2(acc[j * MT + mt][0], acc[j * MT + mt][1]);
+        pk[mt].y = rx_f2bf2(acc[j * MT + mt][2], acc[j * MT + mt][3]);
         if (TRAIN || !last)
-          *reinterpret_cast<uint2*>(dstT + c * XS + ((((mt * 16 + lg * 4) >> 3) ^ tsw) << 3) + ((lg & 1) << 2)) = pk;
+          *reinterpret_cast<uint2*>(dstT + c * XS + ((((mt * 16 + lg * 4) >> 3) ^ tsw) << 3) + ((lg & 1) << 2)) = pk[mt];
       }
+      rx_publish_rows<MT>(R, RS, c, lane, pk);
     }
   }
   // zero the K padding columns [out_n, out_k) of R so the next GEMM's K tail is exact
@@ -822,7 +907,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
 // PS (persistent epoch kernel): once this layer's dgrad has read its last weight byte and its
 // G^T export has drained, lane 0 publishes flag `sync[32 l] = step + 1` -- the optimizer
 // workgroups of layer l may then compute dW_l and rewrite W_l / Wt_l while the backward goes on.
-template <int MT, bool PS, class D, class LY, class PV, class MWT = NoMw>
+template <int MT, bool PS, bool FULL = false, class D, class LY, class PV, class MWT = NoMw>
 __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const PV& pv, int l, char* smem,
                                                const u16* __restrict__ img, const float* __restrict__ P,
                                                float* __restrict__ Gr, int nvalid, const float* __restrict__ scratch,
@@ -847,11 +932,11 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
   bf16x8 wpre[RX_PJ][RX_PK];
   float svp[RX_PJ][MT * 4];
   if (l != 0) {
+    gemm_prefetch_flat<PS>(wpre, img, ly.wt_img, ntiles_d, ly.out_k, wave, lr, lg);
 #pragma unroll
     for (int j = 0; j < RX_PJ; ++j) {
       if (j * RX_NW < ntiles_d) {
         const int n = min(wave + j * RX_NW, ntiles_d - 1);
-        gemm_prefetch<PS>(wpre[j], img, ly.wt_img + (n * 16 + lr) * ly.out_k, ly.out_k, lg);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const f32x4 t = *reinterpret_cast<const RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(pv.r_off, n, mt, lane));
@@ -951,7 +1036,9 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       }
     }
   }
+#ifdef RX_LAYER_STAMPS
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[20 + 4 * l] = __builtin_amdgcn_s_memtime();
+#endif
   if (l == 0) return;
 
   // ---- dgrad: dX[b][i] = sum_o G[b][o] W[o][i]  (A = R, B = Wt, K = out_k) ----
@@ -966,33 +1053,36 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     const int n = wave + j * RX_NW;
     if (n < ntiles) {
       const int boff = ly.wt_img + (n * 16 + lr) * ly.out_k;
-      if (j < RX_PJ)
-        gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg, lg ^ rx_rsw(lr), wpre[j < RX_PJ ? j : 0]);
-      else
-        gemm_tile<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg, lg ^ rx_rsw(lr));
+      gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg, lg ^ rx_rsw(lr), wpre, j);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
   }
+#ifdef RX_LAYER_STAMPS
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[21 + 4 * l] = __builtin_amdgcn_s_memtime();
+#endif
   if constexpr (PS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's G^T export drained
   __syncthreads();  // all reads of G_l (R, GT) are done; they are overwritten with G_{l-1}
   if constexpr (PS) {
     if (rx_tid<PS>() == 0) __hip_atomic_store(rx_g(sync) + 32 * l, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#ifdef RX_LAYER_STAMPS
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[22 + 4 * l] = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---- post-op backward of layer l-1 (BN / act), producing G_{l-1} ----
   // mode 0: one workgroup, batch sums from its own rows. Multi-workgroup with BN: mode 1
   // publishes this workgroup's partial sums of dL/dy and dL/dy * x_hat, a grid barrier, then
   // mode 2 recomputes the (cheap) per-element terms and finishes with the batch sums.
-  const int n_batch = MWT::on ? mw->n_total : nvalid;
+  const int n_batch = MWT::on ? mw->n_total : (FULL ? T::BP : nvalid);
+  const float inv_n = 1.f / (float)n_batch;
+  const bool cols_full = pv.out == pv.out_n;
   float bsg[T::NTW], bsgx[T::NTW];
   auto post = [&](int j, int mode) {
     const int n = wave + j * RX_NW;
     if (n >= ntiles) return;
     const int c = n * 16 + lr;
-    const bool colok = c < pv.out;
+    const bool colok = cols_full || c < pv.out;
     // The forward saved this layer's BN input / activation (fp32) for every padded row and
     // column: issue all loads back to back, unconditionally (a load under a per-element
     // branch is waited for on its own -> one dependent L2 round trip per element).
@@ -1009,9 +1099,10 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       }
     }
 #pragma unroll
-    for (int q = 0; q < MT * 4; ++q) {
-      const int row = (q >> 2) * 16 + lg * 4 + (q & 3);
-      g[q] = (row < nvalid && colok) ? acc[j * MT + (q >> 2)][q & 3] : 0.f;
+    for (int mt = 0; mt < MT; ++mt) {
+      const f32x4 gm = colok ? rx_rowmask<FULL>(acc[j * MT + mt], mt, lg, nvalid) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g[mt * 4 + r] = gm[r];
     }
     if (pv.bn == 0) {
       if (pv.act == 1) {
@@ -1026,26 +1117,33 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       const float bet = ppr[2 * pv.out_n + c];
       const bool relu_after = pv.bn == 2 && pv.act == 1;
       const bool relu_before = pv.bn == 1 && pv.act == 1;
-      float xh[MT * 4];
+      // x_hat = (x - mean) * invstd as one fma: x * invstd + (-mean * invstd)
+      const float xb = -mean * invstd;
+      f32x4 xh4[MT], g4[MT];
 #pragma unroll
-      for (int q = 0; q < MT * 4; ++q) {
-        xh[q] = (sv[q] - mean) * invstd;
-        g[q] = (relu_after && !(fmaf(xh[q], gam, bet) > 0.f)) ? 0.f : g[q];
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x4 sv4 = f32x4{sv[mt * 4], sv[mt * 4 + 1], sv[mt * 4 + 2], sv[mt * 4 + 3]};
+        xh4[mt] = __builtin_elementwise_fma(sv4, f32x4{invstd, invstd, invstd, invstd}, f32x4{xb, xb, xb, xb});
+        g4[mt] = f32x4{g[mt * 4], g[mt * 4 + 1], g[mt * 4 + 2], g[mt * 4 + 3]};
+        if (relu_after) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g4[mt][r] = fmaf(xh4[mt][r], gam, bet) > 0.f ? g4[mt][r] : 0.f;
+        }
       }
       float sg, sgx;
       if (mode == 2) {
         sg = bsg[j];
         sgx = bsgx[j];
       } else {
-        sg = 0.f;
-        sgx = 0.f;
+        // batch sums of dL/dy and dL/dy * x_hat: packed-fp32 trees, then across the lane groups
+        f32x4 a4 = g4[0], b4 = g4[0] * xh4[0];
 #pragma unroll
-        for (int q = 0; q < MT * 4; ++q) {
-          sg += g[q];
-          sgx = fmaf(g[q], xh[q], sgx);
+        for (int mt = 1; mt < MT; ++mt) {
+          a4 += g4[mt];
+          b4 = __builtin_elementwise_fma(g4[mt], xh4[mt], b4);
         }
-        sg = rx_colsum16(sg);
-        sgx = rx_colsum16(sgx);
+        sg = rx_colsum16((a4[0] + a4[1]) + (a4[2] + a4[3]));
+        sgx = rx_colsum16((b4[0] + b4[1]) + (b4[2] + b4[3]));
       }
       if (mode == 1) {
         if (colok && lg == 0) {
@@ -1058,45 +1156,47 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
         return;
       }
       bool owner = true;   // gamma / beta gradients are batch sums: one workgroup writes them
-      if constexpr (MWT::on) owner = mw->wg == 0;
+      if constexpr (MWT::on) owner = mw->wg == 0 && mw->ok;
       if (colok && lg == 0 && owner) {
         if (pv.g_off >= 0) Gr[pv.g_off + c] = sgx;
         if (pv.be_off >= 0) Gr[pv.be_off + c] = sg;
       }
-      const float inv_n = 1.f / (float)n_batch;
+      // dz = gamma * invstd * (g - sg / n - x_hat * sgx / n) = k1 * g + (c1 - x_hat * c2)
       const float k1 = gam * invstd;
+      const float c1 = -k1 * (sg * inv_n), c2 = k1 * (sgx * inv_n);
+      const f32x4 k14 = f32x4{k1, k1, k1, k1}, c14 = f32x4{c1, c1, c1, c1}, c24 = f32x4{-c2, -c2, -c2, -c2};
 #pragma unroll
-      for (int q = 0; q < MT * 4; ++q) {
-        const int row = (q >> 2) * 16 + lg * 4 + (q & 3);
-        float dz = k1 * (fmaf(-sg, inv_n, g[q]) - xh[q] * (sgx * inv_n));
-        dz = (relu_before && !(sv[q] > 0.f)) ? 0.f : dz;
-        g[q] = (row < nvalid && colok) ? dz : 0.f;
+      for (int mt = 0; mt < MT; ++mt) {
+        f32x4 dz = __builtin_elementwise_fma(g4[mt], k14, __builtin_elementwise_fma(xh4[mt], c24, c14));
+        if (relu_before) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dz[r] = sv[mt * 4 + r] > 0.f ? dz[r] : 0.f;
+        }
+        dz = colok ? rx_rowmask<FULL>(dz, mt, lg, nvalid) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g[mt * 4 + r] = dz[r];
       }
     }
     // bias grad of layer l-1 (multi-workgroup: this workgroup's partial, reduced at step end)
-    float bs = 0.f;
+    f32x4 bs4 = f32x4{g[0], g[1], g[2], g[3]};
 #pragma unroll
-    for (int q = 0; q < MT * 4; ++q) bs += g[q];
-    bs = rx_colsum16(bs);
+    for (int mt = 1; mt < MT; ++mt) bs4 += f32x4{g[mt * 4], g[mt * 4 + 1], g[mt * 4 + 2], g[mt * 4 + 3]};
+    const float bs = rx_colsum16((bs4[0] + bs4[1]) + (bs4[2] + bs4[3]));
     if (colok && lg == 0 && pv.b_off >= 0) {
       if constexpr (MWT::on)
         rx_st_sc1f(mw_bias(mw->part, mw->stride, pv, mw->wg) + c, bs);
       else
         Gr[pv.b_off + c] = bs;
     }
-    // publish G_{l-1} (same hoisted swizzle as the forward publish)
-    u16* Rc = R + lg * 4 * RS + ((((c >> 3) ^ rx_rsw(lg * 4)) << 3) | (c & 7));
+    // publish G_{l-1}: transposed into GT, row-major into R (quad-transposed 8-B stores)
+    uint2 pk[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      uint2 pk;
-      pk.x = rx_f2bf2(g[mt * 4 + 0], g[mt * 4 + 1]);
-      pk.y = rx_f2bf2(g[mt * 4 + 2], g[mt * 4 + 3]);
-      Rc[(mt * 16 + 0) * RS] = (u16)pk.x;
-      Rc[(mt * 16 + 1) * RS] = (u16)(pk.x >> 16);
-      Rc[(mt * 16 + 2) * RS] = (u16)pk.y;
-      Rc[(mt * 16 + 3) * RS] = (u16)(pk.y >> 16);
-      *reinterpret_cast<uint2*>(GT + T::tix(c, mt * 16 + lg * 4)) = pk;
+      pk[mt].x = rx_f2bf2(g[mt * 4 + 0], g[mt * 4 + 1]);
+      pk[mt].y = rx_f2bf2(g[mt * 4 + 2], g[mt * 4 + 3]);
+      *reinterpret_cast<uint2*>(GT + T::tix(c, mt * 16 + lg * 4)) = pk[mt];
     }
+    rx_publish_rows<MT>(R, RS, c, lane, pk);
   };
   bool split = false;
   if constexpr (MWT::on) split = pv.bn != 0;
@@ -1104,7 +1204,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     if constexpr (MWT::on) {
 #pragma unroll
       for (int j = 0; j < T::NTW; ++j) post(j, 1);
-      mw_barrier(*mw, ++mw->k);
+      mw->ok = mw_barrier(*mw, ++mw->k) && mw->ok;
 #pragma unroll
       for (int j = 0; j < T::NTW; ++j) {
         const int n = wave + j * RX_NW;
@@ -1123,7 +1223,9 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 #pragma unroll
     for (int j = 0; j < T::NTW; ++j) post(j, 0);
   }
+#ifdef RX_LAYER_STAMPS
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[23 + 4 * l] = __builtin_amdgcn_s_memtime();
+#endif
   // zero the K tail [out_n, out_k) of G_{l-1} in R for the next dgrad
   const int kpad = pv.out_k - pv.out_n;
   if (kpad > 0) {
@@ -1346,16 +1448,23 @@ __device__ __forceinline__ void mlp_train_step_body(
   float labp[MT * 4];
   prefetch_labels<MT, false>(d, labels, rowidx, labp);
   RX_STAMP();
-  C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
-    layer_forward<MT, true, false>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre,
-                                   true, l, stamps, labp);
-    RX_STAMP();
-  });
-  store_running_stats<C>(d, smem, rstats);
-  C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
-    layer_backward<MT, false>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, stamps);
-    RX_STAMP();
-  });
+  auto body = [&](auto full) {
+    constexpr bool F = decltype(full)::value;
+    C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
+      layer_forward<MT, true, false, F>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics,
+                                        wpre, true, l, stamps, labp);
+      RX_STAMP();
+    });
+    store_running_stats<C>(d, smem, rstats);
+    C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
+      layer_backward<MT, false, F>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, stamps);
+      RX_STAMP();
+    });
+  };
+  if (nvalid == Tile<MT>::BP)
+    body(rx_bool<true>{});
+  else
+    body(rx_bool<false>{});
   if (d.front_n > 0) front_backward<MT>(d, dp, C::first(d), smem, img, Gr, feats, rowidx, nvalid);
 #undef RX_STAMP
 }
@@ -1374,6 +1483,7 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
   constexpr int BP = Tile<MT>::BP;
   mw.wg = (int)blockIdx.x;
   mw.k = 0;
+  mw.ok = 1;
   const int nvalid = mw_rows(mw.n_total, mw.wg, BP);
   const int r0 = row0 + mw.wg * BP;
   float* sc = scratch + (size_t)mw.wg * (size_t)scratch_stride;
@@ -1393,15 +1503,15 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
                                    true, l, nullptr, labp, &mw);
   });
   // every workgroup computed the same batch statistics: one stores the running averages
-  if (mw.wg == 0) store_running_stats<C>(d, smem, rstats);
+  if (mw.wg == 0 && mw.ok) store_running_stats<C>(d, smem, rstats);
   C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
     layer_backward<MT, false>(d, ly, pv, l, smem, img, P, Gr, nvalid, sc, nullptr, nullptr, 0, true, &mw);
   });
   // bias gradients: the workgroups' partial column sums, added in workgroup order, each
   // (layer, column) by one thread of the grid
-  mw_barrier(mw, ++mw.k);
+  mw.ok = mw_barrier(mw, ++mw.k) && mw.ok;
   C::each_layer(d, [&](const auto& ly, int) {
-    if (ly.b_off >= 0) {
+    if (ly.b_off >= 0 && mw.ok) {   // (after a timed-out barrier the partials are incomplete)
       for (int c = (int)blockIdx.x * RX_THREADS + rx_tid<false>(); c < ly.out; c += mw.G * RX_THREADS) {
         // G loads in flight 8 at a time, added in workgroup order
         const float* p0 = mw_bias(mw.part, mw.stride, ly, 0) + c;

@@ -238,19 +238,31 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       if (flag_lds[0]) return;
     }
     stamp(s, 2);
+#ifdef RX_LAYER_STAMPS
     unsigned long long* lst =
         (stamps != nullptr && s == sstep) ? stamps + RX_PS_STEP_STAMPS + nsteps + 1 : nullptr;
+#else
+    unsigned long long* lst = nullptr;
+#endif
     bf16x8 wpre[RX_PJ][RX_PK];
     fwd_prefetch<true>(C::first(d), img, wpre);
-    C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
-      layer_forward<MT, true, true>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics, wpre,
-                                    ps_wt, l, lst, labp);
-    });
-    stamp(s, 3);
-    C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
-      layer_backward<MT, true>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, lst, sync, s, ps_wt);
-      stamp(s, 8 + l);
-    });
+    // every step but a ragged last one fills the tile: the full-batch body has no row masks
+    auto body = [&](auto full) {
+      constexpr bool F = decltype(full)::value;
+      C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
+        layer_forward<MT, true, true, F>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics,
+                                         wpre, ps_wt, l, lst, labp);
+      });
+      stamp(s, 3);
+      C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
+        layer_backward<MT, true, F>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, lst, sync, s, ps_wt);
+        stamp(s, 8 + l);
+      });
+    };
+    if (nvalid == Tile<MT>::BP)
+      body(rx_bool<true>{});
+    else
+      body(rx_bool<false>{});
     // layer 0's backward ends with its G^T export (no dgrad)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -10,6 +10,12 @@ typedef unsigned short u16;
 
 #define RX_WAVE 64
 
+// compile-time bool carried through a generic lambda's argument
+template <bool B>
+struct rx_bool {
+  static constexpr bool value = B;
+};
+
 // Pointers read out of a descriptor in memory are "generic" to the compiler, so every access
 // through them becomes a flat_* instruction -- and a flat load is waited for with vmcnt(0) AND
 // lgkmcnt(0), serialising everything around it. Casting them to the global address space
@@ -61,11 +67,48 @@ __device__ __forceinline__ float rx_colsum16(float v) {
   return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 
-__device__ __forceinline__ float rx_wavesum(float v) {
-  v = rx_colsum16(v);
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+// DPP lane moves inside a row of 16 lanes (one VALU op, no LDS round trip):
+// quad_perm [1,0,3,2] (lane ^ 1), quad_perm [2,3,0,1] (lane ^ 2), row_half_mirror, row_mirror
+#define RX_DPP_XOR1 0xB1
+#define RX_DPP_XOR2 0x4E
+#define RX_DPP_HALF_MIRROR 0x141
+#define RX_DPP_MIRROR 0x140
+template <int CTRL>
+__device__ __forceinline__ float rx_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t rx_dppu(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+
+// sum over the 16 lanes of a row (lane & ~15): four DPP steps; every lane of the row gets the
+// bit-identical total (each step adds a value and its mirror image, and a + b == b + a)
+__device__ __forceinline__ float rx_rowsum16(float v) {
+  v += rx_dpp<RX_DPP_XOR1>(v);
+  v += rx_dpp<RX_DPP_XOR2>(v);
+  v += rx_dpp<RX_DPP_HALF_MIRROR>(v);
+  v += rx_dpp<RX_DPP_MIRROR>(v);
   return v;
+}
+
+// whole-wave sum: rows by DPP, then the four row sums by the permlane swaps (no LDS pipeline)
+__device__ __forceinline__ float rx_wavesum(float v) { return rx_colsum16(rx_rowsum16(v)); }
+
+// Transpose of a bf16 4x4 block held by the 4 lanes of a quad: lane q holds column q of rows
+// 0..3 as {p.x = (row 0, row 1), p.y = (row 2, row 3)} (an MFMA accumulator's 4 rows, packed);
+// afterwards lane q holds row q of columns 0..3 as {(col 0, col 1), (col 2, col 3)}, i.e. 8
+// contiguous bytes of a row-major image -- one ds_write_b64 instead of four ds_write_b16.
+// Two exchange rounds (lane ^ 2, then lane ^ 1): 3 DPP moves, 3 selects, 2 byte permutes.
+__device__ __forceinline__ uint2 rx_quad_transpose(uint2 p, int q) {
+  const bool hi2 = (q & 2) != 0;
+  const uint32_t y = rx_dppu<RX_DPP_XOR2>(hi2 ? p.x : p.y);
+  const uint32_t a = hi2 ? y : p.x;   // rows (q & 2) .. +1 of column q & 1
+  const uint32_t b = hi2 ? p.y : y;   //                  ... of column (q & 1) + 2
+  const uint32_t pa = rx_dppu<RX_DPP_XOR1>(a), pb = rx_dppu<RX_DPP_XOR1>(b);
+  // even lanes keep the low halves (their row is even): (own, partner); odd: (partner, own)
+  const uint32_t sel = (q & 1) ? 0x03020706u : 0x05040100u;
+  return make_uint2(__builtin_amdgcn_perm(pa, a, sel), __builtin_amdgcn_perm(pb, b, sel));
 }
 
 __device__ __forceinline__ f32x4 rx_mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {

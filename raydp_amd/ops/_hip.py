@@ -64,7 +64,8 @@ class MwArgs(ctypes.Structure):
     """Multi-workgroup step of one fused model (csrc/hip/fused_mlp.hip MwArgs)."""
     _fields_ = [("part", ctypes.c_void_p), ("ctl", ctypes.c_void_p), ("G", ctypes.c_int),
                 ("resident_ok", ctypes.c_int), ("stride", ctypes.c_int), ("pad_", ctypes.c_int),
-                ("scratch_stride", ctypes.c_longlong), ("ticks", ctypes.c_ulonglong)]
+                ("scratch_stride", ctypes.c_longlong), ("ticks", ctypes.c_ulonglong),
+                ("wpart", ctypes.c_void_p), ("wctr", ctypes.c_void_p)]
 
 
 class OptSeg(ctypes.Structure):

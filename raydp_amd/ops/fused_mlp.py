@@ -388,6 +388,13 @@ class FusedMLPTrainer:
         o.nesterov, o.maximize = int(cfg.get("nesterov", False)), int(cfg.get("maximize", False))
         o.act_off, o.act_floats, o.bp, o.wgrad_mode = act_off, act_floats, bp_all, wmode
         self.opt = o
+        if G > 1 and wmode == 1:
+            # split-K weight-gradient partials + per-tile arrival counters of the multi-workgroup
+            # optimizer (csrc/hip/fused_mlp.hip mw_wgrad_opt_kernel, RX_WSPLIT_K rows per split)
+            splits = -(-int(bp_all) // 256)
+            tiles = sum(((sg.out + 31) // 32) * ((sg.in_ + 31) // 32) for sg in o.seg[:o.nseg] if sg.kind == 1)
+            self._arena_zero += [("mw_wpart", max(1, tiles * splits * 1024), torch.float32),
+                                 ("mw_wctr", max(1, tiles), torch.int32)]
         self.lds_bytes = lds
         # descriptors live in device memory: the kernels index them with runtime layer ids
         self._materialize(bytes(d), bytes(o), rs_init)
@@ -405,6 +412,8 @@ class FusedMLPTrainer:
             a.part, a.ctl, a.G = self.mw_part.data_ptr(), self.mw_ctl.data_ptr(), G
             a.stride = self._mw_stride
             a.scratch_stride = self._scratch_stride
+            if self.mw_wpart is not None:
+                a.wpart, a.wctr = self.mw_wpart.data_ptr(), self.mw_wctr.data_ptr()
             from raydp_amd.utils.config import get as conf_get
             khz = 100000
             a.ticks = int(float(conf_get("spark.ray.mi355x.mlp_persistent.timeout_s")) * khz * 1000)
@@ -453,6 +462,8 @@ class FusedMLPTrainer:
         self.grads, self.m, self.v = view("grads"), view("m"), view("v")
         self.scratch, self.metrics, self.img = view("scratch"), view("metrics"), view("img")
         self.mw_part, self.mw_ctl = view("mw_part"), view("mw_ctl")
+        self.mw_wpart = view("mw_wpart") if "mw_wpart" in where else None
+        self.mw_wctr = view("mw_wctr") if "mw_wctr" in where else None
         self._desc_buf = arena[desc_off:desc_off + len(desc_bytes)]
         base = self.img.data_ptr()
         o = self.opt
@@ -571,6 +582,15 @@ class FusedMLPTrainer:
         pp = ctypes.c_void_p
         perm_p = pp(perm.data_ptr()) if perm is not None else pp(0)
         gscale = 1.0 / world_size
+        mw_snap = None
+        if self.G > 1:
+            # device snapshot of what the epoch mutates (one multi-tensor copy into kept buffers):
+            # a grid-barrier timeout rolls the epoch back (see below)
+            live = self._mw_live()
+            mw_snap = getattr(self, "_mw_snap", None)
+            if mw_snap is None:
+                mw_snap = self._mw_snap = [torch.empty_like(t) for t in live]
+            torch._foreach_copy_(mw_snap, live)
         if xg is None and comm is None and allreduce is None and world_size == 1 and \
                 self._run_persistent(feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream):
             pass
@@ -615,8 +635,18 @@ class FusedMLPTrainer:
             # the multi-workgroup barriers' timeout word comes back with the metrics (one sync)
             back = self._readback([self.mw_ctl[2:3], self.metrics])
             if int(back[0][0]) != 0:
+                # from the timed-out step on, the steps stored no gradients and the optimizer
+                # updated nothing; roll the whole epoch back and clear the control words so the
+                # trainer is usable again
+                if mw_snap is not None:
+                    torch._foreach_copy_(self._mw_live(), mw_snap)
+                    self.step_count -= nsteps
+                self.mw_ctl.zero_()
+                if self.mw_wctr is not None:
+                    self.mw_wctr.zero_()
+                self.metrics.zero_()
                 raise RuntimeError("fused MLP multi-workgroup step: a grid barrier wait timed out "
-                                   "(a step workgroup was not resident)")
+                                   "(a step workgroup was not resident); the epoch was rolled back")
             pre = back[1].copy()
         out = self._read_metrics(pre)
         if xg is not None and out["xg_vote"] != 0.0:
@@ -624,6 +654,9 @@ class FusedMLPTrainer:
             raise CollectiveError("xGMI all-reduce: a peer did not arrive within the timeout "
                                   f"(vote {out['xg_vote']:g})")
         return out
+
+    def _mw_live(self):
+        return [self.params, self.m, self.v, self.rstats, self.img]
 
     def step_times_us(self) -> Optional[np.ndarray]:
         """Device time of every step of the last persistent epoch (microseconds; the 100 MHz

@@ -42,7 +42,11 @@ def _f(x: float) -> str:
 
 def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
     L = desc.L
-    out = ['#include "mlp_persist.h"', "", "namespace {", "", "struct JD {"]
+    out = []
+    if os.environ.get("RAYDP_MLP_LAYER_STAMPS") == "1":
+        # diagnostic build: the persistent epoch's middle step writes intra-layer s_memtime stamps
+        out.append("#define RX_LAYER_STAMPS 1")
+    out += ['#include "mlp_persist.h"', "", "namespace {", "", "struct JD {"]
     for k in _DESC_INT:
         out.append(f"  static constexpr int {k} = {int(getattr(desc, k))};")
     out.append(f"  static constexpr float beta = {_f(desc.beta)};")

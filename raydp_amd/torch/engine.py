@@ -398,13 +398,8 @@ class TorchLoopEngine:
         self.seed = _epoch_seed_base(config)
         self.epoch = 0
         self.graphed = None
-        self.dlrm_step = None
-        self.dlrm_status = self._dlrm_step_plan(config)
         from raydp_amd.torch import graphs
-        if self.dlrm_status == "enabled":
-            self.name = "dlrm_step_hip"
-            self.graph_status = "not needed (one persistent launch per step)"
-        elif graphs.graphs_requested():
+        if graphs.graphs_requested():
             why = graphs.supported(self)
             if why is None:
                 self.metrics.to(device)
@@ -450,65 +445,6 @@ class TorchLoopEngine:
                     m.fused_sgd_lr = lr_of[id(w)]
                     w._raydp_sparse_grad = False
                     self.fusions.append("embedding_sgd" if sharded or self.world == 1 else "embedding_sgd_xgmi_gather")
-
-    def _dlrm_step_plan(self, config) -> str:
-        """"enabled" when the whole training step of this run is the persistent DLRM launch
-        (raydp_amd.ops.dlrm_step: one GPU, replicated tables, plain SGD, BCE, no metrics, no
-        scheduler), else why not."""
-        if self.device.type != "cuda":
-            return "not on a GPU"
-        from raydp_amd.utils.config import get as conf_get
-        if not conf_get("spark.ray.mi355x.dlrm_step"):
-            return "disabled (spark.ray.mi355x.dlrm_step)"
-        if self.world != 1:
-            return "world_size > 1"
-        if self.scheduler is not None:
-            return "LR scheduler"
-        if self.metrics.names:
-            return "metrics requested"
-        from raydp_amd.ops.dlrm_step import supported
-        return supported(self.raw_model, self.optimizer, self.loss, self.batch) or "enabled"
-
-    def _train_epoch_dlrm(self):
-        """One epoch as ``ceil(n / batch)`` persistent step launches over the epoch permutation."""
-        d = self.train
-        mats = getattr(d, "mats", None)
-        if mats is None or "f" not in mats or "i" not in mats or d.labels is None:
-            raise RuntimeError("persistent DLRM step needs the float / int64 shard matrices")
-        if self.dlrm_step is None:
-            from raydp_amd.ops.dlrm_step import DlrmStep
-            lr = float(self.optimizer.param_groups[0]["lr"])
-            try:
-                self.dlrm_step = DlrmStep(self.raw_model, lr, self.batch, self.device)
-            except (RuntimeError, ValueError) as e:   # residency / shape limits: the torch loop
-                self.dlrm_status = f"unavailable: {e}"
-                self.name = "torch_loop"
-                return self._train_epoch_eager()
-            self.fusions.append("dlrm_persistent_step")
-        st = self.dlrm_step
-        self.model.train()
-        n, b = d.n, self.batch
-        if self.shuffle:
-            idx = random_permutation(n, self.seed + self.epoch, self.device).long()
-            self.epoch += 1
-        else:
-            idx = torch.arange(n, device=self.device)
-        nsteps = n // b
-        last = b
-        if n % b and not self.drop_last:
-            nsteps += 1
-            last = n % b
-        lab = d.labels.reshape(-1) if d.labels.dim() > 1 and d.labels.shape[1] == 1 else d.labels
-        st.bind_data(mats["f"], mats["i"], lab)
-        st.loss_acc.zero_()
-        if nsteps:
-            st.steps(idx.contiguous(), 0, nsteps, last)
-        loss = float(st.loss_acc.item()) / max(nsteps, 1)     # syncs the device
-        st.check()
-        st.after_training()
-        res = self.metrics.compute()
-        self._reset_metrics()
-        return res, loss
 
     def _embedding_sync(self, m, config):
         """(xGMI communicator, world) for a replicated table's row all-gather, or None."""
@@ -570,10 +506,7 @@ class TorchLoopEngine:
             self.metrics.reset()
 
     def train_epoch(self):
-        if self.dlrm_status == "enabled":
-            out = self._train_epoch_dlrm()
-        else:
-            out = self.graphed.train_epoch() if self.graphed is not None else self._train_epoch_eager()
+        out = self.graphed.train_epoch() if self.graphed is not None else self._train_epoch_eager()
         if self.world > 1 and hasattr(self.model, "check_comm"):
             # the epoch's metrics readback synced the device already: a timed-out xGMI exchange
             # surfaces here as CollectiveError (the trainer restarts the group) instead of

@@ -139,11 +139,6 @@ register("spark.ray.mi355x.ddp.comm_stream", "str", "auto",
          "comm kernel spins for its peer on the CUs the peer's backward needs; "
          "profiles/r4_ddp_bucket_sweep.txt)", env="RAYDP_DDP_COMM_STREAM",
          choices=["auto", "on", "off", "true", "false", "1", "0"])
-register("spark.ray.mi355x.dlrm_step", "bool", False,
-         "train a single-GPU Dlrm (replicated tables, plain SGD, BCEWithLogitsLoss) with the whole "
-         "step as one persistent HIP launch (csrc/hip/dlrm_step.hip); off by default while the "
-         "HIP-graph replay of the launch-per-op step is faster (profiles/r4_dlrm_step_phases.jsonl)",
-         env="RAYDP_DLRM_STEP")
 register("spark.ray.mi355x.fused", "str", "auto",
          "TorchEstimator engine: auto (fused HIP MLP when the model is an MLP), on (required), off",
          env="RAYDP_FUSED", choices=["auto", "on", "off"])
