@@ -507,6 +507,13 @@ int rx_xg_error(void* ctx) {
   return (int)v;
 }
 
+// Stream-ordered copy of the error word into (pinned) host memory: a step loop reads the value a
+// few steps later instead of synchronising the device (and it is legal inside a graph capture).
+int rx_xg_error_async(void* ctx, unsigned* host, hipStream_t stream) {
+  XgHost* h = (XgHost*)ctx;
+  return (int)hipMemcpyAsync(host, h->dev.err, sizeof(unsigned), hipMemcpyDeviceToHost, stream);
+}
+
 int rx_xg_destroy(void* ctx) {
   XgHost* h = (XgHost*)ctx;
   if (!h) return 0;

@@ -224,8 +224,15 @@ int build_column(const std::vector<Field>& cells, size_t ncol, size_t nrow, size
   bool any_real = false, any_text = false, any_value = false;
   for (size_t r = 0; r < nrow; ++r) {
     // one surely-text value decides the column (Arrow's ladder ends on string whatever the
-    // other values are; "" stays the only null): the rest need no classification
-    if (any_text) break;
+    // other values are; "" stays the only null): the rest need no classification -- only a
+    // check that they are ASCII (a byte >= 0x80 may be invalid UTF-8, which Arrow types as
+    // binary: then the column is Arrow's to decide)
+    if (any_text) {
+      const Field& f = cells[(r + 1) * ncol + c];
+      for (int32_t j = 0; j < f.n; ++j)
+        if (static_cast<unsigned char>(f.p[j]) >= 0x80) return 0;
+      continue;
+    }
     const Kind k = classify(cells[(r + 1) * ncol + c], &ivals[r], &dvals[r]);
     if (k == kAmbiguous) return 0;
     kinds[r] = k;

@@ -368,8 +368,10 @@ class _Fusion:
 
     def finish(self):
         self.steps += 1
-        if self._sum is not None and self.steps % 256 == 0:
-            self._sum.check()   # a timed-out xGMI exchange raises instead of drifting silently
+        if self._sum is not None and self.steps % 64 == 0:
+            # a timed-out xGMI exchange raises instead of drifting silently: the error word comes
+            # back by a stream-ordered copy examined 64 steps later (no device sync in the loop)
+            self._sum.check_async()
         for b in range(len(self.buckets)):   # buckets never completed (unused params)
             if self.ready[b] != len(self.buckets[b]) and not any(x[0] == b for x in self.pending):
                 self._launch(b)

@@ -199,10 +199,39 @@ class XgmiComm:
         exchange on it timed out. A set error word makes every later launch skip its exchange,
         so the callers read it at their sync points (epoch end) instead of letting replicas
         drift apart silently."""
-        if self.error():
+        self._raise_for(self.error())
+
+    def _raise_for(self, err: int):
+        if err < 0:
+            raise RuntimeError("xGMI communicator: reading its error word failed (device error)")
+        if err:
             from raydp_amd.exceptions import CollectiveError
             forget_xgmi(self)
             raise CollectiveError("xGMI all-reduce: a peer did not arrive within the timeout")
+
+    def check_async(self):
+        """Non-blocking form of :meth:`check` for step loops: queue a stream-ordered copy of the
+        error word into pinned host memory and examine the copy queued by the previous call
+        (complete by then: its event is queried, never waited on). No device sync; legal
+        inside a graph capture (the examination is skipped while capturing)."""
+        import torch
+        if not self.ctx:
+            return
+        if getattr(self, "_err_host", None) is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._err_event = None
+        capturing = torch.cuda.is_current_stream_capturing()
+        ev = self._err_event
+        if ev is not None and not capturing and ev.query():
+            self._err_event = None
+            self._raise_for(int(self._err_host[0]))
+        if self._err_event is None and not capturing:
+            rc = self.lib.rx_xg_error_async(ctypes.c_void_p(self.ctx), ctypes.c_void_p(self._err_host.data_ptr()),
+                                            _hip.stream_ptr(torch.device("cuda", torch.cuda.current_device())))
+            if rc != 0:
+                raise RuntimeError(f"xGMI communicator: error-word copy failed ({rc})")
+            self._err_event = torch.cuda.Event()
+            self._err_event.record()
 
     def close(self):
         if self.ctx:
@@ -508,6 +537,15 @@ class BucketAllreduce:
         if self.xg is not None:
             try:
                 self.xg.check()
+            finally:
+                if self.xg.ctx is None or _XGMI_DISABLED:
+                    self.xg = None
+
+    def check_async(self):
+        """:meth:`check` without a device sync (``XgmiComm.check_async``): for step loops."""
+        if self.xg is not None:
+            try:
+                self.xg.check_async()
             finally:
                 if self.xg.ctx is None or _XGMI_DISABLED:
                     self.xg = None

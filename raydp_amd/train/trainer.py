@@ -554,11 +554,14 @@ class _TrainWorker:
     def deliver_shards(self, chan: str, payload: Optional[bytes], error: Optional[bytes] = None) -> bool:
         """The shards of a fit started with deferred datasets (runs beside ``run`` on the
         actor's second thread): ``{name: Dataset}`` pickled, or the conversion's failure."""
+        import concurrent.futures as cf
         import cloudpickle
         with self._chan_lock:
+            # checked and created in ONE critical section: a fit ending in between must not leave
+            # a channel behind that nothing will ever remove
             if chan in self._closed:     # the fit failed before its shards came: nothing waits
                 return False
-        fut = self._chan(chan)
+            fut = self._chans.setdefault(chan, cf.Future())
         if error is not None:
             fut.set_exception(cloudpickle.loads(error))
         else:

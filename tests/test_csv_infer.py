@@ -107,6 +107,8 @@ def test_nyc_shaped_file_is_read_natively(tmp_path):
     b"a\n\n\n",                        # header only (after empty lines)
     b"a,b\n,\n,\n",                    # all-null columns
     "a\ncafé\n".encode(),         # non-ASCII
+    b"a\nabc\n\xff\xfe\n",            # invalid UTF-8 AFTER the first text value (Arrow: binary)
+    "a,b\nabc,1\ncafé,2\n".encode(),  # valid non-ASCII after the first text value
 ])
 def test_edge_inputs_fall_back_or_match(data):
     got = native_exec.read_csv_infer(data)
