@@ -73,6 +73,8 @@ struct MlpLayer {
   int pr_off;        // float offset of [bias|gamma|beta|run_mean|run_var] (x out_n) in LDS
   int xg_off;        // wgrad_mode 1: bf16 offset of X^T_l [in_n][BP] in the exported activation area
   int gg_off;        //               bf16 offset of G^T_l [out_n][BP]
+  int sv_lds;        // LDS byte offset of the saved BN inputs / ReLU sources (fragment-major like
+                     // r_off), or -1: they live in the global scratch buffer at r_off
 };
 
 // Embedding front (MlpDesc::front_n > 0): column k of the first Linear's input is either a copy
@@ -141,8 +143,14 @@ struct Tile {
   // (12 -> 4 export at MT 2); the 8-B stores stay at 8 (2 dwords per lane over 32 banks: 2-way is
   // the floor for a 16-B permutation). The padded stride BP + 8 this replaces gave 8 / 8 / 8.
   static constexpr int XS = BP;
+  // chosen with a bank model (MI355X_MICROARCH.md §LDS) over the image's three access kinds:
+  // ds_read_b64_tr_b16 A-operand reads (rows 8 apart in a 32-lane half: ideal 1 cycle per half),
+  // the publish step's 8-B stores (unchanged) and the export's 16-B row reads (ideal)
   __host__ __device__ static constexpr int swz(int r) {
-    return MT == 1 ? (r >> 2) & 1 : MT == 8 ? r & 15 : (r >> 1) & (2 * MT - 1);
+    return MT == 1   ? (r >> 2) & 1
+           : MT == 2 ? ((r >> 1) & 1) | (((r >> 3) & 1) << 1)
+           : MT == 4 ? (r & 3) | (((r >> 3) & 1) << 2)
+                     : (r & 3) | (((r ^ (r >> 3)) & 1) << 2) | ((r & 1) << 3);
   }
   // element index of (row r, batch column e) in a transposed matrix
   __host__ __device__ static constexpr int tix(int r, int e) { return r * XS + (((e >> 3) ^ swz(r)) << 3) + (e & 7); }
@@ -397,12 +405,40 @@ __device__ __forceinline__ bf16x8 ld_w(const u16* __restrict__ img, int off) {
     return *reinterpret_cast<const RX_GLOBAL bf16x8*>(rx_g(img) + off);
 }
 
+#define RX_LDS __attribute__((address_space(3)))
+typedef short rx_v4s __attribute__((ext_vector_type(4)));
+
+// A operand of the GEMMs: the layer input (forward) / G_l (dgrad), 16 batch rows x 8 k per lane.
+//  * R mode (d.r_lds_off >= 0): the row-major image R, one ds_read_b128 per fragment;
+//  * T mode (no R image): straight from the TRANSPOSED image [k][batch] the previous step
+//    published for the export anyway, two ds_read_b64_tr_b16 per fragment (gfx950's hardware
+//    transpose read: lane 4q + p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16
+//    block; lane i receives column i of the 4 rows). No row-major copy is written at all.
+struct AOp {
+  const u16* base;  // R or the transposed image
+  int RS;           // R's row stride (R mode)
+  bool tr;          // T mode
+};
+
+template <int MT>
+__device__ __forceinline__ bf16x8 ld_afrag(const AOp& A, int ks, int mt, int lane) {
+  if (A.tr) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int r0 = ks * 32 + 8 * g + q, e = mt * 16 + 4 * p;
+    const rx_v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RX_LDS rx_v4s*)(A.base + Tile<MT>::tix(r0, e)));
+    const rx_v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RX_LDS rx_v4s*)(A.base + Tile<MT>::tix(r0 + 4, e)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+  const int lr = lane & 15, lg = lane >> 4;
+  const int k0 = ks * 32 + 8 * (lg ^ rx_rsw(lr));   // R's chunk swizzle
+  return *reinterpret_cast<const bf16x8*>(A.base + (mt * 16 + lr) * A.RS + k0);
+}
+
 template <int MT, bool PS>
-__device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
-                                          const u16* __restrict__ img, int boff, int K, int lg, int alg) {
+__device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const AOp& A, int lane, const u16* __restrict__ img,
+                                          int boff, int ks0, int nks, int lg) {
   constexpr int KC = 8;
-  const int nks = K >> 5;
-  for (int kc = 0; kc < nks; kc += KC) {
+  for (int kc = ks0; kc < nks; kc += KC) {
     bf16x8 bfr[KC];
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
@@ -412,12 +448,8 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const u16* __restric
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
       if (kc + s < nks) {
-        const int k0 = (kc + s) * 32 + 8 * alg;   // alg = lg ^ rx_rsw(row): R's chunk swizzle
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(Arow + mt * 16 * RS + k0);
-          acc[mt] = rx_mfma16(a, bfr[s], acc[mt]);
-        }
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = rx_mfma16(ld_afrag<MT>(A, kc + s, mt, lane), bfr[s], acc[mt]);
       }
     }
   }
@@ -493,24 +525,48 @@ __device__ __forceinline__ void export_rows(const u16* lds, int rows, float* __r
 // Tile j of this wave: the k-steps held in the flat prefetch buffer first (fragment f = j * nks +
 // s, statically indexed), the rest loaded here in one burst.
 template <int MT, bool PS>
-__device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const u16* __restrict__ Arow, int RS,
-                                              const u16* __restrict__ img, int boff, int K, int lg, int alg,
-                                              const bf16x8 (&pre)[RX_PJ][RX_PK], int j) {
+__device__ __forceinline__ void gemm_tile_pre(f32x4 (&acc)[MT], const AOp& A, int lane, const u16* __restrict__ img,
+                                              int boff, int K, int lg, const bf16x8 (&pre)[RX_PJ][RX_PK], int j) {
   const int nks = K >> 5;
 #pragma unroll
   for (int f = 0; f < RX_PF; ++f) {
     const int s = f - j * nks;
     if (s >= 0 && s < nks) {
-      const int k0 = s * 32 + 8 * alg;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Arow + mt * 16 * RS + k0);
-        acc[mt] = rx_mfma16(a, pre[f >> 2][f & 3], acc[mt]);
-      }
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = rx_mfma16(ld_afrag<MT>(A, s, mt, lane), pre[f >> 2][f & 3], acc[mt]);
     }
   }
   const int done = max(0, min(nks, RX_PF - j * nks));
-  if (nks > done) gemm_tile<MT, PS>(acc, Arow + done * 32, RS, img, boff + done * 32, K - done * 32, lg, alg);
+  if (nks > done) gemm_tile<MT, PS>(acc, A, lane, img, boff, done, nks, lg);
+}
+
+// Saved forward values (BN inputs / ReLU sources) of layer `ly`: fragment-major, in LDS when the
+// host found room (sv_lds >= 0: no global round trip on the step's critical chain), else in the
+// global scratch buffer.
+template <int MT, class LY>
+__device__ __forceinline__ void sv_store(const LY& ly, char* smem, float* __restrict__ scratch, int n, int mt, int lane,
+                                         const f32x4& v) {
+  if (ly.sv_lds >= 0)
+    *reinterpret_cast<f32x4*>(smem + ly.sv_lds + frag_off<MT>(0, n, mt, lane) * 4) = v;
+  else
+    *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) = v;
+}
+template <int MT, class LY>
+__device__ __forceinline__ f32x4 sv_load(const LY& ly, const char* smem, const float* __restrict__ scratch, int n, int mt,
+                                         int lane) {
+  if (ly.sv_lds >= 0) return *reinterpret_cast<const f32x4*>(smem + ly.sv_lds + frag_off<MT>(0, n, mt, lane) * 4);
+  return *reinterpret_cast<const RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane));
+}
+
+// Zero rows [r0, r1) of a transposed image (the K tail the next GEMM reads: T mode's analogue of
+// zeroing R's padding columns), 16 B per thread and pass.
+template <int MT, bool PS>
+__device__ __forceinline__ void zero_t_rows(u16* Tm, int r0, int r1) {
+  constexpr int CH = Tile<MT>::BP / 8;
+  for (int idx = rx_tid<PS>(); idx < (r1 - r0) * CH; idx += RX_THREADS) {
+    const int r = r0 + idx / CH, c = idx % CH;
+    *reinterpret_cast<u32x4*>(Tm + r * Tile<MT>::XS + (c << 3)) = u32x4{0u, 0u, 0u, 0u};
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -541,6 +597,8 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   u16* GT = reinterpret_cast<u16*>(smem + d.gt_lds_off);
   float* stats = reinterpret_cast<float*>(smem + d.stats_lds_off);
   const int ntiles = ly.out_n >> 4;
+  const bool tmode = d.r_lds_off < 0;   // no R image: A operands by transposed reads of XT_l
+  const AOp Aop{tmode ? reinterpret_cast<const u16*>(smem + ly.xt_off) : R, RS, tmode};
   fst(0);
 
   f32x4 acc[T::NTW * MT];
@@ -552,7 +610,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     const int n = wave + j * RX_NW;
     if (n < ntiles) {
       const int boff = ly.w_img + (n * 16 + lr) * ly.in_k;
-      gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.in_k, lg, lg ^ rx_rsw(lr), wpre, j);
+      gemm_tile_pre<MT, PS>(part, Aop, lane, img, boff, ly.in_k, lg, wpre, j);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
@@ -619,8 +677,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       }
       // save the BN input for the backward pass (fragment-major, see frag_off)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) = acc[j * MT + mt];
+      for (int mt = 0; mt < MT; ++mt) sv_store<MT>(ly, smem, scratch, n, mt, lane, acc[j * MT + mt]);
     }
   };
   auto epi_b = [&](int j) {
@@ -665,11 +722,8 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     } else if (TRAIN && !last) {
       // ReLU mask source for the backward pass
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(ly.r_off, n, mt, lane)) =
-            colok ? acc[j * MT + mt] : z;
-      }
+      for (int mt = 0; mt < MT; ++mt)
+        sv_store<MT>(ly, smem, scratch, n, mt, lane, colok ? acc[j * MT + mt] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
     // padded rows / columns carry exact zeros through every GEMM
     if (!(FULL && cols_full)) {
@@ -886,12 +940,14 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         if (TRAIN || !last)
           *reinterpret_cast<uint2*>(dstT + c * XS + ((((mt * 16 + lg * 4) >> 3) ^ tsw) << 3) + ((lg & 1) << 2)) = pk[mt];
       }
-      rx_publish_rows<MT>(R, RS, c, lane, pk);
+      if (!tmode) rx_publish_rows<MT>(R, RS, c, lane, pk);
     }
   }
-  // zero the K padding columns [out_n, out_k) of R so the next GEMM's K tail is exact
+  // zero the K padding [out_n, out_k) of the next GEMM's A operand so its K tail is exact
   const int kpad = (last ? ly.out_k : nx.in_k) - ly.out_n;
-  if (kpad > 0) {
+  if (tmode) {
+    if (kpad > 0) zero_t_rows<MT, PS>(dstT, ly.out_n, ly.out_n + kpad);
+  } else if (kpad > 0) {
     for (int idx = rx_tid<PS>(); idx < T::BP * kpad; idx += RX_THREADS) {
       const int row = idx / kpad, cc = ly.out_n + idx % kpad;
       R[rx_rix(row, cc, RS)] = 0;
@@ -939,7 +995,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
         const int n = min(wave + j * RX_NW, ntiles_d - 1);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const f32x4 t = *reinterpret_cast<const RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(pv.r_off, n, mt, lane));
+          const f32x4 t = sv_load<MT>(pv, smem, scratch, n, mt, lane);
 #pragma unroll
           for (int r = 0; r < 4; ++r) svp[j][mt * 4 + r] = t[r];
         }
@@ -1041,9 +1097,11 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 #endif
   if (l == 0) return;
 
-  // ---- dgrad: dX[b][i] = sum_o G[b][o] W[o][i]  (A = R, B = Wt, K = out_k) ----
+  // ---- dgrad: dX[b][i] = sum_o G[b][o] W[o][i]  (A = R or the G^T image, B = Wt, K = out_k) ----
   // pv (layer l-1) owns the post-ops between layer l-1 and l
   const int ntiles = ly.in_n >> 4;
+  const bool tmode = d.r_lds_off < 0;
+  const AOp Aop{tmode ? GT : R, RS, tmode};
   f32x4 acc[T::NTW * MT];
 #pragma unroll
   for (int j = 0; j < T::NTW; ++j) {
@@ -1053,7 +1111,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     const int n = wave + j * RX_NW;
     if (n < ntiles) {
       const int boff = ly.wt_img + (n * 16 + lr) * ly.out_k;
-      gemm_tile_pre<MT, PS>(part, R + lr * RS, RS, img, boff, ly.out_k, lg, lg ^ rx_rsw(lr), wpre, j);
+      gemm_tile_pre<MT, PS>(part, Aop, lane, img, boff, ly.out_k, lg, wpre, j);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
@@ -1093,7 +1151,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     } else {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const f32x4 t = *reinterpret_cast<const RX_GLOBAL f32x4*>(rx_g(scratch) + frag_off<MT>(pv.r_off, n, mt, lane));
+        const f32x4 t = sv_load<MT>(pv, smem, scratch, n, mt, lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) sv[mt * 4 + r] = t[r];
       }
@@ -1196,7 +1254,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       pk[mt].y = rx_f2bf2(g[mt * 4 + 2], g[mt * 4 + 3]);
       *reinterpret_cast<uint2*>(GT + T::tix(c, mt * 16 + lg * 4)) = pk[mt];
     }
-    rx_publish_rows<MT>(R, RS, c, lane, pk);
+    if (!tmode) rx_publish_rows<MT>(R, RS, c, lane, pk);
   };
   bool split = false;
   if constexpr (MWT::on) split = pv.bn != 0;
@@ -1226,9 +1284,11 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 #ifdef RX_LAYER_STAMPS
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[23 + 4 * l] = __builtin_amdgcn_s_memtime();
 #endif
-  // zero the K tail [out_n, out_k) of G_{l-1} in R for the next dgrad
+  // zero the K tail [out_n, out_k) of G_{l-1} for the next dgrad
   const int kpad = pv.out_k - pv.out_n;
-  if (kpad > 0) {
+  if (tmode) {
+    if (kpad > 0) zero_t_rows<MT, PS>(GT, pv.out_n, pv.out_k);
+  } else if (kpad > 0) {
     for (int idx = rx_tid<PS>(); idx < T::BP * kpad; idx += RX_THREADS) {
       const int row = idx / kpad, cc = pv.out_n + idx % kpad;
       R[rx_rix(row, cc, RS)] = 0;
@@ -1356,8 +1416,8 @@ __device__ __forceinline__ void front_backward(const D& d, const MlpDesc* __rest
     f32x4 part[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_tile<MT, false>(part, R + lr * RS, RS, img, l0.wt_img + (n * 16 + lr) * l0.out_k, l0.out_k, lg,
-                         lg ^ rx_rsw(lr));
+    const AOp A{R, RS, false};   // (the embedding front always keeps the R image)
+    gemm_tile<MT, false>(part, A, lane, img, l0.wt_img + (n * 16 + lr) * l0.out_k, 0, l0.out_k >> 5, lg);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -1399,15 +1459,20 @@ __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem
   }
   using T = Tile<MT>;
   const int RS = d.max_k + RX_RPAD;
+  const bool tmode = d.r_lds_off < 0;   // the GEMM reads XT_0 itself
+  need_t = need_t || tmode;
   u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
   u16* XT = reinterpret_cast<u16*>(smem + l0.xt_off);
   const int in_n = l0.in_n;
   const int chunks = d.feat_k >> 3;  // 8 bf16 per 16-B chunk
+  if (tmode && l0.in_k > in_n) {    // K tail rows [in_n, in_k) of XT_0 (never written below)
+    zero_t_rows<MT, PS>(XT, in_n, l0.in_k);
+  }
   for (int idx = rx_tid<PS>(); idx < T::BP * chunks; idx += RX_THREADS) {
     const int row = idx / chunks, ch = idx % chunks;
     u32x4 v = *reinterpret_cast<const RX_GLOBAL u32x4*>(rx_g(feats) + (size_t)rowidx[row] * d.feat_k + ch * 8);
     if (row >= nvalid) v = u32x4{0u, 0u, 0u, 0u};
-    *reinterpret_cast<u32x4*>(R + row * RS + ((ch ^ rx_rsw(row)) << 3)) = v;
+    if (!tmode) *reinterpret_cast<u32x4*>(R + row * RS + ((ch ^ rx_rsw(row)) << 3)) = v;
     if (need_t) {
       const u16* h = reinterpret_cast<const u16*>(&v);
 #pragma unroll

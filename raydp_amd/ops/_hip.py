@@ -26,6 +26,7 @@ class MlpLayer(ctypes.Structure):
         ("eps", ctypes.c_float), ("momentum", ctypes.c_float),
         ("xt_off", ctypes.c_int), ("stat_off", ctypes.c_int), ("r_off", ctypes.c_int),
         ("pr_off", ctypes.c_int), ("xg_off", ctypes.c_int), ("gg_off", ctypes.c_int),
+        ("sv_lds", ctypes.c_int),
     ]
 
 

@@ -218,8 +218,20 @@ class FusedMLPTrainer:
             lds = _ru(lds + nbytes, 16)
             return start
 
-        d.r_lds_off = alloc(bp * (max_k + 16) * 2)   # row stride max_k + RX_RPAD (csrc/hip/mlp_core.h)
-        d.gt_lds_off = alloc(max_n * xs * 2)
+        wmode = wgrad_mode() if G == 1 else 1   # multi-workgroup: dW over the whole batch
+        # T mode (csrc/hip/mlp_core.h AOp): with the weight gradients on the optimizer side
+        # (wgrad_mode 1) no layer's transposed image outlives the next publish, so ONE transposed
+        # image serves as every X^T_l and as G^T, and the GEMMs read their A operands from it by
+        # transposed LDS reads -- no row-major R image. The freed LDS keeps the saved BN inputs
+        # on chip (sv_lds).
+        tmode = wmode == 1 and not spec.front and mt >= 2
+        if tmode:
+            d.r_lds_off = -1
+            t_off = alloc(max_k * xs * 2)          # rows up to every layer's K padding
+            d.gt_lds_off = t_off
+        else:
+            d.r_lds_off = alloc(bp * (max_k + 16) * 2)   # row stride max_k + RX_RPAD (csrc/hip/mlp_core.h)
+            d.gt_lds_off = alloc(max_n * xs * 2)
         stat_total = sum(2 * dm[5] for dm in dims)
         d.stats_lds_off = alloc(stat_total * 4)
         scratch_off = 0
@@ -229,7 +241,6 @@ class FusedMLPTrainer:
         nseg = 0
         seg_images = []
         act = 0           # bf16 elements of the exported X^T_l / G^T_l area (wgrad_mode 1)
-        wmode = wgrad_mode() if G == 1 else 1   # multi-workgroup: dW over the whole batch
 
         def vseg(start, n):
             # bias / BN gamma+beta vectors: plain element-wise optimizer segments
@@ -298,7 +309,8 @@ class FusedMLPTrainer:
                     rs_init.append((bn, rs_total, oo))
                     rs_total += 2 * oo
                 x.eps, x.momentum = float(bn.eps), float(bn.momentum if bn.momentum is not None else 0.1)
-            x.xt_off = alloc(in_n * xs * 2)
+            x.xt_off = t_off if tmode else alloc(in_n * xs * 2)
+            x.sv_lds = -1
             x.stat_off = stat_off
             stat_off += 2 * out_n
             x.r_off = scratch_off
@@ -344,6 +356,15 @@ class FusedMLPTrainer:
         d.acc_thr = float(self.acc_thr) if self.acc_thr is not None else 0.5
         d.pr_lds_off = alloc(pr_total * 4)
         d.pr_total = pr_total
+        # saved BN inputs / ReLU sources in LDS, largest first, while they fit (the rest stays in
+        # the global scratch buffer); T mode only (R mode has no room for them)
+        if tmode:
+            budget = 160 * 1024 - 1024     # static LDS of the kernels (row indices, flags)
+            saves = [(bp * d.layer[li].out_n * 4, li) for li, ly in enumerate(spec.layers)
+                     if ly.bn or li != L - 1]
+            for nbytes, li in sorted(saves, reverse=True):
+                if lds + nbytes <= budget:
+                    d.layer[li].sv_lds = alloc(nbytes)
         d.lds_bytes = lds
         d.max_k, d.max_n = max_k, max_n
         d.loss, d.beta = self.loss_code, self.beta

@@ -31,7 +31,8 @@ _lock = threading.Lock()
 _loaded = {}
 
 _LAYER_INT = ("in_", "out", "in_k", "out_k", "in_n", "out_n", "w_img", "wt_img", "w_off", "b_off", "act", "bn",
-              "g_off", "be_off", "rs_off", "xt_off", "stat_off", "r_off", "pr_off", "xg_off", "gg_off", "mw_off")
+              "g_off", "be_off", "rs_off", "xt_off", "stat_off", "r_off", "pr_off", "xg_off", "gg_off", "mw_off",
+              "sv_lds")
 _DESC_INT = ("L", "r_lds_off", "gt_lds_off", "stats_lds_off", "lds_bytes", "max_k", "max_n", "loss", "out_dim",
              "feat_k", "pr_lds_off", "pr_total", "act_off", "wgrad_mode", "front_n", "front_q", "acc_mode")
 

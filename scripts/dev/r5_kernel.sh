@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5 fused-MLP iteration: GPU numerics tests of the fused engine, then the persistent NYC
-# epoch timing (plain and with intra-layer stamps).
+# epoch timing (plain and with intra-layer stamps) and the wide-batch step timing.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -10,5 +10,9 @@ timeout -k 10 600 $T tests/test_gpu_kernels.py tests/test_gpu_mw.py tests/test_g
 rc=$?; grep -E "passed|failed|^E  |FAIL" gpurun_out/r5_kernel_tests.log | tail -15; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 150 python -u scripts/dev/persist_ab.py . >> gpurun_out/r5_persist.jsonl 2>> gpurun_out/r5_persist.err || exit 3
 RAYDP_MLP_LAYER_STAMPS=1 timeout -k 10 150 python -u scripts/dev/persist_ab.py . >> gpurun_out/r5_persist.jsonl 2>> gpurun_out/r5_persist.err || exit 4
-timeout -k 10 150 python -u scripts/dev/persist_ab.py . >> gpurun_out/r5_persist.jsonl 2>> gpurun_out/r5_persist.err || exit 5
-tail -3 gpurun_out/r5_persist.jsonl | cut -c1-400
+timeout -k 10 150 python -u scripts/dev/mw_time.py 4096 1000 >> gpurun_out/r5_mw.jsonl 2>> gpurun_out/r5_mw.err || exit 5
+tail -2 gpurun_out/r5_persist.jsonl | cut -c1-300; tail -2 gpurun_out/r5_mw.jsonl
+for v in base fused_adam native_bn rocblas all; do
+  ES_VARIANT=$v timeout -k 10 120 python -u scripts/dev/eager_step_bench.py >> gpurun_out/r5_eager.jsonl 2>> gpurun_out/r5_eager.err || exit 6
+done
+cat gpurun_out/r5_eager.jsonl
