@@ -207,6 +207,7 @@ struct MwCtx {
   int G, wg;                   // workgroups of the step, this one's index
   int n_total;                 // valid rows of the whole batch
   unsigned long long ticks;    // wall-clock bound of one barrier wait
+  unsigned long long* tstamp;  // optional: workgroup 0 stores the step's start (wall clock) here
 };
 
 // Partial blocks: every (layer, phase) region of every workgroup starts on its own 128-B line. A
@@ -1549,6 +1550,8 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
   mw.wg = (int)blockIdx.x;
   mw.k = 0;
   mw.ok = 1;
+  // per-step device timeline (the step-time histogram of multi-workgroup epochs)
+  if (mw.tstamp != nullptr && mw.wg == 0 && threadIdx.x == 0) *rx_g(mw.tstamp) = wall_clock64();
   const int nvalid = mw_rows(mw.n_total, mw.wg, BP);
   const int r0 = row0 + mw.wg * BP;
   float* sc = scratch + (size_t)mw.wg * (size_t)scratch_stride;

@@ -623,6 +623,12 @@ class FusedMLPTrainer:
                 lrs, bc1, bc2, ctypes.c_float(gscale), int(self.step_count == 0), stream, pp(xg.ctx))
             _hip.check(rc, "rx_mlp_train_steps_xg")
         elif comm is not None or allreduce is None:
+            mw_stamps = None
+            if self.G > 1 and self.record_steps:
+                # multi-workgroup epoch: workgroup 0 of every step stores the step's start time
+                mw_stamps = self._dev_buf("stamps", 32 + nsteps + 1 + _PS_LAYER_STAMPS, torch.int64)
+                mw_stamps.zero_()
+                self.bufs.stamps = mw_stamps.data_ptr()
             ar_fn = comm.fn_ptr if comm is not None else pp(0)
             ar_ctx = pp(comm.ctx) if comm is not None else pp(0)
             rc = self.lib.rx_mlp_train_steps(
@@ -630,7 +636,10 @@ class FusedMLPTrainer:
                 pp(self.m.data_ptr()), pp(self.v.data_ptr()),
                 pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, 0, nsteps,
                 lrs, bc1, bc2, ctypes.c_float(gscale), int(self.step_count == 0), stream, ar_fn, ar_ctx)
+            self.bufs.stamps = 0
             _hip.check(rc, "rx_mlp_train_steps")
+            if mw_stamps is not None:
+                self._mw_stamps_dev = mw_stamps
         else:
             for s in range(nsteps):
                 rc = self.lib.rx_mlp_fwdbwd(
@@ -654,7 +663,13 @@ class FusedMLPTrainer:
         pre, self._metrics_np = getattr(self, "_metrics_np", None), None
         if self.G > 1 and pre is None:
             # the multi-workgroup barriers' timeout word comes back with the metrics (one sync)
-            back = self._readback([self.mw_ctl[2:3], self.metrics])
+            mws = getattr(self, "_mw_stamps_dev", None)
+            self._mw_stamps_dev = None
+            back = self._readback([self.mw_ctl[2:3], self.metrics] + ([mws] if mws is not None else []))
+            if mws is not None:
+                # step starts only (no end stamp): the last step's time is not recorded
+                st = back[2].copy()
+                self._step_stamps = st[:32 + nsteps] if nsteps > 1 else None
             if int(back[0][0]) != 0:
                 # from the timed-out step on, the steps stored no gradients and the optimizer
                 # updated nothing; roll the whole epoch back and clear the control words so the
@@ -686,7 +701,10 @@ class FusedMLPTrainer:
         if st is None:
             return None
         self._step_stamps = None
-        t = np.asarray(st)[32:-_PS_LAYER_STAMPS].astype(np.float64)
+        t = np.asarray(st)[32:].astype(np.float64)
+        if t.size > _PS_LAYER_STAMPS and not t[-_PS_LAYER_STAMPS:].any():
+            t = t[:-_PS_LAYER_STAMPS]       # a persistent epoch's buffer: drop the layer-stamp tail
+        t = t[t > 0] if t.size and (t <= 0).any() else t
         return np.diff(t) * 0.01 if t.size > 1 else None
 
     def snapshot(self):

@@ -16,3 +16,5 @@ for v in base fused_adam native_bn rocblas all; do
   ES_VARIANT=$v timeout -k 10 120 python -u scripts/dev/eager_step_bench.py >> gpurun_out/r5_eager.jsonl 2>> gpurun_out/r5_eager.err || exit 6
 done
 cat gpurun_out/r5_eager.jsonl
+
+bash scripts/dev/pmc_step.sh || exit 8
