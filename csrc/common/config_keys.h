@@ -46,6 +46,8 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.step_times", "RAYDP_STEP_TIMES", "1"},
     {"spark.ray.mi355x.udf_verify", "RAYDP_UDF_VERIFY", "sampled"},
     {"spark.ray.mi355x.native_executor", "RAYDP_NATIVE_EXECUTOR", "1"},
+    {"spark.ray.mi355x.fused_optimizer", "RAYDP_FUSED_OPTIMIZER", "1"},
+    {"spark.ray.mi355x.native_batchnorm", "RAYDP_NATIVE_BATCHNORM", "1"},
 };
 
 // Value of a key: its environment variable when set and non-empty, else the default.

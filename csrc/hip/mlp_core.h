@@ -25,6 +25,9 @@
 #pragma once
 #include "rx_common.h"
 #include "rx_grid.h"
+#include "mlp_opt.h"
+
+#include <type_traits>
 
 // No implicit multiply-add contraction in the training kernels: whether the compiler fuses an
 // a * b + c depends on the inlining context (and on what the SLP vectorizer pairs into v_pk_*
@@ -107,6 +110,11 @@ struct MlpDesc {
   float acc_thr;
   FrontCol front[RX_MAXF];
   int front_qbase[RX_MAXF];  // prefix of `rows` over the front's embedding columns
+  int loss_lds_off;  // >= 0: one output column, regression / BCE loss run a row per lane through
+                     //       this LDS area (BP floats); -1: the tile-layout loss
+  int w0s_lds_off;   // >= 0 (persistent epoch): layer 0's fp32 master weight and Adam / SGD moments
+                     //       live here, updated by the step workgroup (mlp_persist.h ps_l0_update)
+  int x0c_lds_off;   //       with its copy of X^T_0 ([in_k rows][BP], Tile::tix layout) here
 };
 
 // run-time descriptor: loops over layers are ordinary loops
@@ -209,6 +217,85 @@ struct MwCtx {
   unsigned long long ticks;    // wall-clock bound of one barrier wait
   unsigned long long* tstamp;  // optional: workgroup 0 stores the step's start (wall clock) here
 };
+
+// The persistent step's per-layer weight wait (mlp_persist.h PsNxWait): layer_forward(l) issues
+// the read of layer l+1's optimizer counter at its start and waits on it only where it prefetches
+// layer l+1's weights. NoNxWait: nothing (every other kernel).
+struct NoNxWait {
+  __device__ void issue(int) {}
+  __device__ void wait(int) {}
+};
+
+// Persistent epoch kernel: the bias / BatchNorm affine parameters are updated where their
+// gradients are produced. The four lanes holding a column's batch sums (every lane of a column
+// gets them from the cross-lane reductions) each own one parameter -- lane group 0 the bias, 1
+// gamma, 2 beta -- and apply the optimizer to it in place in the LDS parameter block, with its
+// two moments prefetched at the start of the layer. No vector-update phase of its own, no
+// gradient round trip through memory. `o == nullptr`: off (the optimizer kernel / the
+// end-of-step update owns these parameters). O: OptDesc, or a specialised kernel's constexpr
+// hyperparameter struct (C::Opt). The step's scalars live in LDS (sc: lr, -(lr / bc1),
+// 1 / sqrt(bc2), first) and are read where they are used: nothing of this stays in SGPRs across
+// the layers (the step body is at the SGPR limit; every extra live value is a spill).
+template <class O = OptDesc>
+struct PsVec {
+  const O* o = nullptr;
+  float* m = nullptr;
+  float* v = nullptr;
+  const float* sc = nullptr;
+};
+
+// the optimizer-hyperparameter type of a layer configuration: C::Opt where it has one
+template <class C, class = void>
+struct rx_opt_type {
+  using type = OptDesc;
+};
+template <class C>
+struct rx_opt_type<C, std::void_t<typename C::Opt>> {
+  using type = typename C::Opt;
+};
+// the hyperparameters as a reference: the runtime descriptor itself, or an (empty) constexpr struct
+template <class O>
+struct rx_opt_holder {
+  O v;
+  __device__ const O& get(const OptDesc&) const { return v; }
+};
+template <>
+struct rx_opt_holder<OptDesc> {
+  __device__ const OptDesc& get(const OptDesc& o) const { return o; }
+};
+
+// flat parameter index of column c of layer ly that lane group lg updates (-1: none)
+template <class LY>
+__device__ __forceinline__ int ps_vec_index(const LY& ly, int lg, int c) {
+  const int off = lg == 0 ? ly.b_off : (lg == 1 ? ly.g_off : (lg == 2 ? ly.be_off : -1));
+  return off >= 0 ? off + c : -1;
+}
+
+// both moments of this lane's parameter of column c (address-clamped: issued unconditionally)
+template <class VO, class LY>
+__device__ __forceinline__ void ps_vec_prefetch(const VO& vo, const LY& ly, int lg, int c, float& mm,
+                                                float& vv) {
+  const int idx = c < ly.out ? ps_vec_index(ly, lg, c) : -1;
+  const int q = idx >= 0 ? idx : 0;
+  mm = rx_g(vo.m)[q];
+  vv = rx_g(vo.v)[q];
+}
+
+// the update itself (same arithmetic as every other optimizer path: opt_update_reg)
+template <class VO, class LY>
+__device__ __forceinline__ void ps_vec_update(const VO& vo, const LY& ly, float* pr, int lg, int c, bool colok,
+                                              float grad, float mm, float vv) {
+  const int idx = ps_vec_index(ly, lg, c);
+  if (colok && idx >= 0) {
+    float* slot = pr + ly.pr_off + lg * ly.out_n + c;   // [bias | gamma | beta | ...] of the layer
+    float p = *slot;
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(vo.sc);
+    opt_update_pre(*vo.o, p, mm, vv, grad, sc[0], sc[1], sc[2], 1.f, sc[3] != 0.f ? 1 : 0);
+    *slot = p;
+    rx_g(vo.m)[idx] = mm;
+    if (vo.o->algo != 2) rx_g(vo.v)[idx] = vv;
+  }
+}
 
 // Partial blocks: every (layer, phase) region of every workgroup starts on its own 128-B line. A
 // consumer's XCD must not hold a line of a region before that region's last write of the step
@@ -435,6 +522,18 @@ __device__ __forceinline__ bf16x8 ld_afrag(const AOp& A, int ks, int mt, int lan
   return *reinterpret_cast<const bf16x8*>(A.base + (mt * 16 + lr) * A.RS + k0);
 }
 
+// A fragment of a K = 32 GEMM in the k order pi(g, j) = 16 (j >> 2) + 4 g + (j & 3) (transposed
+// reads only): the order in which ps_l0_update's accumulators hold a layer-0 weight row, so the
+// forward consumes those registers as B fragments directly (mlp_persist.h)
+template <int MT>
+__device__ __forceinline__ bf16x8 ld_afrag_pi(const AOp& A, int mt, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int r0 = 4 * g + q, e = mt * 16 + 4 * p;
+  const rx_v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RX_LDS rx_v4s*)(A.base + Tile<MT>::tix(r0, e)));
+  const rx_v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RX_LDS rx_v4s*)(A.base + Tile<MT>::tix(r0 + 16, e)));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 template <int MT, bool PS>
 __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const AOp& A, int lane, const u16* __restrict__ img,
                                           int boff, int ks0, int nks, int lg) {
@@ -462,6 +561,7 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[MT], const AOp& A, int la
 // every GEMM (layer 1 forward: 1 tile x 8 k-steps; layer 1 dgrad: 2 tiles x 4), so no GEMM issues
 // a load of its own: a load issued after the layer's stores would be waited for behind them
 // (vmcnt retires in issue order).
+constexpr int RX_W0J = 2;   // layer-0 weight tiles per wave the step workgroup can update (out <= 256)
 constexpr int RX_PJ = 2;
 constexpr int RX_PK = 4;
 constexpr int RX_PF = RX_PJ * RX_PK;
@@ -480,9 +580,34 @@ __device__ __forceinline__ void gemm_prefetch_flat(bf16x8 (&pre)[RX_PJ][RX_PK], 
 }
 
 // This wave's forward weight fragments of layer `ly` (W_l rows, K = in_k).
+// pi: layer 0 of a model laid out for the persistent kernel's own layer-0 update
+// (MlpDesc::w0s_lds_off >= 0, K = 32): every kernel of that model runs layer 0's GEMM in the k
+// order pi of ld_afrag_pi, so the persistent epoch and the launch-per-step loop round alike --
+// the fragment is two 8-B reads, columns 4 lg .. +3 and 16 + 4 lg .. +3.
 template <bool PS, class LY>
-__device__ __forceinline__ void fwd_prefetch(const LY& ly, const u16* __restrict__ img, bf16x8 (&wpre)[RX_PJ][RX_PK]) {
+__device__ __forceinline__ void fwd_prefetch(const LY& ly, const u16* __restrict__ img, bf16x8 (&wpre)[RX_PJ][RX_PK],
+                                             bool pi = false) {
   const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
+  if (pi) {
+    const int ntiles = ly.out_n >> 4, lr = lane & 15, lg = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < RX_PJ; ++j) {
+      const int n = min(wave + j * RX_NW, ntiles - 1);
+      const int off = ly.w_img + (n * 16 + lr) * ly.in_k + 4 * lg;
+      uint2 a, b;
+      if constexpr (PS) {
+        a = rx_load8_sc1(img, off * 2);
+        b = rx_load8_sc1(img, (off + 16) * 2);
+      } else {
+        const rx_u32x2 x = *reinterpret_cast<const RX_GLOBAL rx_u32x2*>(rx_g(img) + off);
+        const rx_u32x2 y = *reinterpret_cast<const RX_GLOBAL rx_u32x2*>(rx_g(img) + off + 16);
+        a = make_uint2(x[0], x[1]);
+        b = make_uint2(y[0], y[1]);
+      }
+      wpre[j][0] = __builtin_bit_cast(bf16x8, u32x4{a.x, a.y, b.x, b.y});
+    }
+    return;
+  }
   gemm_prefetch_flat<PS>(wpre, img, ly.w_img, ly.out_n >> 4, ly.in_k, wave, lane & 15, lane >> 4);
 }
 
@@ -575,14 +700,16 @@ __device__ __forceinline__ void zero_t_rows(u16* Tm, int r0, int r1) {
 // act/BN) in R (row-major) and in XT_{l+1}; for the last layer computes loss, metrics and
 // writes dL/dy into R/GT as G_{L-1}.
 // ------------------------------------------------------------------------------------------
-template <int MT, bool TRAIN, bool PS, bool FULL = false, class D, class LY, class NX, class MWT = NoMw>
+template <int MT, bool TRAIN, bool PS, bool FULL = false, class D, class LY, class NX, class MWT = NoMw,
+          class VO = PsVec<>, class NXW = NoNxWait>
 __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX& nx, bool last, char* smem,
                                               const u16* __restrict__ img, const float* __restrict__ P,
                               float* __restrict__ Gr, const float* __restrict__ labels,
                               const int* __restrict__ rowidx, int nvalid, float* __restrict__ scratch,
                               double* __restrict__ metrics, bf16x8 (&wpre)[RX_PJ][RX_PK], bool ps_wt = true,
                               int l = 0, unsigned long long* __restrict__ stamps = nullptr,
-                              const float* lab_pre = nullptr, MWT* mw = nullptr) {
+                              const float* lab_pre = nullptr, MWT* mw = nullptr, VO vo = VO{},
+                              const bf16x8* w0b = nullptr, NXW* nxw = nullptr) {
   // optional intra-layer timeline (wave 0, s_memtime): [40 + 5 l ..] export, GEMM, epilogue,
   // first barrier, publish + second barrier
   auto fst = [&](int k) {
@@ -600,7 +727,17 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   const int ntiles = ly.out_n >> 4;
   const bool tmode = d.r_lds_off < 0;   // no R image: A operands by transposed reads of XT_l
   const AOp Aop{tmode ? reinterpret_cast<const u16*>(smem + ly.xt_off) : R, RS, tmode};
+  if (nxw != nullptr && !last) nxw->issue(l + 1);   // (its latency hides behind this layer's GEMM)
   fst(0);
+  // the last layer's bias moments for the in-epilogue update (persistent kernel)
+  float vm_pre[T::NTW], vv_pre[T::NTW];
+  if constexpr (PS && TRAIN) {
+    if (last && vo.o != nullptr) {
+#pragma unroll
+      for (int j = 0; j < T::NTW; ++j)
+        if (j * RX_NW < ntiles) ps_vec_prefetch(vo, ly, lg, min(wave + j * RX_NW, ntiles - 1) * 16 + lr, vm_pre[j], vv_pre[j]);
+    }
+  }
 
   f32x4 acc[T::NTW * MT];
 #pragma unroll
@@ -610,8 +747,18 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     for (int mt = 0; mt < MT; ++mt) part[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int n = wave + j * RX_NW;
     if (n < ntiles) {
-      const int boff = ly.w_img + (n * 16 + lr) * ly.in_k;
-      gemm_tile_pre<MT, PS>(part, Aop, lane, img, boff, ly.in_k, lg, wpre, j);
+      if (w0b != nullptr || (l == 0 && d.w0s_lds_off >= 0)) {
+        // layer 0 in the k order pi (fwd_prefetch): B from the registers ps_l0_update left (the
+        // persistent epoch) or from the prefetched image fragments; the A reads follow pi
+        if (j < RX_W0J) {
+          const bf16x8 bw = w0b != nullptr ? w0b[j] : wpre[j][0];
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) part[mt] = rx_mfma16(ld_afrag_pi<MT>(Aop, mt, lane), bw, part[mt]);
+        }
+      } else {
+        const int boff = ly.w_img + (n * 16 + lr) * ly.in_k;
+        gemm_tile_pre<MT, PS>(part, Aop, lane, img, boff, ly.in_k, lg, wpre, j);
+      }
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = part[mt];
@@ -620,8 +767,11 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   // the next layer's weights travel while this layer's epilogue runs -- issued before this
   // layer's stores (the X^T export, the saved BN inputs), so the next GEMM's wait for them does
   // not also wait for those stores
-  if (!last) fwd_prefetch<PS>(nx, img, wpre);
-  if (TRAIN && d.wgrad_mode == 1) {  // X^T_l (published by the previous layer / the input load)
+  if (!last) {
+    if (nxw != nullptr) nxw->wait(l + 1);
+    fwd_prefetch<PS>(nx, img, wpre);
+  }
+  if (TRAIN && d.wgrad_mode == 1 && w0b == nullptr) {  // X^T_l (published by the previous layer / the input load)
     if constexpr (MWT::on)
       export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
                           ps_wt, mw->G * T::BP, mw->wg * T::BP);
@@ -738,6 +888,79 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       const float inv_n = inv_nb * (1.f / (float)ly.out);
       const int lcode = d.loss;
       const float beta = d.beta;
+      if constexpr (!MWT::on) {
+        if (d.loss_lds_off >= 0 && lcode != 4) {
+          // One output column: only the 4 lanes of column 0 hold real values (MT * 4 rows
+          // each), so the tile-layout loss would run its terms 4 * MT times per lane on 4 lanes.
+          // Those lanes pass their rows through LDS instead, every lane takes one row (two at
+          // 128 rows), and dL/dy goes back the same way into the accumulator layout.
+          constexpr int RPL = T::BP > 64 ? T::BP / 64 : 1;   // rows per lane
+          float* xs = reinterpret_cast<float*>(smem + d.loss_lds_off);
+          if (lr == 0) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<f32x4*>(xs + mt * 16 + lg * 4) = acc[j * MT + mt];
+          }
+          const float hb = 0.5f * beta, inv_beta = 1.f / beta, h_inv_beta = 0.5f * inv_beta;
+          float gv[RPL];
+#pragma unroll
+          for (int k = 0; k < RPL; ++k) {
+            const int row = lane + 64 * k;
+            const bool inb = row < T::BP;
+            const bool ok = inb && (FULL || row < nvalid);
+            const float x = inb ? xs[row] : 0.f;
+            const float t = lab_pre != nullptr ? lab_pre[k] : rx_g(labels)[rowidx[inb ? row : 0] * d.out_dim];
+            const float e = x - t;
+            const float ae = fabsf(e);
+            float li, gi;
+            if (lcode == 3) {
+              li = fmaxf(x, 0.f) - x * t + log1pf(__expf(-fabsf(x)));
+              gi = 1.f / (1.f + __expf(-x)) - t;
+            } else {
+              const bool quad = ae < beta;
+              li = quad ? e * e * h_inv_beta : ae - hb;
+              const float sgn = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+              gi = lcode == 0 ? 2.f * e : (lcode == 1 && quad ? e * inv_beta : sgn);
+            }
+            lsum += ok ? li : 0.f;
+            asum += ok ? ae : 0.f;
+            ssum = ok ? fmaf(e, e, ssum) : ssum;
+            if (d.acc_mode == 1) csum += (ok && (x > d.acc_thr ? 1 : 0) == (int)t) ? 1.f : 0.f;
+            gv[k] = ok ? gi * inv_n : 0.f;
+            gsum += gv[k];
+          }
+          lsum = rx_wavesum(lsum);
+          asum = rx_wavesum(asum);
+          ssum = rx_wavesum(ssum);
+          if (d.acc_mode == 1) csum = rx_wavesum(csum);
+          if (lcode == 0) lsum = ssum;
+          else if (lcode == 2) lsum = asum;
+          if (lane == 0) {
+            atomicAdd(&metrics[0], (double)(lsum * inv_n));
+            atomicAdd(&metrics[1], (double)asum);
+            atomicAdd(&metrics[2], (double)ssum);
+            if (d.acc_mode == 1) atomicAdd(&metrics[5], (double)csum);
+            atomicAdd(&metrics[3], (double)nvalid);
+            atomicAdd(&metrics[4], 1.0);
+          }
+          if (TRAIN) {
+#pragma unroll
+            for (int k = 0; k < RPL; ++k)
+              if (lane + 64 * k < T::BP) xs[lane + 64 * k] = gv[k];
+            if (lr == 0) {
+#pragma unroll
+              for (int mt = 0; mt < MT; ++mt) acc[j * MT + mt] = *reinterpret_cast<const f32x4*>(xs + mt * 16 + lg * 4);
+            }
+            gsum = rx_wavesum(gsum);
+            if (lane == 0 && ly.b_off >= 0) Gr[ly.b_off] = gsum;
+            if constexpr (PS) {
+              if (vo.o != nullptr && lg == 0)
+                ps_vec_update(vo, ly, reinterpret_cast<float*>(smem + d.pr_lds_off), 0, c, colok, gsum, vm_pre[j],
+                              vv_pre[j]);
+            }
+          }
+          return;
+        }
+      }
       // labels of all padded rows, loaded back to back (padded rows read row 0)
       const int cl = colok ? c : 0;
       float tl[MT * 4];
@@ -814,6 +1037,11 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         if (TRAIN) {
           gsum = rx_colsum16(gsum);
           if (colok && lg == 0 && ly.b_off >= 0) Gr[ly.b_off + c] = gsum;
+          if constexpr (PS) {
+            if (vo.o != nullptr && lg == 0)
+              ps_vec_update(vo, ly, reinterpret_cast<float*>(smem + d.pr_lds_off), 0, c, colok, gsum, vm_pre[j],
+                            vv_pre[j]);
+          }
         }
       } else {
         // branch-free: every element computes its terms, invalid ones (padded rows / columns)
@@ -882,6 +1110,11 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
               rx_st_sc1f(mw_bias(mw->part, mw->stride, ly, mw->wg) + c, gsum);
             else
               Gr[ly.b_off + c] = gsum;
+          }
+          if constexpr (PS) {
+            if (vo.o != nullptr && lg == 0)
+              ps_vec_update(vo, ly, reinterpret_cast<float*>(smem + d.pr_lds_off), 0, c, colok, gsum, vm_pre[j],
+                            vv_pre[j]);
           }
         }
       }  // regression / BCE losses
@@ -964,13 +1197,13 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
 // PS (persistent epoch kernel): once this layer's dgrad has read its last weight byte and its
 // G^T export has drained, lane 0 publishes flag `sync[32 l] = step + 1` -- the optimizer
 // workgroups of layer l may then compute dW_l and rewrite W_l / Wt_l while the backward goes on.
-template <int MT, bool PS, bool FULL = false, class D, class LY, class PV, class MWT = NoMw>
+template <int MT, bool PS, bool FULL = false, class D, class LY, class PV, class MWT = NoMw, class VO = PsVec<>>
 __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const PV& pv, int l, char* smem,
                                                const u16* __restrict__ img, const float* __restrict__ P,
                                                float* __restrict__ Gr, int nvalid, const float* __restrict__ scratch,
                                                unsigned long long* __restrict__ stamps,
                                                unsigned* __restrict__ sync = nullptr, int step = 0,
-                                               bool ps_wt = true, MWT* mw = nullptr) {
+                                               bool ps_wt = true, MWT* mw = nullptr, VO vo = VO{}) {
   using T = Tile<MT>;
   const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
   const int lr = lane & 15, lg = lane >> 4;
@@ -1001,6 +1234,16 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
           for (int r = 0; r < 4; ++r) svp[j][mt * 4 + r] = t[r];
         }
       }
+    }
+  }
+  // moments of the parameters of layer l-1 this lane updates in the post-op (persistent kernel)
+  float vm_pre[T::NTW], vv_pre[T::NTW];
+  if constexpr (PS) {
+    if (l != 0 && vo.o != nullptr) {
+#pragma unroll
+      for (int j = 0; j < T::NTW; ++j)
+        if (j * RX_NW < ntiles_d)
+          ps_vec_prefetch(vo, pv, lg, min(wave + j * RX_NW, ntiles_d - 1) * 16 + lr, vm_pre[j], vv_pre[j]);
     }
   }
 
@@ -1163,6 +1406,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 #pragma unroll
       for (int r = 0; r < 4; ++r) g[mt * 4 + r] = gm[r];
     }
+    float sg = 0.f, sgx = 0.f;   // batch sums of dL/dy and dL/dy * x_hat (BatchNorm)
     if (pv.bn == 0) {
       if (pv.act == 1) {
 #pragma unroll
@@ -1189,7 +1433,6 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
           for (int r = 0; r < 4; ++r) g4[mt][r] = fmaf(xh4[mt][r], gam, bet) > 0.f ? g4[mt][r] : 0.f;
         }
       }
-      float sg, sgx;
       if (mode == 2) {
         sg = bsg[j];
         sgx = bsgx[j];
@@ -1246,6 +1489,11 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
         rx_st_sc1f(mw_bias(mw->part, mw->stride, pv, mw->wg) + c, bs);
       else
         Gr[pv.b_off + c] = bs;
+    }
+    if constexpr (PS) {
+      if (vo.o != nullptr)
+        ps_vec_update(vo, pv, reinterpret_cast<float*>(smem + d.pr_lds_off), lg, c, colok,
+                      lg == 0 ? bs : (lg == 1 ? sgx : sg), vm_pre[j], vv_pre[j]);
     }
     // publish G_{l-1}: transposed into GT, row-major into R (quad-transposed 8-B stores)
     uint2 pk[MT];
@@ -1350,6 +1598,12 @@ template <int MT, bool PS, class D>
 __device__ __forceinline__ void prefetch_labels(const D& d, const float* __restrict__ labels, const int* rowidx,
                                                 float (&tl)[MT * 4]) {
   const int lane = rx_tid<PS>() & 63, lr = lane & 15, lg = lane >> 4;
+  if (d.loss_lds_off >= 0 && d.loss != 4) {   // the row-per-lane loss (layer_forward): row lane + 64 k
+    constexpr int BP = Tile<MT>::BP;
+#pragma unroll
+    for (int k = 0; k < (BP > 64 ? BP / 64 : 1); ++k) tl[k] = rx_g(labels)[rowidx[lane + 64 * k < BP ? lane + 64 * k : 0] * d.out_dim];
+    return;
+  }
   const int cl = lr < d.out_dim ? lr : 0;
 #pragma unroll
   for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
@@ -1464,6 +1718,9 @@ __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem
   need_t = need_t || tmode;
   u16* R = reinterpret_cast<u16*>(smem + d.r_lds_off);
   u16* XT = reinterpret_cast<u16*>(smem + l0.xt_off);
+  // persistent epoch with layer 0 updated in the step workgroup: a second copy of X^T_0 that
+  // outlives the forward (the transposed image is reused by every later layer)
+  u16* XC = d.x0c_lds_off >= 0 ? reinterpret_cast<u16*>(smem + d.x0c_lds_off) : nullptr;
   const int in_n = l0.in_n;
   const int chunks = d.feat_k >> 3;  // 8 bf16 per 16-B chunk
   if (tmode && l0.in_k > in_n) {    // K tail rows [in_n, in_k) of XT_0 (never written below)
@@ -1480,10 +1737,46 @@ __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem
       for (int e = 0; e < 8; ++e) {
         const int k = ch * 8 + e;
         if (k < in_n) XT[T::tix(k, row)] = h[e];
+        if (XC != nullptr && k < in_n) XC[T::tix(k, row)] = h[e];
       }
     }
   }
   __syncthreads();
+}
+
+// The batch gather split in two for the persistent step's prefetch (mlp_persist.h): the global
+// read of chunk `idx` (row idx / chunks, 16 B of its features; zeros past nvalid) issued during
+// the previous step's backward and kept in a register, and its LDS scatter at the start of the
+// step -- one chunk per thread (BP * feat_k / 8 <= RX_THREADS), no embedding front.
+template <int MT, class D>
+__device__ __forceinline__ u32x4 gather_input_chunk(const D& d, const u16* __restrict__ feats, const int* rowidx,
+                                                   int nvalid, int idx) {
+  const int chunks = d.feat_k >> 3;
+  const int row = idx / chunks, ch = idx - (idx / chunks) * chunks;
+  const int r = row < Tile<MT>::BP ? row : 0;
+  const u32x4 v = *reinterpret_cast<const RX_GLOBAL u32x4*>(rx_g(feats) + (size_t)rowidx[r] * d.feat_k + ch * 8);
+  return row < nvalid ? v : u32x4{0u, 0u, 0u, 0u};
+}
+template <int MT, class D, class L0>
+__device__ __forceinline__ void scatter_input_chunk(const D& d, const L0& l0, char* smem, int idx, const u32x4& v) {
+  using T = Tile<MT>;
+  const int chunks = d.feat_k >> 3;
+  const int row = idx / chunks, ch = idx - (idx / chunks) * chunks;
+  if (row >= T::BP) return;
+  const bool tmode = d.r_lds_off < 0;
+  const int RS = d.max_k + RX_RPAD;
+  if (!tmode) *reinterpret_cast<u32x4*>(reinterpret_cast<u16*>(smem + d.r_lds_off) + row * RS + ((ch ^ rx_rsw(row)) << 3)) = v;
+  u16* XT = reinterpret_cast<u16*>(smem + l0.xt_off);
+  u16* XC = d.x0c_lds_off >= 0 ? reinterpret_cast<u16*>(smem + d.x0c_lds_off) : nullptr;
+  const u16* h = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = ch * 8 + e;
+    if (k < l0.in_n) {
+      XT[T::tix(k, row)] = h[e];
+      if (XC != nullptr) XC[T::tix(k, row)] = h[e];
+    }
+  }
 }
 
 // One training step (forward, loss, backward -> gradients in Gr) for rows
@@ -1505,7 +1798,7 @@ __device__ __forceinline__ void mlp_train_step_body(
   } while (0)
   RX_STAMP();
   bf16x8 wpre[RX_PJ][RX_PK];
-  fwd_prefetch<false>(C::first(d), img, wpre);
+  fwd_prefetch<false>(C::first(d), img, wpre, d.w0s_lds_off >= 0);
   for (int i = rx_tid<false>(); i < Tile<MT>::BP; i += RX_THREADS)
     rowidx[i] = i < nvalid ? (perm ? rx_g(perm)[row0 + i] : row0 + i) : (perm ? rx_g(perm)[row0] : row0);
   load_params<C>(d, smem, P, rstats);
@@ -1556,7 +1849,7 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
   const int r0 = row0 + mw.wg * BP;
   float* sc = scratch + (size_t)mw.wg * (size_t)scratch_stride;
   bf16x8 wpre[RX_PJ][RX_PK];
-  fwd_prefetch<false>(C::first(d), img, wpre);
+  fwd_prefetch<false>(C::first(d), img, wpre, d.w0s_lds_off >= 0);
   // padded rows (and every row of a workgroup past a short last batch) read the batch's first
   // row: always inside the input, masked to zero on load
   for (int i = rx_tid<false>(); i < BP; i += RX_THREADS)
@@ -1623,7 +1916,7 @@ __device__ __forceinline__ void mlp_eval_body(const MlpDesc* __restrict__ dp, co
     load_params<C>(d, smem, P, rstats);
     __syncthreads();
     load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, false, dp, P, metrics);
-    fwd_prefetch<false>(C::first(d), img, wpre);
+    fwd_prefetch<false>(C::first(d), img, wpre, d.w0s_lds_off >= 0);
     MwCtx ev{};
     ev.n_total = nb;   // the loss mean runs over the whole batch; chunk 0 counts the batch
     ev.wg = q;
@@ -1640,9 +1933,9 @@ __device__ __forceinline__ void mlp_eval_body(const MlpDesc* __restrict__ dp, co
   load_params<C>(d, smem, P, rstats);
   __syncthreads();
   load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, false, dp, P, metrics);
-  fwd_prefetch<false>(C::first(d), img, wpre);
+  fwd_prefetch<false>(C::first(d), img, wpre, d.w0s_lds_off >= 0);
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
     layer_forward<MT, false, false>(d, ly, nx, last, smem, img, P, nullptr, labels, rowidx, nvalid, nullptr, metrics,
-                             wpre);
+                                    wpre, true, l);
   });
 }

@@ -33,14 +33,22 @@ struct OptDesc {
   int act_floats;  // its size
   int bp;          // padded batch rows (K of the optimizer-side wgrad)
   int wgrad_mode;  // mirrors MlpDesc::wgrad_mode
+  int ps_l0_inline; // persistent epoch: layer 0's weight is updated by the step workgroup itself
+                    // (MlpDesc::w0s_lds_off), no optimizer workgroups for its segment
 };
 
 // One element: p, m, v in registers (the persistent kernel keeps them there for a whole epoch).
 // Every multiply-add is an explicit fmaf: left to the compiler, contraction depends on the
 // inlining context, and the same update would round differently in the launch-per-step
 // optimizer kernel and in the persistent kernel (the two must agree bit for bit).
-__device__ __forceinline__ void opt_update_reg(const OptDesc& o, float& pv, float& mv, float& vv, float gsum,
-                                               float lr, float bc1, float bc2, float gscale, int first) {
+// `o`: the runtime descriptor, or (specialised kernels) an empty struct whose hyperparameters are
+// static constexpr members -- the branches on the algorithm fold away. nlr_bc1 = -(lr / bc1) and
+// rs_bc2 = 1 / sqrt(bc2) are the step's element-independent factors (opt_update_reg computes
+// them from lr, bc1, bc2; a caller updating elements one at a time passes them precomputed --
+// the same values, so the same bits).
+template <class O>
+__device__ __forceinline__ void opt_update_pre(const O& o, float& pv, float& mv, float& vv, float gsum, float lr,
+                                               float nlr_bc1, float rs_bc2, float gscale, int first) {
   float gr = gsum * gscale;
   if (o.maximize) gr = -gr;
   if (o.algo == 2) {
@@ -56,13 +64,18 @@ __device__ __forceinline__ void opt_update_reg(const OptDesc& o, float& pv, floa
     else if (o.wd != 0.f) gr = fmaf(o.wd, pv, gr);
     mv = fmaf(o.b1, mv, (1.f - o.b1) * gr);
     vv = fmaf(o.b2, vv, ((1.f - o.b2) * gr) * gr);
-    // element-independent factors are exact (hoisted by the compiler); the per-element sqrt /
-    // reciprocal are the 1-ulp hardware ones (v_sqrt_f32 / v_rcp_f32) instead of the ~10-
-    // instruction correctly rounded sequences: the update is VALU-bound where one workgroup
-    // updates many elements (the persistent kernel's vector parameters)
-    const float den = fmaf(__builtin_amdgcn_sqrtf(vv), 1.f / sqrtf(bc2), o.eps);
-    pv = fmaf(-(lr / bc1), mv * __builtin_amdgcn_rcpf(den), pv);
+    // the per-element sqrt / reciprocal are the 1-ulp hardware ones (v_sqrt_f32 / v_rcp_f32)
+    // instead of the ~10-instruction correctly rounded sequences: the update is VALU-bound where
+    // one workgroup updates many elements
+    const float den = fmaf(__builtin_amdgcn_sqrtf(vv), rs_bc2, o.eps);
+    pv = fmaf(nlr_bc1, mv * __builtin_amdgcn_rcpf(den), pv);
   }
+}
+
+template <class O>
+__device__ __forceinline__ void opt_update_reg(const O& o, float& pv, float& mv, float& vv, float gsum, float lr,
+                                               float bc1, float bc2, float gscale, int first) {
+  opt_update_pre(o, pv, mv, vv, gsum, lr, -(lr / bc1), 1.f / sqrtf(bc2), gscale, first);
 }
 
 // gsum: this element's gradient (summed over ranks when the reduction is fused in)

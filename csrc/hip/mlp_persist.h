@@ -7,7 +7,8 @@
 // backward layer. Here:
 //   * block 0 (the step workgroup) runs forward + loss + backward exactly as the step kernel does
 //     (mlp_core.h, PS = true), keeps the bias / BatchNorm parameters and running statistics in
-//     LDS for the whole epoch and updates those vector parameters itself at the end of each step;
+//     LDS for the whole epoch and updates those vector parameters itself, inside the epilogue
+//     that produces each gradient (mlp_core.h PsVec);
 //   * blocks 1.. (optimizer workgroups) each own two 32x32 tiles of one Linear weight, with the
 //     fp32 master weight and both Adam moments of those tiles in REGISTERS for the whole epoch.
 //     As soon as the backward has finished with layer l (its G^T exported and its dgrad done),
@@ -71,36 +72,46 @@ __device__ __forceinline__ unsigned rx_xcc_id() {
 // optimizer workgroups of a weight segment (two 32x32 tiles each)
 __host__ __device__ __forceinline__ int ps_seg_blocks(const OptSeg& sg) { return (opt_seg_blocks(sg) + 1) / 2; }
 
+// optimizer workgroups of the l-th weight segment (q: its index in o.seg); none for layer 0 when
+// the step workgroup updates it itself (OptDesc::ps_l0_inline)
+__host__ __device__ __forceinline__ int ps_seg_workers(const OptDesc& o, int q, int l) {
+  return (l == 0 && o.ps_l0_inline) ? 0 : ps_seg_blocks(o.seg[q]);
+}
+
 __host__ __device__ __forceinline__ int ps_grid_blocks(const OptDesc& o) {
-  int nb = 1;
+  int nb = 1, l = 0;
   for (int s = 0; s < o.nseg; ++s)
-    if (o.seg[s].kind == 1) nb += ps_seg_blocks(o.seg[s]);
+    if (o.seg[s].kind == 1) nb += ps_seg_workers(o, s, l++);
   return nb;
 }
 
-// Bias / BatchNorm gamma, beta of every layer: one optimizer update per element from this
-// step's gradients in Gr (written by this workgroup), parameters in the LDS parameter block.
-// The elements of all layers are dealt round-robin over the 512 threads (column-per-thread would
-// leave the first 16 threads with 15 updates each while 256 threads idle: the update is VALU
-// bound), and every gradient / moment load of a thread's elements is issued before its first
-// update.
+// Bias / BatchNorm gamma, beta of every layer: one optimizer update per element from a step's
+// gradients in Gr (written by this workgroup), parameters in the LDS parameter block.
+// The elements of all layers are dealt round-robin over the worker threads [64, 512) -- waves
+// 1..7; wave 0 meanwhile polls the optimizer workgroups' layer counters, so the update of step
+// s - 1 runs in the shadow of the wait for layer 0's new weights of step s (column-per-thread
+// would leave the first 16 threads with 15 updates each: the update is VALU bound) -- and every
+// gradient / moment load of a thread's elements is issued before its first update.
+#define RX_PS_VEC_T0 64
 template <class C, class D>
 __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, char* smem, const float* __restrict__ Gr,
                                                  float* __restrict__ m, float* __restrict__ v, float lr, float bc1,
                                                  float bc2, int first) {
   constexpr int J = 4;  // elements per thread per pass
+  constexpr int NW = RX_THREADS - RX_PS_VEC_T0;
   float* pr = reinterpret_cast<float*>(smem + d.pr_lds_off);
   int total = 0;
   C::each_layer(d, [&](const auto& ly, int) {
     total += ((ly.b_off >= 0) + (ly.g_off >= 0) + (ly.be_off >= 0)) * ly.out;
   });
-  const int tid = rx_tid();
-  for (int e0 = 0; e0 < total; e0 += J * RX_THREADS) {
+  const int tid = rx_tid() - RX_PS_VEC_T0;
+  if (tid < 0) return;
+  for (int e0 = 0; e0 < total; e0 += J * NW) {
     int idx[J], slot[J];
     float g[J], mv[J], vv[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int e = e0 + j * RX_THREADS + tid;
+      const int e = e0 + j * NW + tid;
       int base = 0, id = -1, sl = 0;
       C::each_layer(d, [&](const auto& ly, int) {
         const int offs[3] = {ly.b_off, ly.g_off, ly.be_off};
@@ -148,6 +159,186 @@ __device__ __forceinline__ void ps_store_vectors(const D& d, const char* smem, f
   });
 }
 
+// Layer l's weights are first read where layer l-1's forward prefetches them: each wave reads
+// layer l's optimizer counter at the start of layer l-1 (issue) and compares it with this step's
+// target there (wait), polling on only if the optimizer workgroups are not done yet -- no wait for
+// every layer at the start of the step, no workgroup barrier (every wave that reads the weights
+// has matched the counter itself: MI355X_MICROARCH.md valid forms, first row). After a timeout
+// or another workgroup's failure the waits stop: the epoch runs to its end and the host rolls it
+// back.
+struct PsNxWait {
+  unsigned* sync;
+  const int* workers;       // LDS: optimizer workgroups per layer
+  int s;
+  unsigned long long ticks;
+  unsigned v = 0;
+  __device__ void issue(int l) { v = rx_ps_load(sync + RX_PS_CNT(l)); }
+  __device__ void wait(int l) {
+    const unsigned target = (unsigned)(workers[l] * s);
+    if (__builtin_amdgcn_readfirstlane(v) >= target) return;
+    const unsigned long long t0 = wall_clock64();
+    for (int k = 1;; ++k) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_readfirstlane(rx_ps_load(sync + RX_PS_CNT(l))) >= target) return;
+      if ((k & 15) == 0) {
+        if (__builtin_amdgcn_readfirstlane(rx_ps_load(sync + RX_PS_ERR)) != 0u) return;
+        if (wall_clock64() - t0 > ticks) {
+          if ((rx_tid() & 63) == 0)
+            __hip_atomic_store(rx_g(sync) + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return;
+        }
+      }
+    }
+  }
+};
+
+// ---- layer 0 updated by the step workgroup (OptDesc::ps_l0_inline) ----
+// Layer 0's update sat between one step's backward and the next step's forward: G^T_0 export ->
+// flag -> optimizer workgroups (sc1 reads of X^T_0 / G^T_0, wgrad, update, image stores) ->
+// counter -> the step workgroup's weight reads, ~4 us of hand-off latency per step (profiles/
+// r5_persist_*). Its weight is small (NYC: 256 x 20): the step workgroup keeps the fp32 master
+// and both moments in LDS (w0s_lds_off), computes dW_0^T = X_0^T G_0 from its own LDS images (the
+// X^T_0 copy load_inputs kept, G^T_0 the backward left), updates, and keeps the new bf16 weight
+// in REGISTERS as the next forward's B fragments: wave w owns output tiles n = w + 8 j (j < 2,
+// as in the forward) and both 16-column halves mi of the K = 32 input padding, so lane (lr, lg)
+// holds W_0[16 n + lr][16 mi + 4 lg + r] -- a forward B fragment in the k order pi (mlp_core.h
+// ld_afrag_pi). Eligible: one workgroup, in <= 20, in_k == 32, out == out_n <= 256.
+// State slots (fp32 each of master | m | v, real elements only): half mi = 0 at
+// ((2 w + j) 64 + lane) 4 + r, half mi = 1 (lanes lg == 0: columns 16..19) at
+// 16 * 64 * 4 + ((2 w + j) 16 + lr) 4 + r.
+#define RX_W0S_N (16 * 64 * 4 + 16 * 16 * 4)   // elements per array (5120)
+
+__device__ __forceinline__ int ps_w0_slot(int w, int j, int mi, int lane) {
+  return mi == 0 ? ((2 * w + j) * 64 + lane) * 4 : 16 * 64 * 4 + ((2 * w + j) * 16 + (lane & 15)) * 4;
+}
+
+// epoch start: state from P / m / v (row-major [out][in] at w_off), B fragments from the master
+template <class LY>
+__device__ __forceinline__ void ps_l0_load(const LY& ly, char* smem, int w0s_off, const float* __restrict__ P,
+                                           const float* __restrict__ m, const float* __restrict__ v,
+                                           bf16x8 (&w0b)[RX_W0J]) {
+  const int lane = rx_tid() & 63, wave = rx_wave(), lr = lane & 15, lg = lane >> 4;
+  float* S = reinterpret_cast<float*>(smem + w0s_off);
+  const int ntiles = ly.out_n >> 4;
+#pragma unroll
+  for (int j = 0; j < RX_W0J; ++j) {
+    const int n = wave + j * RX_NW;
+    float h[8];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int i0 = 16 * mi + 4 * lg;
+      const int slot = ps_w0_slot(wave, j, mi, lane);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool real = n < ntiles && i0 + r < ly.in;
+        const int idx = ly.w_off + (n * 16 + lr) * ly.in + i0 + r;
+        const float pv = real ? rx_g(P)[idx] : 0.f;
+        if (real) {
+          S[slot + r] = pv;
+          S[RX_W0S_N + slot + r] = rx_g(m)[idx];
+          S[2 * RX_W0S_N + slot + r] = rx_g(v)[idx];
+        }
+        h[4 * mi + r] = pv;
+      }
+    }
+    w0b[j] = __builtin_bit_cast(bf16x8, u32x4{rx_f2bf2(h[0], h[1]), rx_f2bf2(h[2], h[3]), rx_f2bf2(h[4], h[5]),
+                                              rx_f2bf2(h[6], h[7])});
+  }
+}
+
+// end of a step's backward (G^T_0 in the transposed image): dW_0, the update, the new B fragments
+template <int MT, class D, class LY, class O>
+__device__ __forceinline__ void ps_l0_update(const D& d, const LY& ly, char* smem, const O& hp, const float* vsc,
+                                             bf16x8 (&w0b)[RX_W0J]) {
+  using T = Tile<MT>;
+  constexpr int KS = T::BP / 32;
+  const int lane = rx_tid() & 63, wave = rx_wave(), lr = lane & 15, lg = lane >> 4;
+  const u16* GT = reinterpret_cast<const u16*>(smem + d.gt_lds_off);
+  const u16* XC = reinterpret_cast<const u16*>(smem + d.x0c_lds_off);
+  float* S = reinterpret_cast<float*>(smem + d.w0s_lds_off);
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(vsc);   // lr, -(lr / bc1), 1 / sqrt(bc2), first
+  const int first = sc[3] != 0.f ? 1 : 0;
+  const int ntiles = ly.out_n >> 4;
+#pragma unroll
+  for (int j = 0; j < RX_W0J; ++j) {
+    const int n = wave + j * RX_NW;
+    if (n >= ntiles) continue;
+    bf16x8 gb[KS], xa[2][KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      gb[ks] = *reinterpret_cast<const bf16x8*>(GT + T::tix(n * 16 + lr, ks * 32 + 8 * lg));
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+        xa[mi][ks] = *reinterpret_cast<const bf16x8*>(XC + T::tix(16 * mi + lr, ks * 32 + 8 * lg));
+    }
+    float h[8];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) a4 = rx_mfma16(xa[mi][ks], gb[ks], a4);
+      const bool real = 16 * mi + 4 * lg < ly.in;   // (the slot exists; its columns past `in` stay 0)
+      const int slot = ps_w0_slot(wave, j, mi, lane);
+      f32x4 pv = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (real) {
+        pv = *reinterpret_cast<const f32x4*>(S + slot);
+        f32x4 mv = *reinterpret_cast<const f32x4*>(S + RX_W0S_N + slot);
+        f32x4 vv = *reinterpret_cast<const f32x4*>(S + 2 * RX_W0S_N + slot);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (16 * mi + 4 * lg + r < ly.in) {
+            float p_ = pv[r], m_ = mv[r], v_ = vv[r];
+            opt_update_pre(hp, p_, m_, v_, a4[r], sc[0], sc[1], sc[2], 1.f, first);
+            pv[r] = p_;
+            mv[r] = m_;
+            vv[r] = v_;
+          }
+        }
+        *reinterpret_cast<f32x4*>(S + slot) = pv;
+        *reinterpret_cast<f32x4*>(S + RX_W0S_N + slot) = mv;
+        *reinterpret_cast<f32x4*>(S + 2 * RX_W0S_N + slot) = vv;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[4 * mi + r] = 16 * mi + 4 * lg + r < ly.in ? pv[r] : 0.f;   // padding: 0
+    }
+    w0b[j] = __builtin_bit_cast(bf16x8, u32x4{rx_f2bf2(h[0], h[1]), rx_f2bf2(h[2], h[3]), rx_f2bf2(h[4], h[5]),
+                                              rx_f2bf2(h[6], h[7])});
+  }
+}
+
+// epoch end: master / moments back to P / m / v, the bf16 W_0 image (zeros in its padding)
+template <class LY>
+__device__ __forceinline__ void ps_l0_store(const LY& ly, const char* smem, int w0s_off, float* __restrict__ P,
+                                            float* __restrict__ m, float* __restrict__ v, u16* __restrict__ W) {
+  const int lane = rx_tid() & 63, wave = rx_wave(), lr = lane & 15, lg = lane >> 4;
+  const float* S = reinterpret_cast<const float*>(smem + w0s_off);
+  const int ntiles = ly.out_n >> 4;
+#pragma unroll
+  for (int j = 0; j < RX_W0J; ++j) {
+    const int n = wave + j * RX_NW;
+    if (n >= ntiles) continue;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int i0 = 16 * mi + 4 * lg;
+      const int slot = ps_w0_slot(wave, j, mi, lane);
+      float h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool real = i0 + r < ly.in;
+        h[r] = real ? S[slot + r] : 0.f;
+        if (real) {
+          const int idx = ly.w_off + (n * 16 + lr) * ly.in + i0 + r;
+          rx_g(P)[idx] = h[r];
+          rx_g(m)[idx] = S[RX_W0S_N + slot + r];
+          rx_g(v)[idx] = S[2 * RX_W0S_N + slot + r];
+        }
+      }
+      *reinterpret_cast<RX_GLOBAL rx_u32x2*>(rx_g(W) + ly.w_img + (n * 16 + lr) * ly.in_k + i0) =
+          rx_u32x2{rx_f2bf2(h[0], h[1]), rx_f2bf2(h[2], h[3])};
+    }
+  }
+}
+
 // stamps[0..31]: phase stamps of the middle step (diagnostics); stamps[32 + s]: start of step s,
 // stamps[32 + nsteps]: end of the last step; stamps[33 + nsteps + k], k < RX_PS_LAYER_STAMPS:
 // the middle step's intra-layer shader-clock stamps (s_memtime; layer_forward [40 + 5 l + k],
@@ -186,9 +377,40 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     flag_lds[1] = same ? 0 : 1;
   }
   load_params<C>(d, smem, P, rstats);
+  // optimizer workgroups per layer (PsNxWait targets), in LDS
+  int* workers = flag_lds + 8;
+  if (rx_tid() == 0) {
+    int l = 0;
+    for (int q = 0; q < o.nseg && l < RX_MAXL; ++q)
+      if (o.seg[q].kind == 1) {
+        workers[l] = ps_seg_workers(o, q, l);
+        ++l;
+      }
+  }
+  // layer 0 updated here (see ps_l0_update): its state into LDS, its first B fragments
+  const bool l0_in = o.ps_l0_inline != 0 && d.w0s_lds_off >= 0;
+  bf16x8 w0b[RX_W0J];
+  if (l0_in) ps_l0_load(C::first(d), smem, d.w0s_lds_off, P, m, v, w0b);
   __syncthreads();
   if (flag_lds[0]) return;
   const bool ps_wt = flag_lds[1] != 0;
+  // bias / BatchNorm affine updates inside the epilogues (mlp_core.h PsVec) unless the last
+  // layer carries a BatchNorm (its affine gradients are not produced by a post-op)
+  bool last_affine = false;
+  C::each_layer(d, [&](const auto& ly, int) { last_affine = ly.g_off >= 0 || ly.be_off >= 0; });
+  const bool vec_inline = !last_affine;
+  using O = typename rx_opt_type<C>::type;
+  const rx_opt_holder<O> oh;
+  const O& oc = oh.get(o);
+  float* vsc = reinterpret_cast<float*>(flag_lds + 4);   // the step's optimizer scalars (PsVec::sc)
+  // next-batch prefetch during the backward (one input chunk per thread, no embedding front):
+  // rowidx holds 2 BP entries, the second half the next step's rows
+  const bool pf = Tile<MT>::BP * (d.feat_k >> 3) <= RX_THREADS && d.front_n == 0;
+  int* rowidx_n = rowidx + Tile<MT>::BP;
+  u32x4 xin = u32x4{0u, 0u, 0u, 0u};
+  float labn[MT * 4], labp[MT * 4];
+#pragma unroll
+  for (int q = 0; q < MT * 4; ++q) labn[q] = 0.f;
   for (int s = 0; s < nsteps; ++s) {
     stamp(s, 0);
     // per-step start times (stamps[32 + s], one lane, one vector store): the step-time
@@ -196,16 +418,39 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     if (stamps != nullptr && rx_tid() == 0) rx_g(stamps)[RX_PS_STEP_STAMPS + s] = wall_clock64();
     const int row0 = s * batch;
     const int nvalid = min(batch, n_rows - row0);
-    for (int i = rx_tid(); i < Tile<MT>::BP; i += RX_THREADS)
-      rowidx[i] = i < nvalid ? (perm ? rx_g(perm)[row0 + i] : row0 + i) : (perm ? rx_g(perm)[row0] : row0);
-    __syncthreads();
-    // the batch gather does not depend on the weights: it overlaps the last optimizer tiles
-    load_inputs<MT, true>(d, C::first(d), smem, feats, rowidx, nvalid, true, dp, P, metrics);
-    float labp[MT * 4];
-    prefetch_labels<MT, true>(d, labels, rowidx, labp);
+    if (rx_tid() == 0) {
+      const float lr = rx_g(sched)[s], bc1 = rx_g(sched)[nsteps + s], bc2 = rx_g(sched)[2 * nsteps + s];
+      *reinterpret_cast<f32x4*>(vsc) = f32x4{lr, -(lr / bc1), 1.f / sqrtf(bc2), (opt_first && s == 0) ? 1.f : 0.f};
+    }
+    if (s > 0 && pf) {
+      // this batch was fetched during the previous step's backward: rows, features and labels
+      // are already in registers / the second row-index array
+      for (int i = rx_tid(); i < Tile<MT>::BP; i += RX_THREADS) rowidx[i] = rowidx_n[i];
+      scatter_input_chunk<MT>(d, C::first(d), smem, rx_tid(), xin);
+      if (d.r_lds_off < 0 && C::first(d).in_k > C::first(d).in_n)   // T mode: XT_0's K tail rows
+        zero_t_rows<MT, true>(reinterpret_cast<u16*>(smem + C::first(d).xt_off), C::first(d).in_n,
+                              C::first(d).in_k);
+#pragma unroll
+      for (int q = 0; q < MT * 4; ++q) labp[q] = labn[q];
+      __syncthreads();
+    } else {
+      for (int i = rx_tid(); i < Tile<MT>::BP; i += RX_THREADS)
+        rowidx[i] = i < nvalid ? (perm ? rx_g(perm)[row0 + i] : row0 + i) : (perm ? rx_g(perm)[row0] : row0);
+      __syncthreads();
+      // the batch gather does not depend on the weights: it overlaps the last optimizer tiles
+      load_inputs<MT, true>(d, C::first(d), smem, feats, rowidx, nvalid, true, dp, P, metrics);
+      prefetch_labels<MT, true>(d, labels, rowidx, labp);
+    }
     stamp(s, 1);
-    if (s > 0) {
-      if (rx_tid() < 64) {
+    // waves 1..7: the vector update of step s - 1 when it is not inside the epilogues (its flag
+    // is out, its gradients are in Gr), beside wave 0's counter poll
+    if (s > 0 && !vec_inline)
+      ps_vector_update<C>(d, o, smem, Gr, m, v, rx_g(sched)[s - 1], rx_g(sched)[nsteps + s - 1],
+                          rx_g(sched)[2 * nsteps + s - 1], (opt_first && s == 1) ? 1 : 0);
+    // layers >= 1 are waited for where their weights are first read (PsNxWait); layer 0 here,
+    // unless the step workgroup updates it itself
+    if (s > 0 && !l0_in) {
+      if (rx_tid() < RX_PS_VEC_T0) {
         // lane l polls layer l's counter: all layers in flight at once (a sequential poll pays
         // one L2 round trip per layer even when the counters are long complete)
         const int lane = rx_tid();
@@ -213,7 +458,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
         int l = 0;
         for (int q = 0; q < o.nseg; ++q) {
           if (o.seg[q].kind != 1) continue;
-          if (l == lane) target = (unsigned)(ps_seg_blocks(o.seg[q]) * s);
+          if (l == lane && l == 0) target = (unsigned)(ps_seg_workers(o, q, l) * s);
           ++l;
         }
         const unsigned* cnt = sync + RX_PS_CNT(lane < RX_MAXL ? lane : 0);
@@ -236,6 +481,8 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       }
       __syncthreads();
       if (flag_lds[0]) return;
+    } else if (s > 0 && !vec_inline) {
+      __syncthreads();   // the vector update's parameter writes before the forward reads them
     }
     stamp(s, 2);
 #ifdef RX_LAYER_STAMPS
@@ -244,18 +491,49 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
 #else
     unsigned long long* lst = nullptr;
 #endif
+    PsNxWait nxw{sync, workers, s, ticks};
+    PsVec<O> vo;
+    if (vec_inline) {
+      vo.o = &oc;
+      vo.m = m;
+      vo.v = v;
+      vo.sc = vsc;
+    }
     bf16x8 wpre[RX_PJ][RX_PK];
-    fwd_prefetch<true>(C::first(d), img, wpre);
+    if (!l0_in) fwd_prefetch<true>(C::first(d), img, wpre, d.w0s_lds_off >= 0);
     // every step but a ragged last one fills the tile: the full-batch body has no row masks
     auto body = [&](auto full) {
       constexpr bool F = decltype(full)::value;
       C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
         layer_forward<MT, true, true, F>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, scratch, metrics,
-                                         wpre, ps_wt, l, lst, labp);
+                                         wpre, ps_wt, l, lst, labp, static_cast<NoMw*>(nullptr), vo,
+                                         (l == 0 && l0_in) ? w0b : nullptr, &nxw);
       });
       stamp(s, 3);
+      // next batch, part 1: its row indices (a global read whose latency the backward hides)
+      const bool pf_next = pf && s + 1 < nsteps;
+      const int row0n = row0 + batch, nvalid_n = min(batch, n_rows - row0n);
+      int pn = 0;
+      if (pf_next && rx_tid() < Tile<MT>::BP) {
+        const int i = rx_tid();
+        pn = i < nvalid_n ? (perm ? rx_g(perm)[row0n + i] : row0n + i) : (perm ? rx_g(perm)[row0n] : row0n);
+      }
+      bool first_bwd = true;
       C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
-        layer_backward<MT, true, F>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, lst, sync, s, ps_wt);
+        if (l == 0 && l0_in)
+          ps_l0_update<MT>(d, ly, smem, oc, vsc, w0b);
+        else
+          layer_backward<MT, true, F>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, lst, sync, s, ps_wt,
+                                      static_cast<NoMw*>(nullptr), vo);
+        if (first_bwd && pf_next) {
+          // part 2, after the first backward layer: the rows to LDS, then the feature chunks and
+          // labels into registers (held until the next step scatters them)
+          if (rx_tid() < Tile<MT>::BP) rowidx_n[rx_tid()] = pn;
+          __syncthreads();
+          xin = gather_input_chunk<MT>(d, feats, rowidx_n, nvalid_n, rx_tid());
+          prefetch_labels<MT, true>(d, labels, rowidx_n, labn);
+        }
+        first_bwd = false;
         stamp(s, 8 + l);
       });
     };
@@ -263,46 +541,63 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       body(rx_bool<true>{});
     else
       body(rx_bool<false>{});
-    // layer 0's backward ends with its G^T export (no dgrad)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (rx_tid() == 0)
-      __hip_atomic_store(rx_g(sync) + RX_PS_FLAG(0), (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!l0_in) {
+      // layer 0's backward ends with its G^T export (no dgrad): drained, then its flag
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (rx_tid() == 0)
+        __hip_atomic_store(rx_g(sync) + RX_PS_FLAG(0), (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __syncthreads();   // every read of this step's LDS images is done before the next batch lands
+    }
     stamp(s, 4);
-    ps_vector_update<C>(d, o, smem, Gr, m, v, rx_g(sched)[s], rx_g(sched)[nsteps + s], rx_g(sched)[2 * nsteps + s],
-                        (opt_first && s == 0) ? 1 : 0);
-    stamp(s, 6);
-    __syncthreads();
     stamp(s, 5);
   }
+  // the last step's vector update (the others ran under the next step's counter wait)
+  if (nsteps > 0 && !vec_inline) {
+    const int s = nsteps - 1;
+    ps_vector_update<C>(d, o, smem, Gr, m, v, rx_g(sched)[s], rx_g(sched)[nsteps + s], rx_g(sched)[2 * nsteps + s],
+                        (opt_first && s == 0) ? 1 : 0);
+    __syncthreads();
+  }
   if (stamps != nullptr && rx_tid() == 0) rx_g(stamps)[RX_PS_STEP_STAMPS + nsteps] = wall_clock64();
+  if (l0_in) ps_l0_store(C::first(d), smem, d.w0s_lds_off, P, m, v, const_cast<u16*>(img));
   ps_store_vectors<C>(d, smem, P);
   store_running_stats<C>(d, smem, rstats);
 }
 
-// dW tile [o0, o0+32) x [i0, i0+32) of one half-workgroup (4 waves) from the exported X^T / G^T,
-// every byte read with an sc1 load (written by the step workgroup of this launch).
-__device__ __forceinline__ void ps_wgrad_tile(const OptSeg& sg, const OptDesc& o, int o0, int i0,
-                                              const float* __restrict__ Gr, float (*gtile)[33]) {
-  const int lane = rx_tid() & 63, wh = rx_wave() & 3;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int ms = wh >> 1, ns = wh & 1;
-  const int orow = min(o0 + ms * 16 + lr, sg.out_n - 1);
-  const int irow = min(i0 + ns * 16 + lr, sg.in_n - 1);
-  const int base = o.act_off * 4;
-  const int xo = base + (sg.xg_off + irow * o.bp + 8 * lg) * 2;
-  const int go = base + (sg.gg_off + orow * o.bp + 8 * lg) * 2;
-  f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < o.bp; k0 += 32) {
-    const bf16x8 a = __builtin_bit_cast(bf16x8, rx_load16_sc1(Gr, xo + k0 * 2));
-    const bf16x8 b = __builtin_bit_cast(bf16x8, rx_load16_sc1(Gr, go + k0 * 2));
-    a4 = rx_mfma16(a, b, a4);
-  }
+// One wave's 16x16 block of the dW tile [o0, o0+32) x [i0, i0+32) of its half-workgroup (4
+// waves: wh = 2 ms + ns) from the exported X^T / G^T, every byte read with an sc1 load (written
+// by the step workgroup of this launch). xo / go: this lane's byte offsets of its X^T and G^T
+// rows (computed once per epoch); nk: 32-row k-steps of the batch. All loads are issued back to
+// back, address-clamped and unconditional (one L2 round trip, not one per k-step; a load under a
+// branch is waited for before the next one issues). Lane (lr, lg) gets
+// dW[o0 + 16 ms + lr][i0 + 16 ns + 4 lg + r], r = 0..3 -- the elements it owns.
+__device__ __forceinline__ f32x4 ps_wgrad_block(const float* __restrict__ Gr, int xo, int go, int nk) {
+  constexpr int KMAX = 4;   // bp <= 128: the persistent kernel runs one-workgroup batches
+  u32x4 xa[KMAX], gb[KMAX];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) gtile[ms * 16 + lr][ns * 16 + lg * 4 + r] = a4[r];
+  for (int k = 0; k < KMAX; ++k) {
+    const int kk = k < nk ? k : 0;
+    xa[k] = rx_load16_sc1(Gr, xo + kk * 64);
+    gb[k] = rx_load16_sc1(Gr, go + kk * 64);
+  }
+  f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (k < nk) a4 = rx_mfma16(__builtin_bit_cast(bf16x8, xa[k]), __builtin_bit_cast(bf16x8, gb[k]), a4);
+  return a4;
 }
 
-__device__ __forceinline__ void ps_opt_wg(const OptDesc& o, int b, float* __restrict__ P, const float* __restrict__ Gr,
+// An optimizer workgroup: two 32x32 tiles of one Linear weight (one per half-workgroup), master
+// weight and moments in registers for the epoch. Per step: wait for the layer's flag, wgrad (the
+// MFMA accumulator IS the update's input: each lane updates the 4 elements it holds), bf16
+// image stores straight from registers -- W_l rows as 8-B stores, Wt_l rows through a quad
+// transpose (rx_quad_transpose) as 8-B stores; layer 0 has no dgrad and no Wt image to keep --
+// drain, count. No LDS round trip and one barrier between flag and counter.
+template <class O>
+__device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, float* __restrict__ P,
+                                          const float* __restrict__ Gr,
                                           float* __restrict__ m, float* __restrict__ v, const float* __restrict__ sched,
                                           int nsteps, int opt_first, unsigned* __restrict__ sync,
                                           unsigned long long ticks, char* smem, int* flag_lds,
@@ -311,7 +606,7 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, int b, float* __rest
   int seg = -1, l = 0;
   for (int q = 0; q < o.nseg; ++q) {
     if (o.seg[q].kind != 1) continue;
-    const int nbk = ps_seg_blocks(o.seg[q]);
+    const int nbk = ps_seg_workers(o, q, l);
     if (b < nbk) {
       seg = q;
       break;
@@ -321,87 +616,91 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, int b, float* __rest
   }
   if (seg < 0) return;
   const OptSeg& sg = o.seg[seg];
-  const int half = rx_tid() >> 8, ht = rx_tid() & 255;
+  const int half = rx_tid() >> 8;
   const int t = 2 * b + half;
   const bool valid = t < opt_seg_blocks(sg);
   const int tiles_i = (sg.in + 31) / 32;
   const int o0 = valid ? (t / tiles_i) * 32 : 0, i0 = valid ? (t % tiles_i) * 32 : 0;
-  const int ti = ht & 31, to = ht >> 5;
+  const int lane = rx_tid() & 63, wh = rx_wave() & 3;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int oo = o0 + (wh >> 1) * 16 + lr;             // this lane's weight row
+  const int ib = i0 + (wh & 1) * 16 + 4 * lg;          // and its 4 columns ib .. ib + 3
+  // everything the step loop needs from the descriptors, read once (inside the loop every field
+  // would be a scalar load behind an lgkmcnt wait, on the layer-0 critical path)
+  const int nk = (o.bp + 31) / 32;
+  const int xo = o.act_off * 4 + (sg.xg_off + min(i0 + (wh & 1) * 16 + lr, sg.in_n - 1) * o.bp + 8 * lg) * 2;
+  const int go = o.act_off * 4 + (sg.gg_off + min(o0 + (wh >> 1) * 16 + lr, sg.out_n - 1) * o.bp + 8 * lg) * 2;
+  u16* const Wimg = sg.W;
+  u16* const Wtimg = sg.Wt;
+  const int in_k = sg.in_k, out_k = sg.out_k;
+
   float pr_[4], mr[4], vr[4];
   int idx[4];
   bool ok[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int oo = o0 + to + 8 * r, ii = i0 + ti;
-    ok[r] = valid && oo < sg.out && ii < sg.in;
-    idx[r] = ok[r] ? sg.start + oo * sg.in + ii : sg.start;
+    ok[r] = valid && oo < sg.out && ib + r < sg.in;
+    idx[r] = ok[r] ? sg.start + oo * sg.in + ib + r : sg.start;
     pr_[r] = rx_g(P)[idx[r]];
     mr[r] = rx_g(m)[idx[r]];
     vr[r] = rx_g(v)[idx[r]];
   }
+  // image rows this lane writes: W_l row oo (cols ib..+3) and, after the quad transpose, Wt_l row
+  // i0 + 16 ns + 4 lg + (lr & 3) (cols o0 + 16 ms + (lr & ~3) .. +3); padding rows stay unwritten
+  const bool w_row = valid && oo < sg.out_n;
+  const int it = i0 + (wh & 1) * 16 + 4 * lg + (lr & 3);
+  const int ot = o0 + (wh >> 1) * 16 + (lr & ~3);
+  const bool wt_row = valid && l > 0 && it < sg.in_n && ot < sg.out_n;
   // plain (L2-resident) image stores when this workgroup shares the step workgroup's XCD,
   // write-through (sc1) ones otherwise; the step workgroup reads them with sc1 loads either way
   if (rx_tid() == 0) {
     const unsigned me = rx_xcc_id() + 1u;
     __hip_atomic_store(rx_g(sync) + RX_PS_XCC + 1 + bw, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool ok = rx_ps_wait(sync, sync + RX_PS_XCC, 1u, ticks);
-    flag_lds[0] = ok ? 0 : 1;
-    flag_lds[1] = (ok && rx_ps_load(sync + RX_PS_XCC) == me) ? 0 : 1;
+    const bool okw = rx_ps_wait(sync, sync + RX_PS_XCC, 1u, ticks);
+    flag_lds[0] = okw ? 0 : 1;
+    flag_lds[1] = (okw && rx_ps_load(sync + RX_PS_XCC) == me) ? 0 : 1;
   }
   __syncthreads();
   const bool wt_ = flag_lds[1] != 0;
-  float (*gtile)[33] = reinterpret_cast<float (*)[33]>(smem) + half * 32;
-  u16 (*wt)[40] = reinterpret_cast<u16 (*)[40]>(smem + 2 * 32 * 33 * 4) + half * 32;
   for (int s = 0; s < nsteps; ++s) {
-    const float lr = rx_g(sched)[s], bc1 = rx_g(sched)[nsteps + s], bc2 = rx_g(sched)[2 * nsteps + s];
+    const float lr_ = rx_g(sched)[s], bc1 = rx_g(sched)[nsteps + s], bc2 = rx_g(sched)[2 * nsteps + s];
     if (rx_tid() == 0 && flag_lds[0] == 0)
       flag_lds[0] = rx_ps_wait(sync, sync + RX_PS_FLAG(l), (unsigned)(s + 1), ticks) ? 0 : 1;
     __syncthreads();
     if (flag_lds[0]) break;
     const bool st = stamps != nullptr && s == nsteps / 2 && b == 0 && rx_tid() == 0;
     if (st) rx_g(stamps)[16 + 2 * l] = wall_clock64();
-    if (valid) ps_wgrad_tile(sg, o, o0, i0, Gr, gtile);
-    __syncthreads();
+    const f32x4 gw = ps_wgrad_block(Gr, xo, go, nk);
+    if (st && l == 0) {   // layer 0: its X^T / G^T fragments arrived
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      rx_g(stamps)[28] = wall_clock64();
+    }
     const int first = (opt_first && s == 0) ? 1 : 0;
+    float h[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      u16 h = 0;
-      if (ok[r]) {
-        opt_update_reg(o, pr_[r], mr[r], vr[r], gtile[to + 8 * r][ti], lr, bc1, bc2, 1.f, first);
-        h = rx_f2bf(pr_[r]);
-      }
-      wt[to + 8 * r][ti] = h;
+      if (ok[r]) opt_update_reg(hp, pr_[r], mr[r], vr[r], gw[r], lr_, bc1, bc2, 1.f, first);
+      h[r] = ok[r] ? pr_[r] : 0.f;   // zeros in the padding, which the images must keep
     }
-    __syncthreads();
-    // W_l rows [o0, o0+32) x cols [i0, i0+32) and Wt_l rows [i0, i0+32) x cols [o0, o0+32):
-    // 16-B write-through stores (zeros in the padding, which the images must keep)
-    if (valid) {
-      if (ht < 128) {
-        const int row = ht >> 2, ch = ht & 3;
-        if (o0 + row < sg.out_n) {
-          const u32x4 val = *reinterpret_cast<const u32x4*>(&wt[row][ch * 8]);
-          const int off = (o0 + row) * sg.in_k + i0 + ch * 8;
-          if (wt_)
-            rx_store16_sc1(sg.W, off * 2, val);
-          else
-            *reinterpret_cast<RX_GLOBAL u32x4*>(rx_g(sg.W) + off) = val;
-        }
-      } else {
-        const int q = ht - 128, row = q >> 2, ch = q & 3;
-        if (i0 + row < sg.in_n) {
-          u32x4 pk;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            pk[e] = (uint32_t)wt[ch * 8 + 2 * e][row] | ((uint32_t)wt[ch * 8 + 2 * e + 1][row] << 16);
-          const int off = (i0 + row) * sg.out_k + o0 + ch * 8;
-          if (wt_)
-            rx_store16_sc1(sg.Wt, off * 2, pk);
-          else
-            *reinterpret_cast<RX_GLOBAL u32x4*>(rx_g(sg.Wt) + off) = pk;
-        }
-      }
+    if (st && l == 0) rx_g(stamps)[26] = wall_clock64();   // layer 0: wgrad + update done
+    const uint2 wv = make_uint2(rx_f2bf2(h[0], h[1]), rx_f2bf2(h[2], h[3]));
+    const uint2 tv = rx_quad_transpose(wv, lr & 3);   // (every lane of the quad takes part)
+    if (w_row) {
+      const int off = oo * in_k + ib;
+      if (wt_)
+        rx_store8_sc1(Wimg, off * 2, wv);
+      else
+        *reinterpret_cast<RX_GLOBAL rx_u32x2*>(rx_g(Wimg) + off) = rx_u32x2{wv.x, wv.y};
+    }
+    if (wt_row) {
+      const int off = it * out_k + ot;
+      if (wt_)
+        rx_store8_sc1(Wtimg, off * 2, tv);
+      else
+        *reinterpret_cast<RX_GLOBAL rx_u32x2*>(rx_g(Wtimg) + off) = rx_u32x2{tv.x, tv.y};
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (st && l == 0) rx_g(stamps)[27] = wall_clock64();   // its image stores drained
     __syncthreads();
     if (rx_tid() == 0) __hip_atomic_fetch_add(rx_g(sync) + RX_PS_CNT(l), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (st) rx_g(stamps)[17 + 2 * l] = wall_clock64();
@@ -435,9 +734,13 @@ __device__ __forceinline__ void mlp_persist_body(const MlpDesc* __restrict__ dp,
   if ((int)blockIdx.x % stride != 0) return;
   const int w = (int)blockIdx.x / stride;
   if (w >= nw) return;
-  if (w == 0)
+  if (w == 0) {
     ps_step_wg<C, MT>(dp, o, img, rstats, P, Gr, feats, labels, perm, n_rows, batch, nsteps, scratch, metrics, m, v,
                       sched, opt_first, sync, ticks, smem, rowidx, flag_lds, stamps);
-  else
-    ps_opt_wg(o, w - 1, P, Gr, m, v, sched, nsteps, opt_first, sync, ticks, smem, flag_lds, stamps);
+  } else {
+    // hyperparameters: compile-time constants in a specialised kernel (C::Opt), else the descriptor
+    using O = typename rx_opt_type<C>::type;
+    const rx_opt_holder<O> oh;
+    ps_opt_wg(o, oh.get(o), w - 1, P, Gr, m, v, sched, nsteps, opt_first, sync, ticks, smem, flag_lds, stamps);
+  }
 }

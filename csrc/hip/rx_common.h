@@ -7,6 +7,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
+typedef unsigned int rx_u32x2 __attribute__((ext_vector_type(2)));
 
 #define RX_WAVE 64
 

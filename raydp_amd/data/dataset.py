@@ -247,14 +247,18 @@ class Dataset:
 
     def to_torch(self, *, label_column=None, feature_columns=None, label_column_dtype=None,
                  feature_column_dtypes=None, batch_size=1, prefetch_blocks=0, drop_last=False,
-                 unsqueeze_label_tensor=True, unsqueeze_feature_tensors=True, device="cpu"):
+                 unsqueeze_label_tensor=True, unsqueeze_feature_tensors=True, device=None):
         """Legacy Ray-Data ``to_torch`` contract used by the reference estimator.
 
         Returns an iterable of ``(features, label)``. ``feature_columns`` as a list of names
         with one dtype → one ``[B, F]`` tensor; a list of lists → a list of tensors; a dict
-        → a dict of tensors.
+        → a dict of tensors. ``device=None``: inside a GPU train worker the worker's GPU (the
+        shard is ingested into HBM once and batches are slices of it -- a user loop's
+        ``.to(device)`` is then a no-op), else the CPU.
         """
         from raydp_amd.data.torch_iter import TorchBatchIterable
+        if device is None:
+            device = _worker_device()
         return TorchBatchIterable(self, label_column, feature_columns, label_column_dtype,
                                   feature_column_dtypes, batch_size, drop_last,
                                   unsqueeze_label_tensor, device)
@@ -456,3 +460,13 @@ def from_spark(df, parallelism: Optional[int] = None) -> Dataset:
     """``ray.data.from_spark`` equivalent (recoverable conversion)."""
     from raydp_amd.spark.dataset import spark_dataframe_to_ray_dataset
     return spark_dataframe_to_ray_dataset(df, parallelism)
+
+
+def _worker_device():
+    """The GPU of the train worker this runs in (raydp_amd.train.session), else "cpu"."""
+    try:
+        from raydp_amd.train import session
+        dev = session.get_device()
+    except Exception:  # noqa: BLE001 - not inside a train worker
+        return "cpu"
+    return dev if dev is not None and getattr(dev, "type", "cpu") == "cuda" else "cpu"

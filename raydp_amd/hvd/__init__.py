@@ -411,6 +411,8 @@ def DistributedOptimizer(optimizer, named_parameters=None, compression=None, bac
     fusion = _Fusion(params, threshold, op, compression, gscale) if world > 1 else None
     counter = {"n": 0}
     base_cls = optimizer.__class__
+    from raydp_amd.utils import config as C
+    fused = {"on": bool(C.get("spark.ray.mi355x.fused_optimizer"))}
 
     class _HvdOptimizer(base_cls):
         def __init__(self):
@@ -449,6 +451,13 @@ def DistributedOptimizer(optimizer, named_parameters=None, compression=None, bac
                 return None
             if not self._skip_sync:
                 self.synchronize()
+            if closure is None and fused["on"]:
+                # the wrapped Adam / AdamW / SGD on the multi-tensor HIP kernels (one launch per 24
+                # tensors; torch's state layout kept): csrc/hip/fused_optim.hip
+                from raydp_amd.ops.fused_optim import fused_step
+                if fused_step(optimizer):
+                    return None
+                fused["on"] = False    # not covered (CPU / sparse / amsgrad ...): torch from now on
             return base_cls.step(self, closure)
 
         def zero_grad(self, set_to_none: bool = True):

@@ -51,6 +51,7 @@ class MlpDesc(ctypes.Structure):
         ("act_off", ctypes.c_int), ("wgrad_mode", ctypes.c_int),
         ("front_n", ctypes.c_int), ("front_q", ctypes.c_int), ("acc_mode", ctypes.c_int),
         ("acc_thr", ctypes.c_float), ("front", FrontCol * MAXF), ("front_qbase", ctypes.c_int * MAXF),
+        ("loss_lds_off", ctypes.c_int), ("w0s_lds_off", ctypes.c_int), ("x0c_lds_off", ctypes.c_int),
     ]
 
 
@@ -86,7 +87,7 @@ class OptDesc(ctypes.Structure):
         ("nesterov", ctypes.c_int), ("maximize", ctypes.c_int),
         ("seg", OptSeg * MAXSEG),
         ("act_off", ctypes.c_int), ("act_floats", ctypes.c_int), ("bp", ctypes.c_int),
-        ("wgrad_mode", ctypes.c_int),
+        ("wgrad_mode", ctypes.c_int), ("ps_l0_inline", ctypes.c_int),
     ]
 
 

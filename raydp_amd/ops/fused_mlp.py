@@ -108,6 +108,9 @@ def wgrad_mode() -> int:
     return 1 if conf_get("spark.ray.mi355x.mlp_wgrad") == "opt" else 0
 
 
+W0S_N = 16 * 64 * 4 + 16 * 16 * 4   # csrc/hip/mlp_persist.h RX_W0S_N
+
+
 def persistent_enabled() -> bool:
     """One-GPU epochs as one persistent launch (``spark.ray.mi355x.mlp_persistent``)."""
     from raydp_amd.utils.config import get as conf_get
@@ -356,12 +359,33 @@ class FusedMLPTrainer:
         d.acc_thr = float(self.acc_thr) if self.acc_thr is not None else 0.5
         d.pr_lds_off = alloc(pr_total * 4)
         d.pr_total = pr_total
+        # one output column, regression / BCE loss, one workgroup: the loss runs a row per lane
+        # through a BP-float LDS area (csrc/hip/mlp_core.h MlpDesc::loss_lds_off)
+        d.loss_lds_off = -1
+        if G == 1 and spec.layers[-1].linear.out_features == 1 and self.loss_code != 4 \
+                and lds + bp * 4 <= 160 * 1024 - 1536:
+            d.loss_lds_off = alloc(bp * 4)
+        # persistent epoch: layer 0 updated by the step workgroup itself (csrc/hip/mlp_persist.h
+        # ps_l0_update) -- its fp32 master + both moments (RX_W0S_N floats each) and a copy of
+        # X^T_0 in LDS; layer 0's saved BN inputs then go to the global scratch buffer instead
+        d.w0s_lds_off = d.x0c_lds_off = -1
+        l00 = spec.layers[0].linear
+        # (decided without looking at whether epochs run persistent: every kernel of the model then
+        # runs layer 0 in the same k order, so the persistent epoch and the step loop agree bit for bit)
+        l0_inline = (G == 1 and tmode and wmode == 1 and not front
+                     and l00.in_features <= 20 and dims[0][2] == 32 and l00.out_features % 16 == 0
+                     and l00.out_features <= 256 and L > 1
+                     and lds + 32 * xs * 2 + 3 * W0S_N * 4 <= 160 * 1024 - 1536)
+        if l0_inline:
+            d.x0c_lds_off = alloc(32 * xs * 2)
+            d.w0s_lds_off = alloc(3 * W0S_N * 4)
+        self.l0_inline = l0_inline
         # saved BN inputs / ReLU sources in LDS, largest first, while they fit (the rest stays in
         # the global scratch buffer); T mode only (R mode has no room for them)
         if tmode:
-            budget = 160 * 1024 - 1024     # static LDS of the kernels (row indices, flags)
+            budget = 160 * 1024 - 1536     # static LDS of the kernels (2 x BP row indices, flags)
             saves = [(bp * d.layer[li].out_n * 4, li) for li, ly in enumerate(spec.layers)
-                     if ly.bn or li != L - 1]
+                     if (ly.bn or li != L - 1) and not (li == 0 and l0_inline)]
             for nbytes, li in sorted(saves, reverse=True):
                 if lds + nbytes <= budget:
                     d.layer[li].sv_lds = alloc(nbytes)
@@ -408,6 +432,7 @@ class FusedMLPTrainer:
         o.wd, o.momentum, o.dampening = cfg.get("wd", 0.0), cfg.get("momentum", 0.0), cfg.get("dampening", 0.0)
         o.nesterov, o.maximize = int(cfg.get("nesterov", False)), int(cfg.get("maximize", False))
         o.act_off, o.act_floats, o.bp, o.wgrad_mode = act_off, act_floats, bp_all, wmode
+        o.ps_l0_inline = int(self.l0_inline)
         self.opt = o
         if G > 1 and wmode == 1:
             # split-K weight-gradient partials + per-tile arrival counters of the multi-workgroup

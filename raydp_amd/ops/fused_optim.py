@@ -7,6 +7,8 @@
   operand image of every weight a fused Linear tower reads (``linear_ops.FusedLinearTower``),
   so the tower does not rebuild it before the next forward. Sparse gradients (embedding rows)
   keep torch's update. :class:`FusedSGD` is the same as an optimizer class.
+* :func:`adam_step` -- ``torch.optim.Adam`` / ``AdamW`` the same way (Horovod's
+  ``DistributedOptimizer`` runs a wrapped Adam / AdamW / SGD through :func:`fused_step`).
 * :class:`FusedBCEWithLogits` -- ``nn.BCEWithLogitsLoss()`` (mean reduction, no weights): the
   loss is one single-workgroup kernel and its gradient one elementwise kernel computed from the
   saved operands (eager torch: log-sigmoid, mean, sigmoid, sub, mul ... ~6 launches).
@@ -35,6 +37,14 @@ class MtSgd(ctypes.Structure):
                 ("len", ctypes.c_longlong * MT_MAX)]
 
 
+class MtAdam(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("adamw", ctypes.c_int), ("maximize", ctypes.c_int),
+                ("lr", ctypes.c_float), ("b1", ctypes.c_float), ("b2", ctypes.c_float), ("eps", ctypes.c_float),
+                ("wd", ctypes.c_float), ("nlr_bc1", ctypes.c_float * MT_MAX), ("rs_bc2", ctypes.c_float * MT_MAX),
+                ("p", ctypes.c_void_p * MT_MAX), ("g", ctypes.c_void_p * MT_MAX), ("m", ctypes.c_void_p * MT_MAX),
+                ("v", ctypes.c_void_p * MT_MAX), ("len", ctypes.c_longlong * MT_MAX)]
+
+
 _bound = None
 
 
@@ -44,12 +54,16 @@ def _lib():
     if _bound is not L:
         vp, ll = ctypes.c_void_p, ctypes.c_longlong
         L.rx_mt_sgd.argtypes = [vp, vp]
+        L.rx_mt_adam.argtypes = [vp, vp]
         L.rx_bce_logits_fwd.argtypes = [vp, vp, ll, vp, vp]
         L.rx_bce_logits_bwd.argtypes = [vp, vp, vp, ll, vp, vp]
-        for n in ("rx_mt_sgd", "rx_bce_logits_fwd", "rx_bce_logits_bwd", "rx_mt_sgd_size", "rx_mt_sgd_max"):
+        for n in ("rx_mt_sgd", "rx_mt_adam", "rx_bce_logits_fwd", "rx_bce_logits_bwd", "rx_mt_sgd_size",
+                  "rx_mt_sgd_max", "rx_mt_adam_size"):
             getattr(L, n).restype = ctypes.c_int
         if L.rx_mt_sgd_size() != ctypes.sizeof(MtSgd) or L.rx_mt_sgd_max() != MT_MAX:
             raise RuntimeError("MtSgd layout mismatch between Python and csrc/hip/fused_optim.hip")
+        if L.rx_mt_adam_size() != ctypes.sizeof(MtAdam):
+            raise RuntimeError("MtAdam layout mismatch between Python and csrc/hip/fused_optim.hip")
         _bound = L
     return L
 
@@ -138,6 +152,72 @@ def sgd_step(opt) -> None:
                 _hip.check(L.rx_mt_sgd(ctypes.byref(a), _hip.stream_ptr(chunk[0].device)), "rx_mt_sgd")
                 for tower, li in owners:
                     tower.image_updated(li)
+
+
+def adam_supported(opt) -> Optional[str]:
+    """None when :func:`adam_step` reproduces ``opt.step()`` of a ``torch.optim.Adam`` /
+    ``AdamW`` (to fp32 rounding: the kernel's operation order is not torch's); else why not."""
+    if type(opt) not in (torch.optim.Adam, torch.optim.AdamW):
+        return f"{type(opt).__name__} is not torch.optim.Adam / AdamW"
+    for g in opt.param_groups:
+        if g.get("amsgrad") or g.get("capturable") or g.get("differentiable") or g.get("fused"):
+            return "amsgrad / capturable / differentiable / fused groups keep torch's step"
+        if isinstance(g["lr"], torch.Tensor) or any(isinstance(b, torch.Tensor) for b in g["betas"]):
+            return "tensor hyperparameters"
+        for p in g["params"]:
+            if p.grad is None:
+                continue
+            if p.grad.is_sparse or not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous() \
+                    or not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
+                return "parameters must be dense contiguous fp32 CUDA tensors"
+            st = opt.state.get(p)
+            if st and (not st["exp_avg"].is_contiguous() or not st["exp_avg_sq"].is_contiguous()
+                       or st["step"].is_cuda):
+                return "optimizer state not in torch's default (contiguous, host step) layout"
+    return None
+
+
+@torch.no_grad()
+def adam_step(opt) -> None:
+    """One ``torch.optim.Adam`` / ``AdamW`` step of ``opt`` on the multi-tensor kernel: one launch
+    per 24 parameter tensors. The state stays torch's (``step`` a host tensor, ``exp_avg``,
+    ``exp_avg_sq``), so ``state_dict()`` / checkpoints / a later ``opt.step()`` see no difference."""
+    L = _lib()
+    adamw = isinstance(opt, torch.optim.AdamW)
+    for group in opt.param_groups:
+        lr = float(group["lr"])
+        b1, b2 = (float(b) for b in group["betas"])
+        live = [p for p in group["params"] if p.grad is not None]
+        for k in range(0, len(live), MT_MAX):
+            chunk = live[k:k + MT_MAX]
+            a = MtAdam()
+            a.n, a.adamw, a.maximize = len(chunk), int(adamw), int(bool(group.get("maximize", False)))
+            a.lr, a.b1, a.b2, a.eps, a.wd = lr, b1, b2, float(group["eps"]), float(group["weight_decay"])
+            for j, p in enumerate(chunk):
+                st = opt.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                t = float(st["step"])
+                a.nlr_bc1[j] = -lr / (1.0 - b1 ** t)
+                a.rs_bc2[j] = 1.0 / (1.0 - b2 ** t) ** 0.5
+                a.p[j], a.g[j], a.len[j] = p.data_ptr(), p.grad.data_ptr(), p.numel()
+                a.m[j], a.v[j] = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
+            _hip.check(L.rx_mt_adam(ctypes.byref(a), _hip.stream_ptr(chunk[0].device)), "rx_mt_adam")
+
+
+def fused_step(opt) -> bool:
+    """``opt.step()`` on the multi-tensor kernels when they cover ``opt`` (Adam / AdamW / SGD over
+    dense fp32 CUDA parameters); False (nothing done) otherwise."""
+    if adam_supported(opt) is None:
+        adam_step(opt)
+        return True
+    if sgd_supported(opt) is None:
+        sgd_step(opt)
+        return True
+    return False
 
 
 class FusedSGD(torch.optim.SGD):

@@ -34,14 +34,17 @@ _LAYER_INT = ("in_", "out", "in_k", "out_k", "in_n", "out_n", "w_img", "wt_img",
               "g_off", "be_off", "rs_off", "xt_off", "stat_off", "r_off", "pr_off", "xg_off", "gg_off", "mw_off",
               "sv_lds")
 _DESC_INT = ("L", "r_lds_off", "gt_lds_off", "stats_lds_off", "lds_bytes", "max_k", "max_n", "loss", "out_dim",
-             "feat_k", "pr_lds_off", "pr_total", "act_off", "wgrad_mode", "front_n", "front_q", "acc_mode")
+             "feat_k", "pr_lds_off", "pr_total", "act_off", "wgrad_mode", "front_n", "front_q", "acc_mode",
+             "loss_lds_off", "w0s_lds_off", "x0c_lds_off")
 
 
 def _f(x: float) -> str:
     return repr(float(x)) + "f" if "e" in repr(float(x)) or "." in repr(float(x)) else f"{float(x)}f"
 
 
-def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
+def generate_source(desc: "_hip.MlpDesc", mt: int, opt: Optional["_hip.OptDesc"] = None) -> str:
+    """``opt``: the optimizer's hyperparameters become constants too (the persistent kernel's
+    in-epilogue bias / BatchNorm updates, csrc/hip/mlp_core.h PsVec)."""
     L = desc.L
     out = []
     if os.environ.get("RAYDP_MLP_LAYER_STAMPS") == "1":
@@ -61,12 +64,20 @@ def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
         out.append(f"  static constexpr float eps = {_f(ly.eps)};")
         out.append(f"  static constexpr float momentum = {_f(ly.momentum)};")
         out.append("};")
+    if opt is not None:
+        out.append("struct JO {")
+        for k in ("algo", "nesterov", "maximize"):
+            out.append(f"  static constexpr int {k} = {int(getattr(opt, k))};")
+        for k in ("b1", "b2", "eps", "wd", "momentum", "dampening"):
+            out.append(f"  static constexpr float {k} = {_f(getattr(opt, k))};")
+        out.append("};")
     fwd = "; ".join(f"f(JL{li}{{}}, JL{min(li + 1, L - 1)}{{}}, {li}, {'true' if li == L - 1 else 'false'})"
                     for li in range(L))
     bwd = "; ".join(f"f(JL{li}{{}}, JL{max(li - 1, 0)}{{}}, {li})" for li in range(L - 1, -1, -1))
     each = "; ".join(f"f(JL{li}{{}}, {li})" for li in range(L))
     out += [
         "struct JitCfg {",
+        *(["  using Opt = JO;"] if opt is not None else []),
         "  __device__ static JD desc(const MlpDesc*) { return {}; }",
         f"  template <class F> __device__ static void fwd_layers(const JD&, F&& f) {{ {fwd}; }}",
         f"  template <class F> __device__ static void bwd_layers(const JD&, F&& f) {{ {bwd}; }}",
@@ -112,8 +123,8 @@ def generate_source(desc: "_hip.MlpDesc", mt: int) -> str:
         "    float* __restrict__ m, float* __restrict__ v, const float* __restrict__ sched, int opt_first,",
         "    unsigned* __restrict__ sync, unsigned long long ticks, unsigned long long* __restrict__ stamps) {",
         "  extern __shared__ __attribute__((aligned(16))) char smem[];",
-        "  __shared__ int rowidx[Tile<RX_MT>::BP];",
-        "  __shared__ int flag_lds[2];",
+        "  __shared__ int rowidx[2 * Tile<RX_MT>::BP];   // [this step | next step (prefetch)]",
+        "  __shared__ __attribute__((aligned(16))) int flag_lds[16];",
         "  mlp_persist_body<JitCfg, RX_MT>(dp, od, img, rstats, P, Gr, feats, labels, perm, n_rows, batch, nsteps,",
         "                                  scratch, metrics, m, v, sched, opt_first, sync, ticks, smem, rowidx,",
         "                                  flag_lds, stamps);",
@@ -168,10 +179,11 @@ _paths = {}     # (descriptor bytes, MT) -> code-object path: a refit of the sam
 
 
 def compile_for(trainer) -> str:
-    k = (bytes(trainer.desc), int(trainer.mt))
+    opt = getattr(trainer, "opt", None)
+    k = (bytes(trainer.desc), int(trainer.mt), bytes(opt) if opt is not None else b"")
     path = _paths.get(k)
     if path is None or not os.path.exists(path):
-        path = compile_source(generate_source(trainer.desc, trainer.mt))
+        path = compile_source(generate_source(trainer.desc, trainer.mt, opt))
         _paths[k] = path
     return path
 

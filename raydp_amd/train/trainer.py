@@ -145,7 +145,9 @@ def _worker_entry(rank, world, port, payload, queue):
             queue.put(("report", r, metrics, ckpt))
         ctx = S.TrainContext(rank, world, rank, world, 0, device, name, storage)
         S._set_session(S._Session(ctx, shards, reporter, storage))
-        fn(config) if _accepts_arg(fn) else fn()
+        from raydp_amd.train.gpu_policy import worker_policies
+        with worker_policies(use_gpu):
+            fn(config) if _accepts_arg(fn) else fn()
         queue.put(("done", rank, None, None))
     except BaseException as e:  # noqa: BLE001
         queue.put(("error", rank, traceback.format_exc(), None))
@@ -279,8 +281,10 @@ class DataParallelTrainer:
         sess = S._Session(ctx, shards, reporter, storage, self.resume)
         S._set_session(sess)
         from raydp_amd.data.dataset import DeferredDatasetError
+        from raydp_amd.train.gpu_policy import worker_policies
         try:
-            self.fn(self.config) if _accepts_arg(self.fn) else self.fn()
+            with worker_policies(use_gpu):
+                self.fn(self.config) if _accepts_arg(self.fn) else self.fn()
         except DeferredDatasetError:
             raise     # the input failed to materialise: restarting the workers cannot fix it
         except Exception as e:  # noqa: BLE001

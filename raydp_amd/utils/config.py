@@ -217,6 +217,16 @@ register("spark.ray.mi355x.overlap_conversion", "bool", True,
          "the conversion stage runs on the executors; the dataset blocks are awaited at first use",
          env="RAYDP_OVERLAP_CONVERSION")
 
+register("spark.ray.mi355x.fused_optimizer", "bool", True,
+         "Horovod's DistributedOptimizer runs a wrapped torch Adam / AdamW / SGD step on the multi-tensor "
+         "HIP kernels (csrc/hip/fused_optim.hip: one launch per 24 tensors) when every parameter is a dense "
+         "fp32 GPU tensor; torch's own step otherwise", env="RAYDP_FUSED_OPTIMIZER")
+register("spark.ray.mi355x.native_batchnorm", "bool", True,
+         "GPU train workers run BatchNorm layers on PyTorch's native kernels instead of MIOpen's (MIOpen's "
+         "batch-norm path is launch-bound at tabular batch sizes: scripts/dev/eager_step_bench.py, "
+         "profiles/r5_eager_variants.jsonl); only the BatchNorm call is affected, convolutions keep MIOpen",
+         env="RAYDP_NATIVE_BATCHNORM")
+
 
 def _active_conf() -> Optional[Mapping]:
     try:

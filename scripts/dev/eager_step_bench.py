@@ -1,7 +1,9 @@
 """Host-bound eager torch step of a user-written loop (the Horovod NYCTaxi example's step:
 NYC_Model, smooth-L1, Adam, batch 64, a loss.item() every 10 steps), under backend settings the
 framework can choose for its GPU workers without touching user code. One JSON line per run:
-  ES_VARIANT=base|fused_adam|native_bn|rocblas|all python scripts/dev/eager_step_bench.py"""
+  ES_VARIANT=base|fused_adam|native_bn|rocblas|all|rx python scripts/dev/eager_step_bench.py
+rx: what the framework's GPU workers now do -- hvd.DistributedOptimizer's multi-tensor Adam
+(csrc/hip/fused_optim.hip) under the native-BatchNorm worker policy."""
 import json, os, sys, time
 v = os.environ.get("ES_VARIANT", "base")
 if v in ("rocblas", "all"):
@@ -16,6 +18,12 @@ dev = torch.device("cuda")
 torch.manual_seed(0)
 model = _nyc_model(20).to(dev)
 opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"fused": True} if v in ("fused_adam", "all") else {}))
+if v == "rx":
+    import raydp_amd.hvd as hvd
+    from raydp_amd.train.gpu_policy import native_batchnorm
+    hvd.init()
+    opt = hvd.DistributedOptimizer(opt)
+    native_batchnorm(True).__enter__()
 X = torch.randn(64 * 600, 20, device=dev)
 Y = torch.randn(64 * 600, 1, device=dev)
 def run(steps):

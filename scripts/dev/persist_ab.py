@@ -56,5 +56,9 @@ print(json.dumps({"tree": os.path.basename(tree), "us_per_step_min": round(min(t
                   "epoch_ms": [round(t, 2) for t in ts], "loss": round(float(met["loss"]), 6),
                   "grid": getattr(tr, "_ps_grid", None),
                   "phases_us": {"inputs": us(1), "weights": us(2), "fwd": us(3), "bwd": us(4), "vec": us(5)},
+                  # first optimizer workgroup of each layer: flag seen -> counter raised
+                  "opt_us": {f"L{l}": [us(16 + 2 * l), us(17 + 2 * l)] for l in range(5)},
+                  "bwd_layer_done_us": {f"L{l}": us(8 + l) for l in range(5)},
+                  "opt_L0_loaded_updated_drained_us": [us(28), us(26), us(27)],
                   "layer_cycles": layer}),
       flush=True)

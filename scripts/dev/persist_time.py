@@ -48,7 +48,6 @@ t0 = s[0]
 us = lambda k: (s[k] - t0) * 0.01 if s[k] else float("nan")
 print("step WG: start 0 | inputs %.2f | weights ready %.2f | fwd done %.2f | bwd done %.2f | vec done %.2f us"
       % (us(1), us(2), us(3), us(4), us(5)))
-print("  vec (before barrier) %.2f" % us(6))
 print("  bwd layer done: " + " ".join(f"L{l}={us(8 + l):.2f}" for l in range(5)))
 print("  opt (first wg per layer) flag seen -> counted: " +
       " ".join(f"L{l}={us(16 + 2 * l):.2f}->{us(17 + 2 * l):.2f}" for l in range(5)))

@@ -357,7 +357,12 @@ def test_persistent_epoch_matches_step_loop(case, monkeypatch):
     assert torch.equal(p1, p0), ("params", where(p1, p0), "m", where(m1, m0), "v", where(v1, v0),
                                  "rstats", float((r1 - r0).abs().max()), e1, e0)
     assert torch.equal(m1, m0) and torch.equal(v1, v0)
-    assert torch.equal(i1, i0)
+    # bf16 images: all but Wt_0 -- layer 0 has no dgrad, so nothing reads its transposed image and
+    # the persistent kernel's optimizer workgroups do not rewrite it
+    l0 = tr.desc.layer[0]
+    keep = torch.ones_like(i1, dtype=torch.bool)
+    keep[l0.wt_img:l0.wt_img + l0.in_n * l0.out_k] = False
+    assert torch.equal(i1[keep], i0[keep])
     assert torch.equal(r1, r0)
     for a, b in zip(e1, e0):
         assert a["batches"] == b["batches"] and a["count"] == b["count"]

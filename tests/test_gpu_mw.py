@@ -17,14 +17,16 @@ from test_gpu_kernels import NYC, BnFirst, _norm_ratio, _relerr, _setup, emulate
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("batch,nvalid", [(100, 100), (256, 256), (256, 200), (1000, 1000), (4096, 4096),
-                                          (4096, 3001)])
+# batch 100 / 128 run as ONE 128-row workgroup since the transposed-image layout (the widest
+# single-workgroup tile, with the same whole-batch checks); 130 is the narrowest MW case
+@pytest.mark.parametrize("batch,nvalid", [(100, 100), (128, 97), (130, 130), (256, 256), (256, 200),
+                                          (1000, 1000), (4096, 4096), (4096, 3001)])
 def test_multi_workgroup_step_matches_torch(batch, nvalid):
     loss = nn.SmoothL1Loss()
     torch.manual_seed(0)
     model = NYC()
     tr, ref, ropt, feats, Y, X = _setup(model, loss, torch.optim.Adam, batch, nvalid, 20, 1, lr=1e-3)
-    assert tr.G > 1, (tr.mt, tr.G)
+    assert (tr.mt, tr.G) == (8, 1) if batch <= 128 else tr.G > 1, (tr.mt, tr.G)
     g = tr.forward_backward(feats, Y, nvalid).clone()
     m = tr._read_metrics()
     emu = copy.deepcopy(ref)
@@ -196,11 +198,11 @@ def test_reference_estimator_config_trains_on_fused_engine(workers, monkeypatch)
 
 
 def test_batch_100_nyc_no_longer_falls_off_the_fused_engine():
-    """NYC_Model at batch 100 does not fit one workgroup's LDS at 128 rows: it runs as two
-    64-row workgroups instead of raising."""
+    """NYC_Model at batch 100 runs on the fused engine: one 128-row workgroup since the
+    transposed-image layout (two 64-row workgroups before it), never a fallback."""
     model = NYC()
     tr, *_ = _setup(model, nn.MSELoss(), torch.optim.Adam, 100, 100, 20, 1, lr=1e-3)
-    assert (tr.mt, tr.G) == (4, 2)
+    assert (tr.mt, tr.G) == (8, 1)
 
 
 _ = os
