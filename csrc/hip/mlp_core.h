@@ -826,9 +826,12 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         bn_mean[j] = mean;
         bn_var[j] = v * inv_nv;
       }
-      // save the BN input for the backward pass (fragment-major, see frag_off)
+      // save the BN input for the backward pass (fragment-major, see frag_off); layer 0 of a
+      // persistent epoch that updates it in the step workgroup recomputes it instead
+      if (w0b == nullptr) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) sv_store<MT>(ly, smem, scratch, n, mt, lane, acc[j * MT + mt]);
+        for (int mt = 0; mt < MT; ++mt) sv_store<MT>(ly, smem, scratch, n, mt, lane, acc[j * MT + mt]);
+      }
     }
   };
   auto epi_b = [&](int j) {
@@ -874,7 +877,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       // ReLU mask source for the backward pass
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        sv_store<MT>(ly, smem, scratch, n, mt, lane, colok ? acc[j * MT + mt] : f32x4{0.f, 0.f, 0.f, 0.f});
+        if (w0b == nullptr) sv_store<MT>(ly, smem, scratch, n, mt, lane, colok ? acc[j * MT + mt] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
     // padded rows / columns carry exact zeros through every GEMM
     if (!(FULL && cols_full)) {
@@ -1203,8 +1206,14 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
                                                float* __restrict__ Gr, int nvalid, const float* __restrict__ scratch,
                                                unsigned long long* __restrict__ stamps,
                                                unsigned* __restrict__ sync = nullptr, int step = 0,
-                                               bool ps_wt = true, MWT* mw = nullptr, VO vo = VO{}) {
+                                               bool ps_wt = true, MWT* mw = nullptr, VO vo = VO{},
+                                               const bf16x8* w0b = nullptr) {
   using T = Tile<MT>;
+  // persistent epoch with layer 0 updated in the step workgroup: layer 0's saved BN input is not
+  // stored but recomputed here (l == 1) from the X^T_0 copy and the B fragments still in
+  // registers -- the forward's very MFMAs, bias and ReLU, so the same bits -- instead of 64 KB
+  // through memory each way (one CU's bandwidth: ~1.5 us a step at NYC)
+  const bool rec0 = w0b != nullptr && l == 1;
   const int lane = rx_tid<PS>() & 63, wave = rx_wave<PS>();
   const int lr = lane & 15, lg = lane >> 4;
   const int RS = d.max_k + RX_RPAD;
@@ -1225,7 +1234,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     gemm_prefetch_flat<PS>(wpre, img, ly.wt_img, ntiles_d, ly.out_k, wave, lr, lg);
 #pragma unroll
     for (int j = 0; j < RX_PJ; ++j) {
-      if (j * RX_NW < ntiles_d) {
+      if (j * RX_NW < ntiles_d && !rec0) {
         const int n = min(wave + j * RX_NW, ntiles_d - 1);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -1389,7 +1398,22 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     // column: issue all loads back to back, unconditionally (a load under a per-element
     // branch is waited for on its own -> one dependent L2 round trip per element).
     float sv[MT * 4], g[MT * 4];
-    if (j < RX_PJ) {
+    if (rec0) {
+      // layer 0's BN input: z = X_0 W_0^T (k order pi) + b, ReLU first when it precedes the BN
+      const AOp X0{reinterpret_cast<const u16*>(smem + d.x0c_lds_off), 0, true};
+      const float b0 = reinterpret_cast<const float*>(smem + d.pr_lds_off)[pv.pr_off + c];
+      const bf16x8 bw = w0b[j < RX_W0J ? j : 0];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        f32x4 z = rx_mfma16(ld_afrag_pi<MT>(X0, mt, lane), bw, f32x4{0.f, 0.f, 0.f, 0.f}) + f32x4{b0, b0, b0, b0};
+        if (pv.bn != 2 && pv.act == 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z[r] = fmaxf(z[r], 0.f);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sv[mt * 4 + r] = z[r];
+      }
+    } else if (j < RX_PJ) {
 #pragma unroll
       for (int q = 0; q < MT * 4; ++q) sv[q] = svp[j < RX_PJ ? j : 0][q];
     } else {
@@ -1594,19 +1618,41 @@ __device__ __forceinline__ void store_running_stats(const D& d, char* smem, floa
 // The labels the loss of a single-tile output layer (out <= 16 columns: wave 0, tile 0) reads,
 // fetched right after the batch's row indices are known: their dependent global round trip
 // overlaps the forward instead of sitting in the last layer's epilogue.
+// batch row whose label lands in slot q of this lane (-1: unused): the row-per-lane loss reads
+// rows lane + 64 q, the tile layout rows (q >> 2) 16 + 4 lg + (q & 3)
+template <int MT, class D>
+__device__ __forceinline__ int label_row(const D& d, int lane, int q) {
+  constexpr int BP = Tile<MT>::BP;
+  if (d.loss_lds_off >= 0 && d.loss != 4) {
+    const int r = lane + 64 * q;
+    return q < (BP > 64 ? BP / 64 : 1) ? (r < BP ? r : 0) : -1;
+  }
+  return (q >> 2) * 16 + (lane >> 4) * 4 + (q & 3);
+}
+
+// the labels given each slot's data-row index (rix[q], from label_row through the batch's rows)
+template <int MT, bool PS, class D>
+__device__ __forceinline__ void prefetch_labels_rows(const D& d, const float* __restrict__ labels,
+                                                     const int (&rix)[MT * 4], float (&tl)[MT * 4]) {
+  const int lane = rx_tid<PS>() & 63, lr = lane & 15;
+  const bool rowloss = d.loss_lds_off >= 0 && d.loss != 4;
+  const int cl = !rowloss && lr < d.out_dim ? lr : 0;
+#pragma unroll
+  for (int q = 0; q < MT * 4; ++q)
+    if (label_row<MT>(d, lane, q) >= 0) tl[q] = rx_g(labels)[rix[q] * d.out_dim + cl];
+}
+
 template <int MT, bool PS, class D>
 __device__ __forceinline__ void prefetch_labels(const D& d, const float* __restrict__ labels, const int* rowidx,
                                                 float (&tl)[MT * 4]) {
-  const int lane = rx_tid<PS>() & 63, lr = lane & 15, lg = lane >> 4;
-  if (d.loss_lds_off >= 0 && d.loss != 4) {   // the row-per-lane loss (layer_forward): row lane + 64 k
-    constexpr int BP = Tile<MT>::BP;
+  const int lane = rx_tid<PS>() & 63;
+  int rix[MT * 4];
 #pragma unroll
-    for (int k = 0; k < (BP > 64 ? BP / 64 : 1); ++k) tl[k] = rx_g(labels)[rowidx[lane + 64 * k < BP ? lane + 64 * k : 0] * d.out_dim];
-    return;
+  for (int q = 0; q < MT * 4; ++q) {
+    const int r = label_row<MT>(d, lane, q);
+    rix[q] = rowidx[r >= 0 ? r : 0];
   }
-  const int cl = lr < d.out_dim ? lr : 0;
-#pragma unroll
-  for (int q = 0; q < MT * 4; ++q) tl[q] = rx_g(labels)[rowidx[(q >> 2) * 16 + lg * 4 + (q & 3)] * d.out_dim + cl];
+  prefetch_labels_rows<MT, PS>(d, labels, rix, tl);
 }
 
 // Embedding front: build layer 0's input [BP][in_k] from the raw feature rows -- dense columns
@@ -1748,14 +1794,14 @@ __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem
 // read of chunk `idx` (row idx / chunks, 16 B of its features; zeros past nvalid) issued during
 // the previous step's backward and kept in a register, and its LDS scatter at the start of the
 // step -- one chunk per thread (BP * feat_k / 8 <= RX_THREADS), no embedding front.
+// `rix`: the data row of this chunk's batch row (idx / chunks)
 template <int MT, class D>
-__device__ __forceinline__ u32x4 gather_input_chunk(const D& d, const u16* __restrict__ feats, const int* rowidx,
-                                                   int nvalid, int idx) {
+__device__ __forceinline__ u32x4 gather_input_chunk(const D& d, const u16* __restrict__ feats, int rix, int nvalid,
+                                                   int idx) {
   const int chunks = d.feat_k >> 3;
   const int row = idx / chunks, ch = idx - (idx / chunks) * chunks;
-  const int r = row < Tile<MT>::BP ? row : 0;
-  const u32x4 v = *reinterpret_cast<const RX_GLOBAL u32x4*>(rx_g(feats) + (size_t)rowidx[r] * d.feat_k + ch * 8);
-  return row < nvalid ? v : u32x4{0u, 0u, 0u, 0u};
+  const u32x4 v = *reinterpret_cast<const RX_GLOBAL u32x4*>(rx_g(feats) + (size_t)rix * d.feat_k + ch * 8);
+  return row < nvalid && row < Tile<MT>::BP ? v : u32x4{0u, 0u, 0u, 0u};
 }
 template <int MT, class D, class L0>
 __device__ __forceinline__ void scatter_input_chunk(const D& d, const L0& l0, char* smem, int idx, const u32x4& v) {

@@ -390,7 +390,11 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
   // layer 0 updated here (see ps_l0_update): its state into LDS, its first B fragments
   const bool l0_in = o.ps_l0_inline != 0 && d.w0s_lds_off >= 0;
   bf16x8 w0b[RX_W0J];
-  if (l0_in) ps_l0_load(C::first(d), smem, d.w0s_lds_off, P, m, v, w0b);
+  if (l0_in) {
+    ps_l0_load(C::first(d), smem, d.w0s_lds_off, P, m, v, w0b);
+    // the X^T_0 copy's K-tail rows [in_n, in_k): zeros for the whole epoch (nothing writes them)
+    zero_t_rows<MT, true>(reinterpret_cast<u16*>(smem + d.x0c_lds_off), C::first(d).in_n, C::first(d).in_k);
+  }
   __syncthreads();
   if (flag_lds[0]) return;
   const bool ps_wt = flag_lds[1] != 0;
@@ -403,10 +407,9 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
   const rx_opt_holder<O> oh;
   const O& oc = oh.get(o);
   float* vsc = reinterpret_cast<float*>(flag_lds + 4);   // the step's optimizer scalars (PsVec::sc)
-  // next-batch prefetch during the backward (one input chunk per thread, no embedding front):
-  // rowidx holds 2 BP entries, the second half the next step's rows
+  // next-batch prefetch during the backward (one input chunk per thread, no embedding front)
   const bool pf = Tile<MT>::BP * (d.feat_k >> 3) <= RX_THREADS && d.front_n == 0;
-  int* rowidx_n = rowidx + Tile<MT>::BP;
+  int pr_i = 0;                 // next step: this thread's row index (threads < BP)
   u32x4 xin = u32x4{0u, 0u, 0u, 0u};
   float labn[MT * 4], labp[MT * 4];
 #pragma unroll
@@ -424,8 +427,8 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     }
     if (s > 0 && pf) {
       // this batch was fetched during the previous step's backward: rows, features and labels
-      // are already in registers / the second row-index array
-      for (int i = rx_tid(); i < Tile<MT>::BP; i += RX_THREADS) rowidx[i] = rowidx_n[i];
+      // are already in registers
+      if (rx_tid() < Tile<MT>::BP) rowidx[rx_tid()] = pr_i;
       scatter_input_chunk<MT>(d, C::first(d), smem, rx_tid(), xin);
       if (d.r_lds_off < 0 && C::first(d).in_k > C::first(d).in_n)   // T mode: XT_0's K tail rows
         zero_t_rows<MT, true>(reinterpret_cast<u16*>(smem + C::first(d).xt_off), C::first(d).in_n,
@@ -510,13 +513,23 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
                                          (l == 0 && l0_in) ? w0b : nullptr, &nxw);
       });
       stamp(s, 3);
-      // next batch, part 1: its row indices (a global read whose latency the backward hides)
+      // next batch, part 1: the data rows this thread needs (its own row index, its feature
+      // chunk's row, its label slots' rows) -- global reads the first backward layer hides; every
+      // thread reads its own, so no barrier joins the two parts
       const bool pf_next = pf && s + 1 < nsteps;
       const int row0n = row0 + batch, nvalid_n = min(batch, n_rows - row0n);
-      int pn = 0;
-      if (pf_next && rx_tid() < Tile<MT>::BP) {
-        const int i = rx_tid();
-        pn = i < nvalid_n ? (perm ? rx_g(perm)[row0n + i] : row0n + i) : (perm ? rx_g(perm)[row0n] : row0n);
+      int pr_f = 0, pr_l[MT * 4];
+      if (pf_next) {
+        auto prow = [&](int i) {
+          return i < nvalid_n ? (perm ? rx_g(perm)[row0n + i] : row0n + i) : (perm ? rx_g(perm)[row0n] : row0n);
+        };
+        pr_i = prow(rx_tid() < Tile<MT>::BP ? rx_tid() : 0);
+        pr_f = prow(min(rx_tid() / (d.feat_k >> 3), Tile<MT>::BP - 1));
+#pragma unroll
+        for (int q = 0; q < MT * 4; ++q) {
+          const int r = label_row<MT>(d, rx_tid() & 63, q);
+          pr_l[q] = r >= 0 ? prow(r) : 0;
+        }
       }
       bool first_bwd = true;
       C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
@@ -524,14 +537,12 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
           ps_l0_update<MT>(d, ly, smem, oc, vsc, w0b);
         else
           layer_backward<MT, true, F>(d, ly, pv, l, smem, img, P, Gr, nvalid, scratch, lst, sync, s, ps_wt,
-                                      static_cast<NoMw*>(nullptr), vo);
+                                      static_cast<NoMw*>(nullptr), vo, l0_in ? w0b : nullptr);
         if (first_bwd && pf_next) {
-          // part 2, after the first backward layer: the rows to LDS, then the feature chunks and
-          // labels into registers (held until the next step scatters them)
-          if (rx_tid() < Tile<MT>::BP) rowidx_n[rx_tid()] = pn;
-          __syncthreads();
-          xin = gather_input_chunk<MT>(d, feats, rowidx_n, nvalid_n, rx_tid());
-          prefetch_labels<MT, true>(d, labels, rowidx_n, labn);
+          // part 2, after the first backward layer: the feature chunk and the labels into
+          // registers (held until the next step scatters them)
+          xin = gather_input_chunk<MT>(d, feats, pr_f, nvalid_n, rx_tid());
+          prefetch_labels_rows<MT, true>(d, labels, pr_l, labn);
         }
         first_bwd = false;
         stamp(s, 8 + l);

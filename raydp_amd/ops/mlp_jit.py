@@ -123,7 +123,7 @@ def generate_source(desc: "_hip.MlpDesc", mt: int, opt: Optional["_hip.OptDesc"]
         "    float* __restrict__ m, float* __restrict__ v, const float* __restrict__ sched, int opt_first,",
         "    unsigned* __restrict__ sync, unsigned long long ticks, unsigned long long* __restrict__ stamps) {",
         "  extern __shared__ __attribute__((aligned(16))) char smem[];",
-        "  __shared__ int rowidx[2 * Tile<RX_MT>::BP];   // [this step | next step (prefetch)]",
+        "  __shared__ int rowidx[Tile<RX_MT>::BP];",
         "  __shared__ __attribute__((aligned(16))) int flag_lds[16];",
         "  mlp_persist_body<JitCfg, RX_MT>(dp, od, img, rstats, P, Gr, feats, labels, perm, n_rows, batch, nsteps,",
         "                                  scratch, metrics, m, v, sched, opt_first, sync, ticks, smem, rowidx,",
