@@ -48,6 +48,7 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.native_executor", "RAYDP_NATIVE_EXECUTOR", "1"},
     {"spark.ray.mi355x.fused_optimizer", "RAYDP_FUSED_OPTIMIZER", "1"},
     {"spark.ray.mi355x.native_batchnorm", "RAYDP_NATIVE_BATCHNORM", "1"},
+    {"spark.ray.mi355x.graph_user_model", "RAYDP_GRAPH_USER_MODEL", "1"},
 };
 
 // Value of a key: its environment variable when set and non-empty, else the default.

@@ -1794,14 +1794,52 @@ __device__ __forceinline__ void load_inputs(const D& d, const L0& l0, char* smem
 // read of chunk `idx` (row idx / chunks, 16 B of its features; zeros past nvalid) issued during
 // the previous step's backward and kept in a register, and its LDS scatter at the start of the
 // step -- one chunk per thread (BP * feat_k / 8 <= RX_THREADS), no embedding front.
-// `rix`: the data row of this chunk's batch row (idx / chunks)
-template <int MT, class D>
+// Chunk idx -> (batch row, 16-B chunk of its features). QUAD (T mode): the 4 lanes of a quad hold
+// 4 consecutive rows of the same chunk, so scatter_input_quads can transpose them in registers.
+template <bool QUAD>
+__device__ __forceinline__ void input_chunk_pos(int idx, int chunks, int& row, int& ch) {
+  if (QUAD) {
+    ch = (idx >> 2) % chunks;
+    row = ((idx >> 2) / chunks) * 4 + (idx & 3);
+  } else {
+    row = idx / chunks;
+    ch = idx - row * chunks;
+  }
+}
+
+// `rix`: the data row of this chunk's batch row
+template <int MT, bool QUAD, class D>
 __device__ __forceinline__ u32x4 gather_input_chunk(const D& d, const u16* __restrict__ feats, int rix, int nvalid,
                                                    int idx) {
-  const int chunks = d.feat_k >> 3;
-  const int row = idx / chunks, ch = idx - (idx / chunks) * chunks;
+  int row, ch;
+  input_chunk_pos<QUAD>(idx, d.feat_k >> 3, row, ch);
   const u32x4 v = *reinterpret_cast<const RX_GLOBAL u32x4*>(rx_g(feats) + (size_t)rix * d.feat_k + ch * 8);
   return row < nvalid && row < Tile<MT>::BP ? v : u32x4{0u, 0u, 0u, 0u};
+}
+
+// T-mode scatter of quad-mapped chunks: two quad transposes turn 4 rows x 8 features into 8
+// features x 4 rows, written as 8-B stores into XT_0 (and the X^T_0 copy) -- 2 + 2 LDS writes per
+// lane instead of 16 two-byte ones (those hit 4-way bank conflicts: 4 feature rows 1 KB apart)
+template <int MT, class D, class L0>
+__device__ __forceinline__ void scatter_input_quads(const D& d, const L0& l0, char* smem, int idx, const u32x4& v) {
+  using T = Tile<MT>;
+  int row, ch;
+  input_chunk_pos<true>(idx, d.feat_k >> 3, row, ch);
+  const int q = idx & 3, row0 = row - q;
+  const uint2 lo = rx_quad_transpose(make_uint2(v[0], v[1]), q);   // feature ch 8 + q, rows row0 .. +3
+  const uint2 hi = rx_quad_transpose(make_uint2(v[2], v[3]), q);   // feature ch 8 + 4 + q
+  if (row0 >= T::BP) return;
+  u16* XT = reinterpret_cast<u16*>(smem + l0.xt_off);
+  u16* XC = d.x0c_lds_off >= 0 ? reinterpret_cast<u16*>(smem + d.x0c_lds_off) : nullptr;
+  const int k0 = ch * 8 + q, k1 = k0 + 4;
+  if (k0 < l0.in_n) {
+    *reinterpret_cast<uint2*>(XT + T::tix(k0, row0)) = lo;
+    if (XC != nullptr) *reinterpret_cast<uint2*>(XC + T::tix(k0, row0)) = lo;
+  }
+  if (k1 < l0.in_n) {
+    *reinterpret_cast<uint2*>(XT + T::tix(k1, row0)) = hi;
+    if (XC != nullptr) *reinterpret_cast<uint2*>(XC + T::tix(k1, row0)) = hi;
+  }
 }
 template <int MT, class D, class L0>
 __device__ __forceinline__ void scatter_input_chunk(const D& d, const L0& l0, char* smem, int idx, const u32x4& v) {

@@ -410,6 +410,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
   // next-batch prefetch during the backward (one input chunk per thread, no embedding front)
   const bool pf = Tile<MT>::BP * (d.feat_k >> 3) <= RX_THREADS && d.front_n == 0;
   int pr_i = 0;                 // next step: this thread's row index (threads < BP)
+  float sch[3] = {0.f, 1.f, 1.f};   // thread 0: the step's lr, bc1, bc2
   u32x4 xin = u32x4{0u, 0u, 0u, 0u};
   float labn[MT * 4], labp[MT * 4];
 #pragma unroll
@@ -422,14 +423,24 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     const int row0 = s * batch;
     const int nvalid = min(batch, n_rows - row0);
     if (rx_tid() == 0) {
-      const float lr = rx_g(sched)[s], bc1 = rx_g(sched)[nsteps + s], bc2 = rx_g(sched)[2 * nsteps + s];
+      // this step's lr and bias corrections: read during the previous step's backward (a global
+      // read here would hold every wave at the next barrier for its round trip)
+      if (s == 0) {
+        sch[0] = rx_g(sched)[0];
+        sch[1] = rx_g(sched)[nsteps];
+        sch[2] = rx_g(sched)[2 * nsteps];
+      }
+      const float lr = sch[0], bc1 = sch[1], bc2 = sch[2];
       *reinterpret_cast<f32x4*>(vsc) = f32x4{lr, -(lr / bc1), 1.f / sqrtf(bc2), (opt_first && s == 0) ? 1.f : 0.f};
     }
     if (s > 0 && pf) {
       // this batch was fetched during the previous step's backward: rows, features and labels
       // are already in registers
       if (rx_tid() < Tile<MT>::BP) rowidx[rx_tid()] = pr_i;
-      scatter_input_chunk<MT>(d, C::first(d), smem, rx_tid(), xin);
+      if (d.r_lds_off < 0)
+        scatter_input_quads<MT>(d, C::first(d), smem, rx_tid(), xin);
+      else
+        scatter_input_chunk<MT>(d, C::first(d), smem, rx_tid(), xin);
       if (d.r_lds_off < 0 && C::first(d).in_k > C::first(d).in_n)   // T mode: XT_0's K tail rows
         zero_t_rows<MT, true>(reinterpret_cast<u16*>(smem + C::first(d).xt_off), C::first(d).in_n,
                               C::first(d).in_k);
@@ -516,6 +527,11 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       // next batch, part 1: the data rows this thread needs (its own row index, its feature
       // chunk's row, its label slots' rows) -- global reads the first backward layer hides; every
       // thread reads its own, so no barrier joins the two parts
+      if (rx_tid() == 0 && s + 1 < nsteps) {
+        sch[0] = rx_g(sched)[s + 1];
+        sch[1] = rx_g(sched)[nsteps + s + 1];
+        sch[2] = rx_g(sched)[2 * nsteps + s + 1];
+      }
       const bool pf_next = pf && s + 1 < nsteps;
       const int row0n = row0 + batch, nvalid_n = min(batch, n_rows - row0n);
       int pr_f = 0, pr_l[MT * 4];
@@ -524,7 +540,12 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
           return i < nvalid_n ? (perm ? rx_g(perm)[row0n + i] : row0n + i) : (perm ? rx_g(perm)[row0n] : row0n);
         };
         pr_i = prow(rx_tid() < Tile<MT>::BP ? rx_tid() : 0);
-        pr_f = prow(min(rx_tid() / (d.feat_k >> 3), Tile<MT>::BP - 1));
+        int frow, fch;
+        if (d.r_lds_off < 0)
+          input_chunk_pos<true>(rx_tid(), d.feat_k >> 3, frow, fch);
+        else
+          input_chunk_pos<false>(rx_tid(), d.feat_k >> 3, frow, fch);
+        pr_f = prow(min(frow, Tile<MT>::BP - 1));
 #pragma unroll
         for (int q = 0; q < MT * 4; ++q) {
           const int r = label_row<MT>(d, rx_tid() & 63, q);
@@ -541,7 +562,8 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
         if (first_bwd && pf_next) {
           // part 2, after the first backward layer: the feature chunk and the labels into
           // registers (held until the next step scatters them)
-          xin = gather_input_chunk<MT>(d, feats, pr_f, nvalid_n, rx_tid());
+          xin = d.r_lds_off < 0 ? gather_input_chunk<MT, true>(d, feats, pr_f, nvalid_n, rx_tid())
+                                : gather_input_chunk<MT, false>(d, feats, pr_f, nvalid_n, rx_tid());
           prefetch_labels_rows<MT, true>(d, labels, pr_l, labn);
         }
         first_bwd = false;

@@ -9,6 +9,7 @@ once per epoch (the reference syncs on ``loss.item()`` every step,
 ``python/raydp/torch/estimator.py:280``).
 """
 import ctypes
+import os
 import math
 from typing import Callable, Dict, List, Optional
 
@@ -146,7 +147,11 @@ def layout_candidates(batch: int):
     single = pick_mt(batch)
     if single is not None:
         out.append((single, 1))
-    for mt in (8, 4, 2):
+    order = (8, 4, 2)
+    want = int(os.environ.get("RAYDP_MLP_MW_MT", "0") or 0)   # dev knob: prefer this tile
+    if want in order:
+        order = (want,) + tuple(m for m in order if m != want)
+    for mt in order:
         if batch > 16 * mt:
             out.append((mt, -(-batch // (16 * mt))))
     return out

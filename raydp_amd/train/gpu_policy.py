@@ -9,6 +9,15 @@ touching user code (Ray Train's worker setup plays the same role: device placeme
   convolutions keep MIOpen. The autograd node the forward picked (native_batch_norm_backward)
   carries the backward. Config ``spark.ray.mi355x.native_batchnorm``.
 
+* :func:`graph_model` -- ``train.torch.prepare_model`` on a one-worker GPU job replays the
+  model's training forward + backward as HIP graphs (``torch.cuda.make_graphed_callables``) once
+  a batch shape has repeated: a tabular MLP step is ~40 tiny kernels each way, each costing more
+  host time than device time (the stroke tutorial's GPU loop was slower than its CPU loop, B4).
+  Eval / no-grad calls, other shapes, kwargs and models whose forward cannot be captured (a host
+  sync, data-dependent control flow) run eagerly; the capture's warm-up leaves BatchNorm running
+  statistics as they were; outputs are cloned out of the graph's static buffers, so a caller may
+  keep them across steps. Config ``spark.ray.mi355x.graph_user_model``.
+
 Reference role: the worker set-up of Ray Train's ``TorchTrainer`` / ``HorovodTrainer``
 (``tutorials/raytrain_example.ipynb`` cell 40, ``examples/horovod_nyctaxi.py:119-162``).
 """
@@ -48,3 +57,65 @@ def worker_policies(use_gpu: bool):
     """The context a GPU train worker runs its loop in (a no-op context on CPU workers)."""
     from raydp_amd.utils import config as C
     return native_batchnorm(bool(use_gpu) and bool(C.get("spark.ray.mi355x.native_batchnorm")))
+
+
+_MAX_SHAPES = 4        # graphed batch shapes per model (a ragged last batch stays eager)
+_STEADY = 3            # calls with the same shape before it is graphed
+
+
+def graph_model(module):
+    """Patch ``module`` (in place: same object, same ``state_dict``) so its training forward runs
+    from a captured HIP graph per repeated input shape; returns the module."""
+    import torch
+    if getattr(module, "_raydp_graphed", False):
+        return module
+    orig = module.forward
+    graphs, seen = {}, {}
+    state = {"failed": False}
+
+    class _Fwd(torch.nn.Module):       # parameters() = the model's, forward = its original one
+        def __init__(self):
+            super().__init__()
+            self.m = module
+
+        def forward(self, *a):
+            return orig(*a)
+
+    def _capture(args):
+        bufs = [(b, b.detach().clone()) for b in module.buffers()]
+        try:
+            fwd = _Fwd()
+            samples = tuple(a.detach().clone() for a in args)
+            torch.cuda.synchronize()
+            g = torch.cuda.make_graphed_callables(fwd, samples, num_warmup_iters=3)
+            return g
+        except Exception:  # noqa: BLE001 - not capturable: eager from now on
+            state["failed"] = True
+            return None
+        finally:
+            with torch.no_grad():       # the warm-up's BatchNorm statistics are not training steps
+                for b, v in bufs:
+                    b.copy_(v)
+
+    def forward(*args, **kwargs):
+        if (kwargs or state["failed"] or not module.training or not torch.is_grad_enabled()
+                or not args or not all(isinstance(a, torch.Tensor) and a.is_cuda and not a.requires_grad
+                                       for a in args)):
+            return orig(*args, **kwargs)
+        key = tuple((tuple(a.shape), a.dtype) for a in args)
+        g = graphs.get(key)
+        if g is None:
+            n = seen.get(key, 0) + 1
+            seen[key] = n
+            if n < _STEADY or len(graphs) >= _MAX_SHAPES:
+                return orig(*args)
+            g = _capture(args)
+            if g is None:
+                return orig(*args)
+            graphs[key] = g
+        out = g(*args)
+        return torch.utils._pytree.tree_map(lambda t: t.clone() if isinstance(t, torch.Tensor) else t, out)
+
+    module.forward = forward
+    module._raydp_graphed = True
+    return module

@@ -668,4 +668,9 @@ def prepare_model(model, move_to_device=True, parallel_strategy="ddp"):
     if ctx.world_size > 1 and dist.is_initialized():
         from raydp_amd.parallel.ddp import DistributedDataParallel
         model = DistributedDataParallel(model)
+    elif dev.type == "cuda" and move_to_device:
+        from raydp_amd.utils import config as C
+        if C.get("spark.ray.mi355x.graph_user_model"):
+            from raydp_amd.train.gpu_policy import graph_model
+            model = graph_model(model)     # one GPU worker: training forward/backward as HIP graphs
     return model

@@ -227,6 +227,11 @@ register("spark.ray.mi355x.native_batchnorm", "bool", True,
          "profiles/r5_eager_variants.jsonl); only the BatchNorm call is affected, convolutions keep MIOpen",
          env="RAYDP_NATIVE_BATCHNORM")
 
+register("spark.ray.mi355x.graph_user_model", "bool", True,
+         "train.torch.prepare_model on a one-worker GPU job replays the model's training forward + "
+         "backward as HIP graphs per repeated batch shape (raydp_amd/train/gpu_policy.py graph_model); "
+         "eager for eval, other shapes and models that cannot be captured", env="RAYDP_GRAPH_USER_MODEL")
+
 
 def _active_conf() -> Optional[Mapping]:
     try:

@@ -172,3 +172,50 @@ def test_dlrm_step_with_fused_tail_matches_eager():
     for (n, a), (_, b) in zip(ref.state_dict().items(), fused.state_dict().items()):
         if a.dtype.is_floating_point:
             torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5, msg=n)
+
+
+def test_prepare_model_graphs_the_training_step_like_eager():
+    """graph_model (train.torch.prepare_model on one GPU worker): a BatchNorm MLP with a
+    multi-input forward trained for 12 steps, graphed after 3 same-shape calls, with a ragged last
+    batch and an eval pass in between, ends with the same parameters, BatchNorm running statistics
+    and losses as the eager model (the same kernels replayed)."""
+    from raydp_amd.train.gpu_policy import graph_model
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc1, self.bn1, self.fc2 = nn.Linear(6, 32), nn.BatchNorm1d(32), nn.Linear(32, 2)
+
+        def forward(self, *cols):
+            x = torch.cat(cols, dim=1)
+            return self.fc2(self.bn1(torch.relu(self.fc1(x))))
+
+    torch.manual_seed(0)
+    ref = Net().cuda()
+    mine = copy.deepcopy(ref)
+    graph_model(mine)
+    ro = torch.optim.Adam(ref.parameters(), lr=1e-2)
+    mo = torch.optim.Adam(mine.parameters(), lr=1e-2)
+    g = torch.Generator().manual_seed(3)
+    data = [(torch.randn(64 if i < 11 else 37, 6, generator=g).cuda(), torch.randint(0, 2, (64 if i < 11 else 37,),
+                                                                                      generator=g).cuda())
+            for i in range(12)]
+    losses = []
+    for i, (x, y) in enumerate(data):
+        for m, o in ((ref, ro), (mine, mo)):
+            m.train()
+            cols = [x[:, k].unsqueeze(1) for k in range(6)]
+            loss = nn.functional.cross_entropy(m(*cols), y)
+            o.zero_grad()
+            loss.backward()
+            o.step()
+            losses.append(loss.item())
+        if i == 5:
+            for m in (ref, mine):
+                m.eval()
+                with torch.no_grad():
+                    m(*[x[:, k].unsqueeze(1) for k in range(6)])
+    for a, b in zip(ref.state_dict().values(), mine.state_dict().values()):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.tensor(losses[1::2]), torch.tensor(losses[0::2]), rtol=1e-5, atol=1e-6)
+    assert getattr(mine, "_raydp_graphed", False)

@@ -142,7 +142,8 @@ def run(num_executors=1, num_epochs=10, callbacks=None):
     from ray.train import Trainer
     spark = raydp.init_spark("Stroke Prediction (Ray Train)", num_executors, 1, "500M")
     train_ds, test_ds, features = prepare(spark, num_executors)
-    trainer = Trainer(backend="torch", num_workers=num_executors)
+    # (the notebook runs on CPU; on a GPU the workers are GPU workers, as Ray Train's use_gpu)
+    trainer = Trainer(backend="torch", num_workers=num_executors, use_gpu=DEVICE == "cuda")
     trainer.start()
     results = trainer.run(make_train_func(features), config={"num_epochs": num_epochs, "lr": 0.001, "batch_size": 64},
                           callbacks=callbacks or [], dataset={"train": train_ds, "test": test_ds})
