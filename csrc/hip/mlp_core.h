@@ -216,6 +216,9 @@ struct MwCtx {
   int n_total;                 // valid rows of the whole batch
   unsigned long long ticks;    // wall-clock bound of one barrier wait
   unsigned long long* tstamp;  // optional: workgroup 0 stores the step's start (wall clock) here
+  unsigned long long* lstamp;  // diagnostic build (RX_LAYER_STAMPS): workgroup 0's intra-layer
+                               // shader-clock stamps of this step ([20 + 4 l ..] backward, [40 + 5 l ..]
+                               // forward, [0 .. 2] the closing barrier / bias reduction)
 };
 
 // The persistent step's per-layer weight wait (mlp_persist.h PsNxWait): layer_forward(l) issues
@@ -1943,18 +1946,25 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
   load_inputs<MT>(d, C::first(d), smem, feats, rowidx, nvalid, true, dp, P, metrics);
   float labp[MT * 4];
   prefetch_labels<MT, false>(d, labels, rowidx, labp);
+#ifdef RX_LAYER_STAMPS
+  unsigned long long* lst = mw.wg == 0 ? mw.lstamp : nullptr;
+#else
+  unsigned long long* lst = nullptr;
+#endif
   C::fwd_layers(d, [&](const auto& ly, const auto& nx, int l, bool last) {
     layer_forward<MT, true, false>(d, ly, nx, last, smem, img, P, Gr, labels, rowidx, nvalid, sc, metrics, wpre,
-                                   true, l, nullptr, labp, &mw);
+                                   true, l, lst, labp, &mw);
   });
   // every workgroup computed the same batch statistics: one stores the running averages
   if (mw.wg == 0 && mw.ok) store_running_stats<C>(d, smem, rstats);
   C::bwd_layers(d, [&](const auto& ly, const auto& pv, int l) {
-    layer_backward<MT, false>(d, ly, pv, l, smem, img, P, Gr, nvalid, sc, nullptr, nullptr, 0, true, &mw);
+    layer_backward<MT, false>(d, ly, pv, l, smem, img, P, Gr, nvalid, sc, lst, nullptr, 0, true, &mw);
   });
+  if (lst != nullptr && threadIdx.x == 0) rx_g(lst)[0] = __builtin_amdgcn_s_memtime();
   // bias gradients: the workgroups' partial column sums, added in workgroup order, each
   // (layer, column) by one thread of the grid
   mw.ok = mw_barrier(mw, ++mw.k) && mw.ok;
+  if (lst != nullptr && threadIdx.x == 0) rx_g(lst)[1] = __builtin_amdgcn_s_memtime();
   C::each_layer(d, [&](const auto& ly, int) {
     if (ly.b_off >= 0 && mw.ok) {   // (after a timed-out barrier the partials are incomplete)
       for (int c = (int)blockIdx.x * RX_THREADS + rx_tid<false>(); c < ly.out; c += mw.G * RX_THREADS) {

@@ -700,6 +700,7 @@ class FusedMLPTrainer:
                 # step starts only (no end stamp): the last step's time is not recorded
                 st = back[2].copy()
                 self._step_stamps = st[:32 + nsteps] if nsteps > 1 else None
+                self._mw_layer_stamps = st[32 + nsteps + 1:]   # (RAYDP_MLP_LAYER_STAMPS builds)
             if int(back[0][0]) != 0:
                 # from the timed-out step on, the steps stored no gradients and the optimizer
                 # updated nothing; roll the whole epoch back and clear the control words so the
