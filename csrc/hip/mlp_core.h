@@ -418,6 +418,45 @@ __device__ __forceinline__ float mw_m2_sum(const float* p0, int stride, int G, i
   return rx_colsum16(m2);
 }
 
+// mw_pair_sum's first component and mw_m2_sum with ONE round of partial loads when the grid is
+// at most 32 workgroups (each lane's 8 pairs stay in registers for the second pass): the same
+// additions in the same order, one cross-XCD round trip instead of two per BatchNorm layer
+__device__ __forceinline__ void mw_mean_m2(const float* p0, int stride, int G, int q, int n_batch, int bp,
+                                           float& mean, float& m2out) {
+  if (G > 32) {
+    float S, unused;
+    mw_pair_sum(p0, stride, G, q, S, unused);
+    mean = S / (float)n_batch;
+    m2out = mw_m2_sum(p0, stride, G, q, mean, n_batch, bp);
+    return;
+  }
+  float vs[8], vm[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int w = q + 4 * i;
+    const float* pp = p0 + (size_t)(w < G ? w : q) * (size_t)stride;
+    vs[i] = rx_ld_sc1f(pp);
+    vm[i] = rx_ld_sc1f(pp + 1);
+  }
+  float sa = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (q + 4 * i < G) sa += vs[i];
+  mean = rx_colsum16(sa) / (float)n_batch;
+  float m2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int w = q + 4 * i;
+    const int nwi = w < G ? mw_rows(n_batch, w, bp) : 0;
+    if (nwi == 0) continue;
+    const float nw = (float)nwi;
+    const float dm = vs[i] / nw - mean;
+    m2 += vm[i];
+    m2 = fmaf(nw * dm, dm, m2);
+  }
+  m2out = rx_colsum16(m2);
+}
+
 __device__ __forceinline__ float act_fwd(int act, float z) { return act == 1 ? fmaxf(z, 0.f) : z; }
 
 // Element (mt, r) of an accumulator tile is batch row mt * 16 + 4 lg + r. FULL (the batch fills
@@ -1141,10 +1180,8 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
         const int c = n * 16 + lr;
         const int cc = c < ly.out ? c : 0;
         const float* p0 = mw_fwd(mw->part, mw->stride, ly, 0) + 2 * cc;
-        float S, unused;
-        mw_pair_sum(p0, mw->stride, mw->G, lg, S, unused);
-        const float mean = S / (float)n_batch;
-        const float M2 = mw_m2_sum(p0, mw->stride, mw->G, lg, mean, n_batch, T::BP);
+        float mean, M2;
+        mw_mean_m2(p0, mw->stride, mw->G, lg, n_batch, T::BP, mean, M2);
         bn_mean[j] = mean;
         bn_var[j] = M2 / (float)n_batch;
       }

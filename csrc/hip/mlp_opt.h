@@ -72,6 +72,34 @@ __device__ __forceinline__ void opt_update_pre(const O& o, float& pv, float& mv,
   }
 }
 
+// Four elements at once: Adam / AdamW in packed-fp32 operations (v_pk_fma_f32 / v_pk_mul_f32 on
+// pairs), the same operations per element as opt_update_pre -- so the same bits; other algorithms
+// and options element by element.
+template <class O>
+__device__ __forceinline__ void opt_update_pre4(const O& o, f32x4& pv, f32x4& mv, f32x4& vv, f32x4 g, float lr,
+                                                float nlr_bc1, float rs_bc2, int first) {
+  if (o.algo == 2 || o.maximize || (o.algo == 0 && o.wd != 0.f)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float p_ = pv[r], m_ = mv[r], v_ = vv[r];
+      opt_update_pre(o, p_, m_, v_, g[r], lr, nlr_bc1, rs_bc2, 1.f, first);
+      pv[r] = p_;
+      mv[r] = m_;
+      vv[r] = v_;
+    }
+    return;
+  }
+  auto splat = [](float x) { return f32x4{x, x, x, x}; };
+  g = g * splat(1.f);                                        // (gsum * gscale, gscale = 1)
+  if (o.algo == 1) pv *= splat(fmaf(-lr, o.wd, 1.f));
+  mv = __builtin_elementwise_fma(splat(o.b1), mv, splat(1.f - o.b1) * g);
+  vv = __builtin_elementwise_fma(splat(o.b2), vv, (splat(1.f - o.b2) * g) * g);
+  f32x4 q;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) q[r] = __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_sqrtf(vv[r]), rs_bc2, o.eps));
+  pv = __builtin_elementwise_fma(splat(nlr_bc1), mv * q, pv);
+}
+
 template <class O>
 __device__ __forceinline__ void opt_update_reg(const O& o, float& pv, float& mv, float& vv, float gsum, float lr,
                                                float bc1, float bc2, float gscale, int first) {

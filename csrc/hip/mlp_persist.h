@@ -284,14 +284,18 @@ __device__ __forceinline__ void ps_l0_update(const D& d, const LY& ly, char* sme
         pv = *reinterpret_cast<const f32x4*>(S + slot);
         f32x4 mv = *reinterpret_cast<const f32x4*>(S + RX_W0S_N + slot);
         f32x4 vv = *reinterpret_cast<const f32x4*>(S + 2 * RX_W0S_N + slot);
+        if (16 * mi + 4 * lg + 3 < ly.in) {
+          opt_update_pre4(hp, pv, mv, vv, a4, sc[0], sc[1], sc[2], first);   // four real columns
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (16 * mi + 4 * lg + r < ly.in) {
-            float p_ = pv[r], m_ = mv[r], v_ = vv[r];
-            opt_update_pre(hp, p_, m_, v_, a4[r], sc[0], sc[1], sc[2], 1.f, first);
-            pv[r] = p_;
-            mv[r] = m_;
-            vv[r] = v_;
+          for (int r = 0; r < 4; ++r) {
+            if (16 * mi + 4 * lg + r < ly.in) {
+              float p_ = pv[r], m_ = mv[r], v_ = vv[r];
+              opt_update_pre(hp, p_, m_, v_, a4[r], sc[0], sc[1], sc[2], 1.f, first);
+              pv[r] = p_;
+              mv[r] = m_;
+              vv[r] = v_;
+            }
           }
         }
         *reinterpret_cast<f32x4*>(S + slot) = pv;

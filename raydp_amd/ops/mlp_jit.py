@@ -50,6 +50,11 @@ def generate_source(desc: "_hip.MlpDesc", mt: int, opt: Optional["_hip.OptDesc"]
     if os.environ.get("RAYDP_MLP_LAYER_STAMPS") == "1":
         # diagnostic build: the persistent epoch's middle step writes intra-layer s_memtime stamps
         out.append("#define RX_LAYER_STAMPS 1")
+    for dfn in os.environ.get("RAYDP_MLP_DEFINES", "").split():
+        # dev A/B builds: NAME or NAME=VALUE macros for kernel variants measured side by side
+        name, _, val = dfn.partition("=")
+        if name.isidentifier():
+            out.append(f"#define {name} {val or 1}")
     out += ['#include "mlp_persist.h"', "", "namespace {", "", "struct JD {"]
     for k in _DESC_INT:
         out.append(f"  static constexpr int {k} = {int(getattr(desc, k))};")
