@@ -164,6 +164,10 @@ def compile_source(src: str) -> str:
     key = _key(src)
     path = os.path.join(CACHE, f"mlp_{key}.hsaco")
     if os.path.exists(path):
+        try:
+            os.utime(path)      # (used: a cache pruned by age keeps it)
+        except OSError:
+            pass
         return path
     os.makedirs(CACHE, exist_ok=True)
     cpp = os.path.join(CACHE, f"mlp_{key}.hip")
