@@ -216,6 +216,7 @@ struct MwCtx {
   int n_total;                 // valid rows of the whole batch
   unsigned long long ticks;    // wall-clock bound of one barrier wait
   unsigned long long* tstamp;  // optional: workgroup 0 stores the step's start (wall clock) here
+  unsigned seq;                // launch sequence number (host, from 1): tags this launch's granules
   unsigned long long* lstamp;  // diagnostic build (RX_LAYER_STAMPS): workgroup 0's intra-layer
                                // shader-clock stamps of this step ([20 + 4 l ..] backward, [40 + 5 l ..]
                                // forward, [0 .. 2] the closing barrier / bias reduction)
@@ -311,11 +312,11 @@ __device__ __forceinline__ float* mw_fwd(float* part, int stride, const LY& ly, 
 }
 template <class LY>
 __device__ __forceinline__ float* mw_bwd(float* part, int stride, const LY& ly, int w) {
-  return part + (size_t)w * stride + ly.mw_off + rx_ru32(2 * ly.out_n);
+  return part + (size_t)w * stride + ly.mw_off + rx_ru32(4 * ly.out_n);
 }
 template <class LY>
 __device__ __forceinline__ float* mw_bias(float* part, int stride, const LY& ly, int w) {
-  return part + (size_t)w * stride + ly.mw_off + 2 * rx_ru32(2 * ly.out_n);
+  return part + (size_t)w * stride + ly.mw_off + 2 * rx_ru32(4 * ly.out_n);
 }
 
 // Grid barrier number `k` (1-based, counted by the caller) of the step. Every thread of every
@@ -364,6 +365,114 @@ __device__ __forceinline__ void mw_finish(const MwCtx& mw) {
 
 // Rows of workgroup w when the batch's n valid rows are dealt BP per workgroup.
 __device__ __forceinline__ int mw_rows(int n, int w, int bp) { return max(0, min(bp, n - w * bp)); }
+
+// Granule hand-off of the per-workgroup partials (MI355X_MICROARCH.md's R2 form: an 8-B
+// {data, tag} written by ONE sc1 store -- here two of them in one 16-B store -- read with sc1
+// loads until the tag is this launch's): the reader waits for the data itself, so the step needs
+// no grid barrier per BatchNorm reduction (one barrier was ~1.2 us plus the loads' round trip after
+// it). Tag = launch sequence * 32 + phase; the partial buffer starts zeroed (tag 0 never valid).
+// A pair (a, b) of column c of workgroup w: {a, tag, b, tag} at 16 c bytes into w's region.
+__device__ __forceinline__ unsigned mw_tag(const MwCtx& mw, int k) { return mw.seq * 32u + (unsigned)k; }
+__device__ __forceinline__ void mw_put_pair(const MwCtx& mw, const float* at, float a, float b, unsigned tag) {
+  rx_store16_sc1(mw.part, (int)((at - mw.part) * 4), u32x4{__float_as_uint(a), tag, __float_as_uint(b), tag});
+}
+__device__ __forceinline__ void mw_put_one(const MwCtx& mw, const float* at, float a, unsigned tag) {
+  rx_store8_sc1(mw.part, (int)((at - mw.part) * 4), make_uint2(__float_as_uint(a), tag));
+}
+// wait until every granule of v[] (16-B pairs, or 8-B singles when ONE) carries `tag`, reloading
+// the stale ones; wave-uniform exit, bounded by the barrier timeout (then the error word is set,
+// mw.ok cleared and the values are whatever arrived: the host rolls the step back)
+template <int N, bool ONE>
+__device__ __forceinline__ void mw_await(MwCtx& mw, u32x4 (&v)[N], const int (&off)[N], unsigned tag) {
+  auto fresh = [&](const u32x4& x) { return x[1] == tag && (ONE || x[3] == tag); };
+  const unsigned long long t0 = wall_clock64();
+  for (int it = 1;; ++it) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) ok = ok && fresh(v[i]);
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) return;
+    if ((it & 15) == 0) {
+      const bool bad = __hip_atomic_load(rx_g(mw.ctl) + RX_MW_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                       wall_clock64() - t0 > mw.ticks;
+      if (__builtin_amdgcn_readfirstlane(bad ? 1 : 0)) {
+        __hip_atomic_store(rx_g(mw.ctl) + RX_MW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mw.ok = 0;
+        return;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!fresh(v[i])) {
+        if constexpr (ONE) {
+          const uint2 y = rx_load8_sc1(mw.part, off[i]);
+          v[i] = u32x4{y.x, y.y, 0u, 0u};
+        } else {
+          v[i] = rx_load16_sc1(mw.part, off[i]);
+        }
+      }
+  }
+}
+
+// Sums of the G workgroups' pairs of one column (lane group q takes w = q, q + 4, ...; the four
+// lane sums added by rx_colsum16: bit-identical on every lane, in a fixed order), and -- for the
+// forward BatchNorm -- the count-weighted centred second moment (Chan et al.) from the same pairs.
+// `at0`: workgroup 0's pair of the column.
+template <bool M2>
+__device__ __forceinline__ void mw_reduce_pairs(MwCtx& mw, const float* at0, int q, unsigned tag, int n_batch, int bp,
+                                                float& a, float& b) {
+  const int G = mw.G, base = (int)((at0 - mw.part) * 4), wst = mw.stride * 4;
+  float sa = 0.f, sb = 0.f;
+  float keep_a[8], keep_b[8];
+  for (int w0 = q; w0 < G; w0 += 32) {
+    u32x4 v[8];
+    int off[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int w = w0 + 4 * i;
+      off[i] = base + (w < G ? w : q) * wst;
+      v[i] = rx_load16_sc1(mw.part, off[i]);
+    }
+    mw_await<8, false>(mw, v, off, tag);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      keep_a[i] = __uint_as_float(v[i][0]);
+      keep_b[i] = __uint_as_float(v[i][2]);
+      if (w0 + 4 * i < G) {
+        sa += keep_a[i];
+        sb += keep_b[i];
+      }
+    }
+  }
+  a = rx_colsum16(sa);
+  b = rx_colsum16(sb);
+  if constexpr (M2) {
+    const float mean = a / (float)n_batch;
+    float m2 = 0.f;
+    for (int w0 = q; w0 < G; w0 += 32) {
+      if (G > 32) {   // (G <= 32: the one chunk's pairs are still in registers)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const u32x4 x = rx_load16_sc1(mw.part, base + (w0 + 4 * i < G ? w0 + 4 * i : q) * wst);
+          keep_a[i] = __uint_as_float(x[0]);
+          keep_b[i] = __uint_as_float(x[2]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int w = w0 + 4 * i;
+        const int nwi = w < G ? mw_rows(n_batch, w, bp) : 0;
+        if (nwi == 0) continue;      // an empty workgroup published nothing meaningful
+        const float nw = (float)nwi;
+        const float dm = keep_a[i] / nw - mean;
+        m2 += keep_b[i];
+        m2 = fmaf(nw * dm, dm, m2);
+      }
+    }
+    a = mean;
+    b = rx_colsum16(m2);
+  }
+}
 
 // Sums over the G workgroups' partial pairs at p0 + w * stride + {0, 1}. The four lanes that
 // share (lane & 15) split the workgroups (lane group q takes w = q, q + 4, ...), each issuing its
@@ -861,11 +970,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
       const float v = rx_colsum16(rx_lane_sqdev<MT, FULL>(&acc[j * MT], mean, lg, nvalid));
       if constexpr (MWT::on) {
         // this workgroup's (sum, centred second moment) of column c
-        if (colok && lg == 0) {
-          float* pp = mw_fwd(mw->part, mw->stride, ly, mw->wg) + 2 * c;
-          rx_st_sc1f(pp, s);
-          rx_st_sc1f(pp + 1, v);
-        }
+        if (colok && lg == 0) mw_put_pair(*mw, mw_fwd(mw->part, mw->stride, ly, mw->wg) + 4 * c, s, v, mw_tag(*mw, mw->k));
       } else {
         bn_mean[j] = mean;
         bn_var[j] = v * inv_nv;
@@ -1154,7 +1259,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
           gsum = rx_colsum16(gsum);
           if (colok && lg == 0 && ly.b_off >= 0) {
             if constexpr (MWT::on)
-              rx_st_sc1f(mw_bias(mw->part, mw->stride, ly, mw->wg) + c, gsum);
+              mw_put_one(*mw, mw_bias(mw->part, mw->stride, ly, mw->wg) + 2 * c, gsum, mw_tag(*mw, 31));
             else
               Gr[ly.b_off + c] = gsum;
           }
@@ -1173,17 +1278,18 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
     if constexpr (MWT::on) {
 #pragma unroll
       for (int j = 0; j < T::NTW; ++j) epi_a(j);
-      mw->ok = mw_barrier(*mw, ++mw->k) && mw->ok;
-      // batch statistics from every workgroup's (sum, centred second moment), workgroup order
+      // batch statistics from every workgroup's (sum, centred second moment), workgroup order,
+      // read as tagged granules (no grid barrier)
+      const unsigned tag = mw_tag(*mw, mw->k);
+      ++mw->k;
 #pragma unroll
       for (int j = 0; j < T::NTW; ++j) {
         const int n = wave + j * RX_NW;
         if (n >= ntiles) continue;
         const int c = n * 16 + lr;
         const int cc = c < ly.out ? c : 0;
-        const float* p0 = mw_fwd(mw->part, mw->stride, ly, 0) + 2 * cc;
         float mean, M2;
-        mw_mean_m2(p0, mw->stride, mw->G, lg, n_batch, T::BP, mean, M2);
+        mw_reduce_pairs<true>(*mw, mw_fwd(mw->part, mw->stride, ly, 0) + 4 * cc, lg, tag, n_batch, T::BP, mean, M2);
         bn_mean[j] = mean;
         bn_var[j] = M2 / (float)n_batch;
       }
@@ -1515,11 +1621,8 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       }
       if (mode == 1) {
         if (colok && lg == 0) {
-          if constexpr (MWT::on) {
-            float* pp = mw_bwd(mw->part, mw->stride, pv, mw->wg) + 2 * c;
-            rx_st_sc1f(pp, sg);
-            rx_st_sc1f(pp + 1, sgx);
-          }
+          if constexpr (MWT::on)
+            mw_put_pair(*mw, mw_bwd(mw->part, mw->stride, pv, mw->wg) + 4 * c, sg, sgx, mw_tag(*mw, mw->k));
         }
         return;
       }
@@ -1552,7 +1655,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     const float bs = rx_colsum16((bs4[0] + bs4[1]) + (bs4[2] + bs4[3]));
     if (colok && lg == 0 && pv.b_off >= 0) {
       if constexpr (MWT::on)
-        rx_st_sc1f(mw_bias(mw->part, mw->stride, pv, mw->wg) + c, bs);
+        mw_put_one(*mw, mw_bias(mw->part, mw->stride, pv, mw->wg) + 2 * c, bs, mw_tag(*mw, 31));
       else
         Gr[pv.b_off + c] = bs;
     }
@@ -1577,7 +1680,8 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     if constexpr (MWT::on) {
 #pragma unroll
       for (int j = 0; j < T::NTW; ++j) post(j, 1);
-      mw->ok = mw_barrier(*mw, ++mw->k) && mw->ok;
+      const unsigned tag = mw_tag(*mw, mw->k);
+      ++mw->k;
 #pragma unroll
       for (int j = 0; j < T::NTW; ++j) {
         const int n = wave + j * RX_NW;
@@ -1585,7 +1689,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
         const int c = n * 16 + lr;
         const int cc = c < pv.out ? c : 0;
         float sg, sgx;
-        mw_pair_sum(mw_bwd(mw->part, mw->stride, pv, 0) + 2 * cc, mw->stride, mw->G, lg, sg, sgx);
+        mw_reduce_pairs<false>(*mw, mw_bwd(mw->part, mw->stride, pv, 0) + 4 * cc, lg, tag, 0, T::BP, sg, sgx);
         bsg[j] = sg;
         bsgx[j] = sgx;
       }
@@ -2000,25 +2104,31 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
     layer_backward<MT, false>(d, ly, pv, l, smem, img, P, Gr, nvalid, sc, lst, nullptr, 0, true, &mw);
   });
   if (lst != nullptr && threadIdx.x == 0) rx_g(lst)[0] = __builtin_amdgcn_s_memtime();
-  // bias gradients: the workgroups' partial column sums, added in workgroup order, each
-  // (layer, column) by one thread of the grid
-  mw.ok = mw_barrier(mw, ++mw.k) && mw.ok;
+  // bias gradients: the workgroups' partial column sums (tagged granules, phase 31), added in
+  // workgroup order, each (layer, column) by one thread of the grid -- every wave polls (the
+  // granule waits are wave-collective), threads past the columns on a clamped column
   if (lst != nullptr && threadIdx.x == 0) rx_g(lst)[1] = __builtin_amdgcn_s_memtime();
   C::each_layer(d, [&](const auto& ly, int) {
-    if (ly.b_off >= 0 && mw.ok) {   // (after a timed-out barrier the partials are incomplete)
-      for (int c = (int)blockIdx.x * RX_THREADS + rx_tid<false>(); c < ly.out; c += mw.G * RX_THREADS) {
-        // G loads in flight 8 at a time, added in workgroup order
-        const float* p0 = mw_bias(mw.part, mw.stride, ly, 0) + c;
+    if (ly.b_off >= 0) {
+      for (int c0 = (int)blockIdx.x * RX_THREADS; c0 < ly.out; c0 += mw.G * RX_THREADS) {
+        const int c = c0 + rx_tid<false>();
+        const int base = (int)((mw_bias(mw.part, mw.stride, ly, 0) + 2 * (c < ly.out ? c : 0) - mw.part) * 4);
         float s = 0.f;
         for (int w0 = 0; w0 < mw.G; w0 += 8) {
-          float v[8];
+          u32x4 v[8];
+          int off[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) v[i] = rx_ld_sc1f(p0 + (size_t)min(w0 + i, mw.G - 1) * (size_t)mw.stride);
+          for (int i = 0; i < 8; ++i) {
+            off[i] = base + min(w0 + i, mw.G - 1) * mw.stride * 4;
+            const uint2 y = rx_load8_sc1(mw.part, off[i]);
+            v[i] = u32x4{y.x, y.y, 0u, 0u};
+          }
+          mw_await<8, true>(mw, v, off, mw_tag(mw, 31));
 #pragma unroll
           for (int i = 0; i < 8; ++i)
-            if (w0 + i < mw.G) s += v[i];
+            if (w0 + i < mw.G) s += __uint_as_float(v[i][0]);
         }
-        Gr[ly.b_off + c] = s;
+        if (c < ly.out && mw.ok) Gr[ly.b_off + c] = s;   // (a timed-out wait: incomplete partials)
       }
     }
   });

@@ -65,7 +65,7 @@ class StepBufs(ctypes.Structure):
 class MwArgs(ctypes.Structure):
     """Multi-workgroup step of one fused model (csrc/hip/fused_mlp.hip MwArgs)."""
     _fields_ = [("part", ctypes.c_void_p), ("ctl", ctypes.c_void_p), ("G", ctypes.c_int),
-                ("resident_ok", ctypes.c_int), ("stride", ctypes.c_int), ("pad_", ctypes.c_int),
+                ("resident_ok", ctypes.c_int), ("stride", ctypes.c_int), ("seq", ctypes.c_uint),
                 ("scratch_stride", ctypes.c_longlong), ("ticks", ctypes.c_ulonglong),
                 ("wpart", ctypes.c_void_p), ("wctr", ctypes.c_void_p)]
 

@@ -328,7 +328,9 @@ class FusedMLPTrainer:
             # multi-workgroup partials: [fwd 2 out_n | bwd 2 out_n | bias out_n], each region on
             # its own 128-B lines (csrc/hip/mlp_core.h mw_fwd)
             x.mw_off = mw_total
-            mw_total += 2 * _ru(2 * out_n, 32) + _ru(out_n, 32)
+            # [forward pairs | backward pairs | bias singles] as tagged granules (csrc/hip/mlp_core.h
+            # mw_put_pair): 4 and 2 floats per column
+            mw_total += 2 * _ru(4 * out_n, 32) + _ru(2 * out_n, 32)
         # embedding front: every table is one contiguous run of the flat vector (element-wise
         # optimizer segment); front column k reads element [id][j] at poff + id * stride
         front = spec.front or []
