@@ -26,6 +26,7 @@
 #include "rx_common.h"
 #include "rx_grid.h"
 #include "mlp_opt.h"
+#include "mlp_mwopt.h"
 
 #include <type_traits>
 
@@ -220,7 +221,26 @@ struct MwCtx {
   unsigned long long* lstamp;  // diagnostic build (RX_LAYER_STAMPS): workgroup 0's intra-layer
                                // shader-clock stamps of this step ([20 + 4 l ..] backward, [40 + 5 l ..]
                                // forward, [0 .. 2] the closing barrier / bias reduction)
+  unsigned* lcnt;              // per-layer done counters (mlp_mwopt.h; [l] X^T_l / G^T_l exported and
+                               // W_l read for the last time, [RX_LCNT_VEC] bias gradients stored), one
+                               // add per step workgroup in a launch with optimizer workgroups
+  MwOptArgs opt;               // opt.od set: workgroups G.. of the grid are optimizer workgroups
 };
+
+// A step workgroup's count-in on lcnt[idx] (multi-workgroup step with counters): every wave's
+// stores drained, a barrier, one lane's agent-scope add (the producer side of mlp_mwopt.h).
+template <class MWT>
+__device__ __forceinline__ void mw_count_in(MWT* mw, int idx, int idx2 = -1) {
+  if constexpr (MWT::on) {
+    if (mw->opt.od == nullptr) return;   // (a launch without optimizer workgroups)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(rx_g(mw->lcnt) + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (idx2 >= 0) __hip_atomic_fetch_add(rx_g(mw->lcnt) + idx2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 // The persistent step's per-layer weight wait (mlp_persist.h PsNxWait): layer_forward(l) issues
 // the read of layer l+1's optimizer counter at its start and waits on it only where it prefetches
@@ -926,7 +946,7 @@ __device__ __forceinline__ void layer_forward(const D& d, const LY& ly, const NX
   }
   if (TRAIN && d.wgrad_mode == 1 && w0b == nullptr) {  // X^T_l (published by the previous layer / the input load)
     if constexpr (MWT::on)
-      export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
+      export_rows<MT, true>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
                           ps_wt, mw->G * T::BP, mw->wg * T::BP);
     else
       export_rows<MT, PS>(reinterpret_cast<const u16*>(smem + ly.xt_off), ly.in_n, Gr, d.act_off * 4 + ly.xg_off * 2,
@@ -1407,7 +1427,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
   if (d.wgrad_mode == 1) {
     // G^T_l leaves for the optimizer kernel's wgrad (GT is overwritten with G_{l-1} below)
     if constexpr (MWT::on)
-      export_rows<MT, PS>(GT, ly.out_n, Gr, d.act_off * 4 + ly.gg_off * 2, ps_wt, mw->G * T::BP, mw->wg * T::BP);
+      export_rows<MT, true>(GT, ly.out_n, Gr, d.act_off * 4 + ly.gg_off * 2, ps_wt, mw->G * T::BP, mw->wg * T::BP);
     else
       export_rows<MT, PS>(GT, ly.out_n, Gr, d.act_off * 4 + ly.gg_off * 2, ps_wt);
   } else
@@ -1496,7 +1516,7 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 #ifdef RX_LAYER_STAMPS
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[20 + 4 * l] = __builtin_amdgcn_s_memtime();
 #endif
-  if (l == 0) return;
+  if (l == 0) return;   // (multi-workgroup step: layer 0 counts in with the bias gradients)
 
   // ---- dgrad: dX[b][i] = sum_o G[b][o] W[o][i]  (A = R or the G^T image, B = Wt, K = out_k) ----
   // pv (layer l-1) owns the post-ops between layer l-1 and l
@@ -1520,10 +1540,16 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
 #ifdef RX_LAYER_STAMPS
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[21 + 4 * l] = __builtin_amdgcn_s_memtime();
 #endif
-  if constexpr (PS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's G^T export drained
+  bool cnt = PS;
+  if constexpr (MWT::on) cnt = mw->opt.od != nullptr;
+  if (cnt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's X^T / G^T exports drained
   __syncthreads();  // all reads of G_l (R, GT) are done; they are overwritten with G_{l-1}
   if constexpr (PS) {
     if (rx_tid<PS>() == 0) __hip_atomic_store(rx_g(sync) + 32 * l, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if constexpr (MWT::on) {   // layer l's optimizer tasks may start (mlp_mwopt.h)
+    if (cnt && threadIdx.x == 0)
+      __hip_atomic_fetch_add(rx_g(mw->lcnt) + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #ifdef RX_LAYER_STAMPS
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[22 + 4 * l] = __builtin_amdgcn_s_memtime();
@@ -1629,8 +1655,13 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
       bool owner = true;   // gamma / beta gradients are batch sums: one workgroup writes them
       if constexpr (MWT::on) owner = mw->wg == 0 && mw->ok;
       if (colok && lg == 0 && owner) {
-        if (pv.g_off >= 0) Gr[pv.g_off + c] = sgx;
-        if (pv.be_off >= 0) Gr[pv.be_off + c] = sg;
+        if constexpr (MWT::on) {   // write-through: the fused optimizer reads them in this launch
+          if (pv.g_off >= 0) rx_st_sc1f(Gr + pv.g_off + c, sgx);
+          if (pv.be_off >= 0) rx_st_sc1f(Gr + pv.be_off + c, sg);
+        } else {
+          if (pv.g_off >= 0) Gr[pv.g_off + c] = sgx;
+          if (pv.be_off >= 0) Gr[pv.be_off + c] = sg;
+        }
       }
       // dz = gamma * invstd * (g - sg / n - x_hat * sgx / n) = k1 * g + (c1 - x_hat * c2)
       const float k1 = gam * invstd;
@@ -2068,6 +2099,10 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
     const float* __restrict__ P, float* __restrict__ Gr, const u16* __restrict__ feats,
     const float* __restrict__ labels, const int* __restrict__ perm, int row0, float* __restrict__ scratch,
     long long scratch_stride, double* __restrict__ metrics, MwCtx mw, char* smem, int* rowidx) {
+  if (mw.opt.od != nullptr && (int)blockIdx.x >= mw.G) {   // an optimizer workgroup (mlp_mwopt.h)
+    mw_opt_role(mw, mw.opt, smem);
+    return;
+  }
   auto&& d = C::desc(dp);
   constexpr int BP = Tile<MT>::BP;
   mw.wg = (int)blockIdx.x;
@@ -2128,10 +2163,13 @@ __device__ __forceinline__ void mlp_train_step_mw_body(
           for (int i = 0; i < 8; ++i)
             if (w0 + i < mw.G) s += __uint_as_float(v[i][0]);
         }
-        if (c < ly.out && mw.ok) Gr[ly.b_off + c] = s;   // (a timed-out wait: incomplete partials)
+        if (c < ly.out && mw.ok) rx_st_sc1f(Gr + ly.b_off + c, s);   // (a timed-out wait: incomplete partials)
       }
     }
   });
+  // layer 0's G^T export drained while the bias gradients were reduced: its tasks and the vector
+  // parameters' chunks may start
+  mw_count_in(&mw, 0, RX_LCNT_VEC);
   mw_finish(mw);
 }
 

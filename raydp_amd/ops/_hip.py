@@ -67,7 +67,8 @@ class MwArgs(ctypes.Structure):
     _fields_ = [("part", ctypes.c_void_p), ("ctl", ctypes.c_void_p), ("G", ctypes.c_int),
                 ("resident_ok", ctypes.c_int), ("stride", ctypes.c_int), ("seq", ctypes.c_uint),
                 ("scratch_stride", ctypes.c_longlong), ("ticks", ctypes.c_ulonglong),
-                ("wpart", ctypes.c_void_p), ("wctr", ctypes.c_void_p)]
+                ("wpart", ctypes.c_void_p), ("wctr", ctypes.c_void_p), ("lcnt", ctypes.c_void_p),
+                ("nopt", ctypes.c_int), ("fseq", ctypes.c_uint)]
 
 
 class OptSeg(ctypes.Structure):

@@ -441,13 +441,18 @@ class FusedMLPTrainer:
         o.act_off, o.act_floats, o.bp, o.wgrad_mode = act_off, act_floats, bp_all, wmode
         o.ps_l0_inline = int(self.l0_inline)
         self.opt = o
+        self._mw_nopt = 0
         if G > 1 and wmode == 1:
             # split-K weight-gradient partials + per-tile arrival counters of the multi-workgroup
             # optimizer (csrc/hip/fused_mlp.hip mw_wgrad_opt_kernel, RX_WSPLIT_K rows per split)
             splits = -(-int(bp_all) // 256)
             tiles = sum(((sg.out + 31) // 32) * ((sg.in_ + 31) // 32) for sg in o.seg[:o.nseg] if sg.kind == 1)
             self._arena_zero += [("mw_wpart", max(1, tiles * splits * 1024), torch.float32),
-                                 ("mw_wctr", max(1, tiles), torch.int32)]
+                                 ("mw_wctr", max(1, tiles), torch.int32), ("mw_lcnt", 32, torch.int32)]
+            # optimizer workgroups inside the step's launch (csrc/hip/mlp_mwopt.h), two tasks each
+            # (RAYDP_MLP_MW_FUSED_OPT: 0 = the separate launch, N > 1 = at most N workgroups; dev knob)
+            cap = int(os.environ.get("RAYDP_MLP_MW_FUSED_OPT", "1"))
+            self._mw_nopt = 0 if cap == 0 else min(-(-tiles * splits // 2), cap if cap > 1 else 1 << 30)
         self.lds_bytes = lds
         # descriptors live in device memory: the kernels index them with runtime layer ids
         self._materialize(bytes(d), bytes(o), rs_init)
@@ -467,6 +472,7 @@ class FusedMLPTrainer:
             a.scratch_stride = self._scratch_stride
             if self.mw_wpart is not None:
                 a.wpart, a.wctr = self.mw_wpart.data_ptr(), self.mw_wctr.data_ptr()
+                a.lcnt, a.nopt = self.mw_lcnt.data_ptr(), self._mw_nopt
             from raydp_amd.utils.config import get as conf_get
             khz = 100000
             a.ticks = int(float(conf_get("spark.ray.mi355x.mlp_persistent.timeout_s")) * khz * 1000)
@@ -517,6 +523,7 @@ class FusedMLPTrainer:
         self.mw_part, self.mw_ctl = view("mw_part"), view("mw_ctl")
         self.mw_wpart = view("mw_wpart") if "mw_wpart" in where else None
         self.mw_wctr = view("mw_wctr") if "mw_wctr" in where else None
+        self.mw_lcnt = view("mw_lcnt") if "mw_lcnt" in where else None
         self._desc_buf = arena[desc_off:desc_off + len(desc_bytes)]
         base = self.img.data_ptr()
         o = self.opt
@@ -713,6 +720,9 @@ class FusedMLPTrainer:
                 self.mw_ctl.zero_()
                 if self.mw_wctr is not None:
                     self.mw_wctr.zero_()
+                if self.mw_lcnt is not None:   # the done counters restart with the launch count
+                    self.mw_lcnt.zero_()
+                    self._mw_args.fseq = 0
                 self.metrics.zero_()
                 raise RuntimeError("fused MLP multi-workgroup step: a grid barrier wait timed out "
                                    "(a step workgroup was not resident); the epoch was rolled back")

@@ -149,7 +149,7 @@ def _key(src: str) -> str:
     global _headers_digest
     if _headers_digest is None:      # the kernel headers a process compiles against: read once
         h = hashlib.sha256()
-        for f in ("mlp_core.h", "mlp_opt.h", "mlp_persist.h", "rx_common.h", "rx_grid.h"):
+        for f in ("mlp_core.h", "mlp_opt.h", "mlp_mwopt.h", "mlp_persist.h", "rx_common.h", "rx_grid.h"):
             with open(os.path.join(CSRC_HIP, f), "rb") as fh:
                 h.update(fh.read())
         h.update(ARCH.encode())
@@ -171,9 +171,10 @@ def compile_source(src: str) -> str:
         return path
     os.makedirs(CACHE, exist_ok=True)
     cpp = os.path.join(CACHE, f"mlp_{key}.hip")
-    with open(cpp, "w") as f:
+    with open(cpp + f".{threading.get_ident()}", "w") as f:
         f.write(src)
-    tmp = path + f".tmp{os.getpid()}"
+    os.replace(cpp + f".{threading.get_ident()}", cpp)
+    tmp = path + f".tmp{os.getpid()}.{threading.get_ident()}"   # (precompile_many: same source twice)
     cmd = [_hipcc(), "--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-munsafe-fp-atomics",
            "-I", CSRC_HIP, cpp, "-o", tmp]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)

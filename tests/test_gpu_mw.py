@@ -230,3 +230,36 @@ def test_multi_workgroup_consecutive_steps_read_fresh_partials():
             if (id(mod), "weight") in gmap:
                 e = _relerr(gmap[(id(mod), "weight")], emods[name].weight.grad)
                 assert e < 2e-2, (half, name, e)
+
+
+@pytest.mark.parametrize("batch,model_cls,nin,nout", [(4096, NYC, 20, 1), (1000, NYC, 20, 1), (640, BnFirst, 13, 3)])
+def test_fused_optimizer_workgroups_match_the_separate_launch(batch, model_cls, nin, nout, monkeypatch):
+    """The optimizer workgroups inside the step's launch (csrc/hip/mlp_mwopt.h) run the same
+    split-K tasks as the separate optimizer launch: an epoch of either gives bit-identical
+    parameters, moments and running statistics."""
+    from raydp_amd.models.mlp_spec import extract_mlp_spec
+    from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+    dev = torch.device("cuda")
+    torch.manual_seed(5)
+    n = 5 * batch + batch // 3
+    X = torch.randn(n, nin)
+    Y = X[:, :nout] * 2 - X[:, 1:2] + 0.1 * torch.randn(n, nout)
+    model = model_cls()
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("RAYDP_MLP_MW_FUSED_OPT", fused)
+        m = copy.deepcopy(model)
+        tr = FusedMLPTrainer(extract_mlp_spec(m), optimizer_config(torch.optim.Adam(m.parameters(), lr=2e-3)),
+                             loss_code(nn.MSELoss()), batch, dev)
+        assert tr.G > 1 and (tr._mw_nopt > 0) == (fused == "1")
+        feats = torch.zeros(n, tr.feat_k, dtype=torch.bfloat16)
+        feats[:, :nin] = X.to(torch.bfloat16)
+        feats, Yd = feats.to(dev), Y.to(dev)
+        for _ in range(2):
+            met = tr.train_epoch(feats, Yd, n, None)
+        torch.cuda.synchronize()
+        out.append((tr.params[:tr.total].clone(), tr.m[:tr.total].clone(), tr.v[:tr.total].clone(),
+                    tr.rstats.clone(), met["loss"]))
+    for a, b in zip(out[0][:4], out[1][:4]):
+        assert torch.equal(a, b)
+    assert out[0][4] == out[1][4]
