@@ -236,8 +236,8 @@ __device__ __forceinline__ int mw_task_decode_rev(const OptDesc& o, int S, int r
 
 // One lane: wait (bounded) until counter lcnt[idx] reached `need`; a timeout sets the error word.
 // The error word is not polled here: step workgroups count in even after a timed-out wait of
-// their own, and the control line they poll stays off this loop's path (224 pollers of one line
-// slowed every step workgroup's error check ~2x in its BatchNorm hand-offs).
+// their own, and the control line every step workgroup checks while it waits on BatchNorm
+// granules stays off the path of up to 224 pollers.
 template <class MWC>
 __device__ __forceinline__ void mw_wait_count(const MWC& mw, int idx, unsigned need) {
   const unsigned long long t0 = wall_clock64();
