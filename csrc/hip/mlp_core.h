@@ -235,9 +235,10 @@ __device__ __forceinline__ void mw_count_in(MWT* mw, int idx, int idx2 = -1) {
     if (mw->opt.od == nullptr) return;   // (a launch without optimizer workgroups)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-      __hip_atomic_fetch_add(rx_g(mw->lcnt) + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (idx2 >= 0) __hip_atomic_fetch_add(rx_g(mw->lcnt) + idx2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < RX_LCNT_REP) {   // one add per replica, one wave instruction
+      unsigned* c = mw->lcnt + threadIdx.x * 32;
+      __hip_atomic_fetch_add(rx_g(c) + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (idx2 >= 0) __hip_atomic_fetch_add(rx_g(c) + idx2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1548,8 +1549,8 @@ __device__ __forceinline__ void layer_backward(const D& d, const LY& ly, const P
     if (rx_tid<PS>() == 0) __hip_atomic_store(rx_g(sync) + 32 * l, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if constexpr (MWT::on) {   // layer l's optimizer tasks may start (mlp_mwopt.h)
-    if (cnt && threadIdx.x == 0)
-      __hip_atomic_fetch_add(rx_g(mw->lcnt) + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cnt && threadIdx.x < RX_LCNT_REP)
+      __hip_atomic_fetch_add(rx_g(mw->lcnt) + threadIdx.x * 32 + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #ifdef RX_LAYER_STAMPS
   if (stamps != nullptr && rx_tid<PS>() == 0) rx_g(stamps)[22 + 4 * l] = __builtin_amdgcn_s_memtime();

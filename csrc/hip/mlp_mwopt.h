@@ -16,13 +16,14 @@
 // of this launch reads W_l / Wt_l any more); tasks are dealt latest layer first, the order the
 // backward produces them. Vector parameters (biases, BatchNorm) follow lcnt[RX_LCNT_VEC] (every
 // step workgroup's bias gradient stores drained). The counters are never reset: after the n-th
-// fused launch each holds G * n.
+// fused launch each holds G * n. Every counter is kept in RX_LCNT_REP replicas.
 #pragma once
 #include "rx_grid.h"
 #include "mlp_opt.h"
 
 #define RX_WSPLIT_K 256
 #define RX_LCNT_VEC 31
+#define RX_LCNT_REP 8   // replicas of the done counters, one 128-B line each (lcnt[rep * 32 + idx])
 #ifndef RX_MWOPT_SLEEP
 #define RX_MWOPT_SLEEP 10
 #endif
@@ -241,7 +242,11 @@ __device__ __forceinline__ int mw_task_decode_rev(const OptDesc& o, int S, int r
 template <class MWC>
 __device__ __forceinline__ void mw_wait_count(const MWC& mw, int idx, unsigned need) {
   const unsigned long long t0 = wall_clock64();
-  while ((int)(rx_ld_sc1u(mw.lcnt + idx) - need) < 0) {
+  // the replica of this workgroup's XCD (dispatch deals workgroups round-robin over the 8 XCDs):
+  // 28 pollers a line instead of 224 (MI355X_MICROARCH.md valid forms: a counter in R replicas,
+  // each producer adding to every replica with one wave instruction of R active lanes)
+  const unsigned* c = mw.lcnt + (blockIdx.x % RX_LCNT_REP) * 32 + idx;
+  while ((int)(rx_ld_sc1u(c) - need) < 0) {
     if (wall_clock64() - t0 > mw.ticks) {
       __hip_atomic_store(rx_g(mw.ctl) + RX_MW_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;

@@ -448,7 +448,7 @@ class FusedMLPTrainer:
             splits = -(-int(bp_all) // 256)
             tiles = sum(((sg.out + 31) // 32) * ((sg.in_ + 31) // 32) for sg in o.seg[:o.nseg] if sg.kind == 1)
             self._arena_zero += [("mw_wpart", max(1, tiles * splits * 1024), torch.float32),
-                                 ("mw_wctr", max(1, tiles), torch.int32), ("mw_lcnt", 32, torch.int32)]
+                                 ("mw_wctr", max(1, tiles), torch.int32), ("mw_lcnt", 8 * 32, torch.int32)]
             # optimizer workgroups inside the step's launch (csrc/hip/mlp_mwopt.h), two tasks each
             # (RAYDP_MLP_MW_FUSED_OPT: 0 = the separate launch, N > 1 = at most N workgroups; dev knob)
             cap = int(os.environ.get("RAYDP_MLP_MW_FUSED_OPT", "1"))
