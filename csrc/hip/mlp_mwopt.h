@@ -21,7 +21,11 @@
 #include "rx_grid.h"
 #include "mlp_opt.h"
 
-#define RX_WSPLIT_K 256
+#ifndef RX_WSPLIT_K
+#define RX_WSPLIT_K 256   // batch rows per split-K task (dev A/B of the fused role: RAYDP_MLP_DEFINES)
+#endif
+// the partial buffer is sized for 256-row splits (raydp_amd/ops/fused_mlp.py mw_wpart)
+static_assert(RX_WSPLIT_K >= 256 && RX_WSPLIT_K % 32 == 0, "split-K partials sized for 256-row splits");
 #define RX_LCNT_VEC 31
 #define RX_LCNT_REP 8   // replicas of the done counters, one 128-B line each (lcnt[rep * 32 + idx])
 #ifndef RX_MWOPT_SLEEP
