@@ -130,7 +130,19 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
   }
   __syncthreads();
   const bool last = *last_lds != 0;
+  const int ti = t & 31, to = t >> 5;  // 8 rows per pass
+  float pp[4], pm[4], pvv[4];
   if (last) {
+    // this thread's four parameters and moments travel with the partials (one round trip fewer
+    // on the tile's critical path)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int oo = o0 + to + r * 8, ii = i0 + ti;
+      const int idx = sg.start + min(oo, sg.out - 1) * sg.in + min(ii, sg.in - 1);
+      pp[r] = a.p[idx];
+      pm[r] = a.m[idx];
+      pvv[r] = a.v[idx];
+    }
     // the S partials of this wave's subtile summed in split order
     f32x4 t4 = f32x4{0.f, 0.f, 0.f, 0.f};
     const int pbase = (int)((((size_t)tile * S) * 4 + wave) * 64 + lane) * 16;
@@ -147,7 +159,6 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
     for (int r = 0; r < 4; ++r) gtile[(ms * 16 + lc) * 33 + ns * 16 + lg * 4 + r] = t4[r];
   }
   __syncthreads();
-  const int ti = t & 31, to = t >> 5;  // 8 rows per pass
   if (last) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -155,8 +166,11 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
       u16 h = 0;
       if (oo < sg.out && ii < sg.in) {
         const int idx = sg.start + oo * sg.in + ii;
-        const float pv = opt_update(o, idx, a.p, gtile[(to + r * 8) * 33 + ti], a.m, a.v, a.lr, a.bc1, a.bc2, 1.f,
-                                    a.first);
+        float pv = pp[r], mv = pm[r], vv = pvv[r];   // opt_update with the loads hoisted
+        opt_update_reg(o, pv, mv, vv, gtile[(to + r * 8) * 33 + ti], a.lr, a.bc1, a.bc2, 1.f, a.first);
+        a.m[idx] = mv;
+        if (o.algo != 2) a.v[idx] = vv;
+        a.p[idx] = pv;
         h = rx_f2bf(pv);
         rx_g(sg.W)[oo * sg.in_k + ii] = h;
       }
