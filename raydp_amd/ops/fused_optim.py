@@ -183,8 +183,9 @@ def adam_step(opt) -> None:
     per 24 parameter tensors. The state stays torch's (``step`` a host tensor, ``exp_avg``,
     ``exp_avg_sq``), so ``state_dict()`` / checkpoints / a later ``opt.step()`` see no difference."""
     L = _lib()
-    adamw = isinstance(opt, torch.optim.AdamW)
     for group in opt.param_groups:
+        # decoupled decay (p *= 1 - lr * wd): AdamW, or Adam(decoupled_weight_decay=True) in torch >= 2.6
+        adamw = isinstance(opt, torch.optim.AdamW) or bool(group.get("decoupled_weight_decay", False))
         lr = float(group["lr"])
         b1, b2 = (float(b) for b in group["betas"])
         live = [p for p in group["params"] if p.grad is not None]
@@ -208,9 +209,19 @@ def adam_step(opt) -> None:
             _hip.check(L.rx_mt_adam(ctypes.byref(a), _hip.stream_ptr(chunk[0].device)), "rx_mt_adam")
 
 
+def _has_step_hooks(opt) -> bool:
+    """Optimizer step pre/post hooks (per instance or global) that ``opt.step()`` would run."""
+    from torch.optim import optimizer as _o
+    return bool(getattr(opt, "_optimizer_step_pre_hooks", None) or getattr(opt, "_optimizer_step_post_hooks", None)
+                or getattr(_o, "_global_optimizer_pre_hooks", None) or getattr(_o, "_global_optimizer_post_hooks", None))
+
+
 def fused_step(opt) -> bool:
     """``opt.step()`` on the multi-tensor kernels when they cover ``opt`` (Adam / AdamW / SGD over
-    dense fp32 CUDA parameters); False (nothing done) otherwise."""
+    dense fp32 CUDA parameters); False (nothing done) otherwise -- also when step hooks are
+    registered, which only torch's own ``step()`` runs."""
+    if _has_step_hooks(opt):
+        return False
     if adam_supported(opt) is None:
         adam_step(opt)
         return True

@@ -284,6 +284,8 @@ class ActorManager:
             req = {k: opts[k] for k in ("num_cpus", "num_gpus", "memory", "resources") if opts.get(k) is not None}
             if getattr(strat, "node_id", None):
                 req["node_id"] = strat.node_id
+            if opts.get("lifetime") == "detached":
+                req["lifetime"] = "detached"     # the reservation outlives this driver's connection
             remote = gcs.call("place", req, pg.id.hex() if pg is not None else None, bidx)
             from raydp_amd.runtime.node import VirtualNode
             from raydp_amd.runtime.store import attach_store
@@ -309,6 +311,11 @@ class ActorManager:
             self.actors[aid] = a
         _ = sup
         a.start()
+        if remote is not None and opts.get("lifetime") == "detached" and getattr(a, "pid", None):
+            try:
+                gcs.call("watch", remote["token"], int(a.pid))
+            except (OSError, RuntimeError):
+                pass
         return a
 
     def _place(self, opts):

@@ -69,6 +69,22 @@ def _loads(b) -> dict:
 
 # actor options an attached driver may ask the head to place (JSON values only)
 _PLACE_KEYS = ("num_cpus", "num_gpus", "memory", "resources")
+# largest pre-authentication frame on the TCP endpoint (the hello carries a 32-hex-digit token):
+# the length word is checked BEFORE anything is allocated for the frame
+_MAX_HELLO = 4096
+# largest control frame after authentication (control ops carry small JSON documents)
+_MAX_CONTROL_FRAME = 64 << 20
+
+
+def _recv_bounded(conn, limit: int) -> bytes:
+    """One length-prefixed frame (``actor_worker.send_frame`` format) of at most ``limit`` bytes;
+    ValueError (connection closed by the caller) past it."""
+    import struct
+    from raydp_amd.runtime.actor_worker import _recv_exact
+    (n,) = struct.unpack("<Q", _recv_exact(conn, 8))
+    if n > limit:
+        raise ValueError(f"control frame of {n} bytes exceeds {limit}")
+    return _recv_exact(conn, n)
 
 
 class HeadService:
@@ -133,7 +149,7 @@ class HeadService:
             if needs_token:
                 # the first frame must be {"op": "hello", "args": [token]}; anything else closes
                 conn.settimeout(10.0)
-                msg = _loads(recv_frame(conn))
+                msg = _loads(_recv_bounded(conn, _MAX_HELLO))
                 conn.settimeout(None)
                 tok = (msg.get("args") or [""])[0] if msg.get("op") == "hello" else ""
                 if not hmac.compare_digest(str(tok), self.token):
@@ -141,17 +157,19 @@ class HeadService:
                     return
                 send_frame(conn, lock, _dumps({"ok": True, "value": "welcome"}))
             while True:
-                msg = _loads(recv_frame(conn))
+                msg = _loads(_recv_bounded(conn, _MAX_CONTROL_FRAME))
                 try:
                     reply = {"ok": True, "value": self._handle(msg.get("op"), list(msg.get("args") or []), owned)}
                 except Exception as e:  # noqa: BLE001 - reported to the caller
                     reply = {"ok": False, "error": f"{type(e).__name__}: {e}"}
                 send_frame(conn, lock, _dumps(reply))
-        except (ConnectionError, OSError, EOFError, ValueError):
+        except (ConnectionError, OSError, EOFError, ValueError, MemoryError):
             pass
         finally:
             with self._lock:
                 self._conns.discard(conn)
+            # (detached actors' reservations are not in `owned`: they outlive this connection and
+            # are released by an explicit 'release' or when the head sees their process die)
             for token in owned:
                 self._release(token)
             try:
@@ -167,8 +185,13 @@ class HeadService:
             return n.attach_info()
         if op == "place":
             token, reply = self._place(*args)
-            owned.append(token)
+            if str(((args[0] if args else None) or {}).get("lifetime") or "") != "detached":
+                owned.append(token)
             return reply
+        if op == "watch":
+            # a detached actor's process: its reservation is released once the process is gone
+            self._watch(str(args[0]), int(args[1]))
+            return True
         if op == "release":
             self._release(str(args[0]))
             if args[0] in owned:
@@ -230,8 +253,37 @@ class HeadService:
                        "store_path": store.path, "node_ip": vnode.ip if vnode is not None else "",
                        "gpu_ids": [g for g, _ in take]}
 
+    def _watch(self, token: str, pid: int):
+        with self._lock:
+            if token not in self._reservations:
+                return
+            watched = self.__dict__.setdefault("_watched", {})
+            watched[token] = pid
+            if getattr(self, "_watcher", None) is None:
+                self._watcher = threading.Thread(target=self._watch_loop, daemon=True, name="raydp-gcs-watch")
+                self._watcher.start()
+
+    def _watch_loop(self, interval: float = 0.5):
+        import time
+        while not self._closing:
+            with self._lock:
+                items = list(self._watched.items())
+            for token, pid in items:
+                try:
+                    os.kill(pid, 0)
+                    continue
+                except ProcessLookupError:
+                    pass
+                except PermissionError:
+                    continue
+                with self._lock:
+                    self._watched.pop(token, None)
+                self._release(token)
+            time.sleep(interval)
+
     def _release(self, token: str):
         with self._lock:
+            getattr(self, "_watched", {}).pop(token, None)
             r = self._reservations.pop(token, None)
         if r is None:
             return

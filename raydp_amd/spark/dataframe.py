@@ -19,7 +19,7 @@ import pyarrow.compute as pc
 
 from raydp_amd.spark import plan as P
 from raydp_amd.spark import wide as W
-from raydp_amd.spark.column import (AggExpr, Alias, ColRef, Column, Expr, Func, Lit, SortOrder,
+from raydp_amd.spark.column import (AggExpr, Alias, BinOp, ColRef, Column, Expr, Func, Lit, SortOrder,
                                     WindowExpr, _to_expr, as_array, map_children)
 from raydp_amd.spark.row import Row
 from raydp_amd.spark.types import StructType, from_arrow_schema
@@ -204,6 +204,21 @@ class GroupedData:
     def max(self, *cols): return self._simple("max", cols)
 
 
+def _pad_to(target, src, t, i=None):
+    """The unmatched rows ``t`` of an outer join with a residual condition in the joined layout
+    ``target``: column j is ``t``'s column ``src[j]``, or typed nulls where ``src[j]`` is -1
+    (positional: a join keeps both sides' same-named columns)."""
+    cols = [t.column(k).cast(f.type) if k >= 0 else pa.nulls(t.num_rows, f.type) for f, k in zip(target, src)]
+    return pa.Table.from_arrays(cols, schema=target)
+
+
+def _rewrite_refs(e, fn):
+    """Copy of expression ``e`` with every ColRef replaced by ``fn(ref)``."""
+    if isinstance(e, ColRef):
+        return fn(e)
+    return map_children(e, lambda c: _rewrite_refs(c, fn))
+
+
 class DataFrameNaFunctions:
     def __init__(self, df):
         self.df = df
@@ -284,7 +299,7 @@ class DataFrame:
 
     def __getitem__(self, item):
         if isinstance(item, str):
-            return Column(ColRef(item))
+            return Column(self._ref(item))
         if isinstance(item, Column):
             return self.filter(item)
         if isinstance(item, (list, tuple)):
@@ -295,8 +310,13 @@ class DataFrame:
         if name.startswith("_"):
             raise AttributeError(name)
         if name in self.columns:
-            return Column(ColRef(name))
+            return Column(self._ref(name))
         raise AttributeError(f"'DataFrame' object has no attribute '{name}'")
+
+    def _ref(self, name):
+        r = ColRef(name)
+        r.origin = id(self)       # which side of a join condition it belongs to (_join_side)
+        return r
 
     def __repr__(self):
         return "DataFrame[" + ", ".join(f"{n}: {t}" for n, t in self.dtypes) + "]"
@@ -478,6 +498,11 @@ class DataFrame:
         return GroupedData(self, []).agg(*exprs)
 
     def join(self, other: "DataFrame", on=None, how: str = "inner"):
+        """Spark's ``DataFrame.join``: ``on`` is a column name, a list of names, or a condition
+        (``a.k == b.k``, conjunctions with ``&``, a list of conditions). Equalities between a left
+        and a right column become the hash-join keys; every other conjunct is a residual condition
+        that decides which key-matched pairs match (``a.k == b.k & (a.x < b.y)``), also for outer,
+        semi and anti joins (reference: any join is Spark SQL's, ``doc/spark_on_ray.md:187-201``)."""
         how = how or "inner"
         if on is None:
             return self.crossJoin(other)
@@ -487,20 +512,110 @@ class DataFrame:
             lk = rk = list(on)
         else:
             conds = on if isinstance(on, (list, tuple)) else [on]
-            lk, rk = [], []
-            for c in conds:
-                e = c._expr
-                if not (hasattr(e, "op") and e.op == "==" and isinstance(e.left, ColRef)
-                        and isinstance(e.right, ColRef)):
-                    raise NotImplementedError("only equi-joins on column equality are supported")
-                a, b = e.left.col_name, e.right.col_name
-                if a in self.columns and b in other.columns:
-                    lk.append(a)
-                    rk.append(b)
+            conj, stack = [], [c._expr for c in reversed(conds)]
+            while stack:
+                e = stack.pop()
+                if isinstance(e, BinOp) and e.op == "&":
+                    stack += [e.right, e.left]
                 else:
-                    lk.append(b)
-                    rk.append(a)
+                    conj.append(e)
+            lk, rk, residual = [], [], []
+            for e in conj:
+                if isinstance(e, BinOp) and e.op == "==" and isinstance(e.left, ColRef) \
+                        and isinstance(e.right, ColRef):
+                    sa, sb = self._join_side(e.left, other), self._join_side(e.right, other)
+                    if (sa, sb) in (("L", "R"), ("R", "L")):
+                        a, b = (e.left, e.right) if sa == "L" else (e.right, e.left)
+                        lk.append(a.col_name)
+                        rk.append(b.col_name)
+                        continue
+                residual.append(e)
+            if residual:
+                return self._join_residual(other, lk, rk, residual, how)
+            if not lk:
+                raise NotImplementedError("a join condition needs an equality between a left and a "
+                                          "right column (or use crossJoin + filter)")
         return self._with(W.JoinPlan(self._src(), other._src(), lk, rk, how))
+
+    def _join_side(self, ref, other) -> Optional[str]:
+        """'L' / 'R' for a column reference of a join condition: the DataFrame it was taken
+        from (``a["x"]`` / ``a.x``), else the side that has the name (None if both or neither)."""
+        o = getattr(ref, "origin", None)
+        if o is not None and o == id(self) and ref.col_name in self.columns:
+            return "L"
+        if o is not None and o == id(other) and ref.col_name in other.columns:
+            return "R"
+        inl, inr = ref.col_name in self.columns, ref.col_name in other.columns
+        return "L" if inl and not inr else "R" if inr and not inl else None
+
+    def _join_residual(self, other, lk, rk, residual, how):
+        """Join with non-equality conditions: the right side's columns the residual reads are
+        renamed apart first (so ``a.x < b.x`` reads both), the key-matched pairs are filtered, and
+        outer / semi / anti joins are rebuilt from the matched pairs by row ids."""
+        from raydp_amd.spark import functions as F
+        from raydp_amd.spark.wide import _JOIN_TYPES
+        jt = _JOIN_TYPES[how.lower()]
+        tag = f"__j{id(self) & 0xffff:x}"
+        ren = {}
+
+        def ref(e):
+            side = self._join_side(e, other)
+            if side is None:
+                raise ValueError(f"join condition column {e.col_name!r} is ambiguous or unknown; "
+                                 "take it from one DataFrame (a['x'])")
+            if side == "R":
+                ren.setdefault(e.col_name, f"{tag}_r_{e.col_name}")
+                return ColRef(ren[e.col_name])
+            if e.col_name in other.columns:      # the joined rows carry both sides' copies
+                lren.setdefault(e.col_name, f"{tag}_l_{e.col_name}")
+                return ColRef(lren[e.col_name])
+            return ColRef(e.col_name)
+        lren = {}
+        res = [_rewrite_refs(e, ref) for e in residual]
+        cond = Column(res[0])
+        for e in res[1:]:
+            cond = cond & Column(e)
+        # row ids are materialised once (localCheckpoint): the matched pairs and the unmatched rows
+        # must see the same id for a row, whichever stage later evaluates the side
+        left = self.withColumn(tag + "_lid", F.monotonically_increasing_id()).localCheckpoint() \
+            if jt in ("left outer", "full outer", "left semi", "left anti") else self
+        for c, t in lren.items():
+            left = left.withColumn(t, F.col(c))
+        right = other
+        for c, t in ren.items():
+            right = right.withColumn(t, F.col(c))
+        if jt in ("right outer", "full outer"):
+            right = right.withColumn(tag + "_rid", F.monotonically_increasing_id()).localCheckpoint()
+        if lk:
+            matched = left._with(W.JoinPlan(left._src(), right._src(), lk, rk, "inner")).filter(cond)
+        else:
+            matched = left.crossJoin(right).filter(cond)
+        helper = list(ren.values()) + list(lren.values())
+        if jt == "inner":
+            return matched.drop(*helper)
+        if jt in ("left semi", "left anti"):
+            ids = matched.select(tag + "_lid").distinct()
+            return left.join(ids, tag + "_lid", "left_semi" if jt == "left semi" else "left_anti") \
+                .drop(*([tag + "_lid"] + list(lren.values())))
+        target = matched.arrow_schema
+        lc, rc = left.columns, right.columns
+        same = lk == rk and bool(lk)
+        kept = [j for j, c in enumerate(rc) if not (same and c in rk)]
+        if len(target) != len(lc) + len(kept):
+            raise NotImplementedError("outer join with a residual condition: unexpected joined layout")
+        parts = [matched]
+        if jt in ("left outer", "full outer"):
+            src = list(range(len(lc))) + [-1] * len(kept)
+            lost = left.join(matched.select(tag + "_lid"), tag + "_lid", "left_anti")
+            parts.append(lost._map(functools.partial(_pad_to, target, src), "join pad"))
+        if jt in ("right outer", "full outer"):
+            src = [rc.index(rk[lk.index(c)]) if same and c in lk else -1 for c in lc] + kept
+            lost = right.join(matched.select(tag + "_rid"), tag + "_rid", "left_anti")
+            parts.append(lost._map(functools.partial(_pad_to, target, src), "join pad"))
+        out = parts[0]
+        for p_ in parts[1:]:
+            out = out.union(p_)
+        return out.drop(*(helper + [c for c in (tag + "_lid", tag + "_rid") if c in target.names]))
 
     def crossJoin(self, other):
         from raydp_amd.spark import functions as F

@@ -607,19 +607,27 @@ def _join_on(left, right, cond, how, lquals=frozenset(), rquals=frozenset()):
                 rk.append(a)
                 continue
         residual.append(e)
-    if not lk:
+    if not lk and how not in ("inner", "cross"):
         raise SqlError("JOIN ... ON needs at least one equality between a left and a right column")
-    if residual and how != "inner":
-        raise SqlError("non-equality JOIN conditions are supported on inner joins only")
+    if residual:
+        # every column of the residual resolved to its side here (qualifiers), then the
+        # DataFrame join's residual machinery (outer / semi / anti too)
+        from raydp_amd.spark.column import map_children
+
+        def tag(e):
+            if isinstance(e, ColRef):
+                side = _side(e, lcols, rcols, lquals, rquals)
+                r = ColRef(e.col_name)
+                if side is not None:
+                    r.origin = id(left) if side == "L" else id(right)
+                return r
+            return map_children(e, tag)
+        return left._join_residual(right, lk, rk, [tag(e) for e in residual], how)
     if any(a != b for a, b in zip(lk, rk)):
         # the keys are resolved already: build the join on them directly (DataFrame.join would
         # guess the sides again by name, which a self-join cannot disambiguate)
-        out = left._with(W.JoinPlan(left._src(), right._src(), lk, rk, how))
-    else:
-        out = left.join(right, lk, how)
-    for e in residual:
-        out = out.filter(Column(e))
-    return out
+        return left._with(W.JoinPlan(left._src(), right._src(), lk, rk, how))
+    return left.join(right, lk, how)
 
 
 def _empty(session, names=None):

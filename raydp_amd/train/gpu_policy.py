@@ -61,16 +61,37 @@ def worker_policies(use_gpu: bool):
 
 _MAX_SHAPES = 4        # graphed batch shapes per model (a ragged last batch stays eager)
 _STEADY = 3            # calls with the same shape before it is graphed
+# instance attributes graph_model adds (dropped again by copies and pickles of the module)
+_PATCH_ATTRS = ("forward", "_raydp_graphed", "__reduce_ex__", "__deepcopy__")
+
+
+def _plain_state(module):
+    return {k: v for k, v in module.__dict__.items() if k not in _PATCH_ATTRS}
+
+
+def _rebuild_plain(cls, state):
+    """Unpickle target of a graphed module: the same class, without the graphs."""
+    obj = cls.__new__(cls)
+    obj.__dict__.update(state)
+    return obj
 
 
 def graph_model(module):
     """Patch ``module`` (in place: same object, same ``state_dict``) so its training forward runs
-    from a captured HIP graph per repeated input shape; returns the module."""
+    from a captured HIP graph per repeated input shape; returns the module.
+
+    A replayed graph's backward reads the activations its forward left in the graph's static
+    buffers, so a second forward of the same shape before the first one's backward (twin
+    networks, two losses summed, accumulation without an interleaved backward) must not replay
+    the graph again: every replay marks its shape pending until the gradient of its output
+    arrives, and a call on a pending shape runs eagerly. ``copy.deepcopy`` and pickling
+    (``torch.save(model)``) see the plain module: the copy runs its own eager forward."""
+    import copy
     import torch
     if getattr(module, "_raydp_graphed", False):
         return module
     orig = module.forward
-    graphs, seen = {}, {}
+    graphs, seen, pending = {}, {}, set()
     state = {"failed": False}
 
     class _Fwd(torch.nn.Module):       # parameters() = the model's, forward = its original one
@@ -103,6 +124,8 @@ def graph_model(module):
                                        for a in args)):
             return orig(*args, **kwargs)
         key = tuple((tuple(a.shape), a.dtype) for a in args)
+        if key in pending:       # this shape's last replay still waits for its backward
+            return orig(*args)
         g = graphs.get(key)
         if g is None:
             n = seen.get(key, 0) + 1
@@ -114,8 +137,33 @@ def graph_model(module):
                 return orig(*args)
             graphs[key] = g
         out = g(*args)
+        leaves = [t for t in torch.utils._pytree.tree_leaves(out)
+                  if isinstance(t, torch.Tensor) and t.requires_grad]
+        if leaves:
+            pending.add(key)
+            left = [len(leaves)]
+
+            def arrived(grad, key=key, left=left):
+                # the graphed backward runs right after the gradients of its outputs
+                left[0] -= 1
+                if left[0] <= 0:
+                    pending.discard(key)
+                return grad
+            for t in leaves:
+                t.register_hook(arrived)
         return torch.utils._pytree.tree_map(lambda t: t.clone() if isinstance(t, torch.Tensor) else t, out)
+
+    def reduce_ex(proto):
+        return _rebuild_plain, (type(module), _plain_state(module))
+
+    def deepcopy(memo):
+        new = type(module).__new__(type(module))
+        memo[id(module)] = new
+        new.__dict__.update(copy.deepcopy(_plain_state(module), memo))
+        return new
 
     module.forward = forward
     module._raydp_graphed = True
+    module.__reduce_ex__ = reduce_ex
+    module.__deepcopy__ = deepcopy
     return module

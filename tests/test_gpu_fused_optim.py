@@ -19,7 +19,8 @@ def _params(seed=0):
 @pytest.mark.parametrize("cls,cfg", [(torch.optim.Adam, dict(lr=1e-3)),
                                      (torch.optim.Adam, dict(lr=1e-2, betas=(0.8, 0.99), eps=1e-6, weight_decay=1e-2)),
                                      (torch.optim.Adam, dict(lr=1e-3, maximize=True)),
-                                     (torch.optim.AdamW, dict(lr=1e-3, weight_decay=0.05))])
+                                     (torch.optim.AdamW, dict(lr=1e-3, weight_decay=0.05)),
+                                     (torch.optim.Adam, dict(lr=1e-3, weight_decay=0.05, decoupled_weight_decay=True))])
 def test_multi_tensor_adam_matches_torch_adam(cls, cfg):
     """rx_mt_adam (one launch per 24 tensors, >24 tensors here, odd lengths for the scalar tail)
     against torch's own single-tensor Adam / AdamW over 5 steps; the state stays torch's."""
@@ -219,3 +220,50 @@ def test_prepare_model_graphs_the_training_step_like_eager():
         torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(torch.tensor(losses[1::2]), torch.tensor(losses[0::2]), rtol=1e-5, atol=1e-6)
     assert getattr(mine, "_raydp_graphed", False)
+
+
+def test_graph_model_twin_forwards_before_one_backward_and_copies():
+    """Two same-shape forwards before ONE backward (a twin network, two losses summed): the
+    second call must not overwrite the first replay's saved activations, so the gradients equal
+    the eager model's. deepcopy / torch.save of a graphed module give the plain module."""
+    import io
+    from raydp_amd.train.gpu_policy import graph_model
+    torch.manual_seed(0)
+    ref = nn.Sequential(nn.Linear(8, 32), nn.ReLU(), nn.Linear(32, 1)).cuda()
+    mine = copy.deepcopy(ref)
+    graph_model(mine)
+    g = torch.Generator().manual_seed(5)
+    for i in range(8):
+        a = torch.randn(64, 8, generator=g).cuda()
+        b = torch.randn(64, 8, generator=g).cuda()
+        grads = []
+        for m in (ref, mine):
+            m.zero_grad()
+            loss = (m(a) - m(b)).pow(2).mean() + m(a).mean()
+            loss.backward()
+            grads.append([p.grad.clone() for p in m.parameters()])
+        for ga, gb in zip(*grads):
+            torch.testing.assert_close(gb, ga, rtol=1e-5, atol=1e-6)
+    twin = copy.deepcopy(mine)
+    assert not getattr(twin, "_raydp_graphed", False) and "forward" not in twin.__dict__
+    x = torch.randn(64, 8).cuda()
+    torch.testing.assert_close(twin(x), ref(x))
+    buf = io.BytesIO()
+    torch.save(mine, buf)
+    buf.seek(0)
+    back = torch.load(buf, weights_only=False)      # (a file this test wrote itself)
+    torch.testing.assert_close(back(x), ref(x))
+
+
+def test_fused_step_declines_optimizers_with_step_hooks():
+    """Step pre/post hooks run only inside torch's own step(): fused_step leaves such optimizers alone."""
+    from raydp_amd.ops.fused_optim import fused_step
+    ps = _params()
+    o = torch.optim.Adam(ps, lr=1e-3)
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    seen = []
+    h = o.register_step_post_hook(lambda *a: seen.append(1))
+    assert fused_step(o) is False
+    h.remove()
+    assert fused_step(o) is True

@@ -196,3 +196,67 @@ def test_submit_runs_against_callers_node(head, tmp_path):
     assert out == {"session": head.session_dir, "obj": "head object"}
     # the head node is still up and serving after the submitted application detached
     assert runtime.get(ref) == "head object"
+
+
+def test_detached_actor_of_attached_driver_keeps_its_reservation(head):
+    """A detached actor placed by an attached driver keeps its CPU after that driver exits (the
+    head must not hand it to the next actor); the reservation comes back once the actor's
+    process is gone."""
+    import signal
+    import time
+    before = runtime.api.available_resources()["CPU"]
+    out = _child("""
+        import json, os, sys
+        from raydp_amd import runtime
+        runtime.init(address=sys.argv[1])
+
+        @runtime.remote
+        class D:
+            def pid(self):
+                return os.getpid()
+        d = D.options(name="detached_d", lifetime="detached", num_cpus=1).remote()
+        pid = runtime.get(d.pid.remote())
+        print(json.dumps({"pid": pid}))
+    """, runtime.core.address())
+    pid = out["pid"]
+    try:
+        time.sleep(1.5)             # the head noticed the connection close
+        alive = True
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            alive = False
+        assert alive, "the detached actor died with its driver"
+        assert runtime.api.available_resources()["CPU"] == before - 1
+    finally:
+        try:
+            os.kill(pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+    deadline = time.time() + 15
+    while runtime.api.available_resources()["CPU"] != before and time.time() < deadline:
+        time.sleep(0.2)
+    assert runtime.api.available_resources()["CPU"] == before
+
+
+def test_tcp_endpoint_rejects_oversized_hello(monkeypatch):
+    """The pre-authentication frame's length is checked before anything is allocated."""
+    import socket
+    import struct
+    runtime.shutdown()
+    monkeypatch.setenv("RAYDP_RUNTIME_PORT", "0")
+    runtime.init(num_cpus=2)
+    try:
+        node = runtime.core.current_node()
+        host, port = node.gcs_service.tcp_address.split(":")
+        s = socket.create_connection((host, int(port)), timeout=5)
+        s.sendall(struct.pack("<Q", 1 << 40))
+        s.settimeout(5)
+        assert s.recv(16) == b""      # closed by the head
+        s.close()
+        from raydp_amd.runtime.gcs import GcsClient
+        c = GcsClient(f"{node.gcs_service.tcp_address}?token={node.gcs_service.token}")
+        assert c.call("info")["session_dir"] == node.session_dir
+        c.close()
+    finally:
+        runtime.shutdown()

@@ -179,3 +179,31 @@ def test_join_on_ambiguous_bare_name_raises(spark):
         spark.sql("SELECT a.va FROM ta a JOIN tb b ON k = j").collect()
     with pytest.raises(SqlError, match="unknown qualifier"):
         spark.sql("SELECT a.va FROM ta a JOIN tb b ON c.k = a.j").collect()
+
+
+def test_dataframe_join_with_residual_condition(spark_session):
+    """``a.join(b, (a.k == b.k) & (a.x < b.y))``: the equality is the hash key, the rest decides
+    which key-matched pairs match -- for inner, outer, semi and anti joins (Spark semantics), and
+    the same rows as the SQL front end's ``JOIN ... ON a.k = b.k AND a.x < b.x``."""
+    s = spark_session
+    a = s.createDataFrame([(1, 1.0, "a"), (1, 5.0, "b"), (2, 3.0, "c"), (3, 9.0, "d")], ["k", "x", "la"])
+    b = s.createDataFrame([(1, 2.0, "p"), (2, 1.0, "q"), (2, 4.0, "r"), (4, 0.0, "z")], ["k", "x", "lb"])
+
+    def rows(df):
+        return sorted(map(tuple, df.collect()), key=str)
+    cond = (a.k == b.k) & (a.x < b["x"])
+    assert rows(a.join(b, cond)) == [(1, 1.0, "a", 2.0, "p"), (2, 3.0, "c", 4.0, "r")]
+    assert rows(a.join(b, cond, "left")) == [(1, 1.0, "a", 2.0, "p"), (1, 5.0, "b", None, None),
+                                             (2, 3.0, "c", 4.0, "r"), (3, 9.0, "d", None, None)]
+    assert rows(a.join(b, cond, "right")) == [(1, 1.0, "a", 2.0, "p"), (2, 3.0, "c", 4.0, "r"),
+                                              (2, None, None, 1.0, "q"), (4, None, None, 0.0, "z")]
+    assert len(rows(a.join(b, cond, "full"))) == 6
+    assert rows(a.join(b, cond, "left_semi")) == [(1, 1.0, "a"), (2, 3.0, "c")]
+    assert rows(a.join(b, cond, "left_anti")) == [(1, 5.0, "b"), (3, 9.0, "d")]
+    # distinct-named residual columns need no side
+    c = b.withColumnRenamed("x", "y")
+    assert rows(a.join(c, [a.k == c.k, a.x < c.y]).select("la", "lb")) == [("a", "p"), ("c", "r")]
+    a.createOrReplaceTempView("ja")
+    b.createOrReplaceTempView("jb")
+    sql = s.sql("SELECT ja.la, jb.lb FROM ja JOIN jb ON ja.k = jb.k AND ja.x < jb.x")
+    assert rows(sql) == [("a", "p"), ("c", "r")]
