@@ -676,6 +676,28 @@ def main():
     steps_total = args.epochs * (rows_per_gpu // batch)
     value = samples / dt
 
+    # N = 1 through a spawned worker actor (the hop every N > 1 run pays, and the one Ray Train
+    # always takes: reference torch/estimator.py:348-355), measured the same way after its own
+    # warm-up, so the 1 -> 2 step of a scaling curve can be read against it
+    spawned_n1 = None
+    if n_train == 1 and args.topology == "estimator" and workload == "nyc" and args.rows is None \
+            and os.environ.get("RAYDP_BENCH_SPAWNED_N1", "1") != "0":
+        os.environ["RAYDP_TRAIN_INPROCESS"] = "0"
+        try:
+            sdt, sres, sph, sdrv, _ = measure(workload, batch, args.epochs)
+            sh = _train_hist(sres)
+            srows = (sh[0].get("train_rows") if sh else None) or args.steps * batch
+            spawned_n1 = {"value": round(args.epochs * srows / sdt, 1), "unit": "samples/s",
+                          "ms_per_step": round(sdt * 1000.0 / max(1, args.epochs * (srows // batch)), 4),
+                          "wall_s": round(sdt, 4), "engine": sh[0].get("engine") if sh else None,
+                          "step_time_us": sh[0].get("step_time_us") if sh else None,
+                          "breakdown_s": dict({k: round(v, 4) for k, v in sph.items()},
+                                              **{k: round(v, 4) for k, v in sdrv.items()})}
+        except Exception as e:  # noqa: BLE001 - never costs the headline
+            spawned_n1 = {"error": repr(e)[-400:]}
+        finally:
+            os.environ.pop("RAYDP_TRAIN_INPROCESS", None)
+
     # power / HBM / activity telemetry (AMD SMI, sampled every 5 ms by a child process) over one
     # more, untimed run of the same pipeline: sampling inside the timed region slowed it (the
     # sampler competes with the executors for the host), so the timed run stays unobserved
@@ -745,6 +767,10 @@ def main():
                        if driver_gpu else h0.get("hbm_peak_allocated_mib"),
                        "rank0_breakdown_s": phases},
         }
+        if spawned_n1 is not None:
+            out["config"]["n1_spawned_worker"] = dict(
+                spawned_n1, what="the same pipeline with the one training worker in a spawned actor "
+                                 "process (the reference topology's worker hop), value = samples/s")
         if sampler is not None:
             out["config"]["host_resources"] = sampler.summary(cpus)
             out["config"]["train_epoch_samples_per_s"] = [round(m.get("train_samples_per_s", 0), 1)

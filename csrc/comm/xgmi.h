@@ -12,6 +12,7 @@
 // Memory: each rank owns one exchange region allocated uncached (hipDeviceMallocUncached, so
 // no L2 on either side holds a stale line) and exports it with hipIpcGetMemHandle:
 //   [slot 0: nf floats][slot 1: nf floats][flags: RX_XG_MAXR u32][votes: 2 x RX_XG_MAXR u32]
+//   [tile flags: RX_XG_MAXT x RX_XG_MAXR u32]
 // Step s writes its gradient into slot (s & 1) of its own region, then publishes seq = s + base
 // by storing it into flags[rank] of EVERY peer's region, waits until its own flags[p] >= seq for
 // every peer p, and reads slot (s & 1) of every region.
@@ -34,6 +35,8 @@
 #include <hip/hip_runtime.h>
 
 #define RX_XG_MAXR 16
+// per-tile flags of the in-kernel gradient exchange (rx_xg_tile_*): tile ids per region
+#define RX_XG_MAXT 1024
 
 // ctl words (this rank's local device memory, zeroed at create)
 enum : int { kXgErr = 0, kXgDevSeq = 1, kXgArrive = 2, kXgGo = 3, kXgDone = 4, kXgCtlWords = 16 };
@@ -137,5 +140,87 @@ __device__ __forceinline__ float rx_xg_sum(const XgDev& x, int par, int idx) {
   for (int p = 0; p < x.world; ++p)
     s += p == x.rank ? x.region[p][off]
                      : __hip_atomic_load(x.region[p] + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return s;
+}
+
+// ---- per-tile exchange inside a training launch (persistent epoch / multi-workgroup step) ----
+// The gradient all-reduce of the fused NYC engine at world > 1 without a launch, a pass or a
+// rendezvous of its own: the workgroup that finishes a 32x32 weight tile's gradient (or a chunk
+// of the bias / BatchNorm gradients) stores it into its rank's slot at the flat gradient offsets
+// (system-scope write-through stores), drains them, publishes tile id t at the step's sequence
+// number into every peer's tile-flag row, waits until every peer published t, and sums the world
+// values of each of its elements in rank order (bit-identical on every rank) before it updates.
+// 4 KB per tile crosses each link -- the 194 KB NYC gradient per step in all -- instead of the
+// batch-sized X^T / G^T exports (7.8 MB at batch 4096). Slot reuse: a rank rewrites tile t of
+// slot (seq & 1) two steps later, after it saw every peer's flag t of the step between, which each
+// peer publishes after its reads of this step's tile t (same workgroup, program order).
+struct XgStep {
+  const XgDev* xd;  // the communicator's descriptor in DEVICE memory (rx_xg_devptr): read with scalar
+                    // loads, so a kernel argument holding this stays small and register-resident
+  unsigned seq;     // sequence number of this launch's (first) step
+  int on;           // 0: one GPU (nothing exchanged)
+  float gscale;     // 1 / world: the DDP average
+  int pad_;
+};
+
+__device__ __forceinline__ float* rx_xg_region(const XgDev& x, int p) { return x.region[p]; }
+
+__device__ __forceinline__ unsigned* rx_xg_tflags_of(float* region, const XgDev& x) {
+  return reinterpret_cast<unsigned*>(region + 2 * (size_t)x.nf) + 3 * RX_XG_MAXR;
+}
+
+__device__ __forceinline__ float* rx_xg_slotp(const XgDev& x, int p, unsigned seq) {
+  return rx_xg_region(x, p) + (size_t)(seq & 1u) * x.nf;
+}
+
+// write-through (sc0 sc1) store into this rank's slot, and the matching peer load: global_
+// instructions (address space 1), never flat_
+typedef __attribute__((address_space(1))) float rx_xg_gf;
+typedef __attribute__((address_space(1))) unsigned rx_xg_gu;
+__device__ __forceinline__ void rx_xg_put(float* p, float v) {
+  __hip_atomic_store((rx_xg_gf*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float rx_xg_get(const float* p) {
+  return __hip_atomic_load((rx_xg_gf*)const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One lane, after every storing wave of its workgroup drained its rx_xg_put stores and joined a
+// barrier: tile t of sequence seq is in this rank's slot.
+__device__ __forceinline__ void rx_xg_tile_publish(const XgDev& x, int t, unsigned seq) {
+  for (int p = 0; p < x.world; ++p)
+    if (p != x.rank)
+      __hip_atomic_store((rx_xg_gu*)(rx_xg_tflags_of(x.region[p], x) + t * RX_XG_MAXR + x.rank), seq,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One lane (or a whole wave: every lane polls the same words): wait until every peer published
+// tile t of sequence seq. False on timeout (error word set) or when the error word was already set.
+__device__ __forceinline__ bool rx_xg_tile_wait(const XgDev& x, int t, unsigned seq) {
+  const unsigned* mine = rx_xg_tflags_of(rx_xg_region(x, x.rank), x) + t * RX_XG_MAXR;
+  const unsigned long long t0 = wall_clock64();
+  for (int p = 0; p < x.world; ++p) {
+    if (p == x.rank) continue;
+    int k = 0;
+    while ((int)(__hip_atomic_load((rx_xg_gu*)const_cast<unsigned*>(mine + p), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
+      if ((++k & 15) == 0) {
+        if (__hip_atomic_load((rx_xg_gu*)x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return false;
+        if ((unsigned long long)(wall_clock64() - t0) > x.spin_ticks) {
+          rx_xg_fail(x);
+          return false;
+        }
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return true;
+}
+
+// Sum over ranks (rank order) of flat element idx of sequence seq's slots; this rank's own value is
+// `mine` (the bits it stored).
+__device__ __forceinline__ float rx_xg_tile_sum(const XgDev& x, unsigned seq, int idx, float mine) {
+  float s = 0.f;
+  const size_t off = (size_t)(seq & 1u) * x.nf + idx;
+  for (int p = 0; p < x.world; ++p) s += p == x.rank ? mine : rx_xg_get(x.region[p] + off);
   return s;
 }

@@ -40,6 +40,7 @@ struct XgHost {
   int device = 0;
   bool host_seq = false;  // sequence numbers taken on the host (fused step loop) or on the device
   bool opened[RX_XG_MAXR] = {false};
+  XgDev* ddev = nullptr;  // device copy of `dev` (in-launch tile exchange: csrc/comm/xgmi.h XgStep)
 };
 
 constexpr int kThreads = 256;
@@ -295,7 +296,7 @@ void* rx_xg_create(int world, int rank, int device, int n, double timeout_s) {
   XgHost* h = new XgHost();
   h->device = device;
   const int nf = (n + 63) & ~63;
-  h->bytes = (2 * (size_t)nf + 3 * RX_XG_MAXR) * sizeof(float);
+  h->bytes = (2 * (size_t)nf + 3 * RX_XG_MAXR + (size_t)RX_XG_MAXT * RX_XG_MAXR) * sizeof(float);
   if (hipExtMallocWithFlags(&h->base, h->bytes, hipDeviceMallocUncached) != hipSuccess) {
     delete h;
     return nullptr;
@@ -348,8 +349,14 @@ int rx_xg_open(void* ctx, const char* handles) {
     h->dev.region[p] = (float*)ptr;
     h->opened[p] = true;
   }
+  if (h->ddev == nullptr && hipMalloc((void**)&h->ddev, sizeof(XgDev)) != hipSuccess) return -1;
+  if (hipMemcpy(h->ddev, &h->dev, sizeof(XgDev), hipMemcpyHostToDevice) != hipSuccess) return -1;
   return 0;
 }
+
+// The descriptor in device memory (valid after rx_xg_open): what training kernels that exchange
+// inside their launch read (XgStep::xd).
+const XgDev* rx_xg_devptr(void* ctx) { return ((XgHost*)ctx)->ddev; }
 
 const XgDev* rx_xg_devdesc(void* ctx) { return &((XgHost*)ctx)->dev; }
 
@@ -522,6 +529,7 @@ int rx_xg_destroy(void* ctx) {
   for (int p = 0; p < h->dev.world; ++p)
     if (h->opened[p]) (void)hipIpcCloseMemHandle(h->dev.region[p]);
   (void)hipFree(h->dev.ctl);
+  if (h->ddev) (void)hipFree(h->ddev);
   (void)hipFree(h->base);
   delete h;
   return 0;

@@ -17,9 +17,16 @@
 // backward produces them. Vector parameters (biases, BatchNorm) follow lcnt[RX_LCNT_VEC] (every
 // step workgroup's bias gradient stores drained). The counters are never reset: after the n-th
 // fused launch each holds G * n. Every counter is kept in RX_LCNT_REP replicas.
+//
+// World > 1 (MwOptArgs::xs.on): the gradient all-reduce rides in the same tasks -- a tile's last
+// arriver, once it summed the split-K partials, exchanges the 32x32 tile with its peers (csrc/comm/
+// xgmi.h XgStep: write-through store into this rank's slot, tile flag, wait for every peer's flag,
+// rank-order sum) and updates with the rank sum times 1 / world; vector chunks likewise. Only the
+// 194 KB gradient crosses the links, never the batch-sized X^T / G^T exports.
 #pragma once
 #include "rx_grid.h"
 #include "mlp_opt.h"
+#include "../comm/xgmi.h"
 
 #ifndef RX_WSPLIT_K
 #define RX_WSPLIT_K 256   // batch rows per split-K task (dev A/B of the fused role: RAYDP_MLP_DEFINES)
@@ -45,7 +52,16 @@ struct MwOptArgs {
   unsigned* wctr;     // per-tile arrival counters (the last arriver resets its own)
   unsigned need;      // fused launches: every done counter's value once this launch's step
                       // workgroups counted in (G x fused launches so far)
+  XgStep xs;          // world > 1: the in-task gradient exchange (xs.on == 0: one GPU)
 };
+
+// tile ids of the exchange: weight tiles in segment order, then the vector chunks
+__host__ __device__ __forceinline__ int mw_weight_tiles(const OptDesc& o) {
+  int n = 0;
+  for (int s = 0; s < o.nseg; ++s)
+    if (o.seg[s].kind == 1) n += opt_seg_blocks(o.seg[s]);
+  return n;
+}
 
 // Task `b` (weight tiles in segment order, S splits per tile) -> segment, tile ordinal, tile
 // within the segment, split. Returns the segment index (nseg: past the weight tasks).
@@ -159,7 +175,30 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
     for (int r = 0; r < 4; ++r) gtile[(ms * 16 + lc) * 33 + ns * 16 + lg * 4 + r] = t4[r];
   }
   __syncthreads();
-  if (last) {
+  bool xlast = last;
+  if (a.xs.on) {
+    // world > 1: this rank's tile into its slot, the tile flag, every peer's flag (all threads of
+    // the workgroup run the barriers; only a last arriver's half stores / publishes / waits)
+    const XgDev& x = *a.xs.xd;
+    float* mine = rx_xg_slotp(x, x.rank, a.xs.seq);
+    if (last) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int oo = o0 + to + r * 8, ii = i0 + ti;
+        if (oo < sg.out && ii < sg.in) rx_xg_put(mine + sg.start + oo * sg.in + ii, gtile[(to + r * 8) * 33 + ti]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0 && last) {
+      rx_xg_tile_publish(x, tile, a.xs.seq);
+      if (!rx_xg_tile_wait(x, tile, a.xs.seq)) *last_lds = 0;   // a peer never came: no update
+    }
+    __syncthreads();
+    xlast = *last_lds != 0;
+  }
+  if (xlast) {
+    const float gsc = a.xs.on ? a.xs.gscale : 1.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int oo = o0 + to + r * 8, ii = i0 + ti;
@@ -167,7 +206,9 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
       if (oo < sg.out && ii < sg.in) {
         const int idx = sg.start + oo * sg.in + ii;
         float pv = pp[r], mv = pm[r], vv = pvv[r];   // opt_update with the loads hoisted
-        opt_update_reg(o, pv, mv, vv, gtile[(to + r * 8) * 33 + ti], a.lr, a.bc1, a.bc2, 1.f, a.first);
+        const float gl = gtile[(to + r * 8) * 33 + ti];
+        const float gw = a.xs.on ? rx_xg_tile_sum(*a.xs.xd, a.xs.seq, idx, gl) : gl;
+        opt_update_reg(o, pv, mv, vv, gw, a.lr, a.bc1, a.bc2, gsc, a.first);
         a.m[idx] = mv;
         if (o.algo != 2) a.v[idx] = vv;
         a.p[idx] = pv;
@@ -178,7 +219,7 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
     }
   }
   __syncthreads();
-  if (last) {
+  if (xlast) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int ii = i0 + to + r * 8, oo = o0 + ti;
@@ -188,18 +229,56 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
 }
 
 // Vector parameters: chunk `c` (CH elements) of the element-wise segments on NT threads (`t`).
-// sc1: the gradients were stored in this launch (fused role).
+// sc1: the gradients were stored in this launch (fused role). World > 1 (a.xs.on): the chunk is
+// exchanged as tile mw_weight_tiles + c (every thread of the workgroup calls it: barriers).
 template <int CH, int NT>
 __device__ __forceinline__ void mw_vector_chunk(const MwOptArgs& a, int c, int t, bool sc1) {
   const OptDesc& o = *a.od;
+  const int c0 = c;
   for (int s = 0; s < o.nseg; ++s) {
     const OptSeg& sg = o.seg[s];
     if (sg.kind == 1) continue;
     const int nb = (sg.len + CH - 1) / CH;
     if (c < nb) {
-      for (int q = c * CH + t; q < min(sg.len, (c + 1) * CH); q += NT) {
-        const int idx = sg.start + q;
-        opt_update(o, idx, a.p, sc1 ? rx_ld_sc1f(a.g + idx) : a.g[idx], a.m, a.v, a.lr, a.bc1, a.bc2, 1.f, a.first);
+      if (!a.xs.on) {
+        for (int q = c * CH + t; q < min(sg.len, (c + 1) * CH); q += NT) {
+          const int idx = sg.start + q;
+          opt_update(o, idx, a.p, sc1 ? rx_ld_sc1f(a.g + idx) : a.g[idx], a.m, a.v, a.lr, a.bc1, a.bc2, 1.f, a.first);
+        }
+        return;
+      }
+      constexpr int J = CH / NT;
+      const XgDev& x = *a.xs.xd;
+      float* mine = rx_xg_slotp(x, x.rank, a.xs.seq);
+      float gl[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int q = c * CH + t + j * NT;
+        gl[j] = 0.f;
+        if (q < sg.len) {
+          const int idx = sg.start + q;
+          gl[j] = sc1 ? rx_ld_sc1f(a.g + idx) : a.g[idx];
+          rx_xg_put(mine + idx, gl[j]);
+        }
+      }
+      __shared__ int xok;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        const int tid = mw_weight_tiles(o) + c0;
+        rx_xg_tile_publish(x, tid, a.xs.seq);
+        xok = rx_xg_tile_wait(x, tid, a.xs.seq) ? 1 : 0;
+      }
+      __syncthreads();
+      if (!xok) return;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int q = c * CH + t + j * NT;
+        if (q < sg.len) {
+          const int idx = sg.start + q;
+          opt_update(o, idx, a.p, rx_xg_tile_sum(x, a.xs.seq, idx, gl[j]), a.m, a.v, a.lr, a.bc1, a.bc2,
+                     a.xs.gscale, a.first);
+        }
       }
       return;
     }

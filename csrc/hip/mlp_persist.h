@@ -27,12 +27,22 @@
 // Every wait is bounded (wall clock); a timeout sets the error word and every workgroup leaves
 // its loop, so the grid always drains.
 //
+// World > 1 (XgStep::on, one persistent launch per rank and epoch): the data-parallel gradient
+// all-reduce happens inside the same launch. Each optimizer workgroup, once its dW tiles of a step
+// are computed, exchanges them with the peers' workgroups of the same tiles (csrc/comm/xgmi.h:
+// write-through store into this rank's slot, tile flag, wait, rank-order sum) and updates with the
+// rank sum x 1 / world; the step workgroup publishes the step's bias / BatchNorm gradients as one
+// more tile after its backward, and the next step's vector update (waves 1..7, beside wave 0's
+// counter poll) sums them over the ranks. Layer 0 then goes to optimizer workgroups (the host keeps
+// ps_l0_inline off) and the vector updates leave the epilogues (they need every rank's gradient).
+//
 // Reference role: the per-batch train loop of TorchEstimator (python/raydp/torch/estimator.py:
-// 272-293: zero_grad / forward / loss.backward / optimizer.step), same arithmetic as
-// mlp_train_step_body + opt_tiled_body.
+// 272-293: zero_grad / forward / loss.backward / optimizer.step; DDP's all-reduce at :243), same
+// arithmetic as mlp_train_step_body + opt_tiled_body.
 #pragma once
 #include "mlp_core.h"
 #include "mlp_opt.h"
+#include "../comm/xgmi.h"
 
 #define RX_PS_FLAG(l) (32 * (l))
 #define RX_PS_CNT(l) (32 * (RX_MAXL + (l)))
@@ -93,10 +103,13 @@ __host__ __device__ __forceinline__ int ps_grid_blocks(const OptDesc& o) {
 // would leave the first 16 threads with 15 updates each: the update is VALU bound) -- and every
 // gradient / moment load of a thread's elements is issued before its first update.
 #define RX_PS_VEC_T0 64
+// World > 1 (xs.on): the gradients are the rank sums of the step `seq` published (each wave polls
+// the vector tile's flags itself before its loads), times 1 / world.
 template <class C, class D>
 __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, char* smem, const float* __restrict__ Gr,
                                                  float* __restrict__ m, float* __restrict__ v, float lr, float bc1,
-                                                 float bc2, int first) {
+                                                 float bc2, int first, const XgStep& xs, unsigned seq,
+                                                 unsigned* __restrict__ sync) {
   constexpr int J = 4;  // elements per thread per pass
   constexpr int NW = RX_THREADS - RX_PS_VEC_T0;
   float* pr = reinterpret_cast<float*>(smem + d.pr_lds_off);
@@ -106,6 +119,16 @@ __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, c
   });
   const int tid = rx_tid() - RX_PS_VEC_T0;
   if (tid < 0) return;
+  float gsc = 1.f;
+  if (xs.on) {
+    int ok = 1;
+    if ((rx_tid() & 63) == 0) {
+      ok = rx_xg_tile_wait(*xs.xd, mw_weight_tiles(o), seq) ? 1 : 0;
+      if (!ok) __hip_atomic_store(rx_g(sync) + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!__builtin_amdgcn_readfirstlane(ok)) return;
+    gsc = xs.gscale;
+  }
   for (int e0 = 0; e0 < total; e0 += J * NW) {
     int idx[J], slot[J];
     float g[J], mv[J], vv[J];
@@ -131,6 +154,7 @@ __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, c
       slot[j] = sl;
       const int q = id >= 0 ? id : 0;
       g[j] = rx_g(Gr)[q];
+      if (xs.on) g[j] = rx_xg_tile_sum(*xs.xd, seq, q, g[j]);
       mv[j] = rx_g(m)[q];
       vv[j] = rx_g(v)[q];
     }
@@ -138,7 +162,7 @@ __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, c
     for (int j = 0; j < J; ++j) {
       if (idx[j] >= 0) {
         float pv = pr[slot[j]];
-        opt_update_reg(o, pv, mv[j], vv[j], g[j], lr, bc1, bc2, 1.f, first);
+        opt_update_reg(o, pv, mv[j], vv[j], g[j], lr, bc1, bc2, gsc, first);
         pr[slot[j]] = pv;
         rx_g(m)[idx[j]] = mv[j];
         rx_g(v)[idx[j]] = vv[j];
@@ -359,7 +383,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
                                            float* __restrict__ m, float* __restrict__ v, const float* __restrict__ sched,
                                            int opt_first, unsigned* __restrict__ sync, unsigned long long ticks,
                                            char* smem, int* rowidx, int* flag_lds,
-                                           unsigned long long* __restrict__ stamps) {
+                                           unsigned long long* __restrict__ stamps, const XgStep& xs) {
   auto&& d = C::desc(dp);
   // optional timeline of the middle step (wall clock, 100 MHz; scripts/dev/persist_time.py)
   const int sstep = nsteps / 2;
@@ -406,7 +430,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
   // layer carries a BatchNorm (its affine gradients are not produced by a post-op)
   bool last_affine = false;
   C::each_layer(d, [&](const auto& ly, int) { last_affine = ly.g_off >= 0 || ly.be_off >= 0; });
-  const bool vec_inline = !last_affine;
+  const bool vec_inline = !last_affine && !xs.on;   // (world > 1: the rank sums come after the step)
   using O = typename rx_opt_type<C>::type;
   const rx_opt_holder<O> oh;
   const O& oc = oh.get(o);
@@ -464,7 +488,8 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
     // is out, its gradients are in Gr), beside wave 0's counter poll
     if (s > 0 && !vec_inline)
       ps_vector_update<C>(d, o, smem, Gr, m, v, rx_g(sched)[s - 1], rx_g(sched)[nsteps + s - 1],
-                          rx_g(sched)[2 * nsteps + s - 1], (opt_first && s == 1) ? 1 : 0);
+                          rx_g(sched)[2 * nsteps + s - 1], (opt_first && s == 1) ? 1 : 0, xs,
+                          xs.seq + (unsigned)(s - 1), sync);
     // layers >= 1 are waited for where their weights are first read (PsNxWait); layer 0 here,
     // unless the step workgroup updates it itself
     if (s > 0 && !l0_in) {
@@ -584,6 +609,19 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       __syncthreads();
       if (rx_tid() == 0)
         __hip_atomic_store(rx_g(sync) + RX_PS_FLAG(0), (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (xs.on) {
+        // world > 1: the step's bias / BatchNorm gradients (this workgroup's own Gr stores) into
+        // this rank's slot, published as one tile; the peers' arrive with the next step's wait
+        float* mine = rx_xg_slotp(*xs.xd, xs.xd->rank, xs.seq + (unsigned)s);
+        for (int q = 0; q < o.nseg; ++q) {
+          const OptSeg& sg = o.seg[q];
+          if (sg.kind == 1) continue;
+          for (int e = rx_tid(); e < sg.len; e += RX_THREADS) rx_xg_put(mine + sg.start + e, rx_g(Gr)[sg.start + e]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (rx_tid() == 0) rx_xg_tile_publish(*xs.xd, mw_weight_tiles(o), xs.seq + (unsigned)s);
+      }
     } else {
       __syncthreads();   // every read of this step's LDS images is done before the next batch lands
     }
@@ -594,7 +632,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
   if (nsteps > 0 && !vec_inline) {
     const int s = nsteps - 1;
     ps_vector_update<C>(d, o, smem, Gr, m, v, rx_g(sched)[s], rx_g(sched)[nsteps + s], rx_g(sched)[2 * nsteps + s],
-                        (opt_first && s == 0) ? 1 : 0);
+                        (opt_first && s == 0) ? 1 : 0, xs, xs.seq + (unsigned)s, sync);
     __syncthreads();
   }
   if (stamps != nullptr && rx_tid() == 0) rx_g(stamps)[RX_PS_STEP_STAMPS + nsteps] = wall_clock64();
@@ -638,9 +676,9 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, 
                                           float* __restrict__ m, float* __restrict__ v, const float* __restrict__ sched,
                                           int nsteps, int opt_first, unsigned* __restrict__ sync,
                                           unsigned long long ticks, char* smem, int* flag_lds,
-                                          unsigned long long* __restrict__ stamps) {
+                                          unsigned long long* __restrict__ stamps, const XgStep& xs) {
   const int bw = b;
-  int seg = -1, l = 0;
+  int seg = -1, l = 0, tile0 = 0;   // tile0: exchange id of the segment's first tile
   for (int q = 0; q < o.nseg; ++q) {
     if (o.seg[q].kind != 1) continue;
     const int nbk = ps_seg_workers(o, q, l);
@@ -649,6 +687,7 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, 
       break;
     }
     b -= nbk;
+    tile0 += opt_seg_blocks(o.seg[q]);
     ++l;
   }
   if (seg < 0) return;
@@ -707,16 +746,46 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, 
     if (flag_lds[0]) break;
     const bool st = stamps != nullptr && s == nsteps / 2 && b == 0 && rx_tid() == 0;
     if (st) rx_g(stamps)[16 + 2 * l] = wall_clock64();
-    const f32x4 gw = ps_wgrad_block(Gr, xo, go, nk);
+    f32x4 gw = ps_wgrad_block(Gr, xo, go, nk);
     if (st && l == 0) {   // layer 0: its X^T / G^T fragments arrived
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       rx_g(stamps)[28] = wall_clock64();
+    }
+    float gsc = 1.f;
+    if (xs.on) {
+      // world > 1: both halves' tiles into this rank's slot, published; every peer's tiles waited
+      // for; the rank sums (rank order) replace the local gradient
+      const unsigned seq = xs.seq + (unsigned)s;
+      float* mine = rx_xg_slotp(*xs.xd, xs.xd->rank, seq);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (ok[r]) rx_xg_put(mine + idx[r], gw[r]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (rx_tid() == 0) {
+        const int nt = opt_seg_blocks(sg);
+        const int ta = 2 * b, tb = 2 * b + 1;
+        if (ta < nt) rx_xg_tile_publish(*xs.xd, tile0 + ta, seq);
+        if (tb < nt) rx_xg_tile_publish(*xs.xd, tile0 + tb, seq);
+        bool okx = ta >= nt || rx_xg_tile_wait(*xs.xd, tile0 + ta, seq);
+        okx = okx && (tb >= nt || rx_xg_tile_wait(*xs.xd, tile0 + tb, seq));
+        if (!okx) {
+          __hip_atomic_store(rx_g(sync) + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          flag_lds[0] = 1;
+        }
+      }
+      __syncthreads();
+      if (flag_lds[0]) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (ok[r]) gw[r] = rx_xg_tile_sum(*xs.xd, seq, idx[r], gw[r]);
+      gsc = xs.gscale;
     }
     const int first = (opt_first && s == 0) ? 1 : 0;
     float h[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      if (ok[r]) opt_update_reg(hp, pr_[r], mr[r], vr[r], gw[r], lr_, bc1, bc2, 1.f, first);
+      if (ok[r]) opt_update_reg(hp, pr_[r], mr[r], vr[r], gw[r], lr_, bc1, bc2, gsc, first);
       h[r] = ok[r] ? pr_[r] : 0.f;   // zeros in the padding, which the images must keep
     }
     if (st && l == 0) rx_g(stamps)[26] = wall_clock64();   // layer 0: wgrad + update done
@@ -762,7 +831,7 @@ __device__ __forceinline__ void mlp_persist_body(const MlpDesc* __restrict__ dp,
                                                  const float* __restrict__ sched, int opt_first,
                                                  unsigned* __restrict__ sync, unsigned long long ticks, char* smem,
                                                  int* rowidx, int* flag_lds,
-                                                 unsigned long long* __restrict__ stamps) {
+                                                 unsigned long long* __restrict__ stamps, const XgStep& xs) {
   const OptDesc& o = *od;
   // workers are blocks 0, stride, 2 stride, ... (stride 8: one XCD under round-robin dispatch;
   // placement only changes which hand-off form a worker picks, never correctness)
@@ -773,11 +842,11 @@ __device__ __forceinline__ void mlp_persist_body(const MlpDesc* __restrict__ dp,
   if (w >= nw) return;
   if (w == 0) {
     ps_step_wg<C, MT>(dp, o, img, rstats, P, Gr, feats, labels, perm, n_rows, batch, nsteps, scratch, metrics, m, v,
-                      sched, opt_first, sync, ticks, smem, rowidx, flag_lds, stamps);
+                      sched, opt_first, sync, ticks, smem, rowidx, flag_lds, stamps, xs);
   } else {
     // hyperparameters: compile-time constants in a specialised kernel (C::Opt), else the descriptor
     using O = typename rx_opt_type<C>::type;
     const rx_opt_holder<O> oh;
-    ps_opt_wg(o, oh.get(o), w - 1, P, Gr, m, v, sched, nsteps, opt_first, sync, ticks, smem, flag_lds, stamps);
+    ps_opt_wg(o, oh.get(o), w - 1, P, Gr, m, v, sched, nsteps, opt_first, sync, ticks, smem, flag_lds, stamps, xs);
   }
 }

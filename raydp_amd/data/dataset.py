@@ -31,7 +31,25 @@ class RefBundle:
         self.blocks = blocks
 
 
+class BlockSlice:
+    """Rows [offset, offset + length) of a block held in the object store: an equal shard of a
+    dataset references its rows where they already are (a few ids when pickled to a worker,
+    resolved zero-copy from the node's store there), instead of a concatenated copy of them."""
+    __slots__ = ("ref", "offset", "length")
+
+    def __init__(self, ref, offset: int, length: int):
+        self.ref, self.offset, self.length = ref, int(offset), int(length)
+
+    def __getstate__(self):
+        return (self.ref, self.offset, self.length)
+
+    def __setstate__(self, st):
+        self.ref, self.offset, self.length = st
+
+
 def _resolve(b) -> pa.Table:
+    if isinstance(b, BlockSlice):
+        return _resolve(b.ref).slice(b.offset, b.length)
     if isinstance(b, ObjectRef):
         b = _get(b)
     if isinstance(b, (bytes, bytearray, memoryview)):
@@ -173,7 +191,7 @@ class Dataset:
         refs = []
         for i, b in enumerate(self._blocks):
             if not isinstance(b, ObjectRef):
-                b = _put(b)
+                b = _put(_resolve(b) if isinstance(b, BlockSlice) else b)
                 self._blocks[i] = b
             refs.append(b)
         return refs
@@ -287,9 +305,25 @@ class Dataset:
     def split(self, n: int, equal: bool = False, locality_hints=None) -> List["Dataset"]:
         tables = self._get_tables()
         if equal:
-            t = self.to_arrow()
-            per = t.num_rows // n
-            return [Dataset([t.slice(i * per, per)], t.schema) for i in builtins.range(n)]
+            # shard i = global rows [i per, (i + 1) per) in block order, as slices of the blocks
+            # themselves (object-store blocks stay where they are: a shard pickles to a few ids)
+            per = int(sum(t.num_rows for t in tables)) // n
+            schema = self.schema()
+            starts = np.cumsum([0] + [t.num_rows for t in tables])
+            out = []
+            for i in builtins.range(n):
+                lo, hi = i * per, (i + 1) * per
+                parts = []
+                for j, t in enumerate(tables):
+                    a, b = max(lo, int(starts[j])), min(hi, int(starts[j + 1]))
+                    if a >= b:
+                        continue
+                    blk = self._blocks[j]
+                    off = a - int(starts[j])
+                    parts.append(BlockSlice(blk, off, b - a) if isinstance(blk, (ObjectRef, BlockSlice))
+                                 else t.slice(off, b - a))
+                out.append(Dataset(parts or [schema.empty_table()], schema))
+            return out
         if len(tables) >= n:
             # keep blocks whole, balance rows greedily
             sizes = [(t.num_rows, i) for i, t in enumerate(tables)]

@@ -392,6 +392,26 @@ class _Fusion:
         self.reset()
 
 
+def _graph_user_module(named_parameters, params):
+    """The user's loop hands its module in only as ``model.named_parameters()`` (reference
+    ``examples/horovod_nyctaxi.py:133-138``): when that is the module's own generator, its forward
+    + backward are replayed from HIP graphs per repeated batch shape (the ``prepare_model`` policy,
+    ``raydp_amd/train/gpu_policy.py`` graph_model) -- a tabular MLP step is ~40 tiny kernels each
+    way whose launch cost exceeds their run time. Gradients still reach ``.grad`` through autograd
+    (the accumulate hooks that start the bucket all-reduce fire as before), so the wrapped step is
+    unchanged. Config ``spark.ray.mi355x.graph_user_model``; GPU parameters only."""
+    frame = getattr(named_parameters, "gi_frame", None)
+    mod = frame.f_locals.get("self") if frame is not None else None
+    import torch
+    if not isinstance(mod, torch.nn.Module) or not params or not all(p.is_cuda for p in params):
+        return None
+    from raydp_amd.utils import config as C
+    if not C.get("spark.ray.mi355x.graph_user_model"):
+        return None
+    from raydp_amd.train.gpu_policy import graph_model
+    return graph_model(mod)
+
+
 def DistributedOptimizer(optimizer, named_parameters=None, compression=None, backward_passes_per_step: int = 1,
                          op=Average, gradient_predivide_factor: float = 1.0, num_groups: int = 0,
                          groups=None, sparse_as_dense: bool = False, process_set=None):
@@ -399,6 +419,7 @@ def DistributedOptimizer(optimizer, named_parameters=None, compression=None, bac
     _check()
     compression = compression or Compression.none
     params = [p for g in optimizer.param_groups for p in g["params"] if p.requires_grad]
+    _graph_user_module(named_parameters, params)
     if named_parameters is not None:
         names = {id(p): n for n, p in named_parameters}
         missing = [p for p in params if id(p) not in names]

@@ -68,7 +68,7 @@ class MwArgs(ctypes.Structure):
                 ("resident_ok", ctypes.c_int), ("stride", ctypes.c_int), ("seq", ctypes.c_uint),
                 ("scratch_stride", ctypes.c_longlong), ("ticks", ctypes.c_ulonglong),
                 ("wpart", ctypes.c_void_p), ("wctr", ctypes.c_void_p), ("lcnt", ctypes.c_void_p),
-                ("nopt", ctypes.c_int), ("fseq", ctypes.c_uint)]
+                ("nopt", ctypes.c_int), ("fseq", ctypes.c_uint), ("share", ctypes.c_int)]
 
 
 class OptSeg(ctypes.Structure):
@@ -155,9 +155,9 @@ def lib():
     L.rx_jit_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
                               ctypes.POINTER(vp), i]
     # (desc, bufs, opt, opt_dev, mt, m, v, feats, labels, perm, n_rows, batch, nsteps, sched, opt_first,
-    #  sync, timeout_s, stream)
+    #  sync, timeout_s, stream, xg ctx (world > 1, else null), gscale, ranks sharing the device)
     L.rx_mlp_train_persistent.argtypes = [vp, vp, vp, vp, i, vp, vp, vp, vp, vp, i, i, i, vp, i, vp,
-                                          ctypes.c_double, vp]
+                                          ctypes.c_double, vp, vp, f, i]
     L.rx_mlp_train_persistent.restype = i
     L.rx_ps_sync_words.restype = i
     L.rx_mw_args_size.restype = i

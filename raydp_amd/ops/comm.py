@@ -277,7 +277,7 @@ class XgmiComm:
         except Exception as e:  # noqa: BLE001
             err, h = repr(e), b""
         info = [None] * world
-        dist.all_gather_object(info, (socket.gethostname(), h, err), group=group)
+        dist.all_gather_object(info, (socket.gethostname(), h, err, _device_identity()), group=group)
         ok = all(i[2] is None for i in info) and len({i[0] for i in info}) == 1
         if ok:
             ok = comm.open([i[1] for i in info]) == 0
@@ -289,8 +289,13 @@ class XgmiComm:
                 torch.cuda.synchronize()
                 comm.close()
             return None
+        # ranks on the same device as this one (rehearsals put several on one GPU): kernels that
+        # wait on their peers inside a launch size their grids so every rank's fits at once
+        comm.share = max(1, sum(1 for i in info if i[3] == info[rank][3]))
         _cache[key] = comm
         return comm
+
+    share = 1
 
     def _self_test(self) -> bool:
         import torch
@@ -309,6 +314,18 @@ class XgmiComm:
 
 
 _XGMI_DISABLED = False
+
+
+def _device_identity() -> str:
+    """A name of this process' current GPU that is the same in every process that uses it."""
+    import torch
+    dev = torch.cuda.current_device()
+    p = torch.cuda.get_device_properties(dev)
+    for attr in ("uuid", "pci_bus_id"):
+        v = getattr(p, attr, None)
+        if v is not None and str(v):
+            return f"{attr}:{v}"
+    return f"ordinal:{dev}:{os.environ.get('HIP_VISIBLE_DEVICES', os.environ.get('CUDA_VISIBLE_DEVICES', ''))}"
 
 
 class _XgA2A(ctypes.Structure):

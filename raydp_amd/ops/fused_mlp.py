@@ -160,9 +160,15 @@ def layout_candidates(batch: int):
 class FusedMLPTrainer:
     def __init__(self, spec: MlpSpec, opt_cfg: dict, loss: tuple, batch_size: int,
                  device: torch.device, lr_schedule: Optional[Callable[[int], float]] = None,
-                 layout_only: bool = False, acc_thr: Optional[float] = None):
+                 layout_only: bool = False, acc_thr: Optional[float] = None, world: int = 1,
+                 share: int = 1):
         # layout_only: build the descriptors on the host (no GPU needed) -- used to warm the
         # specialised-kernel cache at build time
+        # world > 1: gradients are exchanged inside the training launches (layer 0 is then not
+        # updated by the persistent step workgroup: its gradient must be summed over the ranks
+        # first); share: training ranks on this device (rehearsals), which size the in-launch
+        # optimizer workgroups so every rank's grid is resident at once
+        self.world, self.share = int(world), max(1, int(share))
         self.layout_only = layout_only
         self.spec, self.cfg, self.device = spec, opt_cfg, torch.device("cpu" if layout_only else device)
         self.batch = int(batch_size)
@@ -379,7 +385,7 @@ class FusedMLPTrainer:
         l00 = spec.layers[0].linear
         # (decided without looking at whether epochs run persistent: every kernel of the model then
         # runs layer 0 in the same k order, so the persistent epoch and the step loop agree bit for bit)
-        l0_inline = (G == 1 and tmode and wmode == 1 and not front
+        l0_inline = (G == 1 and tmode and wmode == 1 and not front and self.world == 1
                      and l00.in_features <= 20 and dims[0][2] == 32 and l00.out_features % 16 == 0
                      and l00.out_features <= 256 and L > 1
                      and lds + 32 * xs * 2 + 3 * W0S_N * 4 <= 160 * 1024 - 1536)
@@ -476,6 +482,7 @@ class FusedMLPTrainer:
             from raydp_amd.utils.config import get as conf_get
             khz = 100000
             a.ticks = int(float(conf_get("spark.ray.mi355x.mlp_persistent.timeout_s")) * khz * 1000)
+            a.share = self.share
             a.resident_ok = 0
             if not self.layout_only:
                 if int(self.lib.rx_mw_resident(mt, lds, G)) != 0:
@@ -651,17 +658,29 @@ class FusedMLPTrainer:
             if mw_snap is None:
                 mw_snap = self._mw_snap = [torch.empty_like(t) for t in live]
             torch._foreach_copy_(mw_snap, live)
-        if xg is None and comm is None and allreduce is None and world_size == 1 and \
-                self._run_persistent(feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream):
-            pass
+        if comm is None and allreduce is None and (xg is not None or world_size == 1) and \
+                self._run_persistent(feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream, xg):
+            self.last_path = "persistent_xgmi_tiles" if xg is not None else "persistent"
         elif xg is not None:
+            # multi-workgroup step: per-tile gradient exchange in the optimizer tasks; one workgroup:
+            # the optimizer kernel reduces from the peers' exported activations
+            self.last_path = "mw_xgmi_tiles" if self.G > 1 else "steps_xgmi_activations"
+            mw_stamps = None
+            if self.G > 1 and self.record_steps:
+                mw_stamps = self._dev_buf("stamps", 32 + nsteps + 1 + _PS_LAYER_STAMPS, torch.int64)
+                mw_stamps.zero_()
+                self.bufs.stamps = mw_stamps.data_ptr()
             rc = self.lib.rx_mlp_train_steps_xg(
                 ctypes.byref(self.desc), ctypes.byref(self.bufs), ctypes.byref(self.opt), self._od, self.mt,
                 pp(self.m.data_ptr()), pp(self.v.data_ptr()),
                 pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p, n_rows, self.batch, 0, nsteps,
                 lrs, bc1, bc2, ctypes.c_float(gscale), int(self.step_count == 0), stream, pp(xg.ctx))
+            self.bufs.stamps = 0
             _hip.check(rc, "rx_mlp_train_steps_xg")
+            if mw_stamps is not None:
+                self._mw_stamps_dev = mw_stamps
         elif comm is not None or allreduce is None:
+            self.last_path = "steps_rccl" if comm is not None else ("mw_steps" if self.G > 1 else "steps")
             mw_stamps = None
             if self.G > 1 and self.record_steps:
                 # multi-workgroup epoch: workgroup 0 of every step stores the step's start time
@@ -680,6 +699,7 @@ class FusedMLPTrainer:
             if mw_stamps is not None:
                 self._mw_stamps_dev = mw_stamps
         else:
+            self.last_path = "steps_host_allreduce"
             for s in range(nsteps):
                 rc = self.lib.rx_mlp_fwdbwd(
                     ctypes.byref(self.desc), ctypes.byref(self.bufs), self.mt,
@@ -696,9 +716,10 @@ class FusedMLPTrainer:
                 _hip.check(rc, "rx_opt_step")
         self.step_count += nsteps
         self.steps_in_epoch = nsteps
-        if xg is not None:
+        if xg is not None and not getattr(self, "_voted", False):
             # epoch-end agreement over xGMI, read with the metrics (one D2H copy)
             xg.vote(self.metrics[7:8])
+        self._voted = False
         pre, self._metrics_np = getattr(self, "_metrics_np", None), None
         if self.G > 1 and pre is None:
             # the multi-workgroup barriers' timeout word comes back with the metrics (one sync)
@@ -762,9 +783,11 @@ class FusedMLPTrainer:
         self.step_count = step
         self.metrics.zero_()
 
-    def _run_persistent(self, feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream) -> bool:
+    def _run_persistent(self, feats, labels, n_rows, perm_p, nsteps, lr_np, bc1_np, bc2_np, stream, xg=None) -> bool:
         """The whole epoch as one persistent launch (csrc/hip/mlp_persist.h); False when this
-        model / configuration cannot use it (the caller then runs the launch-per-step loop)."""
+        model / configuration cannot use it (the caller then runs the launch-per-step loop).
+        ``xg`` (world > 1): the gradients are exchanged over xGMI inside the launch; every rank
+        decides alike (same model, same device type), so ranks never mix the two loops."""
         if self.desc.wgrad_mode != 1 or not persistent_enabled() or self.desc.front_n or self.G > 1:
             # (an embedding front's tables are updated between steps by the optimizer kernel,
             # which the persistent epoch does not run)
@@ -774,7 +797,10 @@ class FusedMLPTrainer:
             self._ps_sync = torch.zeros(int(self.lib.rx_ps_sync_words()), dtype=torch.int32, device=self.device)
             self._ps_err = int(self.lib.rx_ps_err_index())
             props = torch.cuda.get_device_properties(self.device)
-            self._ps_ok = self._ps_grid <= int(props.multi_processor_count)
+            # ranks sharing the device (rehearsals) wait on each other inside their launches: all
+            # of their grids must be resident together
+            share = self.share if self.world > 1 else 1
+            self._ps_ok = self._ps_grid * share <= int(props.multi_processor_count)
         if not self._ps_ok:
             return False
         pp = ctypes.c_void_p
@@ -791,9 +817,10 @@ class FusedMLPTrainer:
         # buffers kept across epochs.
         live = [self.params, self.m, self.v, self.rstats, self.img]
         snap = getattr(self, "_snap", None)
-        if snap is None:
-            snap = self._snap = [torch.empty_like(t) for t in live]
-        torch._foreach_copy_(snap, live)
+        if xg is None:       # (world > 1 never reruns an epoch locally: nothing to roll back to)
+            if snap is None:
+                snap = self._snap = [torch.empty_like(t) for t in live]
+            torch._foreach_copy_(snap, live)
         stamps = None
         if self.record_steps:
             # device wall clock at every step start (csrc/hip/mlp_persist.h RX_PS_STEP_STAMPS)
@@ -804,17 +831,30 @@ class FusedMLPTrainer:
             ctypes.byref(self.desc), ctypes.byref(self.bufs), ctypes.byref(self.opt), self._od, self.mt,
             pp(self.m.data_ptr()), pp(self.v.data_ptr()), pp(feats.data_ptr()), pp(labels.data_ptr()), perm_p,
             n_rows, self.batch, nsteps, pp(sched.data_ptr()), int(self.step_count == 0),
-            pp(self._ps_sync.data_ptr()), ctypes.c_double(timeout), stream)
+            pp(self._ps_sync.data_ptr()), ctypes.c_double(timeout), stream,
+            pp(xg.ctx) if xg is not None else pp(0), ctypes.c_float(1.0 / max(1, self.world)),
+            int(self.share if xg is not None else 1))
         self.bufs.stamps = 0
-        if rc in (-3, -4):
+        if rc in (-2, -3, -4, -6):
             return False
         _hip.check(rc, "rx_mlp_train_persistent")
         self._ps_sched = sched   # kept alive until the launch has consumed it
+        if xg is not None:
+            # the epoch-end vote (every rank's xGMI error word) rides the same readback
+            xg.vote(self.metrics[7:8])
+            self._voted = True
         # ONE synchronisation for everything the epoch reports: the wait-timeout word, the
         # metrics and the step stamps come back together
         back = self._readback([self._ps_sync[self._ps_err:self._ps_err + 1], self.metrics] +
                               ([stamps] if stamps is not None else []))
         self._step_stamps = back[2].copy() if stamps is not None else None
+        if int(back[0][0]) != 0 and xg is not None:
+            # world > 1: no local rerun (the ranks would leave the same collective schedule). This
+            # rank fails the epoch; its peers' waits on it time out and fail their votes: every rank
+            # raises, and the worker group restarts from its newest checkpoint
+            from raydp_amd.exceptions import CollectiveError
+            xg._inject_error()
+            raise CollectiveError("persistent fused-MLP epoch at world > 1: a wait timed out")
         if int(back[0][0]) != 0:
             import warnings
             warnings.warn("persistent fused-MLP epoch: a workgroup wait timed out; rolled back and "

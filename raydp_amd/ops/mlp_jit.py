@@ -126,13 +126,14 @@ def generate_source(desc: "_hip.MlpDesc", mt: int, opt: Optional["_hip.OptDesc"]
         "    const u16* __restrict__ feats, const float* __restrict__ labels, const int* __restrict__ perm,",
         "    int n_rows, int batch, int nsteps, float* __restrict__ scratch, double* __restrict__ metrics,",
         "    float* __restrict__ m, float* __restrict__ v, const float* __restrict__ sched, int opt_first,",
-        "    unsigned* __restrict__ sync, unsigned long long ticks, unsigned long long* __restrict__ stamps) {",
+        "    unsigned* __restrict__ sync, unsigned long long ticks, unsigned long long* __restrict__ stamps,",
+        "    XgStep xs) {",
         "  extern __shared__ __attribute__((aligned(16))) char smem[];",
         "  __shared__ int rowidx[Tile<RX_MT>::BP];",
         "  __shared__ __attribute__((aligned(16))) int flag_lds[16];",
         "  mlp_persist_body<JitCfg, RX_MT>(dp, od, img, rstats, P, Gr, feats, labels, perm, n_rows, batch, nsteps,",
         "                                  scratch, metrics, m, v, sched, opt_first, sync, ticks, smem, rowidx,",
-        "                                  flag_lds, stamps);",
+        "                                  flag_lds, stamps, xs);",
         "}",
     ]
     return "\n".join(out) + "\n"
@@ -149,7 +150,8 @@ def _key(src: str) -> str:
     global _headers_digest
     if _headers_digest is None:      # the kernel headers a process compiles against: read once
         h = hashlib.sha256()
-        for f in ("mlp_core.h", "mlp_opt.h", "mlp_mwopt.h", "mlp_persist.h", "rx_common.h", "rx_grid.h"):
+        for f in ("mlp_core.h", "mlp_opt.h", "mlp_mwopt.h", "mlp_persist.h", "rx_common.h", "rx_grid.h",
+                  os.path.join("..", "comm", "xgmi.h")):
             with open(os.path.join(CSRC_HIP, f), "rb") as fh:
                 h.update(fh.read())
         h.update(ARCH.encode())
@@ -240,14 +242,15 @@ def precompile(model, optimizer, loss, batch_size: int, acc_thr=None) -> str:
 
 
 def precompile_many(jobs, workers: Optional[int] = None):
-    """``precompile`` over ``[(model, optimizer, loss, batch_size, acc_thr), ...]``: the layouts
-    are derived one after the other (spec extraction runs the model), the hipcc builds in
-    parallel. Returns the code-object paths."""
+    """``precompile`` over ``[(model, optimizer, loss, batch_size, acc_thr[, world]), ...]``: the
+    layouts are derived one after the other (spec extraction runs the model), the hipcc builds in
+    parallel. ``world`` > 1: the data-parallel layout (layer 0 on optimizer workgroups). Returns
+    the code-object paths."""
     from concurrent.futures import ThreadPoolExecutor
     from raydp_amd.models.mlp_spec import extract_mlp_spec
     from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
-    trs = [FusedMLPTrainer(extract_mlp_spec(m), optimizer_config(o), loss_code(l), b, None, layout_only=True,
-                           acc_thr=a) for m, o, l, b, a in jobs]
+    trs = [FusedMLPTrainer(extract_mlp_spec(j[0]), optimizer_config(j[1]), loss_code(j[2]), j[3], None,
+                           layout_only=True, acc_thr=j[4], world=j[5] if len(j) > 5 else 1) for j in jobs]
     n = workers or max(1, min(8, os.cpu_count() or 1))
     with ThreadPoolExecutor(n) as ex:
         return list(ex.map(compile_for, trs))

@@ -52,6 +52,13 @@ def set_dispatch_hook(fn) -> None:
     _dispatch_hooks.on_wait = fn
 
 
+def set_block_hook(fn) -> None:
+    """``fn(partition, object_id, node_id, rows, executor_id)`` for every partition a persist
+    stage run on this thread places, as it lands (None: off). The estimator streams the blocks
+    into HBM while the rest of the stage still runs (``raydp_amd/torch/engine.py`` stream_ingest)."""
+    _dispatch_hooks.on_block = fn
+
+
 def _seconds(v) -> float:
     v = str(v).strip().lower()
     for suf, k in (("ms", 1e-3), ("s", 1.0), ("m", 60.0)):
@@ -192,10 +199,15 @@ class ExecutorTaskScheduler(P.TaskScheduler):
         with tracing.span("stage payload", cat="etl"):
             payload, key = self._stage_payload(fn)
         out = []
+        hook = getattr(_dispatch_hooks, "on_block", None)
+
+        def landed(ex_id, lst):
+            for (i, oid, node_id, path, rows) in lst:
+                hook(i, oid, node_id, rows, ex_id)
         try:
             with tracing.span("persist stage", cat="etl", tasks=len(indices)):
                 res = self._dispatch(lambda ex, i: ex.handle.persist_partitions.remote(key, rdd_id, [i]),
-                                 indices, tag=True)
+                                     indices, tag=True, on_done=landed if hook is not None else None)
         finally:
             self._free_payload(payload, key)
         for ex_id, lst in res:
@@ -236,7 +248,7 @@ class ExecutorTaskScheduler(P.TaskScheduler):
                 return pos, least
         return None
 
-    def _dispatch(self, submit, indices, tag=False, prefs=None):
+    def _dispatch(self, submit, indices, tag=False, prefs=None, on_done=None):
         from raydp_amd.runtime import core
         from raydp_amd.runtime.actors import ActorDiedError
         results = [None] * len(indices)
@@ -278,6 +290,11 @@ class ExecutorTaskScheduler(P.TaskScheduler):
                 try:
                     v = f.result()
                     results[pos] = (ex.executor_id, v) if tag else v
+                    if on_done is not None:
+                        try:
+                            on_done(ex.executor_id, v)
+                        except Exception:  # noqa: BLE001 - an observer never fails the stage
+                            pass
                 except ActorDiedError:
                     failures[pos] += 1
                     self.backend.on_executor_failure(ex)

@@ -69,13 +69,16 @@ class _ShardTensors:
     column views are the model inputs."""
 
     def __init__(self, ds, feature_columns, feature_types, label_column, label_type, device,
-                 fused_stride: Optional[int] = None):
-        tables = ds._get_tables() if ds is not None else []
-        self.n = int(sum(t.num_rows for t in tables))
+                 fused_stride: Optional[int] = None, streamed: Optional[dict] = None):
         from raydp_amd.ops.ingest import ingest_columns
         self.groups, self.dtypes, self.multi = _to_tensor_spec(feature_columns, feature_types)
         self.device = device
         self.feats = None
+        if streamed is not None and fused_stride is not None:
+            self._from_stream(ds, streamed, label_column, label_type, fused_stride)
+            return
+        tables = ds._get_tables() if ds is not None else []
+        self.n = int(sum(t.num_rows for t in tables))
         if fused_stride is not None:
             self.feats_bf16 = ingest_columns(tables, self.groups[0], device, True, fused_stride)
         elif self.multi and all(len(g) == 1 for g in self.groups):
@@ -98,6 +101,27 @@ class _ShardTensors:
                              out_i64=(label_type in _INT_DTYPES)) if label_column is not None else None
         self.labels = lab.to(label_type or torch.float32) if lab is not None else None
 
+    def _from_stream(self, ds, streamed, label_column, label_type, stride):
+        """The fused matrix from blocks already ingested while the conversion ran
+        (:func:`stream_ingest`), in partition order; a block that did not stream (or whose final
+        reference differs: a retried task) is ingested now."""
+        from raydp_amd.data.dataset import _resolve
+        from raydp_amd.runtime.objects import ObjectRef
+        fp, lp, n = [], [], 0
+        for j, b in enumerate(ds._blocks):
+            p = streamed.get(j)
+            if p is None or not isinstance(b, ObjectRef) or p[0] != b.id:
+                t = _resolve(b)
+                p = _ingest_block(t, self.groups[0], label_column, self.device, stride)
+            _, rows, f, lab = p
+            fp.append(f)
+            lp.append(lab)
+            n += rows
+        self.n = n
+        self.feats_bf16 = fp[0] if len(fp) == 1 else torch.cat(fp)
+        lab = lp[0] if len(lp) == 1 else torch.cat(lp)
+        self.labels = lab.to(label_type or torch.float32)
+
     def _views(self, mats):
         out = []
         for k, j, d in self.where:
@@ -119,6 +143,37 @@ class _ShardTensors:
             feats = [f.index_select(0, sel) for f in self.feats]
         lab = self.labels[sel] if isinstance(sel, slice) else self.labels.index_select(0, sel)
         return feats, lab
+
+
+def _ingest_block(t, cols, label_column, device, stride):
+    """(object id, rows, bf16 features [rows, stride], fp32 labels [rows, 1]) of one Arrow block."""
+    from raydp_amd.ops.ingest import ingest_columns
+    f = ingest_columns([t], cols, device, True, stride)
+    lab = ingest_columns([t], [label_column], device, False)
+    return None, t.num_rows, f, lab
+
+
+def stream_ingest(ds, cols, label_column, device, stride) -> dict:
+    """Ingest the blocks of a deferred dataset (``ds._stream``: ``(partition, ref)`` as each
+    conversion task lands, raydp_amd/spark/cluster.py set_block_hook) while its conversion still
+    runs; returns ``{partition: (object id, rows, features, labels)}`` once it finished. The DMA of
+    a block overlaps the ETL of the later ones, so after the stage only its last block's copy is
+    left (reference: the per-partition fetch tasks of python/raydp/spark/dataset.py:203-222 feed
+    Ray Data blocks to the trainer the same way, block by block)."""
+    import queue
+    from raydp_amd.data.dataset import _resolve
+    q, fut = ds._stream, ds._pending
+    parts = {}
+    while True:
+        try:
+            i, ref = q.get(timeout=0.0005)
+        except queue.Empty:
+            if fut is None or (fut.done() and q.empty()):
+                break
+            continue
+        t = _resolve(ref)
+        parts[i] = (ref.id,) + _ingest_block(t, cols, label_column, device, stride)[1:]
+    return parts
 
 
 class FusedMLPEngine:
@@ -170,7 +225,7 @@ class FusedMLPEngine:
         self.loss = loss if loss is not None else config.get("loss")   # label encoding (fused_labels)
         self.world = session.get_world_size()
         self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn,
-                                       acc_thr=acc_thr)
+                                       acc_thr=acc_thr, world=session.get_world_size())
         from raydp_amd.utils.config import get as conf_get
         self.trainer.record_steps = bool(conf_get("spark.ray.mi355x.step_times"))
         self.last_step_times = None
@@ -199,7 +254,13 @@ class FusedMLPEngine:
         tr = self.trainer
         self.xg = _xgmi_for(tr)
         if self.xg is not None:
-            self.allreduce_kind = "xgmi_oneshot"
+            # gradients exchanged inside the training launches: the persistent epoch (batch <= 128)
+            # and the multi-workgroup step's optimizer tasks send per-tile gradients
+            self.allreduce_kind = "xgmi_tiles_in_launch" if (tr.G > 1 or persistent_layout(tr)) \
+                else "xgmi_oneshot"
+            tr.share = self.xg.share
+            if tr._mw_args is not None:
+                tr._mw_args.share = self.xg.share
             if tr.params.numel() <= self.xg.max_floats:
                 if dist.get_rank() != 0:
                     tr.params.zero_()
@@ -221,12 +282,21 @@ class FusedMLPEngine:
                 self.ar = ar
         tr.refresh_images()
 
+    def stream_ingest(self, train_ds, config):
+        """Training blocks into HBM as the conversion lands them (world 1, in-process)."""
+        if self.world != 1 or getattr(train_ds, "_stream", None) is None:
+            return
+        groups, _, _ = _to_tensor_spec(config["feature_columns"], config["feature_types"])
+        self._streamed = stream_ingest(train_ds, groups[0], config["label_column"], self.device,
+                                       self.trainer.feat_k)
+
     def load(self, train_ds, eval_ds, config):
         from raydp_amd.ops.fused_mlp import fused_labels
         fc, ft = config["feature_columns"], config["feature_types"]
         k = self.trainer.feat_k
+        streamed, self._streamed = getattr(self, "_streamed", None), None
         self.train = _ShardTensors(train_ds, fc, ft, config["label_column"], torch.float32,
-                                   self.device, fused_stride=k)
+                                   self.device, fused_stride=k, streamed=streamed)
         self.eval = _ShardTensors(eval_ds, fc, ft, config["label_column"], torch.float32, self.device,
                                   fused_stride=k) if eval_ds is not None else None
         classes = self.trainer.desc.out_dim
@@ -347,6 +417,12 @@ def _binary_accuracy_threshold(metrics):
     return thr
 
 
+def persistent_layout(trainer) -> bool:
+    """The trainer's epochs can run as the persistent launch (one-workgroup batch, wgrad mode 1)."""
+    from raydp_amd.ops.fused_mlp import persistent_enabled
+    return trainer.G == 1 and trainer.desc.wgrad_mode == 1 and not trainer.desc.front_n and persistent_enabled()
+
+
 def _xgmi_for(trainer):
     """The one-shot xGMI communicator for this trainer's gradient, or None (RCCL instead).
 
@@ -359,9 +435,11 @@ def _xgmi_for(trainer):
     mode = conf_get("spark.ray.mi355x.allreduce")
     if mode == "rccl" or not torch.cuda.is_available():
         return None
-    # the exchange slot is the whole gradient buffer (flat gradient + exported activations)
-    xg = XgmiComm.create(trainer.grads.numel(), timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"),
-                         host_seq=True)
+    # the exchange slot: the flat gradient for the in-launch tile exchange of the multi-workgroup
+    # step; the whole gradient buffer (flat gradient + exported activations) for one-workgroup
+    # batches, whose launch-per-step fallback reduces from the peers' activations
+    nf = trainer.total if trainer.G > 1 else trainer.grads.numel()
+    xg = XgmiComm.create(nf, timeout_s=conf_get("spark.ray.mi355x.allreduce.timeout_s"), host_seq=True)
     if xg is None and mode == "xgmi":
         raise RuntimeError("spark.ray.mi355x.allreduce=xgmi but the xGMI peer mapping is unavailable")
     return xg

@@ -55,6 +55,9 @@ class _Pick:
     def result(self):
         return self.fut.result()[self.i]
 
+    def done(self):
+        return self.fut.done()
+
 
 def _make_lr_schedule(opt_template: torch.optim.Optimizer, creator, config):
     """Per-step learning rates of ``creator(optimizer, config)`` for the fused engine."""
@@ -308,6 +311,12 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         deferred = [ds for ds in (train_ds, eval_ds) if getattr(ds, "_pending", None) is not None]
         if deferred:   # fit_on_spark built this engine while the conversion stage ran
             with tracing.span("conversion wait", cat="train"):
+                stream = getattr(train_ds, "_stream", None) if train_ds in deferred else None
+                if stream is not None and hasattr(engine, "stream_ingest"):
+                    # the blocks go to HBM as they land: only the last one's DMA is left after
+                    with tracing.span("streamed ingest", cat="train"):
+                        engine.stream_ingest(train_ds, config)
+                    LAST_TIMINGS["streamed_blocks"] = len(getattr(engine, "_streamed", None) or ())
                 for ds in deferred:
                     ds.num_blocks()
             LAST_TIMINGS["conversion_wait"] = time.perf_counter() - t_wait0
@@ -440,7 +449,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         from raydp_amd.utils import tracing
         from raydp_amd.utils.config import get as conf_get
         t_conv0 = time.perf_counter()
-        for k in ("conversion_wait", "etl_and_conversion_concurrent"):
+        for k in ("conversion_wait", "etl_and_conversion_concurrent", "streamed_blocks"):
             LAST_TIMINGS.pop(k, None)
         if fs_directory is None and not stop_spark_after_conversion \
                 and conf_get("spark.ray.mi355x.overlap_conversion"):
@@ -456,12 +465,20 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             from raydp_amd.spark import cluster as spark_cluster
             in_flight = threading.Event()
 
+            # one in-process worker: the training blocks stream into HBM as they land, while the
+            # rest of the stage still runs (the engine's stream_ingest)
+            stream = None
+            if self._num_workers == 1 and conf_get("spark.ray.mi355x.stream_ingest") and \
+                    conf_get("spark.ray.mi355x.train_inprocess"):
+                import queue
+                stream = queue.Queue()
+
             def convert():
                 t0 = time.perf_counter()
                 spark_cluster.set_dispatch_hook(in_flight.set)
                 try:
                     with tracing.span("etl + conversion", cat="etl"):
-                        out = self._convert_via_store(train_df, evaluate_df, None)
+                        out = self._convert_via_store(train_df, evaluate_df, None, stream=stream)
                 finally:
                     spark_cluster.set_dispatch_hook(None)
                     in_flight.set()
@@ -475,6 +492,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                 # the conversion is done, not after the whole training run
                 fut.add_done_callback(lambda _f: sys.setswitchinterval(switch))
                 train_ds = Dataset.deferred(_Pick(fut, 0))
+                train_ds._stream = stream
                 evaluate_ds = Dataset.deferred(_Pick(fut, 1)) if evaluate_df is not None else None
                 in_flight.wait()
                 LAST_TIMINGS["etl_and_conversion"] = time.perf_counter() - t_conv0
@@ -500,11 +518,23 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
             stop_spark(cleanup_data=False)
         return self.fit(train_ds, evaluate_ds, max_retries)
 
-    def _convert_via_store(self, train_df, evaluate_df, owner):
+    def _convert_via_store(self, train_df, evaluate_df, owner, stream=None):
         from raydp_amd.spark.dataset import spark_dataframe_to_ray_dataset
         super().fit_on_spark(train_df, evaluate_df)
         train_df = self._check_and_convert(train_df)
-        train_ds = spark_dataframe_to_ray_dataset(train_df, owner=owner)
+        if stream is not None:
+            # every training partition, as its block lands: (partition, reference) into the stream
+            from raydp_amd.runtime.objects import ObjectRef
+            from raydp_amd.spark import cluster as spark_cluster
+
+            def landed(i, oid, node_id, rows, ex_id):
+                stream.put((i, ObjectRef(oid, owner=f"raydp-executor-{ex_id}", node_id=node_id)))
+            spark_cluster.set_block_hook(landed)
+        try:
+            train_ds = spark_dataframe_to_ray_dataset(train_df, owner=owner)
+        finally:
+            if stream is not None:
+                spark_cluster.set_block_hook(None)
         evaluate_ds = None
         if evaluate_df is not None:
             evaluate_df = self._check_and_convert(evaluate_df)

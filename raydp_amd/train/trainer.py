@@ -5,7 +5,8 @@ by ``torch.distributed`` — backend ``"nccl"`` (= RCCL over xGMI on ROCm) when 
 GPUs, Gloo otherwise — with datasets split into equal row shards (equal shards keep every rank
 on the same step count, so collectives never deadlock). Three launch modes:
 
-* **in-process** — ``num_workers == 1``: the loop runs in the caller (no fork cost).
+* **in-process** — ``num_workers == 1``: the loop runs in the caller (no fork cost; config
+  ``spark.ray.mi355x.train_inprocess`` off sends it through one spawned worker, as Ray Train does).
 * **SPMD** — the caller already is one rank of a ``torchrun`` job (``WORLD_SIZE`` env matches):
   every process runs its own rank in-process; this is how ``bench.py`` scales to 8 GPUs.
 * **spawned** — otherwise ``num_workers`` child processes are started (spawn context), each
@@ -246,7 +247,9 @@ class DataParallelTrainer:
                 ckpts.append(ckpt)
 
         env_world = int(os.environ.get("WORLD_SIZE", "1"))
-        if world == 1 or (env_world == world and "RANK" in os.environ):
+        from raydp_amd.utils.config import get as conf_get
+        inproc_one = world == 1 and bool(conf_get("spark.ray.mi355x.train_inprocess"))
+        if inproc_one or (env_world == world and "RANK" in os.environ and world > 1):
             self._run_inprocess(world, env_world, use_gpu, storage, reporter)
         else:
             self._run_spawned(world, use_gpu, storage, reporter)

@@ -232,6 +232,16 @@ register("spark.ray.mi355x.graph_user_model", "bool", True,
          "backward as HIP graphs per repeated batch shape (raydp_amd/train/gpu_policy.py graph_model); "
          "eager for eval, other shapes and models that cannot be captured", env="RAYDP_GRAPH_USER_MODEL")
 
+register("spark.ray.mi355x.stream_ingest", "bool", True,
+         "fit_on_spark with one in-process worker: the fused engine DMAs each training block into HBM as "
+         "its conversion task lands, while the rest of the stage runs (raydp_amd/torch/engine.py "
+         "stream_ingest)", env="RAYDP_STREAM_INGEST")
+
+register("spark.ray.mi355x.train_inprocess", "bool", True,
+         "a one-worker fit runs its loop in the caller's process (no worker hop); off: through a "
+         "spawned worker actor, as Ray Train always does (the bench's N = 1 worker-hop measurement)",
+         env="RAYDP_TRAIN_INPROCESS")
+
 
 def _active_conf() -> Optional[Mapping]:
     try:

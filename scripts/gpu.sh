@@ -2,6 +2,7 @@
 # One entry point for the GPU-box work (run through gpurun). Every GPU step has its own time
 # limit and the script stops at the first failure.
 #   scripts/gpu.sh tests [pytest -k expr]        GPU test suite, then smoke()
+#   scripts/gpu.sh files FILE...                  selected GPU test files
 #   scripts/gpu.sh bench [N] [STEPS] [WARM] [REPS]  bench.py runs -> gpurun_out/bench.jsonl
 #   scripts/gpu.sh rehearse [N] [STEPS] [WARM]   N ranks on the one GPU: SPMD self-launch (gloo
 #                                                 bootstrap, xGMI gradients) + estimator topology
@@ -27,6 +28,11 @@ case $cmd in
     [ $rc -ne 0 ] && exit $rc
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
     rc=$?; tail -1 gpurun_out/smoke.log; exit $rc;;
+  files)
+    # selected GPU test files (no smoke): scripts/gpu.sh files tests/test_gpu_xgmi.py ...
+    timeout -k 10 1000 $T "$@" -m gpu > gpurun_out/gpu_files.log 2>&1
+    rc=$?; echo "gpu files rc=$rc"; grep -E "passed|failed|^E  |PASSED|FAILED" gpurun_out/gpu_files.log | tail -40
+    exit $rc;;
   bench)
     N=${1:-1}; S=${2:-20}; W=${3:-5}; REPS=${4:-3}
     for i in $(seq $REPS); do

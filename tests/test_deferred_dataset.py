@@ -56,3 +56,23 @@ def test_failed_source_raises_its_own_error_through_the_lazy_shuffle():
             lazy.count()
         # the parent's failure, not a DeferredDatasetError wrapped in another
         assert isinstance(ei.value.original, KeyError)
+
+
+def test_equal_split_references_blocks_instead_of_copying(runtime_local):
+    """Equal shards are slices of the object-store blocks (a few ids when pickled to a worker),
+    with the same rows, in the same order, as slicing the concatenated dataset."""
+    import pickle
+    import pyarrow as pa
+    from raydp_amd import runtime
+    from raydp_amd.data.dataset import BlockSlice, Dataset
+    blocks = [pa.table({"x": list(range(s, s + k))}) for s, k in ((0, 7), (7, 13), (20, 5), (25, 11))]
+    ds = Dataset([runtime.put(t) for t in blocks])
+    whole = pa.concat_tables(blocks)
+    for n in (1, 2, 3, 4, 5):
+        shards = ds.split(n, equal=True)
+        per = whole.num_rows // n
+        for i, sh in enumerate(shards):
+            assert all(isinstance(b, BlockSlice) for b in sh._blocks)
+            assert len(pickle.dumps(sh)) < 2048
+            back = pickle.loads(pickle.dumps(sh))
+            assert back.to_arrow().column("x").to_pylist() == whole.slice(i * per, per).column("x").to_pylist()

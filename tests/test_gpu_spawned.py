@@ -107,3 +107,31 @@ def test_warm_workers_survive_consecutive_graph_captured_fits(runtime_local, tmp
     assert engines == ["torch_loop_hipgraph"] * 2, engines
     assert groups[0] is groups[1], "the second fit must run on the same warm workers (no restart)"
     T.release_worker_groups()
+
+
+def test_streamed_ingest_trains_like_ingest_after_conversion(spark_on_ray_2_executors, tmp_path, monkeypatch):
+    """fit_on_spark with one in-process worker DMAs each training block into HBM as its conversion
+    task lands (engine stream_ingest); the model trains bit for bit as with the whole conversion
+    ingested afterwards (blocks assembled in partition order)."""
+    import pandas as pd
+    from raydp_amd.torch import TorchEstimator
+    from raydp_amd.torch.estimator import LAST_TIMINGS
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((64 * 40, 20)).astype(np.float32)
+    pdf = pd.DataFrame({f"f{i}": x[:, i] for i in range(20)})
+    pdf["y"] = x[:, :4].sum(1) * 0.5 + 1.0
+    df = spark_on_ray_2_executors.createDataFrame(pdf).repartition(8)
+    states = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("RAYDP_STREAM_INGEST", mode)
+        model = _model()
+        est = TorchEstimator(num_workers=1, model=model, optimizer=torch.optim.Adam(model.parameters(), lr=1e-3),
+                             loss=nn.MSELoss(), feature_columns=[f"f{i}" for i in range(20)], label_column="y",
+                             batch_size=64, num_epochs=2, fused="on", shuffle_seed=5,
+                             storage_path=str(tmp_path / mode))
+        est.fit_on_spark(df)
+        states[mode] = {k: v.detach().cpu().clone() for k, v in est.get_model().state_dict().items()}
+        assert "ingest" in LAST_TIMINGS
+        assert (LAST_TIMINGS.get("streamed_blocks", 0) > 0) == (mode == "1"), dict(LAST_TIMINGS)
+    for k in states["0"]:
+        assert torch.equal(states["0"][k], states["1"][k]), k

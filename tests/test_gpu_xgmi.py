@@ -172,6 +172,131 @@ def test_fused_step_loop_with_xgmi_reduce_matches_gloo_allreduce(world):
         assert rel < 1e-4, (rank, rel)
 
 
+def _nyc_full(cols=20):
+    """The flagship NYC_Model (examples/pytorch_nyctaxi.py): 5 Linear + 4 BatchNorm1d."""
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc1, self.fc2, self.fc3 = nn.Linear(cols, 256), nn.Linear(256, 128), nn.Linear(128, 64)
+            self.fc4, self.fc5 = nn.Linear(64, 16), nn.Linear(16, 1)
+            self.bn1, self.bn2 = nn.BatchNorm1d(256), nn.BatchNorm1d(128)
+            self.bn3, self.bn4 = nn.BatchNorm1d(64), nn.BatchNorm1d(16)
+
+        def forward(self, x):
+            x = self.bn1(F.relu(self.fc1(x)))
+            x = self.bn2(F.relu(self.fc2(x)))
+            x = self.bn3(F.relu(self.fc3(x)))
+            x = self.bn4(F.relu(self.fc4(x)))
+            return self.fc5(x)
+    return M()
+
+
+def _tiles_main(rank, world, port, q, batch=64, steps=12):
+    """The data-parallel fused engine with the gradient exchanged INSIDE the training launches
+    (persistent epoch at batch <= 128, the multi-workgroup step's optimizer tasks above), against
+    the same trainer with a gloo all-reduce of materialised gradients between launches."""
+    import torch
+    import torch.distributed as dist
+    import torch.nn as nn
+    _init(rank, world, port)
+    try:
+        from raydp_amd.models.mlp_spec import extract_mlp_spec
+        from raydp_amd.ops.comm import XgmiComm
+        from raydp_amd.ops.fused_mlp import FusedMLPTrainer, loss_code, optimizer_config
+        dev = torch.device("cuda", 0)
+        outs, paths, times = [], [], None
+        for mode in ("xgmi", "gloo"):
+            torch.manual_seed(0)
+            model = _nyc_full()
+            opt = torch.optim.SGD(model.parameters(), lr=1e-2, momentum=0.9)
+            tr = FusedMLPTrainer(extract_mlp_spec(model), optimizer_config(opt), loss_code(nn.SmoothL1Loss()),
+                                 batch, dev, world=world)
+            tr.record_steps = True
+            g = torch.Generator().manual_seed(7 + rank)
+            n = batch * steps
+            feats = torch.zeros(n, tr.feat_k, dtype=torch.bfloat16)
+            feats[:, :20] = torch.randn(n, 20, generator=g).to(torch.bfloat16)
+            labels = torch.randn(n, 1, generator=g) * 3
+            feats, labels = feats.to(dev), labels.to(dev)
+            perm = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(torch.int32).to(dev)
+            if mode == "xgmi":
+                xg = XgmiComm.create(tr.total if tr.G > 1 else tr.grads.numel(), timeout_s=20.0, host_seq=True)
+                if xg is None:
+                    q.put((rank, "create failed", None, None, None, None))
+                    return
+                tr.share = xg.share
+                if tr._mw_args is not None:
+                    tr._mw_args.share = xg.share
+                for _ in range(2):
+                    tr.train_epoch(feats, labels, n, perm, world_size=world, xg=xg)
+                    paths.append(tr.last_path)
+                    st = tr.step_times_us()
+                    times = st if st is not None else times
+            else:
+                def ar(gr):
+                    # every rank's gradient, summed in rank order from zero: the exchange's own
+                    # summation order, so the two paths must agree bit for bit
+                    parts = [torch.empty_like(gr) for _ in range(world)]
+                    dist.all_gather(parts, gr)
+                    acc = torch.zeros_like(gr)
+                    for p_ in parts:
+                        acc = acc + p_
+                    gr.copy_(acc)
+                for _ in range(2):
+                    tr.train_epoch(feats, labels, n, perm, allreduce=ar, world_size=world)
+            torch.cuda.synchronize()
+            outs.append(torch.cat([tr.params.detach().cpu(), tr.rstats.detach().cpu()]).clone())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, outs[0][:tr.total])
+        same = all(bool(torch.equal(gathered[0], x)) for x in gathered)
+        rel = float((outs[0] - outs[1]).abs().max()) / float(outs[1].abs().max())
+        q.put((rank, "ok", same, rel, tuple(paths), None if times is None else float(sorted(times)[len(times) // 2])))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _tiles_b64(rank, world, port, q):
+    _tiles_main(rank, world, port, q, batch=64, steps=16)
+
+
+def _tiles_b1000(rank, world, port, q):
+    _tiles_main(rank, world, port, q, batch=1000, steps=6)
+
+
+def _tiles_b4096(rank, world, port, q):
+    _tiles_main(rank, world, port, q, batch=4096, steps=4)
+
+
+@pytest.mark.parametrize("world,target,path", [(2, "_tiles_b64", "persistent_xgmi_tiles"),
+                                               (4, "_tiles_b64", "persistent_xgmi_tiles"),
+                                               (8, "_tiles_b64", "persistent_xgmi_tiles"),
+                                               (2, "_tiles_b1000", "mw_xgmi_tiles"),
+                                               (4, "_tiles_b1000", "mw_xgmi_tiles"),
+                                               (2, "_tiles_b4096", "mw_xgmi_tiles")])
+def test_in_launch_gradient_exchange_matches_gloo_allreduce(world, target, path):
+    """World > 1 on the one-GPU engine's kernels: batch 64 trains in the persistent epoch launch
+    and batch 1000 / 4096 in the multi-workgroup step, each exchanging per-tile GRADIENTS over
+    xGMI inside the launch (the optimizer workgroups meet their peers per 32x32 tile). Replicas
+    stay bit-identical, and the parameters and BatchNorm statistics equal those of the same
+    trainer fed a gloo all-gather of materialised gradients summed in rank order between
+    launches (the exchange's summation order), and the device step time is recorded at
+    world > 1."""
+    res = _run(globals()[target], world, timeout=200)
+    assert len(res) == world
+    for rank, status, same, rel, paths, step_us in res:
+        assert status == "ok", (rank, status)
+        assert all(p == path for p in paths), (rank, paths)
+        assert same, "replicas diverged across ranks"
+        # persistent: bit-level agreement; multi-workgroup: the local dW is summed over split-K
+        # partials in-launch vs one K chain in the materialising kernel (fp32 order only)
+        assert rel < (1e-6 if path.startswith("persistent") else 1e-4), (rank, rel)
+        assert step_us is not None and step_us > 0, (rank, step_us)
+
+
 def _ddp_main(rank, world, port, q):
     import torch
     import torch.distributed as dist

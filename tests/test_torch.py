@@ -216,3 +216,44 @@ def test_spawned_deferred_conversion_failure_is_raised_once(spark_on_ray_small, 
         est.fit_on_spark(df, max_retries=3)
     assert not isinstance(ei.value, (TrainingFailedError, DeferredDatasetError)), repr(ei.value)
     assert "bad row" in str(ei.value)
+
+
+def test_one_worker_through_a_spawned_actor(spark_on_ray_small, monkeypatch):
+    """``spark.ray.mi355x.train_inprocess`` off: a one-worker fit runs in a spawned worker actor
+    (Ray Train's topology, the hop every N > 1 fit pays) and trains like the in-process loop."""
+    from raydp_amd.train import session
+    monkeypatch.setenv("RAYDP_TRAIN_INPROCESS", "0")
+    df = spark_on_ray_small.createDataFrame([(float(i), 2.0 * i + 1.0) for i in range(64)], ["x", "y"])
+    pids = []
+
+    def fn(config):
+        session.report({"pid": os.getpid(), "world": session.get_world_size()})
+    from raydp_amd.train.trainer import TorchTrainer
+    from raydp_amd.train.config import ScalingConfig
+    res = TorchTrainer(fn, scaling_config=ScalingConfig(num_workers=1, use_gpu=False)).fit()
+    pids.append(res.metrics["pid"])
+    assert res.metrics["world"] == 1 and pids[0] != os.getpid()
+    model = torch.nn.Linear(1, 1)
+    est = TorchEstimator(num_workers=1, model=model, optimizer=torch.optim.Adam(model.parameters(), lr=0.1),
+                         loss=torch.nn.MSELoss(), feature_columns=["x"], feature_types=torch.float,
+                         label_column="y", label_type=torch.float, batch_size=16, num_epochs=2, use_gpu=False)
+    est.fit_on_spark(df)
+    assert any("train_loss" in h for h in est.results.metrics_history)
+
+
+def test_persist_stage_reports_every_block_as_it_lands(spark_on_ray_2_executors):
+    """The block hook of a persist stage (what the fused engine's streamed ingest consumes) sees
+    every partition once, with the object the final dataset references."""
+    from raydp_amd.spark import cluster as C
+    from raydp_amd.spark.dataset import spark_dataframe_to_ray_dataset
+    df = _tiny_df(spark_on_ray_2_executors, n=2000).repartition(6)
+    seen = []
+    C.set_block_hook(lambda i, oid, node_id, rows, ex: seen.append((i, oid, rows)))
+    try:
+        ds = spark_dataframe_to_ray_dataset(df)
+    finally:
+        C.set_block_hook(None)
+    assert sorted(i for i, _, _ in seen) == list(range(ds.num_blocks()))
+    by_i = {i: (oid, rows) for i, oid, rows in seen}
+    assert [by_i[i][0] for i in range(ds.num_blocks())] == [b.id for b in ds._blocks]
+    assert sum(r for _, r in by_i.values()) == 2000
