@@ -92,7 +92,7 @@ def graph_model(module):
         return module
     orig = module.forward
     graphs, seen, pending = {}, {}, set()
-    state = {"failed": False}
+    state = {"failed": False, "outstanding": 0}   # forwards (any shape) whose backward is still to come
 
     class _Fwd(torch.nn.Module):       # parameters() = the model's, forward = its original one
         def __init__(self):
@@ -124,33 +124,44 @@ def graph_model(module):
                                        for a in args)):
             return orig(*args, **kwargs)
         key = tuple((tuple(a.shape), a.dtype) for a in args)
+        graphed = False
         if key in pending:       # this shape's last replay still waits for its backward
-            return orig(*args)
-        g = graphs.get(key)
-        if g is None:
-            n = seen.get(key, 0) + 1
-            seen[key] = n
-            if n < _STEADY or len(graphs) >= _MAX_SHAPES:
-                return orig(*args)
-            g = _capture(args)
+            out = orig(*args)
+        else:
+            g = graphs.get(key)
             if g is None:
-                return orig(*args)
-            graphs[key] = g
-        out = g(*args)
+                n = seen.get(key, 0) + 1
+                seen[key] = n
+                # capture only between iterations: with a forward of this model still waiting for
+                # its backward the capture's own warm-up backward would run inside that graph
+                if n >= _STEADY and len(graphs) < _MAX_SHAPES and state["outstanding"] == 0:
+                    g = _capture(args)
+                    if g is not None:
+                        graphs[key] = g
+            if g is not None:
+                out, graphed = g(*args), True
+            else:
+                out = orig(*args)
         leaves = [t for t in torch.utils._pytree.tree_leaves(out)
                   if isinstance(t, torch.Tensor) and t.requires_grad]
         if leaves:
-            pending.add(key)
+            state["outstanding"] += 1
+            if graphed:
+                pending.add(key)
             left = [len(leaves)]
 
-            def arrived(grad, key=key, left=left):
+            def arrived(grad, key=key, left=left, graphed=graphed):
                 # the graphed backward runs right after the gradients of its outputs
                 left[0] -= 1
-                if left[0] <= 0:
-                    pending.discard(key)
+                if left[0] == 0:
+                    state["outstanding"] -= 1
+                    if graphed:
+                        pending.discard(key)
                 return grad
             for t in leaves:
                 t.register_hook(arrived)
+        if not graphed:
+            return out
         return torch.utils._pytree.tree_map(lambda t: t.clone() if isinstance(t, torch.Tensor) else t, out)
 
     def reduce_ex(proto):
