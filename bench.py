@@ -767,6 +767,9 @@ def main():
                        if driver_gpu else h0.get("hbm_peak_allocated_mib"),
                        "rank0_breakdown_s": phases},
         }
+        from raydp_amd.torch.estimator import STREAM_STATS
+        if STREAM_STATS.get("blocks"):
+            out["config"]["streamed_blocks"] = STREAM_STATS["blocks"]   # DMA'd while the conversion ran
         if spawned_n1 is not None:
             out["config"]["n1_spawned_worker"] = dict(
                 spawned_n1, what="the same pipeline with the one training worker in a spawned actor "

@@ -165,6 +165,14 @@ struct XgStep {
 
 __device__ __forceinline__ float* rx_xg_region(const XgDev& x, int p) { return x.region[p]; }
 
+// A specialised one-GPU code object (raydp_amd/ops/mlp_jit.py, world 1) is compiled with
+// RX_XG_KERNELS 0: every exchange branch of the training kernels folds away and the kernels keep
+// the one-GPU register allocation. The ahead-of-time build keeps them (1).
+#ifndef RX_XG_KERNELS
+#define RX_XG_KERNELS 1
+#endif
+__device__ __forceinline__ bool rx_xg_active(const XgStep& xs) { return RX_XG_KERNELS && xs.on; }
+
 __device__ __forceinline__ unsigned* rx_xg_tflags_of(float* region, const XgDev& x) {
   return reinterpret_cast<unsigned*>(region + 2 * (size_t)x.nf) + 3 * RX_XG_MAXR;
 }

@@ -49,6 +49,7 @@ constexpr Key kKeys[] = {
     {"spark.ray.mi355x.fused_optimizer", "RAYDP_FUSED_OPTIMIZER", "1"},
     {"spark.ray.mi355x.native_batchnorm", "RAYDP_NATIVE_BATCHNORM", "1"},
     {"spark.ray.mi355x.graph_user_model", "RAYDP_GRAPH_USER_MODEL", "1"},
+    {"spark.ray.mi355x.graph_hvd_model", "RAYDP_GRAPH_HVD_MODEL", "0"},
     {"spark.ray.mi355x.stream_ingest", "RAYDP_STREAM_INGEST", "1"},
     {"spark.ray.mi355x.train_inprocess", "RAYDP_TRAIN_INPROCESS", "1"},
 };

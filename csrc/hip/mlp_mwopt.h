@@ -176,7 +176,7 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
   }
   __syncthreads();
   bool xlast = last;
-  if (a.xs.on) {
+  if (rx_xg_active(a.xs)) {
     // world > 1: this rank's tile into its slot, the tile flag, every peer's flag (all threads of
     // the workgroup run the barriers; only a last arriver's half stores / publishes / waits)
     const XgDev& x = *a.xs.xd;
@@ -198,7 +198,7 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
     xlast = *last_lds != 0;
   }
   if (xlast) {
-    const float gsc = a.xs.on ? a.xs.gscale : 1.f;
+    const float gsc = rx_xg_active(a.xs) ? a.xs.gscale : 1.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int oo = o0 + to + r * 8, ii = i0 + ti;
@@ -207,7 +207,7 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
         const int idx = sg.start + oo * sg.in + ii;
         float pv = pp[r], mv = pm[r], vv = pvv[r];   // opt_update with the loads hoisted
         const float gl = gtile[(to + r * 8) * 33 + ti];
-        const float gw = a.xs.on ? rx_xg_tile_sum(*a.xs.xd, a.xs.seq, idx, gl) : gl;
+        const float gw = rx_xg_active(a.xs) ? rx_xg_tile_sum(*a.xs.xd, a.xs.seq, idx, gl) : gl;
         opt_update_reg(o, pv, mv, vv, gw, a.lr, a.bc1, a.bc2, gsc, a.first);
         a.m[idx] = mv;
         if (o.algo != 2) a.v[idx] = vv;
@@ -240,7 +240,7 @@ __device__ __forceinline__ void mw_vector_chunk(const MwOptArgs& a, int c, int t
     if (sg.kind == 1) continue;
     const int nb = (sg.len + CH - 1) / CH;
     if (c < nb) {
-      if (!a.xs.on) {
+      if (!rx_xg_active(a.xs)) {
         for (int q = c * CH + t; q < min(sg.len, (c + 1) * CH); q += NT) {
           const int idx = sg.start + q;
           opt_update(o, idx, a.p, sc1 ? rx_ld_sc1f(a.g + idx) : a.g[idx], a.m, a.v, a.lr, a.bc1, a.bc2, 1.f, a.first);

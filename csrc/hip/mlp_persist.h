@@ -120,7 +120,7 @@ __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, c
   const int tid = rx_tid() - RX_PS_VEC_T0;
   if (tid < 0) return;
   float gsc = 1.f;
-  if (xs.on) {
+  if (rx_xg_active(xs)) {
     int ok = 1;
     if ((rx_tid() & 63) == 0) {
       ok = rx_xg_tile_wait(*xs.xd, mw_weight_tiles(o), seq) ? 1 : 0;
@@ -154,7 +154,7 @@ __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, c
       slot[j] = sl;
       const int q = id >= 0 ? id : 0;
       g[j] = rx_g(Gr)[q];
-      if (xs.on) g[j] = rx_xg_tile_sum(*xs.xd, seq, q, g[j]);
+      if (rx_xg_active(xs)) g[j] = rx_xg_tile_sum(*xs.xd, seq, q, g[j]);
       mv[j] = rx_g(m)[q];
       vv[j] = rx_g(v)[q];
     }
@@ -430,7 +430,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
   // layer carries a BatchNorm (its affine gradients are not produced by a post-op)
   bool last_affine = false;
   C::each_layer(d, [&](const auto& ly, int) { last_affine = ly.g_off >= 0 || ly.be_off >= 0; });
-  const bool vec_inline = !last_affine && !xs.on;   // (world > 1: the rank sums come after the step)
+  const bool vec_inline = !last_affine && !rx_xg_active(xs);   // (world > 1: the rank sums come after the step)
   using O = typename rx_opt_type<C>::type;
   const rx_opt_holder<O> oh;
   const O& oc = oh.get(o);
@@ -609,7 +609,7 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       __syncthreads();
       if (rx_tid() == 0)
         __hip_atomic_store(rx_g(sync) + RX_PS_FLAG(0), (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (xs.on) {
+      if (rx_xg_active(xs)) {
         // world > 1: the step's bias / BatchNorm gradients (this workgroup's own Gr stores) into
         // this rank's slot, published as one tile; the peers' arrive with the next step's wait
         float* mine = rx_xg_slotp(*xs.xd, xs.xd->rank, xs.seq + (unsigned)s);
@@ -752,7 +752,7 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, 
       rx_g(stamps)[28] = wall_clock64();
     }
     float gsc = 1.f;
-    if (xs.on) {
+    if (rx_xg_active(xs)) {
       // world > 1: both halves' tiles into this rank's slot, published; every peer's tiles waited
       // for; the rank sums (rank order) replace the local gradient
       const unsigned seq = xs.seq + (unsigned)s;

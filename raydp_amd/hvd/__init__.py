@@ -399,14 +399,15 @@ def _graph_user_module(named_parameters, params):
     ``raydp_amd/train/gpu_policy.py`` graph_model) -- a tabular MLP step is ~40 tiny kernels each
     way whose launch cost exceeds their run time. Gradients still reach ``.grad`` through autograd
     (the accumulate hooks that start the bucket all-reduce fire as before), so the wrapped step is
-    unchanged. Config ``spark.ray.mi355x.graph_user_model``; GPU parameters only."""
+    unchanged. Configs ``spark.ray.mi355x.graph_user_model`` and ``graph_hvd_model`` (off by
+    default); GPU parameters only."""
     frame = getattr(named_parameters, "gi_frame", None)
     mod = frame.f_locals.get("self") if frame is not None else None
     import torch
     if not isinstance(mod, torch.nn.Module) or not params or not all(p.is_cuda for p in params):
         return None
     from raydp_amd.utils import config as C
-    if not C.get("spark.ray.mi355x.graph_user_model"):
+    if not (C.get("spark.ray.mi355x.graph_user_model") and C.get("spark.ray.mi355x.graph_hvd_model")):
         return None
     from raydp_amd.train.gpu_policy import graph_model
     return graph_model(mod)

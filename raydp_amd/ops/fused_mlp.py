@@ -461,7 +461,9 @@ class FusedMLPTrainer:
             self._mw_nopt = 0 if cap == 0 else min(-(-tiles * splits // 2), cap if cap > 1 else 1 << 30)
         self.lds_bytes = lds
         # descriptors live in device memory: the kernels index them with runtime layer ids
-        self._materialize(bytes(d), bytes(o), rs_init)
+        from raydp_amd.utils import tracing
+        with tracing.span("trainer arena", cat="train"):
+            self._materialize(bytes(d), bytes(o), rs_init)
         self._dd = ctypes.c_void_p(self._desc_buf.data_ptr())
         self._od = ctypes.c_void_p(self._opt_buf.data_ptr())
         b = _hip.StepBufs()
@@ -494,7 +496,8 @@ class FusedMLPTrainer:
             return
         if jit_enabled():
             from raydp_amd.ops import mlp_jit
-            self.jit = mlp_jit.load_specialized(self)
+            with tracing.span("jit load", cat="train"):
+                self.jit = mlp_jit.load_specialized(self)
         self.refresh_images()
 
     def _materialize(self, desc_bytes: bytes, opt_bytes: bytes, rs_init):

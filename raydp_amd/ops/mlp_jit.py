@@ -42,11 +42,13 @@ def _f(x: float) -> str:
     return repr(float(x)) + "f" if "e" in repr(float(x)) or "." in repr(float(x)) else f"{float(x)}f"
 
 
-def generate_source(desc: "_hip.MlpDesc", mt: int, opt: Optional["_hip.OptDesc"] = None) -> str:
+def generate_source(desc: "_hip.MlpDesc", mt: int, opt: Optional["_hip.OptDesc"] = None,
+                    xg: bool = True) -> str:
     """``opt``: the optimizer's hyperparameters become constants too (the persistent kernel's
-    in-epilogue bias / BatchNorm updates, csrc/hip/mlp_core.h PsVec)."""
+    in-epilogue bias / BatchNorm updates, csrc/hip/mlp_core.h PsVec). ``xg`` False (a one-GPU
+    trainer): the in-launch gradient exchange is compiled out (csrc/comm/xgmi.h RX_XG_KERNELS)."""
     L = desc.L
-    out = []
+    out = [] if xg else ["#define RX_XG_KERNELS 0"]
     if os.environ.get("RAYDP_MLP_LAYER_STAMPS") == "1":
         # diagnostic build: the persistent epoch's middle step writes intra-layer s_memtime stamps
         out.append("#define RX_LAYER_STAMPS 1")
@@ -190,12 +192,20 @@ _paths = {}     # (descriptor bytes, MT) -> code-object path: a refit of the sam
                # neither regenerates nor re-hashes the specialised source
 
 
+_OPT_CONSTS = ("algo", "nesterov", "maximize", "b1", "b2", "eps", "wd", "momentum", "dampening")
+
+
 def compile_for(trainer) -> str:
     opt = getattr(trainer, "opt", None)
-    k = (bytes(trainer.desc), int(trainer.mt), bytes(opt) if opt is not None else b"")
+    # (the optimizer descriptor also holds this fit's device pointers to the bf16 images: the key
+    # takes only the fields the generated source reads, so a refit finds its code object here
+    # instead of regenerating and hashing the source)
+    xg = int(getattr(trainer, "world", 1)) > 1
+    k = (bytes(trainer.desc), int(trainer.mt),
+         tuple(getattr(opt, f) for f in _OPT_CONSTS) if opt is not None else (), xg)
     path = _paths.get(k)
     if path is None or not os.path.exists(path):
-        path = compile_source(generate_source(trainer.desc, trainer.mt, opt))
+        path = compile_source(generate_source(trainer.desc, trainer.mt, opt, xg=xg))
         _paths[k] = path
     return path
 

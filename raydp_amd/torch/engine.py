@@ -165,12 +165,17 @@ def stream_ingest(ds, cols, label_column, device, stride) -> dict:
     q, fut = ds._stream, ds._pending
     parts = {}
     while True:
+        # blocking get: the conversion thread ends the stream with None (no polling loop taking
+        # the GIL from the conversion's own Python)
         try:
-            i, ref = q.get(timeout=0.0005)
+            item = q.get(timeout=0.25)
         except queue.Empty:
-            if fut is None or (fut.done() and q.empty()):
+            if fut is None or fut.done():     # (a conversion that died before its sentinel)
                 break
             continue
+        if item is None:
+            break
+        i, ref = item
         t = _resolve(ref)
         parts[i] = (ref.id,) + _ingest_block(t, cols, label_column, device, stride)[1:]
     return parts
@@ -220,12 +225,14 @@ class FusedMLPEngine:
         (parameters, running statistics, hyper-parameters and moments are copied to the device
         once); results are exported from the device buffers and the objects are never written."""
         from raydp_amd.ops.fused_mlp import FusedMLPTrainer
+        from raydp_amd.utils import tracing
         self.model, self.metrics_names, self.device = model, metrics.names, device
         self.detached = detached
         self.loss = loss if loss is not None else config.get("loss")   # label encoding (fused_labels)
         self.world = session.get_world_size()
-        self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn,
-                                       acc_thr=acc_thr, world=session.get_world_size())
+        with tracing.span("fused trainer build", cat="train"):
+            self.trainer = FusedMLPTrainer(spec, oc, lc, config["batch_size"], device, lr_scheduler_fn,
+                                           acc_thr=acc_thr, world=session.get_world_size())
         from raydp_amd.utils.config import get as conf_get
         self.trainer.record_steps = bool(conf_get("spark.ray.mi355x.step_times"))
         self.last_step_times = None
@@ -235,7 +242,8 @@ class FusedMLPEngine:
         self.allreduce_kind = None
         self.max_steps = None
         if self.world > 1:
-            self._setup_collectives()
+            with tracing.span("collectives setup", cat="train", world=self.world):
+                self._setup_collectives()
         self.drop_last = bool(config.get("drop_last", False))
         self.shuffle = bool(config.get("shuffle", True))
         self.seed = _epoch_seed_base(config)
@@ -252,7 +260,9 @@ class FusedMLPEngine:
         import torch.distributed as dist
         from raydp_amd.ops.comm import NativeComm
         tr = self.trainer
-        self.xg = _xgmi_for(tr)
+        from raydp_amd.utils import tracing
+        with tracing.span("xgmi communicator", cat="train"):
+            self.xg = _xgmi_for(tr)
         if self.xg is not None:
             # gradients exchanged inside the training launches: the persistent epoch (batch <= 128)
             # and the multi-workgroup step's optimizer tasks send per-tile gradients

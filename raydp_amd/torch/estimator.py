@@ -35,6 +35,7 @@ from raydp_amd.train.trainer import TorchTrainer
 # wall-clock phase marks of the last fit in this process (bench / profiling); keys ending in
 # "_concurrent" ran beside the other phases and are not part of their sequential sum
 LAST_TIMINGS = {}
+STREAM_STATS = {}    # {"blocks": training blocks the last fit streamed into HBM during its conversion}
 _CONV_POOL = None
 
 
@@ -49,10 +50,12 @@ def _conversion_pool():
 class _Pick:
     """Future-like view of one element of another future's tuple result."""
 
-    def __init__(self, fut, i):
-        self.fut, self.i = fut, i
+    def __init__(self, fut, i, need=None):
+        self.fut, self.i, self.need = fut, i, need
 
     def result(self):
+        if self.need is not None:
+            self.need()     # whoever waits for the data releases a stage still held back
         return self.fut.result()[self.i]
 
     def done(self):
@@ -287,9 +290,11 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         if fused_mode == "off":
             return None
         from raydp_amd.torch.engine import FusedMLPEngine
+        from raydp_amd.utils import tracing
         metrics = config["metrics"].clone()
-        fused = FusedMLPEngine.applicable(model, opt, loss, metrics, device, config["batch_size"],
-                                          config["feature_columns"], config["feature_types"])
+        with tracing.span("fused applicable", cat="train"):
+            fused = FusedMLPEngine.applicable(model, opt, loss, metrics, device, config["batch_size"],
+                                              config["feature_columns"], config["feature_types"])
         if fused is None:
             return None
         spec, lc, oc, acc_thr = fused
@@ -316,7 +321,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                     # the blocks go to HBM as they land: only the last one's DMA is left after
                     with tracing.span("streamed ingest", cat="train"):
                         engine.stream_ingest(train_ds, config)
-                    LAST_TIMINGS["streamed_blocks"] = len(getattr(engine, "_streamed", None) or ())
+                    STREAM_STATS["blocks"] = len(getattr(engine, "_streamed", None) or ())
                 for ds in deferred:
                     ds.num_blocks()
             LAST_TIMINGS["conversion_wait"] = time.perf_counter() - t_wait0
@@ -449,8 +454,9 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         from raydp_amd.utils import tracing
         from raydp_amd.utils.config import get as conf_get
         t_conv0 = time.perf_counter()
-        for k in ("conversion_wait", "etl_and_conversion_concurrent", "streamed_blocks"):
+        for k in ("conversion_wait", "etl_and_conversion_concurrent"):
             LAST_TIMINGS.pop(k, None)
+        STREAM_STATS.clear()
         if fs_directory is None and not stop_spark_after_conversion \
                 and conf_get("spark.ray.mi355x.overlap_conversion"):
             # The Spark stage that materialises the blocks runs on the executors while this
@@ -473,7 +479,15 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                 import queue
                 stream = queue.Queue()
 
+            # N > 1 (spawned workers): the fit payload goes out FIRST and the stage after it; the
+            # workers unpickle it and build their engines while the stage runs (their shards
+            # follow when it is done), instead of starting only once the stage is dispatched
+            early = self._num_workers > 1
+            sent = threading.Event()
+
             def convert():
+                if early:
+                    sent.wait(30.0)     # (set by the trainer on every path; 30 s is a backstop)
                 t0 = time.perf_counter()
                 spark_cluster.set_dispatch_hook(in_flight.set)
                 try:
@@ -491,16 +505,23 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
                 # the short switch interval is only for the overlap: back to normal the moment
                 # the conversion is done, not after the whole training run
                 fut.add_done_callback(lambda _f: sys.setswitchinterval(switch))
-                train_ds = Dataset.deferred(_Pick(fut, 0))
+                train_ds = Dataset.deferred(_Pick(fut, 0, sent.set))
                 train_ds._stream = stream
-                evaluate_ds = Dataset.deferred(_Pick(fut, 1)) if evaluate_df is not None else None
-                in_flight.wait()
+                evaluate_ds = Dataset.deferred(_Pick(fut, 1, sent.set)) if evaluate_df is not None else None
+                if not early:
+                    in_flight.wait()
                 LAST_TIMINGS["etl_and_conversion"] = time.perf_counter() - t_conv0
+                from raydp_amd.train import trainer as _tr
+                if early:
+                    _tr.set_started_hook(sent.set)
                 try:
                     return self.fit(train_ds, evaluate_ds, max_retries)
                 except DeferredDatasetError as e:
                     raise e.original from None
                 finally:
+                    if early:
+                        _tr.set_started_hook(None)
+                        sent.set()     # (a fit that failed before its workers started)
                     cf_wait([fut])     # never leave a stage running behind a failed fit
             finally:
                 sys.setswitchinterval(switch)
@@ -535,6 +556,7 @@ class TorchEstimator(EstimatorInterface, SparkEstimatorInterface):
         finally:
             if stream is not None:
                 spark_cluster.set_block_hook(None)
+                stream.put(None)        # end of the training blocks (the consumer blocks on get)
         evaluate_ds = None
         if evaluate_df is not None:
             evaluate_df = self._check_and_convert(evaluate_df)

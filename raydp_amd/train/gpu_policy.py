@@ -104,6 +104,15 @@ def graph_model(module):
 
     def _capture(args):
         bufs = [(b, b.detach().clone()) for b in module.buffers()]
+        # the worker's native-BatchNorm policy (cudnn switched off around each BatchNorm call)
+        # is lifted while the graph is captured: a capture of that path's backward crashed at
+        # capture end on the GPU box (scripts/dev/hvd_graph_repro.py); the replay then runs the
+        # default BatchNorm kernels, which is what a replay's launch cost no longer cares about
+        from torch.nn.modules.batchnorm import _BatchNorm
+        patched = _BatchNorm.forward
+        plain = getattr(patched, "__wrapped__", None)
+        if plain is not None:
+            _BatchNorm.forward = plain
         try:
             fwd = _Fwd()
             samples = tuple(a.detach().clone() for a in args)
@@ -114,6 +123,8 @@ def graph_model(module):
             state["failed"] = True
             return None
         finally:
+            if plain is not None:
+                _BatchNorm.forward = patched
             with torch.no_grad():       # the warm-up's BatchNorm statistics are not training steps
                 for b, v in bufs:
                     b.copy_(v)

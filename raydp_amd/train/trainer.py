@@ -73,6 +73,44 @@ def _cuda_available() -> bool:
         return False
 
 
+import threading as _threading
+
+_launch_hooks = _threading.local()
+
+
+def set_started_hook(fn) -> None:
+    """``fn()`` once (this thread's next ``fit``) when a warm spawned group with deferred datasets
+    has sent every rank its fit -- or right away on any other path (cold group start, eager
+    shards, in-process run), which needs the data first. ``fit_on_spark`` at N > 1 starts its
+    conversion stage then, so the workers' payload unpickle and engine build run beside the
+    stage instead of after its dispatch."""
+    _launch_hooks.on_started = fn
+
+
+def _fire_started() -> None:
+    fn = getattr(_launch_hooks, "on_started", None)
+    _launch_hooks.on_started = None
+    if fn is not None:
+        fn()
+
+
+def _shard_payloads(datasets: Dict[str, Any], world: int) -> List[bytes]:
+    """Every rank's pickled ``{name: shard}``: each dataset split ONCE (equal shards are block
+    slices, a few ids each), plain pickle first (a shard holds importable classes only; cloudpickle
+    costs ~4x more per call), cloudpickle for anything else."""
+    import pickle
+    import cloudpickle
+    splits = {k: ds.split(world, equal=True) for k, ds in (datasets or {}).items()}
+    out = []
+    for r in range(world):
+        d = {k: sp[r] for k, sp in splits.items()}
+        try:
+            out.append(pickle.dumps(d, protocol=5))
+        except Exception:  # noqa: BLE001 - a dataset of user objects: cloudpickle handles closures
+            out.append(cloudpickle.dumps(d))
+    return out
+
+
 def _shard(datasets: Dict[str, Any], rank: int, world: int) -> Dict[str, Any]:
     if not datasets:
         return {}
@@ -250,6 +288,7 @@ class DataParallelTrainer:
         from raydp_amd.utils.config import get as conf_get
         inproc_one = world == 1 and bool(conf_get("spark.ray.mi355x.train_inprocess"))
         if inproc_one or (env_world == world and "RANK" in os.environ and world > 1):
+            _fire_started()
             self._run_inprocess(world, env_world, use_gpu, storage, reporter)
         else:
             self._run_spawned(world, use_gpu, storage, reporter)
@@ -328,6 +367,8 @@ class DataParallelTrainer:
         key = (world, use_gpu, cpus, gpus, tuple(sorted(res.items())), strategy, backend, tmo,
                tuple(sorted(wenv.items())) if wenv else (), renv)
         group = _GROUPS.take(key)
+        if group is None or not self._deferred_datasets(world):
+            _fire_started()     # a cold start (seconds) or eager shards: the conversion goes first
         if group is None:
             from raydp_amd.runtime.node import ResourceError
             try:
@@ -363,9 +404,10 @@ class DataParallelTrainer:
                 names = list(self.datasets)
                 for w in workers:
                     refs.append(w.run.remote(common, None, chan, names))
+                _fire_started()     # every rank has its fit: the caller may start the conversion now
                 try:
                     with tracing.span("shard split", cat="train", world=world):
-                        payloads = [cloudpickle.dumps(_shard(self.datasets, r, world)) for r in range(world)]
+                        payloads = _shard_payloads(self.datasets, world)
                     for r, w in enumerate(workers):
                         w.deliver_shards.remote(chan, payloads[r])
                 except Exception as e:  # noqa: BLE001 - the conversion failed: stop every rank

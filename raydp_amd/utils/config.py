@@ -232,6 +232,12 @@ register("spark.ray.mi355x.graph_user_model", "bool", True,
          "backward as HIP graphs per repeated batch shape (raydp_amd/train/gpu_policy.py graph_model); "
          "eager for eval, other shapes and models that cannot be captured", env="RAYDP_GRAPH_USER_MODEL")
 
+register("spark.ray.mi355x.graph_hvd_model", "bool", False,
+         "hvd.DistributedOptimizer(named_parameters=model.named_parameters()) also applies the "
+         "graph_user_model policy to that module (raydp_amd/hvd/__init__.py _graph_user_module); off by "
+         "default: a capture inside the Horovod NYC loop under the worker's native-BatchNorm policy "
+         "crashed the process on the GPU box (round 6)", env="RAYDP_GRAPH_HVD_MODEL")
+
 register("spark.ray.mi355x.stream_ingest", "bool", True,
          "fit_on_spark with one in-process worker: the fused engine DMAs each training block into HBM as "
          "its conversion task lands, while the rest of the stage runs (raydp_amd/torch/engine.py "

@@ -115,15 +115,16 @@ def test_streamed_ingest_trains_like_ingest_after_conversion(spark_on_ray_2_exec
     ingested afterwards (blocks assembled in partition order)."""
     import pandas as pd
     from raydp_amd.torch import TorchEstimator
-    from raydp_amd.torch.estimator import LAST_TIMINGS
+    from raydp_amd.torch.estimator import LAST_TIMINGS, STREAM_STATS
     rng = np.random.default_rng(1)
     x = rng.standard_normal((64 * 40, 20)).astype(np.float32)
     pdf = pd.DataFrame({f"f{i}": x[:, i] for i in range(20)})
     pdf["y"] = x[:, :4].sum(1) * 0.5 + 1.0
-    df = spark_on_ray_2_executors.createDataFrame(pdf).repartition(8)
     states = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("RAYDP_STREAM_INGEST", mode)
+        # a fresh DataFrame per fit (an already persisted one is handed out without a stage)
+        df = spark_on_ray_2_executors.createDataFrame(pdf).repartition(8)
         model = _model()
         est = TorchEstimator(num_workers=1, model=model, optimizer=torch.optim.Adam(model.parameters(), lr=1e-3),
                              loss=nn.MSELoss(), feature_columns=[f"f{i}" for i in range(20)], label_column="y",
@@ -132,6 +133,6 @@ def test_streamed_ingest_trains_like_ingest_after_conversion(spark_on_ray_2_exec
         est.fit_on_spark(df)
         states[mode] = {k: v.detach().cpu().clone() for k, v in est.get_model().state_dict().items()}
         assert "ingest" in LAST_TIMINGS
-        assert (LAST_TIMINGS.get("streamed_blocks", 0) > 0) == (mode == "1"), dict(LAST_TIMINGS)
+        assert (STREAM_STATS.get("blocks", 0) > 0) == (mode == "1"), dict(STREAM_STATS)
     for k in states["0"]:
         assert torch.equal(states["0"][k], states["1"][k]), k
