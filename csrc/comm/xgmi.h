@@ -12,7 +12,7 @@
 // Memory: each rank owns one exchange region allocated uncached (hipDeviceMallocUncached, so
 // no L2 on either side holds a stale line) and exports it with hipIpcGetMemHandle:
 //   [slot 0: nf floats][slot 1: nf floats][flags: RX_XG_MAXR u32][votes: 2 x RX_XG_MAXR u32]
-//   [tile flags: RX_XG_MAXT x RX_XG_MAXR u32]
+//   [inbox: 2 x world x nf tagged u64 granules (rx_xg_push)]
 // Step s writes its gradient into slot (s & 1) of its own region, then publishes seq = s + base
 // by storing it into flags[rank] of EVERY peer's region, waits until its own flags[p] >= seq for
 // every peer p, and reads slot (s & 1) of every region.
@@ -35,8 +35,6 @@
 #include <hip/hip_runtime.h>
 
 #define RX_XG_MAXR 16
-// per-tile flags of the in-kernel gradient exchange (rx_xg_tile_*): tile ids per region
-#define RX_XG_MAXT 1024
 
 // ctl words (this rank's local device memory, zeroed at create)
 enum : int { kXgErr = 0, kXgDevSeq = 1, kXgArrive = 2, kXgGo = 3, kXgDone = 4, kXgCtlWords = 16 };
@@ -47,8 +45,13 @@ struct XgDev {
   unsigned* ctl;              // local control words (kXg*)
   unsigned long long spin_ticks;
   int world, rank, nf;        // nf: floats per slot (multiple of 64)
-  int pad_;
+  unsigned layout;            // RX_XG_LAYOUT of the code that allocated the regions
 };
+
+// Region layout version. Training kernels compiled at run time (raydp_amd/ops/mlp_jit.py) index
+// the regions a prebuilt library allocated: a kernel whose layout differs exchanges nothing
+// (rx_xg_usable: error word set, no update) instead of writing past a region.
+#define RX_XG_LAYOUT 0x58470002u
 
 __device__ __forceinline__ unsigned* rx_xg_flags(const XgDev& x, int p) {
   return reinterpret_cast<unsigned*>(x.region[p] + 2 * (size_t)x.nf);
@@ -143,17 +146,13 @@ __device__ __forceinline__ float rx_xg_sum(const XgDev& x, int par, int idx) {
   return s;
 }
 
-// ---- per-tile exchange inside a training launch (persistent epoch / multi-workgroup step) ----
+// ---- gradient exchange inside a training launch (persistent epoch / multi-workgroup step) ----
 // The gradient all-reduce of the fused NYC engine at world > 1 without a launch, a pass or a
-// rendezvous of its own: the workgroup that finishes a 32x32 weight tile's gradient (or a chunk
-// of the bias / BatchNorm gradients) stores it into its rank's slot at the flat gradient offsets
-// (system-scope write-through stores), drains them, publishes tile id t at the step's sequence
-// number into every peer's tile-flag row, waits until every peer published t, and sums the world
-// values of each of its elements in rank order (bit-identical on every rank) before it updates.
-// 4 KB per tile crosses each link -- the 194 KB NYC gradient per step in all -- instead of the
-// batch-sized X^T / G^T exports (7.8 MB at batch 4096). Slot reuse: a rank rewrites tile t of
-// slot (seq & 1) two steps later, after it saw every peer's flag t of the step between, which each
-// peer publishes after its reads of this step's tile t (same workgroup, program order).
+// rendezvous of its own: the lanes that finish a 32x32 weight tile's gradient (or a chunk of the
+// bias / BatchNorm gradients) push it into every peer's inbox and sum the world values of each of
+// their elements in rank order (bit-identical on every rank) before they update (rx_xg_push /
+// rx_xg_pull_sum_n below). The NYC gradient crosses each link once per step as tagged granules
+// (388 KB) instead of the batch-sized X^T / G^T exports (7.8 MB at batch 4096).
 struct XgStep {
   const XgDev* xd;  // the communicator's descriptor in DEVICE memory (rx_xg_devptr): read with scalar
                     // loads, so a kernel argument holding this stays small and register-resident
@@ -173,62 +172,103 @@ __device__ __forceinline__ float* rx_xg_region(const XgDev& x, int p) { return x
 #endif
 __device__ __forceinline__ bool rx_xg_active(const XgStep& xs) { return RX_XG_KERNELS && xs.on; }
 
-__device__ __forceinline__ unsigned* rx_xg_tflags_of(float* region, const XgDev& x) {
-  return reinterpret_cast<unsigned*>(region + 2 * (size_t)x.nf) + 3 * RX_XG_MAXR;
+// (after rx_xg_active) false -- and the error word set -- when the communicator's regions were laid
+// out by other code than this kernel's
+__device__ __forceinline__ bool rx_xg_usable(const XgDev& x) {
+  if (x.layout == RX_XG_LAYOUT) return true;
+  __hip_atomic_store(x.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return false;
 }
 
-__device__ __forceinline__ float* rx_xg_slotp(const XgDev& x, int p, unsigned seq) {
-  return rx_xg_region(x, p) + (size_t)(seq & 1u) * x.nf;
-}
-
-// write-through (sc0 sc1) store into this rank's slot, and the matching peer load: global_
-// instructions (address space 1), never flat_
-typedef __attribute__((address_space(1))) float rx_xg_gf;
 typedef __attribute__((address_space(1))) unsigned rx_xg_gu;
-__device__ __forceinline__ void rx_xg_put(float* p, float v) {
-  __hip_atomic_store((rx_xg_gf*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ float rx_xg_get(const float* p) {
-  return __hip_atomic_load((rx_xg_gf*)const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+
+// ---- tagged push exchange (the persistent epoch at world > 1) ----
+// Latency, not bytes, bounds the per-step exchange of a small model: the flag protocol above is
+// a drain (vmcnt 0) of the slot stores, a flag store, the peer's poll of it and then its read of
+// the data -- two one-way trips plus a round trip before the peer can sum. Here every element
+// travels ONCE, as an 8-B granule (value bits | seq << 32) stored straight into the receiving
+// rank's inbox row for this sender; the receiver polls its own (local) inbox until the tag is the
+// step's seq (MI355X_MICROARCH.md R2: poll the data itself, never a flag beside it). A 64-bit
+// store is single-copy atomic, so a granule whose tag matches carries that step's value. Inbox
+// reuse: parity (seq & 1) rows; a sender overwrites row (seq & 1) two steps later, after its own
+// step seq + 1 summed the receiver's seq + 1 values, which the receiver pushed after it read
+// this step's (program order on the receiving lane).
+__device__ __forceinline__ unsigned long long* rx_xg_inbox(const XgDev& x, int at, int src, unsigned seq) {
+  unsigned* tail = rx_xg_flags(x, at) + 3 * RX_XG_MAXR;   // 8-B aligned: nf % 64 == 0
+  return reinterpret_cast<unsigned long long*>(tail) + ((size_t)(seq & 1u) * x.world + src) * x.nf;
 }
 
-// One lane, after every storing wave of its workgroup drained its rx_xg_put stores and joined a
-// barrier: tile t of sequence seq is in this rank's slot.
-__device__ __forceinline__ void rx_xg_tile_publish(const XgDev& x, int t, unsigned seq) {
+typedef __attribute__((address_space(1))) unsigned long long rx_xg_gq;
+
+// This rank's value of flat element idx at sequence seq, into every peer's inbox.
+__device__ __forceinline__ void rx_xg_push(const XgDev& x, unsigned seq, int idx, float v) {
+  if (x.layout != RX_XG_LAYOUT) return;
+  const unsigned long long g = ((unsigned long long)seq << 32) | __float_as_uint(v);
   for (int p = 0; p < x.world; ++p)
     if (p != x.rank)
-      __hip_atomic_store((rx_xg_gu*)(rx_xg_tflags_of(x.region[p], x) + t * RX_XG_MAXR + x.rank), seq,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store((rx_xg_gq*)(rx_xg_inbox(x, p, x.rank, seq) + idx), g, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One lane (or a whole wave: every lane polls the same words): wait until every peer published
-// tile t of sequence seq. False on timeout (error word set) or when the error word was already set.
-__device__ __forceinline__ bool rx_xg_tile_wait(const XgDev& x, int t, unsigned seq) {
-  const unsigned* mine = rx_xg_tflags_of(rx_xg_region(x, x.rank), x) + t * RX_XG_MAXR;
-  const unsigned long long t0 = wall_clock64();
-  for (int p = 0; p < x.world; ++p) {
-    if (p == x.rank) continue;
-    int k = 0;
-    while ((int)(__hip_atomic_load((rx_xg_gu*)const_cast<unsigned*>(mine + p), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
-      if ((++k & 15) == 0) {
-        if (__hip_atomic_load((rx_xg_gu*)x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return false;
-        if ((unsigned long long)(wall_clock64() - t0) > x.spin_ticks) {
-          rx_xg_fail(x);
-          return false;
+// N elements at once: val[n] (this rank's value on entry) becomes the rank-order sum of element
+// idx[n] (for valid[n]). The loads for up to 4 peers x N elements are issued back to back before
+// any tag is checked, so a lane pays one round trip per 4 peers, not one per element and peer.
+template <int N>
+__device__ __forceinline__ void rx_xg_pull_sum_n(const XgDev& x, unsigned seq, const int (&idx)[N],
+                                                 const bool (&valid)[N], float (&val)[N], bool& ok) {
+  if (!rx_xg_usable(x)) {
+    ok = false;
+    return;
+  }
+  float s[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) s[n] = 0.f;
+  const int world = x.world, rank = x.rank;
+  for (int p0 = 0; p0 < world; p0 += 4) {
+    unsigned long long g[4][N];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = p0 + q;
+      const bool peer = p < world && p != rank;
+      const rx_xg_gq* row = peer ? (const rx_xg_gq*)rx_xg_inbox(x, rank, p, seq) : nullptr;
+#pragma unroll
+      for (int n = 0; n < N; ++n)
+        g[q][n] = (peer && valid[n]) ? __hip_atomic_load(row + idx[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = p0 + q;
+      if (p >= world) break;
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        if (!valid[n]) continue;
+        if (p == rank) {
+          s[n] += val[n];
+          continue;
         }
+        unsigned long long gv = g[q][n];
+        if ((unsigned)(gv >> 32) != seq && ok) {
+          const rx_xg_gq* a = (const rx_xg_gq*)(rx_xg_inbox(x, rank, p, seq) + idx[n]);
+          const unsigned long long t0 = wall_clock64();
+          int k = 0;
+          do {
+            __builtin_amdgcn_s_sleep(1);
+            gv = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((++k & 15) == 0 && (unsigned)(gv >> 32) != seq) {
+              if (__hip_atomic_load((rx_xg_gu*)x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
+                  (unsigned long long)(wall_clock64() - t0) > x.spin_ticks) {
+                rx_xg_fail(x);
+                ok = false;
+                break;
+              }
+            }
+          } while ((unsigned)(gv >> 32) != seq);
+        }
+        s[n] += __uint_as_float((unsigned)gv);
       }
-      __builtin_amdgcn_s_sleep(1);
     }
   }
-  return true;
-}
-
-// Sum over ranks (rank order) of flat element idx of sequence seq's slots; this rank's own value is
-// `mine` (the bits it stored).
-__device__ __forceinline__ float rx_xg_tile_sum(const XgDev& x, unsigned seq, int idx, float mine) {
-  float s = 0.f;
-  const size_t off = (size_t)(seq & 1u) * x.nf + idx;
-  for (int p = 0; p < x.world; ++p) s += p == x.rank ? mine : rx_xg_get(x.region[p] + off);
-  return s;
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+    if (valid[n]) val[n] = s[n];
 }

@@ -296,7 +296,8 @@ void* rx_xg_create(int world, int rank, int device, int n, double timeout_s) {
   XgHost* h = new XgHost();
   h->device = device;
   const int nf = (n + 63) & ~63;
-  h->bytes = (2 * (size_t)nf + 3 * RX_XG_MAXR + (size_t)RX_XG_MAXT * RX_XG_MAXR) * sizeof(float);
+  h->bytes = (2 * (size_t)nf + 3 * RX_XG_MAXR) * sizeof(float) +
+             2 * (size_t)world * nf * sizeof(unsigned long long);   // tagged inbox (rx_xg_push)
   if (hipExtMallocWithFlags(&h->base, h->bytes, hipDeviceMallocUncached) != hipSuccess) {
     delete h;
     return nullptr;
@@ -317,6 +318,7 @@ void* rx_xg_create(int world, int rank, int device, int n, double timeout_s) {
   h->dev.world = world;
   h->dev.rank = rank;
   h->dev.nf = nf;
+  h->dev.layout = RX_XG_LAYOUT;
   h->dev.ctl = ctl;
   h->dev.err = ctl + kXgErr;
   h->dev.spin_ticks = (unsigned long long)(timeout_s * khz * 1000.0);

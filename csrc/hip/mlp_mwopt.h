@@ -175,43 +175,45 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
     for (int r = 0; r < 4; ++r) gtile[(ms * 16 + lc) * 33 + ns * 16 + lg * 4 + r] = t4[r];
   }
   __syncthreads();
-  bool xlast = last;
-  if (rx_xg_active(a.xs)) {
-    // world > 1: this rank's tile into its slot, the tile flag, every peer's flag (all threads of
-    // the workgroup run the barriers; only a last arriver's half stores / publishes / waits)
-    const XgDev& x = *a.xs.xd;
-    float* mine = rx_xg_slotp(x, x.rank, a.xs.seq);
-    if (last) {
+  const bool xlast = last;
+  if (last && rx_xg_active(a.xs)) {
+    // world > 1: this rank's tile pushed into every peer's inbox (tagged granules), before any
+    // of this lane's polls for theirs
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int oo = o0 + to + r * 8, ii = i0 + ti;
-        if (oo < sg.out && ii < sg.in) rx_xg_put(mine + sg.start + oo * sg.in + ii, gtile[(to + r * 8) * 33 + ti]);
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int oo = o0 + to + r * 8, ii = i0 + ti;
+      if (oo < sg.out && ii < sg.in)
+        rx_xg_push(*a.xs.xd, a.xs.seq, sg.start + oo * sg.in + ii, gtile[(to + r * 8) * 33 + ti]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0 && last) {
-      rx_xg_tile_publish(x, tile, a.xs.seq);
-      if (!rx_xg_tile_wait(x, tile, a.xs.seq)) *last_lds = 0;   // a peer never came: no update
-    }
-    __syncthreads();
-    xlast = *last_lds != 0;
   }
   if (xlast) {
     const float gsc = rx_xg_active(a.xs) ? a.xs.gscale : 1.f;
+    bool okx = true;   // (a peer that never came: the error word is set, this element keeps its weight)
+    float gs[4];
+    int gi[4];
+    bool gv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int oo = o0 + to + r * 8, ii = i0 + ti;
+      gv[r] = oo < sg.out && ii < sg.in;
+      gi[r] = gv[r] ? sg.start + oo * sg.in + ii : sg.start;
+      gs[r] = gtile[(to + r * 8) * 33 + ti];
+    }
+    if (rx_xg_active(a.xs)) rx_xg_pull_sum_n<4>(*a.xs.xd, a.xs.seq, gi, gv, gs, okx);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int oo = o0 + to + r * 8, ii = i0 + ti;
       u16 h = 0;
       if (oo < sg.out && ii < sg.in) {
-        const int idx = sg.start + oo * sg.in + ii;
+        const int idx = gi[r];
         float pv = pp[r], mv = pm[r], vv = pvv[r];   // opt_update with the loads hoisted
-        const float gl = gtile[(to + r * 8) * 33 + ti];
-        const float gw = rx_xg_active(a.xs) ? rx_xg_tile_sum(*a.xs.xd, a.xs.seq, idx, gl) : gl;
-        opt_update_reg(o, pv, mv, vv, gw, a.lr, a.bc1, a.bc2, gsc, a.first);
-        a.m[idx] = mv;
-        if (o.algo != 2) a.v[idx] = vv;
-        a.p[idx] = pv;
+        const float gw = gs[r];
+        if (okx) {
+          opt_update_reg(o, pv, mv, vv, gw, a.lr, a.bc1, a.bc2, gsc, a.first);
+          a.m[idx] = mv;
+          if (o.algo != 2) a.v[idx] = vv;
+          a.p[idx] = pv;
+        }
         h = rx_f2bf(pv);
         rx_g(sg.W)[oo * sg.in_k + ii] = h;
       }
@@ -230,11 +232,10 @@ __device__ __forceinline__ void mw_tile_task(const MwOptArgs& a, int s, int tile
 
 // Vector parameters: chunk `c` (CH elements) of the element-wise segments on NT threads (`t`).
 // sc1: the gradients were stored in this launch (fused role). World > 1 (a.xs.on): the chunk is
-// exchanged as tile mw_weight_tiles + c (every thread of the workgroup calls it: barriers).
+// pushed to the peers and summed over the ranks element by element (rx_xg_push / rx_xg_pull_sum_n).
 template <int CH, int NT>
 __device__ __forceinline__ void mw_vector_chunk(const MwOptArgs& a, int c, int t, bool sc1) {
   const OptDesc& o = *a.od;
-  const int c0 = c;
   for (int s = 0; s < o.nseg; ++s) {
     const OptSeg& sg = o.seg[s];
     if (sg.kind == 1) continue;
@@ -247,9 +248,10 @@ __device__ __forceinline__ void mw_vector_chunk(const MwOptArgs& a, int c, int t
         }
         return;
       }
+      // world > 1: the chunk's gradients pushed into every peer's inbox, then each summed over
+      // the ranks from this lane's own inbox
       constexpr int J = CH / NT;
       const XgDev& x = *a.xs.xd;
-      float* mine = rx_xg_slotp(x, x.rank, a.xs.seq);
       float gl[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) {
@@ -258,27 +260,23 @@ __device__ __forceinline__ void mw_vector_chunk(const MwOptArgs& a, int c, int t
         if (q < sg.len) {
           const int idx = sg.start + q;
           gl[j] = sc1 ? rx_ld_sc1f(a.g + idx) : a.g[idx];
-          rx_xg_put(mine + idx, gl[j]);
+          rx_xg_push(x, a.xs.seq, idx, gl[j]);
         }
       }
-      __shared__ int xok;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t == 0) {
-        const int tid = mw_weight_tiles(o) + c0;
-        rx_xg_tile_publish(x, tid, a.xs.seq);
-        xok = rx_xg_tile_wait(x, tid, a.xs.seq) ? 1 : 0;
-      }
-      __syncthreads();
-      if (!xok) return;
+      bool okx = true;
+      int gi[J];
+      bool gv[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const int q = c * CH + t + j * NT;
-        if (q < sg.len) {
-          const int idx = sg.start + q;
-          opt_update(o, idx, a.p, rx_xg_tile_sum(x, a.xs.seq, idx, gl[j]), a.m, a.v, a.lr, a.bc1, a.bc2,
-                     a.xs.gscale, a.first);
-        }
+        gv[j] = q < sg.len;
+        gi[j] = gv[j] ? sg.start + q : sg.start;
+      }
+      rx_xg_pull_sum_n<J>(x, a.xs.seq, gi, gv, gl, okx);
+      if (okx) {
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (gv[j]) opt_update(o, gi[j], a.p, gl[j], a.m, a.v, a.lr, a.bc1, a.bc2, a.xs.gscale, a.first);
       }
       return;
     }

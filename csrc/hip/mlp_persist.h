@@ -29,11 +29,12 @@
 //
 // World > 1 (XgStep::on, one persistent launch per rank and epoch): the data-parallel gradient
 // all-reduce happens inside the same launch. Each optimizer workgroup, once its dW tiles of a step
-// are computed, exchanges them with the peers' workgroups of the same tiles (csrc/comm/xgmi.h:
-// write-through store into this rank's slot, tile flag, wait, rank-order sum) and updates with the
-// rank sum x 1 / world; the step workgroup publishes the step's bias / BatchNorm gradients as one
-// more tile after its backward, and the next step's vector update (waves 1..7, beside wave 0's
-// counter poll) sums them over the ranks. Layer 0 then goes to optimizer workgroups (the host keeps
+// are computed, exchanges them with the peers' workgroups of the same tiles (csrc/comm/xgmi.h
+// rx_xg_push / rx_xg_pull_sum_n: each element goes once, as a tagged 8-B granule, into every peer's
+// inbox; each lane polls its own inbox and sums in rank order) and updates with the rank sum x
+// 1 / world; the step workgroup pushes the step's bias / BatchNorm gradients after its backward,
+// and the next step's vector update (waves 1..7, beside wave 0's counter poll) sums them over the
+// ranks. Layer 0 then goes to optimizer workgroups (the host keeps
 // ps_l0_inline off) and the vector updates leave the epilogues (they need every rank's gradient).
 //
 // Reference role: the per-batch train loop of TorchEstimator (python/raydp/torch/estimator.py:
@@ -103,8 +104,8 @@ __host__ __device__ __forceinline__ int ps_grid_blocks(const OptDesc& o) {
 // would leave the first 16 threads with 15 updates each: the update is VALU bound) -- and every
 // gradient / moment load of a thread's elements is issued before its first update.
 #define RX_PS_VEC_T0 64
-// World > 1 (xs.on): the gradients are the rank sums of the step `seq` published (each wave polls
-// the vector tile's flags itself before its loads), times 1 / world.
+// World > 1 (xs.on): the gradients are the rank sums of step `seq` (each element polled from this
+// rank's inbox, rx_xg_pull_sum_n), times 1 / world.
 template <class C, class D>
 __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, char* smem, const float* __restrict__ Gr,
                                                  float* __restrict__ m, float* __restrict__ v, float lr, float bc1,
@@ -119,16 +120,8 @@ __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, c
   });
   const int tid = rx_tid() - RX_PS_VEC_T0;
   if (tid < 0) return;
-  float gsc = 1.f;
-  if (rx_xg_active(xs)) {
-    int ok = 1;
-    if ((rx_tid() & 63) == 0) {
-      ok = rx_xg_tile_wait(*xs.xd, mw_weight_tiles(o), seq) ? 1 : 0;
-      if (!ok) __hip_atomic_store(rx_g(sync) + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!__builtin_amdgcn_readfirstlane(ok)) return;
-    gsc = xs.gscale;
-  }
+  const float gsc = rx_xg_active(xs) ? xs.gscale : 1.f;
+  bool xok = true;
   for (int e0 = 0; e0 < total; e0 += J * NW) {
     int idx[J], slot[J];
     float g[J], mv[J], vv[J];
@@ -154,9 +147,14 @@ __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, c
       slot[j] = sl;
       const int q = id >= 0 ? id : 0;
       g[j] = rx_g(Gr)[q];
-      if (rx_xg_active(xs)) g[j] = rx_xg_tile_sum(*xs.xd, seq, q, g[j]);
       mv[j] = rx_g(m)[q];
       vv[j] = rx_g(v)[q];
+    }
+    if (rx_xg_active(xs)) {
+      bool val[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) val[j] = idx[j] >= 0;
+      rx_xg_pull_sum_n<J>(*xs.xd, seq, idx, val, g, xok);
     }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -169,6 +167,7 @@ __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, c
       }
     }
   }
+  if (!xok) __hip_atomic_store(rx_g(sync) + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <class C, class D>
@@ -610,17 +609,34 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       if (rx_tid() == 0)
         __hip_atomic_store(rx_g(sync) + RX_PS_FLAG(0), (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (rx_xg_active(xs)) {
-        // world > 1: the step's bias / BatchNorm gradients (this workgroup's own Gr stores) into
-        // this rank's slot, published as one tile; the peers' arrive with the next step's wait
-        float* mine = rx_xg_slotp(*xs.xd, xs.xd->rank, xs.seq + (unsigned)s);
-        for (int q = 0; q < o.nseg; ++q) {
-          const OptSeg& sg = o.seg[q];
-          if (sg.kind == 1) continue;
-          for (int e = rx_tid(); e < sg.len; e += RX_THREADS) rx_xg_put(mine + sg.start + e, rx_g(Gr)[sg.start + e]);
+        // world > 1: the step's bias / BatchNorm gradients (this workgroup's own Gr stores, drained
+        // above) pushed into every peer's inbox; the peers' are summed by the next step's vector
+        // update
+        // (up to 4 elements per thread: their loads in flight together, then the pushes)
+        int nvec = 0;
+        for (int q = 0; q < o.nseg; ++q)
+          if (o.seg[q].kind != 1) nvec += o.seg[q].len;
+        for (int e0 = 0; e0 < nvec; e0 += 4 * RX_THREADS) {
+          int gi[4];
+          float gv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            int e = e0 + j * RX_THREADS + rx_tid();
+            gi[j] = -1;
+            for (int q = 0; q < o.nseg && gi[j] < 0 && e < nvec; ++q) {
+              const OptSeg& sg = o.seg[q];
+              if (sg.kind == 1) continue;
+              if (e < sg.len)
+                gi[j] = sg.start + e;
+              else
+                e -= sg.len;
+            }
+            gv[j] = gi[j] >= 0 ? rx_g(Gr)[gi[j]] : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (gi[j] >= 0) rx_xg_push(*xs.xd, xs.seq + (unsigned)s, gi[j], gv[j]);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (rx_tid() == 0) rx_xg_tile_publish(*xs.xd, mw_weight_tiles(o), xs.seq + (unsigned)s);
       }
     } else {
       __syncthreads();   // every read of this step's LDS images is done before the next batch lands
@@ -678,7 +694,7 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, 
                                           unsigned long long ticks, char* smem, int* flag_lds,
                                           unsigned long long* __restrict__ stamps, const XgStep& xs) {
   const int bw = b;
-  int seg = -1, l = 0, tile0 = 0;   // tile0: exchange id of the segment's first tile
+  int seg = -1, l = 0;
   for (int q = 0; q < o.nseg; ++q) {
     if (o.seg[q].kind != 1) continue;
     const int nbk = ps_seg_workers(o, q, l);
@@ -687,7 +703,6 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, 
       break;
     }
     b -= nbk;
-    tile0 += opt_seg_blocks(o.seg[q]);
     ++l;
   }
   if (seg < 0) return;
@@ -753,32 +768,24 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, 
     }
     float gsc = 1.f;
     if (rx_xg_active(xs)) {
-      // world > 1: both halves' tiles into this rank's slot, published; every peer's tiles waited
-      // for; the rank sums (rank order) replace the local gradient
+      // world > 1: each lane pushes its 4 gradient elements into every peer's inbox and sums the
+      // peers' (rank order, polled from its own inbox) in place of the local gradient
       const unsigned seq = xs.seq + (unsigned)s;
-      float* mine = rx_xg_slotp(*xs.xd, xs.xd->rank, seq);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (ok[r]) rx_xg_put(mine + idx[r], gw[r]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (rx_tid() == 0) {
-        const int nt = opt_seg_blocks(sg);
-        const int ta = 2 * b, tb = 2 * b + 1;
-        if (ta < nt) rx_xg_tile_publish(*xs.xd, tile0 + ta, seq);
-        if (tb < nt) rx_xg_tile_publish(*xs.xd, tile0 + tb, seq);
-        bool okx = ta >= nt || rx_xg_tile_wait(*xs.xd, tile0 + ta, seq);
-        okx = okx && (tb >= nt || rx_xg_tile_wait(*xs.xd, tile0 + tb, seq));
-        if (!okx) {
-          __hip_atomic_store(rx_g(sync) + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          flag_lds[0] = 1;
-        }
+        if (ok[r]) rx_xg_push(*xs.xd, seq, idx[r], gw[r]);
+      if (st && l == 0) rx_g(stamps)[29] = wall_clock64();   // layer 0: pushes issued
+      bool okx = true;
+      float gv[4] = {gw[0], gw[1], gw[2], gw[3]};
+      rx_xg_pull_sum_n<4>(*xs.xd, seq, idx, ok, gv, okx);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gw[r] = gv[r];
+      if (st && l == 0) rx_g(stamps)[31] = wall_clock64();   // lane 0's peer values summed
+      if (__syncthreads_or(okx ? 0 : 1)) {
+        if (rx_tid() == 0) __hip_atomic_store(rx_g(sync) + RX_PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
       }
-      __syncthreads();
-      if (flag_lds[0]) break;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (ok[r]) gw[r] = rx_xg_tile_sum(*xs.xd, seq, idx[r], gw[r]);
+      if (st && l == 0) rx_g(stamps)[30] = wall_clock64();   // the workgroup's sums done
       gsc = xs.gscale;
     }
     const int first = (opt_first && s == 0) ? 1 : 0;

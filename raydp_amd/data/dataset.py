@@ -47,9 +47,34 @@ class BlockSlice:
         self.ref, self.offset, self.length = st
 
 
+class BlockGather:
+    """The rows ``index`` (global row numbers over the concatenation of ``refs``) of object-store
+    blocks, in that order: a shuffled dataset is a permutation over the blocks where they already
+    are, so a shard of it pickles to a few ids plus its row numbers and each worker gathers its
+    own rows (in parallel, zero-copy reads of the store) instead of the driver shuffling and
+    shipping copies of every row."""
+    __slots__ = ("refs", "index")
+
+    def __init__(self, refs, index):
+        self.refs, self.index = tuple(refs), np.asarray(index, dtype=np.int64)
+
+    def __getstate__(self):
+        return (self.refs, self.index)
+
+    def __setstate__(self, st):
+        self.refs, self.index = st
+
+    def __len__(self):
+        return int(self.index.size)
+
+
 def _resolve(b) -> pa.Table:
     if isinstance(b, BlockSlice):
         return _resolve(b.ref).slice(b.offset, b.length)
+    if isinstance(b, BlockGather):
+        ts = [_resolve(r) for r in b.refs]
+        t = ts[0] if len(ts) == 1 else pa.concat_tables(ts, promote_options="permissive")
+        return t.take(pa.array(b.index))
     if isinstance(b, ObjectRef):
         b = _get(b)
     if isinstance(b, (bytes, bytearray, memoryview)):
@@ -178,8 +203,14 @@ class Dataset:
     def columns(self) -> List[str]:
         return list(self.schema().names)
 
+    def _rows(self) -> List[int]:
+        """Rows per block, without resolving gathers or slices (their sizes are known)."""
+        if self._tables is None and all(isinstance(b, (BlockGather, BlockSlice)) for b in self._blocks):
+            return [len(b) if isinstance(b, BlockGather) else b.length for b in self._blocks]
+        return [t.num_rows for t in self._get_tables()]
+
     def count(self) -> int:
-        return int(sum(t.num_rows for t in self._get_tables()))
+        return int(sum(self._rows()))
 
     def num_blocks(self) -> int:
         return len(self._blocks)
@@ -191,7 +222,7 @@ class Dataset:
         refs = []
         for i, b in enumerate(self._blocks):
             if not isinstance(b, ObjectRef):
-                b = _put(_resolve(b) if isinstance(b, BlockSlice) else b)
+                b = _put(_resolve(b) if isinstance(b, (BlockSlice, BlockGather)) else b)
                 self._blocks[i] = b
             refs.append(b)
         return refs
@@ -286,11 +317,19 @@ class Dataset:
         if self._pending is not None:
             # still being produced: the shuffle waits with it (lazy, like Ray Data's)
             return Dataset.deferred(_Then(self, lambda d: d.random_shuffle(seed=seed, num_blocks=num_blocks)))
-        t = self.to_arrow()
         rng = np.random.default_rng(seed)
+        n = num_blocks or max(1, self.num_blocks())
+        blocks = self._blocks
+        if blocks and all(isinstance(b, ObjectRef) for b in blocks):
+            # store-resident blocks stay where they are: the result is n gathers over them (the
+            # same rows, order and block sizes as the materialised shuffle below)
+            total = int(sum(t.num_rows for t in self._get_tables()))
+            perm = rng.permutation(total)
+            bounds = _split_bounds(total, n)
+            return Dataset([BlockGather(blocks, perm[a:b]) for a, b in bounds], self.schema())
+        t = self.to_arrow()
         perm = rng.permutation(t.num_rows)
         t = t.take(pa.array(perm))
-        n = num_blocks or max(1, self.num_blocks())
         return Dataset(_split(t, n), t.schema)
 
     def randomize_block_order(self, seed=None):
@@ -303,27 +342,33 @@ class Dataset:
         return Dataset(_split(t, num_blocks), t.schema)
 
     def split(self, n: int, equal: bool = False, locality_hints=None) -> List["Dataset"]:
-        tables = self._get_tables()
         if equal:
             # shard i = global rows [i per, (i + 1) per) in block order, as slices of the blocks
-            # themselves (object-store blocks stay where they are: a shard pickles to a few ids)
-            per = int(sum(t.num_rows for t in tables)) // n
+            # themselves (object-store blocks stay where they are: a shard pickles to a few ids;
+            # a gather's shard is the gather of its row numbers' slice)
+            rows = self._rows()
+            per = int(sum(rows)) // n
             schema = self.schema()
-            starts = np.cumsum([0] + [t.num_rows for t in tables])
+            starts = np.cumsum([0] + rows)
             out = []
             for i in builtins.range(n):
                 lo, hi = i * per, (i + 1) * per
                 parts = []
-                for j, t in enumerate(tables):
+                for j in builtins.range(len(rows)):
                     a, b = max(lo, int(starts[j])), min(hi, int(starts[j + 1]))
                     if a >= b:
                         continue
                     blk = self._blocks[j]
                     off = a - int(starts[j])
-                    parts.append(BlockSlice(blk, off, b - a) if isinstance(blk, (ObjectRef, BlockSlice))
-                                 else t.slice(off, b - a))
+                    if isinstance(blk, BlockGather):
+                        parts.append(BlockGather(blk.refs, blk.index[off:off + b - a]))
+                    elif isinstance(blk, (ObjectRef, BlockSlice)):
+                        parts.append(BlockSlice(blk, off, b - a))
+                    else:
+                        parts.append(self._get_tables()[j].slice(off, b - a))
                 out.append(Dataset(parts or [schema.empty_table()], schema))
             return out
+        tables = self._get_tables()
         if len(tables) >= n:
             # keep blocks whole, balance rows greedily
             sizes = [(t.num_rows, i) for i, t in enumerate(tables)]
@@ -425,10 +470,14 @@ def _to_table(res) -> pa.Table:
     raise TypeError(type(res))
 
 
-def _split(t: pa.Table, n: int) -> List[pa.Table]:
+def _split_bounds(rows: int, n: int):
     n = max(1, int(n))
-    b = np.linspace(0, t.num_rows, n + 1).astype(np.int64)
-    return [t.slice(int(b[i]), int(b[i + 1] - b[i])) for i in builtins.range(n)]
+    b = np.linspace(0, rows, n + 1).astype(np.int64)
+    return [(int(b[i]), int(b[i + 1])) for i in builtins.range(n)]
+
+
+def _split(t: pa.Table, n: int) -> List[pa.Table]:
+    return [t.slice(a, b - a) for a, b in _split_bounds(t.num_rows, n)]
 
 
 # ------------------------------------------------------------------------------ creation --

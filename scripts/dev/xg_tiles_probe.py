@@ -17,6 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 def main_rank(rank, world, port, args):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
     import torch
     import torch.distributed as dist
     import torch.nn as nn
@@ -40,15 +41,25 @@ def main_rank(rank, world, port, args):
         feats[:, :20] = torch.randn(n, 20, generator=g).to(torch.bfloat16)
         feats, labels = feats.to(dev), torch.randn(n, 1, generator=g).to(dev)
         xg = XgmiComm.create(tr.total if tr.G > 1 else tr.grads.numel(), timeout_s=args.timeout, host_seq=True)
-        tr.share = xg.share
-        if tr._mw_args is not None:
-            tr._mw_args.share = xg.share
-        print(f"rank {rank}: share {xg.share} G {tr.G}", flush=True)
+        if xg is not None:       # (world 1: no communicator, the plain one-GPU kernels)
+            tr.share = xg.share
+            if tr._mw_args is not None:
+                tr._mw_args.share = xg.share
+        print(f"rank {rank}: share {getattr(xg, 'share', 1)} G {tr.G}", flush=True)
         for ep in range(args.epochs):
             t0 = time.perf_counter()
             try:
                 tr.train_epoch(feats, labels, n, None, world_size=world, xg=xg)
+                raw = getattr(tr, "_step_stamps", None)
                 st = tr.step_times_us()
+                if args.timeline and raw is not None and ep == args.epochs - 1 and tr.last_path.startswith("persistent"):
+                    s = [int(x) for x in raw[:32]]
+                    us = lambda k: round((s[k] - s[0]) * 0.01, 2) if s[k] else None   # noqa: E731
+                    print(f"rank {rank} middle step (us from its start): fwd {us(3)} bwd {us(4)} vec {us(5)} | "
+                          f"L0 opt: flag {us(16)} wgrad {us(28)} pushed {us(29)} lane0 summed {us(31)} "
+                          f"wg summed {us(30)} updated {us(26)} images {us(27)} counted {us(17)}", flush=True)
+                    if st is not None:
+                        print(f"rank {rank} step_us p50 {float(np.median(st)):.2f} min {float(st.min()):.2f}", flush=True)
                 print(f"rank {rank} epoch {ep}: {time.perf_counter() - t0:.4f} s path {tr.last_path} "
                       f"step_us {None if st is None else [round(float(x), 1) for x in st[:8]]}", flush=True)
             except Exception:  # noqa: BLE001
@@ -67,6 +78,7 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--timeout", type=float, default=10.0)
+    ap.add_argument("--timeline", action="store_true", help="print the middle step's layer-0 exchange stamps")
     a = ap.parse_args()
     sys.path.insert(0, ROOT)
     from raydp_amd.train.trainer import _free_port

@@ -76,3 +76,34 @@ def test_equal_split_references_blocks_instead_of_copying(runtime_local):
             assert len(pickle.dumps(sh)) < 2048
             back = pickle.loads(pickle.dumps(sh))
             assert back.to_arrow().column("x").to_pylist() == whole.slice(i * per, per).column("x").to_pylist()
+
+
+def test_shuffle_of_store_blocks_is_a_gather_with_the_materialised_rows(runtime_local):
+    """random_shuffle over object-store blocks gives gathers (row numbers over the blocks, no row
+    copies on the driver) holding the same rows, order and block sizes as the materialised
+    shuffle; equal shards of it pickle to ids + row numbers and resolve to the same rows."""
+    import pickle
+    import numpy as np
+    import pyarrow as pa
+    from raydp_amd import runtime
+    from raydp_amd.data.dataset import BlockGather, Dataset, _split
+    blocks = [pa.table({"x": list(range(s, s + k)), "y": [float(v) * 0.5 for v in range(s, s + k)]})
+              for s, k in ((0, 7), (7, 13), (20, 5), (25, 11))]
+    ds = Dataset([runtime.put(t) for t in blocks])
+    whole = pa.concat_tables(blocks)
+    sh = ds.random_shuffle(seed=11)
+    assert all(isinstance(b, BlockGather) for b in sh._blocks) and sh.num_blocks() == 4
+    perm = np.random.default_rng(11).permutation(whole.num_rows)
+    want = whole.take(pa.array(perm))
+    assert sh.count() == whole.num_rows
+    assert sh.to_arrow().to_pylist() == want.to_pylist()
+    assert [len(b) for b in sh._blocks] == [t.num_rows for t in _split(want, 4)]
+    for n in (2, 3):
+        per = whole.num_rows // n
+        for i, part in enumerate(sh.split(n, equal=True)):
+            blob = pickle.dumps(part)
+            assert len(blob) < 2048
+            assert pickle.loads(blob).to_arrow().to_pylist() == want.slice(i * per, per).to_pylist()
+    # inline (not store-resident) blocks keep the materialised shuffle
+    inline = Dataset(blocks).random_shuffle(seed=11)
+    assert inline.to_arrow().to_pylist() == want.to_pylist()
