@@ -200,43 +200,110 @@ __device__ __forceinline__ unsigned long long* rx_xg_inbox(const XgDev& x, int a
 
 typedef __attribute__((address_space(1))) unsigned long long rx_xg_gq;
 
+// Where a lane's granules go and come from. XgView reads the communicator's descriptor (device
+// memory, scalar loads); XgRowsView reads a table of row pointers one lane of the workgroup built
+// in LDS before its step loop (rx_xg_rows_init), so no descriptor load sits between a tile's
+// gradient and its pushes.
+struct XgView {
+  const XgDev& x;
+  __device__ int world() const { return x.world; }
+  __device__ int rank() const { return x.rank; }
+  __device__ bool usable() const { return rx_xg_usable(x); }
+  __device__ unsigned long long* out(int p, unsigned seq) const { return rx_xg_inbox(x, p, x.rank, seq); }
+  __device__ const unsigned long long* in(int p, unsigned seq) const { return rx_xg_inbox(x, x.rank, p, seq); }
+};
+
+struct XgRows {
+  unsigned long long* out0[RX_XG_MAXR];       // peer p's inbox row for this rank, parity 0
+  const unsigned long long* in0[RX_XG_MAXR];  // this rank's inbox row for peer p, parity 0
+  unsigned long long par;                     // elements from a parity-0 row to its parity-1 row
+  int world, rank, ok, pad_;
+};
+
+// one lane; the workgroup joins a barrier before any lane uses the table
+__device__ __forceinline__ void rx_xg_rows_init(const XgDev& x, XgRows* r) {
+  r->world = x.world;
+  r->rank = x.rank;
+  r->ok = x.layout == RX_XG_LAYOUT ? 1 : 0;
+  r->par = (unsigned long long)x.world * x.nf;
+  for (int p = 0; p < x.world && r->ok; ++p) {
+    r->out0[p] = rx_xg_inbox(x, p, x.rank, 0u);
+    r->in0[p] = rx_xg_inbox(x, x.rank, p, 0u);
+  }
+}
+
+struct XgRowsView {
+  const XgRows* r;
+  const XgDev& x;
+  __device__ int world() const { return r->world; }
+  __device__ int rank() const { return r->rank; }
+  __device__ bool usable() const {
+    if (r->ok) return true;
+    return rx_xg_usable(x);
+  }
+  __device__ unsigned long long* out(int p, unsigned seq) const { return r->out0[p] + (seq & 1u) * r->par; }
+  __device__ const unsigned long long* in(int p, unsigned seq) const { return r->in0[p] + (seq & 1u) * r->par; }
+};
+
 // This rank's value of flat element idx at sequence seq, into every peer's inbox.
+template <class V>
+__device__ __forceinline__ void rx_xg_push_v(const V& w, unsigned seq, int idx, float v) {
+  const unsigned long long g = ((unsigned long long)seq << 32) | __float_as_uint(v);
+  const int world = w.world(), rank = w.rank();
+  for (int p = 0; p < world; ++p)
+    if (p != rank) __hip_atomic_store((rx_xg_gq*)(w.out(p, seq) + idx), g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void rx_xg_push(const XgDev& x, unsigned seq, int idx, float v) {
   if (x.layout != RX_XG_LAYOUT) return;
-  const unsigned long long g = ((unsigned long long)seq << 32) | __float_as_uint(v);
-  for (int p = 0; p < x.world; ++p)
-    if (p != x.rank)
-      __hip_atomic_store((rx_xg_gq*)(rx_xg_inbox(x, p, x.rank, seq) + idx), g, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+  rx_xg_push_v(XgView{x}, seq, idx, v);
 }
 
 // N elements at once: val[n] (this rank's value on entry) becomes the rank-order sum of element
-// idx[n] (for valid[n]). The loads for up to 4 peers x N elements are issued back to back before
-// any tag is checked, so a lane pays one round trip per 4 peers, not one per element and peer.
-template <int N>
-__device__ __forceinline__ void rx_xg_pull_sum_n(const XgDev& x, unsigned seq, const int (&idx)[N],
+// idx[n] (for valid[n]). The loads for PG peers x N elements are issued back to back before any
+// tag is checked, so a lane pays one round trip per PG peers, not one per element and peer (PG
+// trades registers for round trips: the multi-workgroup step kernel has none to spare).
+template <int N, int PG = 1, bool SENT = false, class V>
+__device__ __forceinline__ void rx_xg_pull_sum_v(const V& w, const XgDev& x, unsigned seq, const int (&idx)[N],
                                                  const bool (&valid)[N], float (&val)[N], bool& ok) {
-  if (!rx_xg_usable(x)) {
+  if (!w.usable()) {
     ok = false;
     return;
   }
   float s[N];
 #pragma unroll
   for (int n = 0; n < N; ++n) s[n] = 0.f;
-  const int world = x.world, rank = x.rank;
-  for (int p0 = 0; p0 < world; p0 += 4) {
-    unsigned long long g[4][N];
+  const int world = w.world(), rank = w.rank();
+  // SENT: one lane per wave first waits for its LAST element of each peer (a peer lane pushes its
+  // N elements in order, its wave's 64 lanes in one store each): the wave's loads below then find
+  // the granules in place instead of every lane polling HBM while a late peer catches up (off in
+  // the multi-workgroup step kernel: the divergent loop costs it scratch)
+  const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int il = idx[N - 1];
+  if (SENT && lane == 0 && valid[N - 1] && ok) {
+    const unsigned long long t0 = wall_clock64();
+    for (int p = 0; p < world; ++p) {
+      if (p == rank) continue;
+      const rx_xg_gq* a = (const rx_xg_gq*)(w.in(p, seq) + il);
+      int k = 0;
+      while ((unsigned)(__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32) != seq) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++k & 15) == 0 && (unsigned long long)(wall_clock64() - t0) > x.spin_ticks) break;   // (the per-element wait below decides)
+      }
+    }
+  }
+  for (int p0 = 0; p0 < world; p0 += PG) {
+    unsigned long long g[PG][N];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < PG; ++q) {
       const int p = p0 + q;
       const bool peer = p < world && p != rank;
-      const rx_xg_gq* row = peer ? (const rx_xg_gq*)rx_xg_inbox(x, rank, p, seq) : nullptr;
+      const rx_xg_gq* row = peer ? (const rx_xg_gq*)w.in(p, seq) : nullptr;
 #pragma unroll
       for (int n = 0; n < N; ++n)
         g[q][n] = (peer && valid[n]) ? __hip_atomic_load(row + idx[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < PG; ++q) {
       const int p = p0 + q;
       if (p >= world) break;
 #pragma unroll
@@ -248,19 +315,20 @@ __device__ __forceinline__ void rx_xg_pull_sum_n(const XgDev& x, unsigned seq, c
         }
         unsigned long long gv = g[q][n];
         if ((unsigned)(gv >> 32) != seq && ok) {
-          const rx_xg_gq* a = (const rx_xg_gq*)(rx_xg_inbox(x, rank, p, seq) + idx[n]);
+          // (a per-lane poll: a lead-lane poll with wave ballots cost the multi-workgroup step
+          // kernel 224 B of scratch per lane)
+          const rx_xg_gq* a = (const rx_xg_gq*)(w.in(p, seq) + idx[n]);
           const unsigned long long t0 = wall_clock64();
           int k = 0;
           do {
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(2);
             gv = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if ((++k & 15) == 0 && (unsigned)(gv >> 32) != seq) {
-              if (__hip_atomic_load((rx_xg_gu*)x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
-                  (unsigned long long)(wall_clock64() - t0) > x.spin_ticks) {
-                rx_xg_fail(x);
-                ok = false;
-                break;
-              }
+            if ((++k & 15) == 0 && (unsigned)(gv >> 32) != seq &&
+                (__hip_atomic_load((rx_xg_gu*)x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
+                 (unsigned long long)(wall_clock64() - t0) > x.spin_ticks)) {
+              rx_xg_fail(x);
+              ok = false;
+              break;
             }
           } while ((unsigned)(gv >> 32) != seq);
         }
@@ -271,4 +339,9 @@ __device__ __forceinline__ void rx_xg_pull_sum_n(const XgDev& x, unsigned seq, c
 #pragma unroll
   for (int n = 0; n < N; ++n)
     if (valid[n]) val[n] = s[n];
+}
+template <int N, int PG = 1>
+__device__ __forceinline__ void rx_xg_pull_sum_n(const XgDev& x, unsigned seq, const int (&idx)[N],
+                                                 const bool (&valid)[N], float (&val)[N], bool& ok) {
+  rx_xg_pull_sum_v<N, PG>(XgView{x}, x, seq, idx, valid, val, ok);
 }

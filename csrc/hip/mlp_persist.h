@@ -154,7 +154,7 @@ __device__ __forceinline__ void ps_vector_update(const D& d, const OptDesc& o, c
       bool val[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) val[j] = idx[j] >= 0;
-      rx_xg_pull_sum_n<J>(*xs.xd, seq, idx, val, g, xok);
+      rx_xg_pull_sum_v<J, 1, true>(XgView{*xs.xd}, *xs.xd, seq, idx, val, g, xok);
     }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -611,7 +611,8 @@ __device__ __forceinline__ void ps_step_wg(const MlpDesc* __restrict__ dp, const
       if (rx_xg_active(xs)) {
         // world > 1: the step's bias / BatchNorm gradients (this workgroup's own Gr stores, drained
         // above) pushed into every peer's inbox; the peers' are summed by the next step's vector
-        // update
+        // update. (Pushing each where the epilogues produce it would start them earlier, but the
+        // push code inside the epilogues spilled ~700 B per lane of the step body.)
         // (up to 4 elements per thread: their loads in flight together, then the pushes)
         int nvec = 0;
         for (int q = 0; q < o.nseg; ++q)
@@ -750,6 +751,8 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, 
     const bool okw = rx_ps_wait(sync, sync + RX_PS_XCC, 1u, ticks);
     flag_lds[0] = okw ? 0 : 1;
     flag_lds[1] = (okw && rx_ps_load(sync + RX_PS_XCC) == me) ? 0 : 1;
+    // world > 1: the inbox row pointers into LDS (this workgroup leaves its dynamic LDS unused)
+    if (rx_xg_active(xs)) rx_xg_rows_init(*xs.xd, reinterpret_cast<XgRows*>(smem));
   }
   __syncthreads();
   const bool wt_ = flag_lds[1] != 0;
@@ -771,13 +774,14 @@ __device__ __forceinline__ void ps_opt_wg(const OptDesc& o, const O& hp, int b, 
       // world > 1: each lane pushes its 4 gradient elements into every peer's inbox and sums the
       // peers' (rank order, polled from its own inbox) in place of the local gradient
       const unsigned seq = xs.seq + (unsigned)s;
+      const XgRowsView xv{reinterpret_cast<const XgRows*>(smem), *xs.xd};
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (ok[r]) rx_xg_push(*xs.xd, seq, idx[r], gw[r]);
+        if (ok[r]) rx_xg_push_v(xv, seq, idx[r], gw[r]);
       if (st && l == 0) rx_g(stamps)[29] = wall_clock64();   // layer 0: pushes issued
       bool okx = true;
       float gv[4] = {gw[0], gw[1], gw[2], gw[3]};
-      rx_xg_pull_sum_n<4>(*xs.xd, seq, idx, ok, gv, okx);
+      rx_xg_pull_sum_v<4, 4, true>(xv, *xs.xd, seq, idx, ok, gv, okx);
 #pragma unroll
       for (int r = 0; r < 4; ++r) gw[r] = gv[r];
       if (st && l == 0) rx_g(stamps)[31] = wall_clock64();   // lane 0's peer values summed

@@ -16,7 +16,10 @@ touching user code (Ray Train's worker setup plays the same role: device placeme
   Eval / no-grad calls, other shapes, kwargs and models whose forward cannot be captured (a host
   sync, data-dependent control flow) run eagerly; the capture's warm-up leaves BatchNorm running
   statistics as they were; outputs are cloned out of the graph's static buffers, so a caller may
-  keep them across steps. Config ``spark.ray.mi355x.graph_user_model``.
+  keep them across steps. The capture differentiates w.r.t. aliases of the parameters (fresh
+  leaves on the same storage) and replays take the real parameters, so a loop that still holds
+  the previous step's loss at the capture -- every plain training loop -- captures cleanly.
+  Config ``spark.ray.mi355x.graph_user_model``.
 
 Reference role: the worker set-up of Ray Train's ``TorchTrainer`` / ``HorovodTrainer``
 (``tutorials/raytrain_example.ipynb`` cell 40, ``examples/horovod_nyctaxi.py:119-162``).
@@ -62,7 +65,7 @@ def worker_policies(use_gpu: bool):
 _MAX_SHAPES = 4        # graphed batch shapes per model (a ragged last batch stays eager)
 _STEADY = 3            # calls with the same shape before it is graphed
 # instance attributes graph_model adds (dropped again by copies and pickles of the module)
-_PATCH_ATTRS = ("forward", "_raydp_graphed", "__reduce_ex__", "__deepcopy__")
+_PATCH_ATTRS = ("forward", "_raydp_graphed", "_raydp_graphs", "__reduce_ex__", "__deepcopy__")
 
 
 def _plain_state(module):
@@ -94,13 +97,22 @@ def graph_model(module):
     graphs, seen, pending = {}, {}, set()
     state = {"failed": False, "outstanding": 0}   # forwards (any shape) whose backward is still to come
 
-    class _Fwd(torch.nn.Module):       # parameters() = the model's, forward = its original one
-        def __init__(self):
-            super().__init__()
-            self.m = module
+    # the trainable parameters, as (owner module, attribute name, tensor)
+    slots = [(sub, name, p) for sub in module.modules() for name, p in list(sub._parameters.items())
+             if p is not None and p.requires_grad]
 
-        def forward(self, *a):
-            return orig(*a)
+    def _fwd_aliased(*a):
+        # the original forward with each parameter replaced by the alias at the same position of
+        # the trailing arguments: fresh leaves sharing the parameters' storage
+        xs, ps = a[:len(a) - len(slots)], a[len(a) - len(slots):]
+        saved = [sub._parameters[name] for sub, name, _ in slots]
+        try:
+            for (sub, name, _), t in zip(slots, ps):
+                sub._parameters[name] = t
+            return orig(*xs)
+        finally:
+            for (sub, name, _), t in zip(slots, saved):
+                sub._parameters[name] = t
 
     def _capture(args):
         bufs = [(b, b.detach().clone()) for b in module.buffers()]
@@ -114,10 +126,17 @@ def graph_model(module):
         if plain is not None:
             _BatchNorm.forward = plain
         try:
-            fwd = _Fwd()
-            samples = tuple(a.detach().clone() for a in args)
+            # The capture differentiates w.r.t. ALIASES of the parameters (fresh leaves on the
+            # same storage), not the parameters: a parameter's gradient accumulator from an
+            # earlier step is still alive while the caller holds that step's loss, and the
+            # capture's backward then synchronises with the default stream it was made on -- a
+            # crash at capture end on this stack (scripts/dev/graph_bisect.py: gm vs gm_delloss).
+            # A replay gets the real parameters (same storage: nothing copied), so autograd
+            # accumulates their gradients as an eager backward would.
+            samples = tuple(a.detach().clone() for a in args) + tuple(
+                p.detach().requires_grad_(True) for _, _, p in slots)
             torch.cuda.synchronize()
-            g = torch.cuda.make_graphed_callables(fwd, samples, num_warmup_iters=3)
+            g = torch.cuda.make_graphed_callables(_fwd_aliased, samples, num_warmup_iters=3)
             return g
         except Exception:  # noqa: BLE001 - not capturable: eager from now on
             state["failed"] = True
@@ -150,7 +169,7 @@ def graph_model(module):
                     if g is not None:
                         graphs[key] = g
             if g is not None:
-                out, graphed = g(*args), True
+                out, graphed = g(*args, *[p for _, _, p in slots]), True
             else:
                 out = orig(*args)
         leaves = [t for t in torch.utils._pytree.tree_leaves(out)
@@ -186,6 +205,7 @@ def graph_model(module):
 
     module.forward = forward
     module._raydp_graphed = True
+    module._raydp_graphs = graphs      # captured shapes (introspection)
     module.__reduce_ex__ = reduce_ex
     module.__deepcopy__ = deepcopy
     return module

@@ -79,7 +79,11 @@ if __name__ == "__main__":
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--timeout", type=float, default=10.0)
     ap.add_argument("--timeline", action="store_true", help="print the middle step's layer-0 exchange stamps")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="RAYDP_XG_DRYRUN=1: the world > 1 kernels without the exchange (its cost = the difference)")
     a = ap.parse_args()
+    if a.dry_run:
+        os.environ["RAYDP_XG_DRYRUN"] = "1"
     sys.path.insert(0, ROOT)
     from raydp_amd.train.trainer import _free_port
     port = _free_port()

@@ -222,6 +222,49 @@ def test_prepare_model_graphs_the_training_step_like_eager():
     assert getattr(mine, "_raydp_graphed", False)
 
 
+def test_graph_model_captures_while_the_previous_steps_loss_is_alive():
+    """A user loop that keeps last step's ``loss`` (and so its autograd graph and the parameters'
+    gradient accumulators) alive into the step that triggers the capture -- the Horovod NYC loop
+    -- must capture (the capture differentiates w.r.t. parameter aliases; capturing against the
+    live accumulators crashed at capture end) and train like the eager model."""
+    import torch.nn.functional as F
+    from raydp_amd.train.gpu_policy import graph_model
+
+    class NYC(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = nn.ModuleList([nn.Linear(a, b) for a, b in ((20, 256), (256, 128), (128, 64), (64, 16))])
+            self.bn = nn.ModuleList([nn.BatchNorm1d(n) for n in (256, 128, 64, 16)])
+            self.head = nn.Linear(16, 1)
+
+        def forward(self, x):
+            for fc, bn in zip(self.fc, self.bn):
+                x = bn(F.relu(fc(x)))
+            return self.head(x)
+
+    torch.manual_seed(0)
+    ref = NYC().cuda()
+    mine = copy.deepcopy(ref)
+    graph_model(mine)
+    g = torch.Generator().manual_seed(4)
+    data = [(torch.randn(64, 20, generator=g).cuda(), torch.randn(64, 1, generator=g).cuda()) for _ in range(8)]
+    losses = {}
+    for m in (ref, mine):
+        opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+        out, loss = [], None
+        for x, y in data:          # `loss` of the previous step is alive at every forward
+            opt.zero_grad()
+            loss = F.smooth_l1_loss(m(x), y)
+            loss.backward()
+            opt.step()
+            out.append(loss.item())
+        losses[id(m)] = out
+    assert len(mine._raydp_graphs) == 1      # captured (not fallen back to eager)
+    torch.testing.assert_close(torch.tensor(losses[id(mine)]), torch.tensor(losses[id(ref)]), rtol=1e-4, atol=1e-5)
+    for a, b in zip(ref.state_dict().values(), mine.state_dict().values()):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
+
+
 def test_graph_model_twin_forwards_before_one_backward_and_copies():
     """Two same-shape forwards before ONE backward (a twin network, two losses summed): the
     second call must not overwrite the first replay's saved activations, so the gradients equal
