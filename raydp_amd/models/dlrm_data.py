@@ -77,8 +77,9 @@ def transform_log(df, do_log: bool = True):
     from raydp_amd.spark.functions import log
     names = [f"_c{c}" for c in INT_COLS]
     if do_log:
-        for n in names:
-            df = df.withColumn(n, log(df[n] + 3))
+        # one projection for the 13 columns (13 withColumn calls type the 26-join plan 13 times)
+        logged = set(names)
+        df = df.select(*[(log(df[n] + 3).alias(n) if n in logged else df[n]) for n in df.columns])
     return df.fillna(0, names)
 
 
@@ -87,12 +88,12 @@ def pre_process(df, frequency_limit="3", output_ordering: str = "total_random", 
     from raydp_amd.spark.functions import count, lit, monotonically_increasing_id, rand
     from raydp_amd.spark.types import LongType
     ids = assign_ids(value_counts(df, frequency_limit)).cache()
-    models = []
-    sizes = []
-    for c, m in column_models(ids):
-        m = m.cache()
-        sizes.append(int(m.agg(count(lit(1)).alias("size")).collect()[0]["size"]) + 1)
-        models.append((c, m))
+    # every table's size from ONE aggregation over the id table (the notebook counts each
+    # column's model separately: 26 jobs of a few ms each for a few KB of ids)
+    per_col = {int(r["column_id"]): int(r["size"])
+               for r in ids.groupBy("column_id").agg(count(lit(1)).alias("size")).collect()}
+    models = [(c, m.cache()) for c, m in column_models(ids)]
+    sizes = [per_col.get(c - CAT_COLS[0], 0) + 1 for c, _ in models]
     if output_ordering == "total_random":
         df = df.withColumn("ordinal", (rand() * (1 << 52)).cast(LongType()))
     elif output_ordering == "input":
