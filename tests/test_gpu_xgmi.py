@@ -276,7 +276,9 @@ def _tiles_b4096(rank, world, port, q):
                                                (8, "_tiles_b64", "persistent_xgmi_tiles"),
                                                (2, "_tiles_b1000", "mw_xgmi_tiles"),
                                                (4, "_tiles_b1000", "mw_xgmi_tiles"),
-                                               (2, "_tiles_b4096", "mw_xgmi_tiles")])
+                                               (8, "_tiles_b1000", "mw_xgmi_tiles"),
+                                               (2, "_tiles_b4096", "mw_xgmi_tiles"),
+                                               (4, "_tiles_b4096", "mw_xgmi_tiles")])
 def test_in_launch_gradient_exchange_matches_gloo_allreduce(world, target, path):
     """World > 1 on the one-GPU engine's kernels: batch 64 trains in the persistent epoch launch
     and batch 1000 / 4096 in the multi-workgroup step, each exchanging per-tile GRADIENTS over
@@ -284,7 +286,8 @@ def test_in_launch_gradient_exchange_matches_gloo_allreduce(world, target, path)
     stay bit-identical, and the parameters and BatchNorm statistics equal those of the same
     trainer fed a gloo all-gather of materialised gradients summed in rank order between
     launches (the exchange's summation order), and the device step time is recorded at
-    world > 1."""
+    world > 1. (World 8 at batch 4096 is 8 x 64 step workgroups: more than one GPU holds at once,
+    so that shape waits for 8 real GPUs.)"""
     res = _run(globals()[target], world, timeout=200)
     assert len(res) == world
     for rank, status, same, rel, paths, step_us in res:
