@@ -775,7 +775,14 @@ def main():
                 spawned_n1, what="the same pipeline with the one training worker in a spawned actor "
                                  "process (the reference topology's worker hop), value = samples/s")
         if sampler is not None:
-            out["config"]["host_resources"] = sampler.summary(cpus)
+            hr = sampler.summary(cpus)
+            conv = timed_phases.get("etl_and_conversion_concurrent")
+            if conv:
+                # the executors only work while the conversion stage runs (the upper bound above
+                # divides by the whole timed region, training included)
+                hr["executor_cpu_utilisation_during_conversion"] = round(
+                    hr["child_process_cpu_s"] / max(conv * cpus, 1e-9), 3)
+            out["config"]["host_resources"] = hr
             out["config"]["train_epoch_samples_per_s"] = [round(m.get("train_samples_per_s", 0), 1)
                                                           for m in hist if "train_samples_per_s" in m]
     if extras:
