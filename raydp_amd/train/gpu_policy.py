@@ -9,6 +9,10 @@ touching user code (Ray Train's worker setup plays the same role: device placeme
   convolutions keep MIOpen. The autograd node the forward picked (native_batch_norm_backward)
   carries the backward. Config ``spark.ray.mi355x.native_batchnorm``.
 
+* :func:`fused_optimizers` -- torch's Adam / AdamW / SGD ``step()`` in the worker's loop runs on
+  the multi-tensor HIP kernels (``raydp_amd/ops/fused_optim.py``), as behind
+  ``hvd.DistributedOptimizer``. Config ``spark.ray.mi355x.fused_optimizer``.
+
 * :func:`graph_model` -- ``train.torch.prepare_model`` on a one-worker GPU job replays the
   model's training forward + backward as HIP graphs (``torch.cuda.make_graphed_callables``) once
   a batch shape has repeated: a tabular MLP step is ~40 tiny kernels each way, each costing more
@@ -56,10 +60,62 @@ def native_batchnorm(enabled: bool = True):
             _BatchNorm.forward = orig
 
 
+@contextlib.contextmanager
+def fused_optimizers(enabled: bool = True):
+    """While active, ``torch.optim.Adam`` / ``AdamW`` / ``SGD`` steps of a user loop run on the
+    multi-tensor HIP kernels (``raydp_amd.ops.fused_optim.fused_step``: one launch per 24 tensors,
+    torch's state layout kept) -- what ``hvd.DistributedOptimizer`` already does -- instead of
+    torch's foreach chain (~10 launches plus their host time per step). Torch's own step still
+    runs for a closure, inside a graph capture, and for anything ``fused_step`` declines (step
+    hooks, amsgrad / capturable / fused / differentiable groups, CPU or non-fp32 parameters):
+    an optimizer it declines once keeps torch's step."""
+    if not enabled:
+        yield
+        return
+    import torch
+    from torch.optim import Optimizer
+    # (AdamW inherits Adam's step in recent torch: only classes that define their own are patched)
+    classes = tuple(c for c in (torch.optim.Adam, torch.optim.AdamW, torch.optim.SGD) if "step" in c.__dict__)
+    originals, patched = {}, {}
+    for cls in classes:
+        orig = cls.__dict__["step"]
+        if not getattr(orig, "hooked", False):
+            # what torch does to a class's step when its first optimizer is built (the wrapper
+            # that runs the step hooks): done here, so the torch path below keeps the hooks
+            orig = Optimizer.profile_hook_step(orig)
+            orig.hooked = True
+        originals[cls] = orig
+
+    def make(orig):
+        def step(self, closure=None):
+            if closure is None and not self.__dict__.get("_raydp_torch_step") and \
+                    not (torch.cuda.is_initialized() and torch.cuda.is_current_stream_capturing()):
+                from raydp_amd.ops import fused_optim
+                if fused_optim.fused_step(self):      # (declines when step hooks are registered)
+                    return None
+                self._raydp_torch_step = True
+            return orig(self, closure)
+        step.__wrapped__ = orig
+        step.hooked = True       # an optimizer built under the policy must not re-wrap the class step
+        return step
+
+    for cls in classes:
+        patched[cls] = cls.step = make(originals[cls])
+    try:
+        yield
+    finally:
+        for cls in classes:
+            if cls.__dict__.get("step") is patched[cls]:
+                cls.step = originals[cls]
+
+
 def worker_policies(use_gpu: bool):
     """The context a GPU train worker runs its loop in (a no-op context on CPU workers)."""
     from raydp_amd.utils import config as C
-    return native_batchnorm(bool(use_gpu) and bool(C.get("spark.ray.mi355x.native_batchnorm")))
+    stack = contextlib.ExitStack()
+    stack.enter_context(native_batchnorm(bool(use_gpu) and bool(C.get("spark.ray.mi355x.native_batchnorm"))))
+    stack.enter_context(fused_optimizers(bool(use_gpu) and bool(C.get("spark.ray.mi355x.fused_optimizer"))))
+    return stack
 
 
 _MAX_SHAPES = 4        # graphed batch shapes per model (a ragged last batch stays eager)
@@ -95,6 +151,7 @@ def graph_model(module):
         return module
     orig = module.forward
     graphs, seen, pending = {}, {}, set()
+    index_cache = {}     # integer-list indices as device tensors (see _capture)
     state = {"failed": False, "outstanding": 0}   # forwards (any shape) whose backward is still to come
 
     # the trainable parameters, as (owner module, attribute name, tensor)
@@ -136,7 +193,16 @@ def graph_model(module):
             samples = tuple(a.detach().clone() for a in args) + tuple(
                 p.detach().requires_grad_(True) for _, _, p in slots)
             torch.cuda.synchronize()
-            g = torch.cuda.make_graphed_callables(_fwd_aliased, samples, num_warmup_iters=3)
+            # a forward that indexes with a Python list (``x[:, [1, 7, 8]]``: the stroke
+            # tutorial's NET_Model) copies the list to the device on every call, which a capture
+            # refuses: the warm-up iterations turn each such index into a cached device tensor
+            # that the captured graph then reads (the same mode the torch-loop engine's graphs use)
+            from raydp_amd.torch.graphs import _CaptureSafeIndexing
+            with _CaptureSafeIndexing(index_cache):
+                # (parameters the forward never reads -- the tutorial's NET_Model keeps five unused
+                # Linear + BatchNorm layers -- get no gradient, as in an eager backward)
+                g = torch.cuda.make_graphed_callables(_fwd_aliased, samples, num_warmup_iters=3,
+                                                      allow_unused_input=True)
             return g
         except Exception:  # noqa: BLE001 - not capturable: eager from now on
             state["failed"] = True

@@ -218,9 +218,11 @@ register("spark.ray.mi355x.overlap_conversion", "bool", True,
          env="RAYDP_OVERLAP_CONVERSION")
 
 register("spark.ray.mi355x.fused_optimizer", "bool", True,
-         "Horovod's DistributedOptimizer runs a wrapped torch Adam / AdamW / SGD step on the multi-tensor "
-         "HIP kernels (csrc/hip/fused_optim.hip: one launch per 24 tensors) when every parameter is a dense "
-         "fp32 GPU tensor; torch's own step otherwise", env="RAYDP_FUSED_OPTIMIZER")
+         "Horovod's DistributedOptimizer, and a torch Adam / AdamW / SGD stepped in a GPU train worker's "
+         "loop (raydp_amd/train/gpu_policy.py fused_optimizers), run the step on the multi-tensor HIP "
+         "kernels (csrc/hip/fused_optim.hip: one launch per 24 tensors) when every parameter is a dense "
+         "fp32 GPU tensor; torch's own step otherwise (closures, step hooks, graph capture, amsgrad / "
+         "capturable / fused groups)", env="RAYDP_FUSED_OPTIMIZER")
 register("spark.ray.mi355x.native_batchnorm", "bool", True,
          "GPU train workers run BatchNorm layers on PyTorch's native kernels instead of MIOpen's (MIOpen's "
          "batch-norm path is launch-bound at tabular batch sizes: scripts/dev/eager_step_bench.py, "

@@ -265,6 +265,96 @@ def test_graph_model_captures_while_the_previous_steps_loss_is_alive():
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
 
 
+def test_graph_model_captures_a_forward_that_indexes_with_a_list():
+    """The stroke tutorial's NET_Model indexes columns with a Python list (an H2D copy of the list
+    per call, which a capture refuses) and owns layers its forward never uses: graph_model still
+    captures it (cached device indices; unused parameters get no gradient) and trains exactly
+    like the eager model."""
+    from raydp_amd.train.gpu_policy import graph_model
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.emb = nn.Embedding(5, 3)
+            self.fc_dense, self.fc = nn.Linear(3, 8), nn.Linear(11, 2)
+            self.unused = nn.Linear(4, 4)      # (as the tutorial model's unused layers)
+
+        def forward(self, *cols):
+            x = torch.cat(cols, dim=1)
+            dense = x[:, [1, 2, 3]]
+            return self.fc(torch.cat([self.fc_dense(dense), self.emb(x[:, 0].long())], dim=1))
+
+    torch.manual_seed(0)
+    ref = Net().cuda()
+    mine = copy.deepcopy(ref)
+    graph_model(mine)
+    g = torch.Generator().manual_seed(6)
+    losses = {}
+    for m in (ref, mine):
+        opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+        crit = nn.CrossEntropyLoss(weight=torch.tensor([0.35, 0.65], device="cuda"))
+        out = []
+        g.manual_seed(6)
+        for _ in range(8):
+            x = torch.cat([torch.randint(0, 5, (64, 1), generator=g).float(), torch.randn(64, 3, generator=g)], 1).cuda()
+            y = torch.randint(0, 2, (64,), generator=g).cuda()
+            loss = crit(m(*[x[:, i].unsqueeze(1) for i in range(4)]), y)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            out.append(loss.item())
+        losses[id(m)] = out
+    assert len(mine._raydp_graphs) == 1
+    torch.testing.assert_close(torch.tensor(losses[id(mine)]), torch.tensor(losses[id(ref)]), rtol=1e-5, atol=1e-6)
+
+
+def test_worker_policy_runs_torch_optimizers_on_the_fused_kernels(monkeypatch):
+    """Under the GPU worker's policies a user loop's plain torch.optim.Adam / SGD step runs on the
+    multi-tensor kernels (fused_step), and trains like torch's own step; outside the policies (and
+    for an optimizer with a step hook) torch's step runs."""
+    from raydp_amd.ops import fused_optim
+    from raydp_amd.train.gpu_policy import fused_optimizers
+    calls = {"n": 0}
+    real = fused_optim.fused_step
+
+    def counting(opt):
+        ok = real(opt)
+        calls["n"] += int(ok)
+        return ok
+    monkeypatch.setattr(fused_optim, "fused_step", counting)
+    for make in (lambda ps: torch.optim.Adam(ps, lr=1e-2, weight_decay=0.01),
+                 lambda ps: torch.optim.SGD(ps, lr=1e-2, momentum=0.9)):
+        torch.manual_seed(0)
+        ref = nn.Sequential(nn.Linear(16, 32), nn.ReLU(), nn.Linear(32, 1)).cuda()
+        mine = copy.deepcopy(ref)
+        g = torch.Generator().manual_seed(2)
+        data = [(torch.randn(64, 16, generator=g).cuda(), torch.randn(64, 1, generator=g).cuda()) for _ in range(6)]
+        o_ref = make(ref.parameters())
+        for x, y in data:
+            o_ref.zero_grad()
+            nn.functional.mse_loss(ref(x), y).backward()
+            o_ref.step()
+        before = calls["n"]
+        with fused_optimizers(True):
+            o = make(mine.parameters())
+            for x, y in data:
+                o.zero_grad()
+                nn.functional.mse_loss(mine(x), y).backward()
+                o.step()
+        assert calls["n"] - before == len(data)
+        for a, b in zip(ref.parameters(), mine.parameters()):
+            torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+    with fused_optimizers(True):   # a step hook keeps torch's step
+        p = nn.Parameter(torch.randn(8, device="cuda"))
+        o = torch.optim.Adam([p], lr=0.1)
+        seen = []
+        o.register_step_post_hook(lambda *a: seen.append(1))
+        p.grad = torch.randn(8, device="cuda")
+        n0 = calls["n"]
+        o.step()
+        assert seen == [1] and calls["n"] == n0
+
+
 def test_graph_model_twin_forwards_before_one_backward_and_copies():
     """Two same-shape forwards before ONE backward (a twin network, two losses summed): the
     second call must not overwrite the first replay's saved activations, so the gradients equal
