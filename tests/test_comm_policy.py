@@ -38,3 +38,32 @@ def test_without_a_process_group_auto_means_on(monkeypatch):
     assert C.comm_stream_wanted() is True
     monkeypatch.setenv("RAYDP_DDP_COMM_STREAM", "off")
     assert C.comm_stream_wanted() is False
+
+
+def test_fused_optimizer_policy_patches_and_restores_torch_steps():
+    """gpu_policy.fused_optimizers: inside, torch's Adam / SGD classes step through the policy
+    (CPU parameters: declined once, then torch's own step, with its step hooks); an optimizer
+    built inside does not re-wrap the class step; on exit the classes have torch's hooked step."""
+    import torch
+    from raydp_amd.train.gpu_policy import fused_optimizers
+    m = torch.nn.Linear(3, 2)
+    ref = torch.nn.Linear(3, 2)
+    ref.load_state_dict(m.state_dict())
+    x = torch.randn(5, 3)
+    o_ref = torch.optim.Adam(ref.parameters(), lr=0.1)
+    ref(x).sum().backward()
+    o_ref.step()
+    with fused_optimizers(True):
+        inside = torch.optim.Adam.__dict__["step"]
+        o = torch.optim.Adam(m.parameters(), lr=0.1)
+        hooked = []
+        o.register_step_post_hook(lambda *a: hooked.append(1))
+        m(x).sum().backward()
+        o.step()
+        assert torch.optim.Adam.__dict__["step"] is inside      # not re-wrapped by the new optimizer
+        assert o.__dict__.get("_raydp_torch_step") and hooked == [1]
+    assert torch.optim.Adam.__dict__["step"] is not inside and getattr(torch.optim.Adam.step, "hooked", False)
+    for a, b in zip(ref.parameters(), m.parameters()):
+        assert torch.equal(a, b)
+    with fused_optimizers(False):
+        assert torch.optim.Adam.__dict__["step"] is not inside

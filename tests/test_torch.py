@@ -177,8 +177,24 @@ def test_spawned_workers_build_their_engines_before_their_shards_exist(spark_on_
         seen.append(v)
         return v
     monkeypatch.setattr(T.DataParallelTrainer, "_deferred_datasets", spy)
+    # the overlapped fit sends every rank its fit BEFORE the conversion stage starts (the started
+    # hook fires, then the stage runs), and never waits out the hook's 30 s backstop
+    import time as _t
+    events = []
+    fire = T._fire_started
+
+    def fire_spy():
+        events.append(("fired", _t.perf_counter()))
+        fire()
+    monkeypatch.setattr(T, "_fire_started", fire_spy)
+    conv = TorchEstimator._convert_via_store
+
+    def conv_spy(self, *a, **k):
+        events.append(("stage", _t.perf_counter()))
+        return conv(self, *a, **k)
+    monkeypatch.setattr(TorchEstimator, "_convert_via_store", conv_spy)
     df = _tiny_df(spark_on_ray_small)
-    outs = []
+    outs, walls = [], []
     for ov in ("0", "1"):
         monkeypatch.setenv("RAYDP_OVERLAP_CONVERSION", ov)
         torch.manual_seed(0)
@@ -187,9 +203,15 @@ def test_spawned_workers_build_their_engines_before_their_shards_exist(spark_on_
                              loss=torch.nn.MSELoss(), feature_columns=["x", "y"], feature_types=torch.float,
                              label_column="z", label_type=torch.float, batch_size=32, num_epochs=2,
                              use_gpu=False, shuffle_seed=7, drop_last=True)
+        del events[:]
+        t0 = _t.perf_counter()
         est.fit_on_spark(df)
+        walls.append(_t.perf_counter() - t0)
         outs.append(est)
     assert seen == [False, True], seen
+    kinds = [k for k, _ in events]          # (the overlapped, warm-group fit)
+    assert "fired" in kinds and "stage" in kinds and kinds.index("fired") < kinds.index("stage"), events
+    assert walls[1] < 20.0, walls
     sa, sb = outs[0].get_model().state_dict(), outs[1].get_model().state_dict()
     for k in sa:
         assert torch.equal(sa[k], sb[k]), k
