@@ -107,3 +107,21 @@ def test_shuffle_of_store_blocks_is_a_gather_with_the_materialised_rows(runtime_
     # inline (not store-resident) blocks keep the materialised shuffle
     inline = Dataset(blocks).random_shuffle(seed=11)
     assert inline.to_arrow().to_pylist() == want.to_pylist()
+
+
+def test_gather_shuffle_edge_shapes(runtime_local):
+    """More blocks than rows, and more shards than rows: empty gathers resolve to empty tables of
+    the schema; the rows are all still there exactly once."""
+    import pickle
+    import pyarrow as pa
+    from raydp_amd import runtime
+    from raydp_amd.data.dataset import Dataset
+    blocks = [pa.table({"x": [1, 2]}), pa.table({"x": [3]})]
+    ds = Dataset([runtime.put(t) for t in blocks]).random_shuffle(seed=3, num_blocks=5)
+    assert ds.num_blocks() == 5 and ds.count() == 3
+    assert sorted(ds.to_arrow().column("x").to_pylist()) == [1, 2, 3]
+    shards = ds.split(4, equal=True)
+    assert all(pickle.loads(pickle.dumps(s)).count() == 0 for s in shards)   # 3 rows // 4 = 0 each
+    shards = ds.split(3, equal=True)
+    got = sorted(v for s in shards for v in pickle.loads(pickle.dumps(s)).to_arrow().column("x").to_pylist())
+    assert got == [1, 2, 3]
